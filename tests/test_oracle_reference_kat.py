@@ -1,0 +1,150 @@
+"""Pin the oracle (oracle/bjx_oracle.c) against the reference's own tests.
+
+Each test restates a reference Go test at the consumeLine boundary with the
+injected clock now_ns (the Go tests use time.Now(); every line they feed is
+<= 10 s old or in the future, so OldLine never fires there either).
+"""
+import random
+
+import pytest
+
+from oracle import oracle as O
+
+S = 1_000_000_000
+
+
+def line(ts, rest):
+    return ("%f %s\n" % (ts, rest)).encode()
+
+
+def test_consume_line_sequence():
+    """regex_rate_limiter_test.go:77-260 TestConsumeLine."""
+    cfg = O.Config()
+    cfg.add_rule("rule1", r"GET example\.com GET .*", 5 * S, 2, O.NGINX_BLOCK)
+    cfg.add_rule("rule2", r"POST .*", 5 * S, 1, O.CHALLENGE)
+    cfg.add_rule("instant block", r".*blockme.*", 1 * S, 0, O.NGINX_BLOCK, site="per-site.com")
+    st = O.State()
+    t0 = 1700000000.123456
+    now = int(t0 * 1e9)
+    ua = "AppleWebKit/537.36 (KHTML, like Gecko) Chrome/51.0.2704.103 Safari/537.36 -"
+    get = "1.2.3.4 GET example.com GET /whatever HTTP/1.1 " + ua
+    post = "1.2.3.4 POST example.com POST /whatever HTTP/1.1 " + ua
+
+    st.consume(cfg, line(t0, get), now)
+    assert st.get("1.2.3.4", "rule1")[0] == 1
+    assert st.banned_ip() == ""
+    st.consume(cfg, line(t0 + 4, get), now)
+    assert st.get("1.2.3.4", "rule1")[0] == 2
+    assert st.banned_ip() == ""
+    st.consume(cfg, line(t0 + 5.5, get), now)
+    assert st.get("1.2.3.4", "rule1")[0] == 1
+    assert st.banned_ip() == ""
+    st.consume(cfg, line(t0 + 6.5, post), now)
+    assert st.get("1.2.3.4", "rule1")[0] == 1
+    assert st.get("1.2.3.4", "rule2")[0] == 1
+    assert st.banned_ip() == ""
+    st.consume(cfg, line(t0 + 7.0, post), now)
+    assert st.get("1.2.3.4", "rule1")[0] == 1
+    assert st.get("1.2.3.4", "rule2")[0] == 0
+    assert st.banned_ip() == "1.2.3.4"
+    st.consume(cfg, line(t0 + 20, "1.6.6.6 GET per-site.com GET /blockme/?a HTTP/1.1 " + ua), now)
+    assert st.get("1.6.6.6", "instant block") is not None
+    st.consume(cfg, line(t0 + 22, "1.6.6.7 GET no-per-site.com GET /blockme/?a HTTP/1.1 " + ua), now)
+    assert st.get("1.6.6.7", "instant block") is None and len(st) == 2
+
+
+def test_consume_line_hosts_to_skip():
+    """regex_rate_limiter_test.go:262-297 TestConsumeLineHostsToSkip."""
+    cfg = O.Config()
+    cfg.add_rule("rule1", r"^GET https?:\/\/\.*", 5 * S, 2, O.NGINX_BLOCK, hosts_to_skip=["skiphost.com"])
+    st = O.State()
+    t0 = 1700000000.5
+    flags, res, _ = st.consume(cfg, line(t0, "1.2.3.4 GET skiphost.com GET /whatever HTTP/1.1 x"), int(t0 * 1e9))
+    assert len(st) == 0
+    # rest is "GET skiphost.com GET ..." -> "^GET https?://" does not match: no RuleResult at all
+    assert res == []
+    # a matching line on a skipped host yields SkipHost and no state
+    flags, res, _ = st.consume(cfg, line(t0, "1.2.3.4 GET skiphost.com GET http://x HTTP/1.1 x"), int(t0 * 1e9))
+    flags, res, _ = st.consume(cfg, line(t0, "1.2.3.4 GET https://a.b GET /x HTTP/1.1 x"), int(t0 * 1e9))
+    assert len(res) == 1 and res[0].skip_host == 0 and len(st) == 1
+
+
+def test_per_site_regex_stress_structure():
+    """regex_rate_limiter_test.go:299-365 TestPerSiteRegexStress (structural;
+    the reference draws unseeded gofakeit data, here a seeded equivalent)."""
+    rnd = random.Random(7)
+    n = 1500
+    cfg = O.Config()
+    domains, paths = [], []
+    for i in range(n):
+        d = "%s%d.%s" % (rnd.choice(["acme", "shop", "news", "blog"]), i, rnd.choice(["com", "org", "net"]))
+        p = "/%s/%d" % (rnd.choice(["a", "img", "api"]), rnd.randrange(10 ** 6))
+        cfg.add_rule("rule%d" % i, r"GET %s GET \%s HTTP\/[0-2.]+ .*" % (d.replace(".", r"\."), p),
+                     1 * S, 0, O.NGINX_BLOCK)
+        domains.append(d)
+        paths.append(p)
+    st = O.State()
+    base = 1700000000
+    for j in range(n):
+        ip = "%d.%d.%d.%d" % (rnd.randrange(1, 255), rnd.randrange(256), rnd.randrange(256), rnd.randrange(256))
+        ln = "%f %s GET %s GET %s HTTP/2.0 Mozilla/5.0 (X11)\n" % (float(base + j), ip, domains[j], paths[j])
+        st.consume(cfg, ln.encode(), (base + j) * S)
+        got = st.get(ip, "rule%d" % j)
+        assert got is not None and got[0] == 0
+        assert st.banned_ip() == ip
+
+
+@pytest.mark.parametrize("pat,text,exp", [
+    (r"Macintosh.*Firefox/\d+", "Mozilla/5.0 (Macintosh; Intel Mac OS X 10.15; rv:149.0) Gecko/20100101 Firefox/149.0", True),
+    (r"Macintosh.*Firefox/\d+", "Mozilla/5.0 (Windows NT 10.0; Win64; x64; rv:149.0) Gecko/20100101 Firefox/149.0", False),
+    (r"(?i)scrapy|mechanize", "Scrapy/2.11.2 (+https://scrapy.org)", True),
+    (r"(?i)scrapy|mechanize", "Python-Mechanize/0.4.9", True),
+    (r"(?i)scrapy|mechanize", "Mozilla/5.0 (compatible; Googlebot/2.1)", False),
+])
+def test_user_agent_regex_known_answers(pat, text, exp):
+    """user_agent_decision_test.go:28-45 (Go regexp known answers)."""
+    assert O.Regex(pat).match(text) is exp
+
+
+def test_invalid_regex_is_a_compile_error():
+    """user_agent_decision_test.go:47-50 and config.go:110-113."""
+    assert O.compile_error("(?invalid") == "error parsing regexp: invalid or unsupported Perl syntax: `(?in`"
+    cfg = O.Config()
+    with pytest.raises(ValueError):
+        cfg.add_rule("bad", "(?invalid", S, 0, O.ALLOW)
+
+
+def test_allow_lists_exempt():
+    """banjax_integration_test.go:387-407 TestRegexesWithRatesAllowList with the
+    fixtures/banjax-config-test.yaml decision lists."""
+    cfg = O.Config()
+    cfg.add_rule("instant block_local", ".*block_local", S, 0, O.NGINX_BLOCK, site="localhost:8081")
+    cfg.add_rule("instant block", ".*blockme.*", S, 0, O.NGINX_BLOCK)
+    cfg.add_decision_ip(O.ALLOW, "20.20.20.20")
+    for ip in ("8.8.8.8", "60.60.60.60", "192.168.1.0/24"):
+        cfg.add_decision_ip(O.CHALLENGE, ip)
+    cfg.add_decision_ip(O.ALLOW, "90.90.90.90", site="localhost:8081")
+    cfg.add_decision_ip(O.ALLOW, "171.171.171.0/24", site="localhost:8081")
+    st = O.State()
+    t = 1700000000.0
+    buf = b"".join([
+        line(t, "171.171.171.171 GET localhost:8081 GET /block_local HTTP/1.1 Go"),
+        line(t, "20.20.20.20 GET localhost:8081 GET /blockme/ HTTP/1.1 Go"),
+        line(t, "171.171.172.1 GET localhost:8081 GET /block_local HTTP/1.1 Go"),
+        line(t, "171.171.171.9 GET other.com GET /blockme/ HTTP/1.1 Go"),
+    ])
+    flags, res, _ = st.consume(cfg, buf, int(t * 1e9))
+    assert flags == [O.LINE_EXEMPTED, O.LINE_EXEMPTED, 0, 0]
+    assert [r.exceeded for r in res] == [1, 1]
+
+
+def test_line_errors_and_old_lines():
+    cfg = O.Config()
+    cfg.add_rule("all", ".*", S, 100, O.CHALLENGE)
+    st = O.State()
+    t = 1700000000.0
+    now = int(t * 1e9)
+    buf = b"\n" + b"x\n" + b"1.5 1.2.3.4\n" + b"abc 1.2.3.4 GET h GET / x\n" + b"1700000000 1.2.3.4 GET\n" \
+        + line(t - 11, "1.2.3.4 GET h GET / x") + line(t - 9, "1.2.3.4 GET h GET / x") + b"1e400 1.2.3.4 GET h x\n"
+    flags, res, _ = st.consume(cfg, buf, now)
+    assert flags == [1, 1, 1, 1, 1, 2, 0, 1]
