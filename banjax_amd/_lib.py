@@ -1,0 +1,127 @@
+"""ctypes binding of libbanjax_gpu.so (include/banjax_gpu.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no GPU
+is visible, the calls below raise.  Build it with `python -m banjax_amd.build`
+(or __graft_entry__.build()).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libbanjax_gpu.so")
+
+OK = 0
+ERR_REGEX, ERR_ARG, ERR_DEVICE, ERR_NOMEM, ERR_TOO_COMPLEX, ERR_CAPACITY, ERR_DECISION = -1, -2, -3, -4, -5, -6, -7
+INPUT_DEVICE, COPY_RESULTS = 1, 2
+
+
+class Str(C.Structure):
+    _fields_ = [("ptr", C.c_char_p), ("len", C.c_size_t)]
+
+
+class RuleSpec(C.Structure):
+    _fields_ = [("name", Str), ("regex", Str), ("interval_ns", C.c_int64), ("hits_per_interval", C.c_int64),
+                ("decision", C.c_int32), ("hosts_to_skip", C.POINTER(Str)), ("n_hosts_to_skip", C.c_size_t)]
+
+
+class SiteRules(C.Structure):
+    _fields_ = [("host", Str), ("rules", C.POINTER(RuleSpec)), ("n_rules", C.c_size_t)]
+
+
+class EngineOptions(C.Structure):
+    _fields_ = [("ip_capacity", C.c_uint64), ("state_capacity", C.c_uint64), ("ip_arena_bytes", C.c_uint64)]
+
+
+class DecisionEntry(C.Structure):
+    _fields_ = [("site", Str), ("decision", C.c_int32), ("ip", Str)]
+
+
+class RuleResult(C.Structure):
+    _fields_ = [("line_idx", C.c_uint64), ("rule_idx", C.c_uint32), ("rule_pos", C.c_uint16),
+                ("skip_host", C.c_uint8), ("seen_ip", C.c_uint8), ("match_type", C.c_uint8),
+                ("exceeded", C.c_uint8), ("_pad", C.c_uint8 * 2)]
+
+
+class Trip(C.Structure):
+    _fields_ = [("line_idx", C.c_uint64), ("line_offset", C.c_uint64), ("line_len", C.c_uint32),
+                ("rule_idx", C.c_uint32), ("ts_ns", C.c_int64), ("ip_off", C.c_uint32), ("ip_len", C.c_uint32),
+                ("host_off", C.c_uint32), ("host_len", C.c_uint32), ("rest_off", C.c_uint32),
+                ("decision", C.c_int32)]
+
+
+class BatchResult(C.Structure):
+    _fields_ = [("n_lines", C.c_uint64), ("consumed_bytes", C.c_uint64), ("n_results", C.c_uint64),
+                ("n_events", C.c_uint64), ("n_trips", C.c_uint64), ("line_flags", C.POINTER(C.c_uint8)),
+                ("results", C.POINTER(RuleResult)), ("trips", C.POINTER(Trip)), ("device_ms", C.c_double),
+                ("match_kernel_ms", C.c_double)]
+
+
+# every symbol include/banjax_gpu.h declares
+EXPORTS = [
+    "bjx_abi_version", "bjx_ruleset_compile", "bjx_ruleset_release", "bjx_ruleset_num_rules",
+    "bjx_ruleset_rule_info", "bjx_engine_create", "bjx_engine_destroy", "bjx_engine_set_decision_lists",
+    "bjx_process_batch", "bjx_state_get", "bjx_state_len", "bjx_state_clear", "bjx_state_dump",
+    "bjx_engine_last_error",
+]
+
+_lib = None
+
+
+class BanjaxGpuError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s (code %d)" % (msg, code))
+        self.code = code
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise BanjaxGpuError(ERR_DEVICE, "libbanjax_gpu.so not built (run __graft_entry__.build()); "
+                                         "there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    vp, sz = C.c_void_p, C.c_size_t
+    L.bjx_abi_version.restype = C.c_int
+    L.bjx_ruleset_compile.restype = C.c_int
+    L.bjx_ruleset_compile.argtypes = [C.POINTER(RuleSpec), sz, C.POINTER(SiteRules), sz, C.POINTER(vp),
+                                      C.POINTER(C.c_int64), C.c_char_p, sz]
+    L.bjx_ruleset_release.argtypes = [vp]
+    L.bjx_ruleset_num_rules.restype = sz
+    L.bjx_ruleset_num_rules.argtypes = [vp]
+    L.bjx_ruleset_rule_info.restype = C.c_int
+    L.bjx_ruleset_rule_info.argtypes = [vp, sz, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+    L.bjx_engine_create.restype = C.c_int
+    L.bjx_engine_create.argtypes = [C.c_int, C.POINTER(EngineOptions), C.POINTER(vp), C.c_char_p, sz]
+    L.bjx_engine_destroy.argtypes = [vp]
+    L.bjx_engine_set_decision_lists.restype = C.c_int
+    L.bjx_engine_set_decision_lists.argtypes = [vp, C.POINTER(DecisionEntry), sz]
+    L.bjx_process_batch.restype = C.c_int
+    L.bjx_process_batch.argtypes = [vp, vp, vp, sz, C.c_int64, C.c_uint32, C.POINTER(BatchResult)]
+    L.bjx_state_get.restype = C.c_int
+    L.bjx_state_get.argtypes = [vp, C.c_char_p, sz, C.c_char_p, sz, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    L.bjx_state_len.restype = C.c_int64
+    L.bjx_state_len.argtypes = [vp]
+    L.bjx_state_clear.restype = C.c_int
+    L.bjx_state_clear.argtypes = [vp]
+    L.bjx_state_dump.restype = sz
+    L.bjx_state_dump.argtypes = [vp, C.c_char_p, sz]
+    L.bjx_debug_rule_match_host.restype = C.c_int
+    L.bjx_debug_rule_match_host.argtypes = [vp, sz, C.c_char_p, sz]
+    L.bjx_debug_rule_literal.restype = sz
+    L.bjx_debug_rule_literal.argtypes = [vp, sz, C.c_char_p, sz]
+    L.bjx_engine_last_error.restype = C.c_char_p
+    L.bjx_engine_last_error.argtypes = [vp]
+    _lib = L
+    return L
+
+
+def b(x) -> bytes:
+    return x if isinstance(x, bytes) else str(x).encode()
+
+
+def mkstr(x) -> Str:
+    bx = b(x)
+    return Str(bx, len(bx))

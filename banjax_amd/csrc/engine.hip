@@ -1,0 +1,1527 @@
+// MI355X engine for banjax's regex rate-limiting log tailer.
+//
+// One bjx_process_batch = the reference's consumeLine applied to every line of
+// a '\n'-framed chunk (internal/regex_rate_limiter.go:113-269), with the
+// per-(ip, rule-name) fixed-window counters of RegexRateLimitStates.Apply
+// (internal/rate_limit.go:37-78) kept resident in HBM across batches.
+//
+// Pipeline (DESIGN.md "Kernels"):
+//   k_nl_count / k_nl_write    line framing: '\n' positions (coalesced 16 B/lane)
+//   k_parse_match<FAST>        per line: SplitN header parse, ParseFloat fast path,
+//                              host lookup, CheckIsAllowed, then every applicable
+//                              rule's DFA over the rest -> match bitmask
+//   k_parse_match<SLOW>        lines whose timestamp needs the general ParseFloat
+//   scan + k_emit              RuleResults in reference order + rate-limit events
+//   radix sort by IP hash      groups events per IP, preserving (line, rule) order
+//   k_heads + k_ratelimit      one thread per IP: the Apply state machine in order
+//   trip compaction            RateLimitResult.Exceeded -> host replays the Banner
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/banjax_gpu.h"
+#include "bjx_common.h"
+#include "engine_types.h"
+#include "regex_compiler.h"
+
+using namespace bjx;
+
+namespace {
+
+struct BjxError : std::runtime_error {
+  int code;
+  BjxError(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIP_OK(expr)                                                                                   \
+  do {                                                                                                 \
+    hipError_t e_ = (expr);                                                                            \
+    if (e_ != hipSuccess)                                                                              \
+      throw BjxError(BJX_ERR_DEVICE, std::string(#expr " failed: ") + hipGetErrorString(e_));          \
+  } while (0)
+
+constexpr uint32_t kTile = 4096;   // bytes per framing tile (256 lanes x 16 B)
+constexpr int kBlock = 256;
+
+// =====================================================================
+//                              device code
+// =====================================================================
+
+// --------------------------------------------------------------- framing
+
+__device__ __forceinline__ uint32_t nl_mask_word(uint32_t v) {
+  // exact per-byte '\n' detector: returns 0x80 in each byte equal to 0x0A
+  uint32_t x = v ^ 0x0A0A0A0Au;
+  uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;
+  return ~t & 0x80808080u;
+}
+
+__global__ __launch_bounds__(kBlock) void k_nl_count(const uint8_t *__restrict__ buf, uint64_t n,
+                                                     uint32_t *__restrict__ tile_counts) {
+  typedef hipcub::BlockReduce<uint32_t, kBlock> BR;
+  __shared__ typename BR::TempStorage tmp;
+  const uint64_t base = (uint64_t)blockIdx.x * kTile + threadIdx.x * 16u;
+  uint32_t cnt = 0;
+  if (base + 16 <= n) {
+    uint4 v = *reinterpret_cast<const uint4 *>(buf + base);
+    cnt = __popc(nl_mask_word(v.x)) + __popc(nl_mask_word(v.y)) + __popc(nl_mask_word(v.z)) + __popc(nl_mask_word(v.w));
+  } else {
+    for (uint64_t k = base; k < n && k < base + 16; ++k) cnt += buf[k] == '\n';
+  }
+  uint32_t tot = BR(tmp).Sum(cnt);
+  if (threadIdx.x == 0) tile_counts[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kBlock) void k_nl_write(const uint8_t *__restrict__ buf, uint64_t n,
+                                                     const uint64_t *__restrict__ tile_base, uint64_t *__restrict__ nl) {
+  typedef hipcub::BlockScan<uint32_t, kBlock> BS;
+  __shared__ typename BS::TempStorage tmp;
+  const uint64_t base = (uint64_t)blockIdx.x * kTile + threadIdx.x * 16u;
+  uint32_t m[4] = {0, 0, 0, 0};
+  uint32_t cnt = 0;
+  if (base + 16 <= n) {
+    uint4 v = *reinterpret_cast<const uint4 *>(buf + base);
+    m[0] = nl_mask_word(v.x); m[1] = nl_mask_word(v.y); m[2] = nl_mask_word(v.z); m[3] = nl_mask_word(v.w);
+  } else {
+    for (uint64_t k = base; k < n && k < base + 16; ++k)
+      if (buf[k] == '\n') m[(k - base) >> 2] |= 0x80u << (8 * ((k - base) & 3));
+  }
+  cnt = __popc(m[0]) + __popc(m[1]) + __popc(m[2]) + __popc(m[3]);
+  uint32_t off;
+  BS(tmp).ExclusiveSum(cnt, off);
+  uint64_t o = tile_base[blockIdx.x] + off;
+  for (int w = 0; w < 4; ++w) {
+    uint32_t x = m[w];
+    while (x) {
+      int b = __ffs(x) - 1;
+      nl[o++] = base + 4 * w + (b >> 3);
+      x &= x - 1;
+    }
+  }
+}
+
+// --------------------------------------------------------------- lookups
+
+__device__ __forceinline__ uint32_t find_space(const uint8_t *p, uint32_t i, uint32_t n) {
+  while (i < n && p[i] != ' ') ++i;
+  return i;
+}
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t *a, const uint8_t *b, uint32_t n) {
+  for (uint32_t k = 0; k < n; ++k)
+    if (a[k] != b[k]) return false;
+  return true;
+}
+
+// host string -> host id (per_site_regexes_with_rates key / skip host / allow-list site)
+__device__ int32_t host_lookup(const Bind &B, const uint8_t *h, uint32_t n) {
+  if (B.n_hd == 0) return -1;
+  const uint64_t hh = hash_bytes(h, n);
+  uint32_t lo = 0, hi = B.n_hd;
+  while (lo < hi) {
+    uint32_t m = (lo + hi) >> 1;
+    if (B.hd_hash[m] < hh) lo = m + 1; else hi = m;
+  }
+  for (; lo < B.n_hd && B.hd_hash[lo] == hh; ++lo)
+    if (B.hd_len[lo] == n && bytes_eq(B.hd_bytes + B.hd_off[lo], h, n)) return (int32_t)B.hd_id[lo];
+  return -1;
+}
+
+__device__ __forceinline__ uint64_t be64(const uint8_t *a) {
+  uint64_t v = 0;
+  for (int k = 0; k < 8; ++k) v = (v << 8) | a[k];
+  return v;
+}
+
+// IPFilter.Allowed restricted to one scope (decision.go:185-216 with
+// github.com/jeremy5189/ipfilter-no-iploc/v2: exact canonical IPs, then subnets).
+__device__ bool scope_allows_addr(const Bind &B, int sc, const uint8_t a[16]) {
+  const uint64_t hi = be64(a), lo = be64(a + 8);
+  uint32_t b = B.sc_addr_off[sc], e = B.sc_addr_off[sc + 1];
+  while (b < e) {
+    uint32_t m = (b + e) >> 1;
+    uint64_t mh = B.sc_addr[2 * m], ml = B.sc_addr[2 * m + 1];
+    if (mh < hi || (mh == hi && ml < lo)) b = m + 1; else e = m;
+  }
+  if (b < B.sc_addr_off[sc + 1] && B.sc_addr[2 * b] == hi && B.sc_addr[2 * b + 1] == lo) return true;
+  const bool v4 = is_v4_mapped(a);
+  for (uint32_t k = B.sc_sub_off[sc]; k < B.sc_sub_off[sc + 1]; ++k) {
+    const Subnet &s = B.sc_sub[k];
+    const uint8_t *ip = v4 ? a + 12 : a;
+    const uint32_t l = v4 ? 4 : 16;
+    if (l != s.netlen) continue;
+    bool ok = true;
+    for (uint32_t i = 0; i < l; ++i)
+      if ((s.net[i] & s.mask[i]) != (ip[i] & s.mask[i])) { ok = false; break; }
+    if (ok) return true;
+  }
+  return false;
+}
+// exact-map Allow entries that net.ParseIP refuses (compared byte for byte)
+__device__ bool scope_allows_str(const Bind &B, int sc, uint64_t h, const uint8_t *s, uint32_t n) {
+  uint32_t b = B.sc_str_off[sc], e = B.sc_str_off[sc + 1];
+  while (b < e) {
+    uint32_t m = (b + e) >> 1;
+    if (B.sc_str_hash[m] < h) b = m + 1; else e = m;
+  }
+  for (; b < B.sc_str_off[sc + 1] && B.sc_str_hash[b] == h; ++b)
+    if (B.sc_str_len[b] == n && bytes_eq(B.sc_str_bytes + B.sc_str_boff[b], s, n)) return true;
+  return false;
+}
+// StaticDecisionLists.CheckIsAllowed(site, clientIp)
+__device__ bool check_is_allowed(const Bind &B, int32_t host_id, const uint8_t *ip, uint32_t n) {
+  const int32_t site_sc = host_id >= 0 ? B.host_scope[host_id] : -1;
+  uint8_t a[16];
+  bool is4;
+  const bool ok = go_parse_addr(ip, n, a, &is4);
+  uint64_t h = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    const int sc = pass == 0 ? site_sc : 0;
+    if (sc < 0) continue;
+    if (ok) {
+      if (scope_allows_addr(B, sc, a)) return true;
+    } else {
+      if (!h) h = hash_bytes(ip, n);
+      if (scope_allows_str(B, sc, h, ip, n)) return true;
+    }
+  }
+  return false;
+}
+
+__device__ __forceinline__ bool is_skip(const Bind &B, uint32_t rule, int32_t host_id) {
+  if (host_id < 0 || B.n_skip == 0) return false;
+  const uint64_t k = ((uint64_t)rule << 32) | (uint32_t)host_id;
+  uint32_t lo = 0, hi = B.n_skip;
+  while (lo < hi) {
+    uint32_t m = (lo + hi) >> 1;
+    if (B.skip_keys[m] < k) lo = m + 1; else hi = m;
+  }
+  return lo < B.n_skip && B.skip_keys[lo] == k;
+}
+
+// --------------------------------------------------------------- regex
+
+// (*Regexp).Match over rest, via the rule's rune-class DFA.
+__device__ bool rule_match(const Bind &B, uint32_t r, const uint8_t *t, uint32_t n) {
+  const DevRule R = B.rules[r];
+  if (R.flags & kRuleAlways) return true;
+  if (R.flags & kRuleNever) return false;
+  const uint16_t *tr = B.trans + R.trans_off;
+  const uint8_t *ac = B.ascii_cls + (size_t)r * 128;
+  const uint32_t ncls = R.ncls;
+  uint32_t st = R.start;
+  uint32_t i = 0;
+  while (i < n) {
+    const uint8_t b = t[i];
+    uint32_t c;
+    if (b < 0x80) {
+      c = ac[b];
+      ++i;
+    } else {
+      int w;
+      const int32_t rune = decode_rune_hd(t + i, n - i, &w);
+      i += (uint32_t)w;
+      const uint32_t *na = B.nonascii + 2 * R.na_off;
+      uint32_t lo = 0, hi = R.n_na;  // last interval with start <= rune
+      while (hi - lo > 1) {
+        uint32_t m = (lo + hi) >> 1;
+        if (na[2 * m] <= (uint32_t)rune) lo = m; else hi = m;
+      }
+      c = na[2 * lo + 1];
+    }
+    st = tr[st * ncls + c];
+    if (st <= 1) break;
+  }
+  return B.accept_end[R.ae_off + st] != 0;
+}
+
+// --------------------------------------------------------------- per line
+
+template <bool SLOW>
+__device__ void parse_and_match(const Bind &B, const uint8_t *__restrict__ p, uint32_t n, uint64_t j, int64_t now_ns,
+                                const Lines &L, uint32_t *slow_list, unsigned long long *slow_count) {
+  uint8_t fl = 0;
+  L.counts[j] = 0;
+  const uint32_t sp1 = find_space(p, 0, n);
+  if (sp1 >= n) { L.flags[j] = kLineError; return; }
+  const uint32_t sp2 = find_space(p, sp1 + 1, n);
+  if (sp2 >= n) { L.flags[j] = kLineError; return; }
+  const uint32_t sp3 = find_space(p, sp2 + 1, n);
+  if (sp3 >= n) { L.flags[j] = kLineError; return; }
+  const uint32_t sp4 = find_space(p, sp3 + 1, n);
+  if (sp4 >= n) { L.flags[j] = kLineError; return; }
+  const uint32_t ip_off = sp1 + 1, ip_len = sp2 - sp1 - 1;
+  const uint32_t rest_off = sp2 + 1, host_off = sp3 + 1, host_len = sp4 - sp3 - 1;
+  int32_t hid;
+  bool exempt;
+  double f;
+  if (!SLOW) {
+    hid = host_lookup(B, p + host_off, host_len);
+    exempt = B.any_allow && check_is_allowed(B, hid, p + ip_off, ip_len);
+    L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
+    L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
+    L.host_id[j] = hid;
+    L.ip_hash[j] = hash_bytes(p + ip_off, ip_len);
+    if (parse_float_fast(p, sp1, &f) != 0) {
+      // rare: exotic timestamp token -> general ParseFloat kernel
+      L.flags[j] = kLineSlowTs | (exempt ? kLineExemptPending : 0);
+      unsigned long long k = atomicAdd(slow_count, 1ull);
+      slow_list[k] = (uint32_t)j;
+      return;
+    }
+  } else {
+    hid = L.host_id[j];
+    exempt = (L.flags[j] & kLineExemptPending) != 0;
+    Decimal dec;
+    if (go_parse_float(p, sp1, &f, &dec) != 0) { L.flags[j] = kLineError; return; }
+  }
+  const int64_t ts = ns_from_seconds(f);
+  L.ts[j] = ts;
+  if (go_sub(now_ns, ts) > 10000000000LL) fl = kLineOld;
+  else if (exempt) fl = kLineExempt;
+  L.flags[j] = fl;
+  if (fl) return;
+
+  // per-site rules first, then global rules, in YAML order (regex_rate_limiter.go:175-211)
+  const uint8_t *rest = p + rest_off;
+  const uint32_t rest_len = n - rest_off;
+  uint64_t *mask = L.masks + j * B.mask_words;
+  uint64_t word = 0;
+  uint32_t pos = 0, wi = 0, nres = 0, nev = 0;
+  uint32_t s_begin = 0, s_end = 0;
+  if (hid >= 0) { s_begin = B.site_off[hid]; s_end = B.site_off[hid + 1]; }
+  const uint32_t napp = (s_end - s_begin) + B.n_global;
+  for (uint32_t k = 0; k < napp; ++k) {
+    const uint32_t r = k < s_end - s_begin ? B.site_rules[s_begin + k] : B.global_rules[k - (s_end - s_begin)];
+    if (rule_match(B, r, rest, rest_len)) {
+      word |= 1ull << (pos & 63);
+      ++nres;
+      nev += is_skip(B, r, hid) ? 0u : 1u;
+    }
+    ++pos;
+    if ((pos & 63) == 0) { mask[wi++] = word; word = 0; }
+  }
+  if (pos & 63) mask[wi] = word;
+  L.counts[j] = ((uint64_t)nres << 32) | nev;
+}
+
+template <bool SLOW>
+__global__ __launch_bounds__(kBlock) void k_parse_match(Bind B, const uint8_t *__restrict__ buf,
+                                                        const uint64_t *__restrict__ nl, uint64_t n_lines,
+                                                        const uint32_t *__restrict__ list, int64_t now_ns, Lines L,
+                                                        uint32_t *slow_list, unsigned long long *slow_count) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_lines) return;
+  const uint64_t j = SLOW ? list[t] : t;
+  const uint64_t s = j ? nl[j - 1] + 1 : 0;
+  const uint32_t n = (uint32_t)(nl[j] - s);
+  parse_and_match<SLOW>(B, buf + s, n, j, now_ns, L, slow_list, slow_count);
+}
+
+// RuleResults (reference order) and rate-limit events from the per-line masks.
+__global__ __launch_bounds__(kBlock) void k_emit(Bind B, uint64_t n_lines, Lines L, const uint64_t *__restrict__ offs,
+                                                 uint64_t *__restrict__ res_seq, uint32_t *__restrict__ res_rule,
+                                                 uint32_t *__restrict__ ev_key, uint32_t *__restrict__ ev_res) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_lines) return;
+  if (L.counts[j] == 0) return;
+  uint64_t ro = offs[j] >> 32, eo = offs[j] & 0xFFFFFFFFull;
+  const int32_t hid = L.host_id[j];
+  uint32_t s_begin = 0, s_end = 0;
+  if (hid >= 0) { s_begin = B.site_off[hid]; s_end = B.site_off[hid + 1]; }
+  const uint32_t nsite = s_end - s_begin;
+  const uint32_t napp = nsite + B.n_global;
+  const uint32_t key = (uint32_t)L.ip_hash[j];
+  const uint64_t *mask = L.masks + j * B.mask_words;
+  for (uint32_t w = 0; w * 64 < napp; ++w) {
+    uint64_t m = mask[w];
+    while (m) {
+      const uint32_t b = (uint32_t)__ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      const uint32_t pos = w * 64 + b;
+      const uint32_t r = pos < nsite ? B.site_rules[s_begin + pos] : B.global_rules[pos - nsite];
+      const bool skip = is_skip(B, r, hid);
+      res_seq[ro] = (j << 16) | pos;
+      res_rule[ro] = r | (skip ? 0x80000000u : 0u);
+      if (!skip) { ev_key[eo] = key; ev_res[eo] = (uint32_t)ro; ++eo; }
+      ++ro;
+    }
+  }
+}
+
+// segment heads of the IP-hash-sorted events + bounds on new IPs / arena bytes
+__global__ __launch_bounds__(kBlock) void k_heads(uint64_t n_ev, const uint32_t *__restrict__ key,
+                                                  const uint32_t *__restrict__ ev_res, const uint64_t *__restrict__ res_seq,
+                                                  Lines L, uint8_t *__restrict__ head, unsigned long long *bounds) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_ev) return;
+  head[t] = (t == 0 || key[t] != key[t - 1]) ? 1 : 0;
+  const uint64_t line = res_seq[ev_res[t]] >> 16;
+  const uint64_t h = L.ip_hash[line];
+  const uint64_t hp = t ? L.ip_hash[res_seq[ev_res[t - 1]] >> 16] : ~h;
+  if (h != hp) {
+    atomicAdd(&bounds[0], 1ull);
+    atomicAdd(&bounds[1], (unsigned long long)L.ip_len[line]);
+  }
+}
+
+// --------------------------------------------------------------- state
+
+__device__ __forceinline__ uint64_t line_start(const uint64_t *nl, uint64_t line) { return line ? nl[line - 1] + 1 : 0; }
+
+// find-or-insert an IP string.  All events of one 64-bit hash are owned by one
+// thread (same segment), so a slot holding this hash was published by an
+// earlier kernel or by this thread; other threads only race on claiming empty
+// slots (CAS), never on reading payloads.
+__device__ uint32_t ip_find_insert(const State &S, uint64_t h, const uint8_t *ip, uint32_t len, bool *existed) {
+  uint64_t i = h & S.ip_mask;
+  for (;;) {
+    uint64_t cur = S.ip_slot_hash[i];
+    if (cur == 0) {
+      unsigned long long prev = atomicCAS((unsigned long long *)&S.ip_slot_hash[i], 0ull, (unsigned long long)h);
+      if (prev == 0) {
+        const uint32_t id = (uint32_t)atomicAdd((unsigned long long *)&S.counters[0], 1ull);
+        const uint64_t off = atomicAdd((unsigned long long *)&S.counters[1], (unsigned long long)len);
+        for (uint32_t k = 0; k < len; ++k) S.arena[off + k] = ip[k];
+        S.ip_off[id] = off;
+        S.ip_len[id] = len;
+        S.ip_slot_id[i] = id;
+        *existed = false;
+        return id;
+      }
+      cur = prev;
+    }
+    if (cur == h) {
+      const uint32_t id = S.ip_slot_id[i];
+      if (S.ip_len[id] == len && bytes_eq(S.arena + S.ip_off[id], ip, len)) { *existed = true; return id; }
+    }
+    i = (i + 1) & S.ip_mask;
+  }
+}
+
+__device__ uint64_t st_find_insert(const State &S, uint64_t key, bool *fresh) {
+  uint64_t i = mix64(key) & S.st_mask;
+  for (;;) {
+    uint64_t cur = S.st_key[i];
+    if (cur == 0) {
+      unsigned long long prev = atomicCAS((unsigned long long *)&S.st_key[i], 0ull, (unsigned long long)key);
+      if (prev == 0) {
+        atomicAdd((unsigned long long *)&S.counters[2], 1ull);
+        *fresh = true;
+        return i;
+      }
+      cur = prev;
+    }
+    if (cur == key) { *fresh = false; return i; }
+    i = (i + 1) & S.st_mask;
+  }
+}
+
+// RegexRateLimitStates.Apply (rate_limit.go:37-78) for every event of one IP
+// group, in (line, rule-position) order.  rl_out bit0 seenIp, bits1-2
+// MatchType, bit3 Exceeded, bit7 valid.
+__global__ __launch_bounds__(kBlock) void k_ratelimit(
+    uint64_t n_seg, uint64_t n_ev, const uint32_t *__restrict__ heads, const uint32_t *__restrict__ ev_res,
+    const uint64_t *__restrict__ res_seq, const uint32_t *__restrict__ res_rule, const uint64_t *__restrict__ nl,
+    const uint8_t *__restrict__ buf, Lines L, const DevRule *__restrict__ rules, State S, uint8_t *__restrict__ rl_out,
+    uint8_t *__restrict__ processed) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_seg) return;
+  const uint64_t b = heads[k], e = (k + 1 < n_seg) ? heads[k + 1] : n_ev;
+  uint64_t first = b;
+  for (;;) {
+    const uint32_t r0 = ev_res[first];
+    const uint64_t line0 = res_seq[r0] >> 16;
+    const uint64_t h0 = L.ip_hash[line0];
+    const uint8_t *ip0 = buf + line_start(nl, line0) + L.ip_off[line0];
+    const uint32_t len0 = L.ip_len[line0];
+    bool existed;
+    const uint32_t ip_id = ip_find_insert(S, h0, ip0, len0, &existed);
+    bool seen = existed;
+    bool other = false;
+    uint64_t next_first = e;
+    for (uint64_t t = first; t < e; ++t) {
+      if (processed[t]) continue;
+      const uint32_t r = ev_res[t];
+      const uint64_t line = res_seq[r] >> 16;
+      if (t != first) {
+        const bool same = L.ip_hash[line] == h0 && L.ip_len[line] == len0 &&
+                          bytes_eq(buf + line_start(nl, line) + L.ip_off[line], ip0, len0);
+        if (!same) {
+          if (!other) { other = true; next_first = t; }
+          continue;
+        }
+      }
+      processed[t] = 1;
+      const DevRule R = rules[res_rule[r] & 0x7FFFFFFFu];
+      const uint64_t key = ((uint64_t)(ip_id + 1) << 24) | R.name_id;
+      bool fresh;
+      const uint64_t slot = st_find_insert(S, key, &fresh);
+      const int64_t ts = L.ts[line];
+      int64_t hits, start;
+      uint8_t mt;
+      if (fresh) { hits = 1; start = ts; mt = BJX_FIRST_TIME; }
+      else {
+        hits = S.st_hits[slot];
+        start = S.st_start[slot];
+        if (go_sub(ts, start) > R.interval_ns) { mt = BJX_OUTSIDE_INTERVAL; hits = 1; start = ts; }
+        else { mt = BJX_INSIDE_INTERVAL; hits++; }
+      }
+      const bool ex = hits > R.hits;
+      if (ex) hits = 0;
+      S.st_hits[slot] = hits;
+      S.st_start[slot] = start;
+      rl_out[r] = (uint8_t)(0x80 | (seen ? 1 : 0) | (mt << 1) | (ex ? 8 : 0));
+      seen = true;
+    }
+    if (!other) break;
+    first = next_first;
+  }
+}
+
+__global__ void k_flag_trips(uint64_t n, const uint8_t *__restrict__ rl_out, uint8_t *__restrict__ f) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) f[i] = (rl_out[i] & 8) ? 1 : 0;
+}
+
+__global__ void k_build_trips(uint64_t n_trips, const uint32_t *__restrict__ idx, const uint64_t *__restrict__ res_seq,
+                              const uint32_t *__restrict__ res_rule, const uint64_t *__restrict__ nl, Lines L,
+                              const DevRule *__restrict__ rules, bjx_trip *__restrict__ out) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_trips) return;
+  const uint32_t r = idx[t];
+  const uint64_t line = res_seq[r] >> 16;
+  bjx_trip tr;
+  tr.line_idx = line;
+  tr.line_offset = line_start(nl, line);
+  tr.line_len = (uint32_t)(nl[line] - tr.line_offset);
+  tr.rule_idx = res_rule[r] & 0x7FFFFFFFu;
+  tr.ts_ns = L.ts[line];
+  tr.ip_off = L.ip_off[line];
+  tr.ip_len = L.ip_len[line];
+  tr.host_off = L.host_off[line];
+  tr.host_len = L.host_len[line];
+  tr.rest_off = L.rest_off[line];
+  tr.decision = rules[tr.rule_idx].decision;
+  out[t] = tr;
+}
+
+__global__ void k_build_results(uint64_t n, const uint64_t *__restrict__ res_seq, const uint32_t *__restrict__ res_rule,
+                                const uint8_t *__restrict__ rl_out, bjx_rule_result *__restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  bjx_rule_result r;
+  r.line_idx = res_seq[i] >> 16;
+  r.rule_pos = (uint16_t)(res_seq[i] & 0xFFFF);
+  r.rule_idx = res_rule[i] & 0x7FFFFFFFu;
+  r.skip_host = (res_rule[i] >> 31) & 1;
+  const uint8_t o = rl_out[i];
+  r.seen_ip = o & 1;
+  r.match_type = (o >> 1) & 3;
+  r.exceeded = (o >> 3) & 1;
+  r._pad[0] = r._pad[1] = 0;
+  out[i] = r;
+}
+
+__global__ void k_final_flags(uint64_t n, uint8_t *__restrict__ f) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) f[i] &= (kLineError | kLineOld | kLineExempt);
+}
+
+// rehash (table growth)
+__global__ void k_rehash_ip(uint64_t old_cap, const uint64_t *__restrict__ oh, const uint32_t *__restrict__ oid,
+                            uint64_t *__restrict__ nh, uint32_t *__restrict__ nid, uint64_t nmask) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= old_cap || oh[i] == 0) return;
+  uint64_t j = oh[i] & nmask;
+  for (;;) {
+    unsigned long long prev = atomicCAS((unsigned long long *)&nh[j], 0ull, (unsigned long long)oh[i]);
+    if (prev == 0) { nid[j] = oid[i]; return; }
+    j = (j + 1) & nmask;
+  }
+}
+__global__ void k_rehash_st(uint64_t old_cap, const uint64_t *__restrict__ ok, const int64_t *__restrict__ ohit,
+                            const int64_t *__restrict__ ost, uint64_t *__restrict__ nk, int64_t *__restrict__ nhit,
+                            int64_t *__restrict__ nst, uint64_t nmask) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= old_cap || ok[i] == 0) return;
+  uint64_t j = mix64(ok[i]) & nmask;
+  for (;;) {
+    unsigned long long prev = atomicCAS((unsigned long long *)&nk[j], 0ull, (unsigned long long)ok[i]);
+    if (prev == 0) { nhit[j] = ohit[i]; nst[j] = ost[i]; return; }
+    j = (j + 1) & nmask;
+  }
+}
+
+// state query (RegexRateLimitStates.Get for one (ip, name))
+__global__ void k_state_get(State S, uint64_t h, const uint8_t *ip, uint32_t len, uint32_t name_id, int64_t *out) {
+  out[0] = 0;
+  uint64_t i = h & S.ip_mask;
+  for (;;) {
+    const uint64_t cur = S.ip_slot_hash[i];
+    if (cur == 0) return;
+    if (cur == h) {
+      const uint32_t id = S.ip_slot_id[i];
+      if (S.ip_len[id] == len && bytes_eq(S.arena + S.ip_off[id], ip, len)) {
+        const uint64_t key = ((uint64_t)(id + 1) << 24) | name_id;
+        uint64_t j = mix64(key) & S.st_mask;
+        for (;;) {
+          const uint64_t k = S.st_key[j];
+          if (k == 0) { out[0] = 1; return; }  // ip known, rule state absent
+          if (k == key) { out[0] = 2; out[1] = S.st_hits[j]; out[2] = S.st_start[j]; return; }
+          j = (j + 1) & S.st_mask;
+        }
+      }
+    }
+    i = (i + 1) & S.ip_mask;
+  }
+}
+
+// =====================================================================
+//                               host side
+// =====================================================================
+
+template <typename T>
+struct DevBuf {
+  T *p = nullptr;
+  size_t n = 0;
+  void ensure(size_t want) {
+    if (want <= n && p) return;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    size_t cap = want < 1024 ? 1024 : want + want / 4;
+    HIP_OK(hipMalloc(&p, cap * sizeof(T)));
+    n = cap;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+inline unsigned grid_for(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+uint64_t next_pow2(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------ ruleset
+
+struct bjx_ruleset {
+  struct Rule {
+    std::string name, regex;
+    int64_t interval_ns = 0, hits = 0;
+    int32_t decision = 0;
+    std::vector<std::string> skip_hosts;
+    CompiledRegex rx;
+  };
+  std::vector<Rule> rules;
+  uint32_t n_global = 0;
+  std::vector<std::pair<std::string, std::vector<uint32_t>>> sites;
+  uint64_t uid = 0;
+};
+
+static std::atomic<uint64_t> g_ruleset_uid{1};
+
+extern "C" int bjx_abi_version(void) { return BJX_ABI_VERSION; }
+
+static void set_err(char *err, size_t len, const std::string &m) {
+  if (!err || !len) return;
+  size_t k = std::min(len - 1, m.size());
+  memcpy(err, m.data(), k);
+  err[k] = 0;
+}
+
+extern "C" int bjx_ruleset_compile(const bjx_rule_spec *global_rules, size_t n_global, const bjx_site_rules *per_site,
+                                   size_t n_sites, bjx_ruleset **out, int64_t *err_rule, char *err, size_t err_len) {
+  if (!out) return BJX_ERR_ARG;
+  *out = nullptr;
+  if (err_rule) *err_rule = -1;
+  try {
+    auto rs = std::make_unique<bjx_ruleset>();
+    auto add = [&](const bjx_rule_spec &s) -> int {
+      if (s.decision < BJX_ALLOW || s.decision > BJX_IPTABLES_BLOCK) {
+        set_err(err, err_len, "invalid decision value");
+        return BJX_ERR_DECISION;
+      }
+      bjx_ruleset::Rule r;
+      r.name.assign(s.name.ptr ? s.name.ptr : "", s.name.len);
+      r.regex.assign(s.regex.ptr ? s.regex.ptr : "", s.regex.len);
+      r.interval_ns = s.interval_ns;
+      r.hits = s.hits_per_interval;
+      r.decision = s.decision;
+      for (size_t k = 0; k < s.n_hosts_to_skip; ++k) r.skip_hosts.emplace_back(s.hosts_to_skip[k].ptr, s.hosts_to_skip[k].len);
+      std::string e;
+      int rc = compile_regex(r.regex, &r.rx, &e);
+      if (rc != 0) {
+        set_err(err, err_len, e);
+        return rc;
+      }
+      rs->rules.push_back(std::move(r));
+      return 0;
+    };
+    for (size_t i = 0; i < n_global; ++i) {
+      int rc = add(global_rules[i]);
+      if (rc) { if (err_rule) *err_rule = (int64_t)i; return rc; }
+    }
+    rs->n_global = (uint32_t)n_global;
+    size_t max_site = 0;
+    for (size_t s = 0; s < n_sites; ++s) {
+      std::string host(per_site[s].host.ptr ? per_site[s].host.ptr : "", per_site[s].host.len);
+      for (auto &p : rs->sites)
+        if (p.first == host) { set_err(err, err_len, "duplicate per-site host: " + host); return BJX_ERR_ARG; }
+      std::vector<uint32_t> ids;
+      for (size_t k = 0; k < per_site[s].n_rules; ++k) {
+        int rc = add(per_site[s].rules[k]);
+        if (rc) { if (err_rule) *err_rule = (int64_t)(rs->rules.size()); return rc; }
+        ids.push_back((uint32_t)rs->rules.size() - 1);
+      }
+      max_site = std::max(max_site, ids.size());
+      rs->sites.emplace_back(host, std::move(ids));
+    }
+    if (max_site + n_global >= 65536) { set_err(err, err_len, "more than 65535 rules apply to one host"); return BJX_ERR_TOO_COMPLEX; }
+    rs->uid = g_ruleset_uid++;
+    *out = rs.release();
+    return BJX_OK;
+  } catch (const std::exception &e) {
+    set_err(err, err_len, e.what());
+    return BJX_ERR_NOMEM;
+  }
+}
+
+extern "C" void bjx_ruleset_release(bjx_ruleset *rs) { delete rs; }
+extern "C" size_t bjx_ruleset_num_rules(const bjx_ruleset *rs) { return rs ? rs->rules.size() : 0; }
+extern "C" int bjx_ruleset_rule_info(const bjx_ruleset *rs, size_t i, uint32_t *states, uint32_t *classes, uint32_t *flags) {
+  if (!rs || i >= rs->rules.size()) return BJX_ERR_ARG;
+  const auto &rx = rs->rules[i].rx;
+  if (states) *states = rx.nstates;
+  if (classes) *classes = rx.ncls;
+  if (flags) *flags = rx.flags | (rx.literal_equivalent ? 0x100u : 0u);
+  return BJX_OK;
+}
+
+// ------------------------------------------------------------ engine
+
+struct bjx_engine {
+  int device = 0;
+  std::mutex mu;
+  std::string last_error;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, evm0 = nullptr, evm1 = nullptr;
+
+  // decision lists (config order)
+  struct Entry { bool global; std::string site; int32_t decision; std::string ip; };
+  std::vector<Entry> decisions;
+  uint64_t decisions_version = 1;
+
+  // rule names -> ids (state keys survive reloads)
+  std::unordered_map<std::string, uint32_t> name_ids;
+  std::vector<std::string> names;
+
+  // binding cache
+  uint64_t bound_uid = 0, bound_dec_version = 0;
+  DevBuf<uint8_t> bind_blob;
+  Bind bind{};
+  std::vector<DevRule> host_rules;
+
+  // persistent state
+  State S{};
+  uint64_t ip_cap = 0, st_cap = 0, max_ips = 0;
+  uint64_t host_counters[3] = {0, 0, 0};
+
+  // batch workspace
+  DevBuf<uint8_t> staging;
+  DevBuf<uint32_t> tile_counts;
+  DevBuf<uint64_t> tile_base, nl;
+  DevBuf<int64_t> l_ts;
+  DevBuf<uint64_t> l_iph, l_counts, l_offs, l_masks;
+  DevBuf<uint32_t> l_ipoff, l_iplen, l_hoff, l_hlen, l_roff, slow_list;
+  DevBuf<int32_t> l_hid;
+  DevBuf<uint8_t> l_flags;
+  DevBuf<unsigned long long> scalars;  // [0] slow count, [1..2] bounds, [3] selected
+  DevBuf<uint64_t> res_seq;
+  DevBuf<uint32_t> res_rule, ev_key, ev_res, ev_key2, ev_res2, heads, trip_idx;
+  DevBuf<uint8_t> head_flag, rl_out, processed, trip_flag;
+  DevBuf<bjx_trip> d_trips;
+  DevBuf<bjx_rule_result> d_results;
+  DevBuf<uint8_t> cub_tmp;
+  DevBuf<int64_t> q_out;
+  DevBuf<uint8_t> q_ip;
+
+  // host copies of the last batch
+  std::vector<bjx_trip> trips;
+  std::vector<bjx_rule_result> results;
+  std::vector<uint8_t> line_flags;
+};
+
+namespace {
+
+uint32_t intern_name(bjx_engine *e, const std::string &n) {
+  auto it = e->name_ids.find(n);
+  if (it != e->name_ids.end()) return it->second;
+  uint32_t id = (uint32_t)e->names.size();
+  if (id >= (1u << 24)) throw BjxError(BJX_ERR_CAPACITY, "too many distinct rule names");
+  e->names.push_back(n);
+  e->name_ids.emplace(n, id);
+  return id;
+}
+
+uint64_t be64_host(const uint8_t *a) {
+  uint64_t v = 0;
+  for (int k = 0; k < 8; ++k) v = (v << 8) | a[k];
+  return v;
+}
+
+struct BlobBuilder {
+  std::vector<uint8_t> bytes;
+  template <typename T>
+  size_t add(const std::vector<T> &v) {
+    size_t off = (bytes.size() + 15) & ~size_t(15);
+    bytes.resize(off + v.size() * sizeof(T) + 16, 0);
+    if (!v.empty()) memcpy(bytes.data() + off, v.data(), v.size() * sizeof(T));
+    return off;
+  }
+};
+
+// net.ParseCIDR + IPNet/To4 handling of ipfilter's ToggleIP (allow entries)
+bool parse_allow_entry(const std::string &s, std::vector<std::array<uint8_t, 16>> &addrs, std::vector<Subnet> &subs) {
+  auto slash = s.find('/');
+  const uint8_t *p = reinterpret_cast<const uint8_t *>(s.data());
+  if (slash != std::string::npos) {
+    uint8_t a[16];
+    bool is4;
+    std::string addr = s.substr(0, slash), mask = s.substr(slash + 1);
+    if (!go_parse_addr(reinterpret_cast<const uint8_t *>(addr.data()), (uint32_t)addr.size(), a, &is4)) return false;
+    if (addr.find('%') != std::string::npos) return false;
+    long bits = 0;
+    size_t i = 0;
+    for (; i < mask.size() && mask[i] >= '0' && mask[i] <= '9'; ++i) {
+      bits = bits * 10 + (mask[i] - '0');
+      if (bits >= 0xFFFFFF) return false;
+    }
+    if (i == 0 || i != mask.size()) return false;
+    const int bitlen = is4 ? 32 : 128;
+    if (bits > bitlen) return false;
+    if (bits == bitlen) {  // single address
+      std::array<uint8_t, 16> x;
+      memcpy(x.data(), a, 16);
+      addrs.push_back(x);
+      return true;
+    }
+    Subnet sn;
+    memset(&sn, 0, sizeof sn);
+    auto mk = [&](int k) -> uint8_t {
+      int b = (int)bits - 8 * k;
+      return b >= 8 ? 0xFF : (b <= 0 ? 0 : (uint8_t)(0xFF << (8 - b)));
+    };
+    if (is4) {
+      sn.netlen = 4;
+      for (int k = 0; k < 4; ++k) { sn.mask[k] = mk(k); sn.net[k] = a[12 + k] & sn.mask[k]; }
+    } else {
+      uint8_t net[16], m[16];
+      for (int k = 0; k < 16; ++k) { m[k] = mk(k); net[k] = a[k] & m[k]; }
+      if (is_v4_mapped(net)) { sn.netlen = 4; memcpy(sn.net, net + 12, 4); memcpy(sn.mask, m + 12, 4); }
+      else { sn.netlen = 16; memcpy(sn.net, net, 16); memcpy(sn.mask, m, 16); }
+    }
+    subs.push_back(sn);
+    return true;
+  }
+  uint8_t a[16];
+  bool is4;
+  if (go_parse_addr(p, (uint32_t)s.size(), a, &is4)) {
+    std::array<uint8_t, 16> x;
+    memcpy(x.data(), a, 16);
+    addrs.push_back(x);
+    return true;
+  }
+  return false;
+}
+
+void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs) {
+  if (e->bound_uid == rs->uid && e->bound_dec_version == e->decisions_version) return;
+  // host dictionary: per-site hosts, skip hosts, allow-list sites
+  std::map<std::string, uint32_t> hosts;
+  auto host_id = [&](const std::string &h) {
+    auto it = hosts.find(h);
+    if (it != hosts.end()) return it->second;
+    uint32_t id = (uint32_t)hosts.size();
+    hosts.emplace(h, id);
+    return id;
+  };
+  for (auto &s : rs->sites) host_id(s.first);
+  for (auto &r : rs->rules)
+    for (auto &h : r.skip_hosts) host_id(h);
+  // scopes: 0 = global, then one per site that appears in the decision lists
+  std::map<std::string, int32_t> scope_of_site;
+  for (auto &d : e->decisions)
+    if (!d.global && !scope_of_site.count(d.site)) {
+      int32_t sc = (int32_t)scope_of_site.size() + 1;
+      scope_of_site.emplace(d.site, sc);
+      host_id(d.site);
+    }
+  const uint32_t n_hosts = (uint32_t)hosts.size();
+  const uint32_t n_scopes = (uint32_t)scope_of_site.size() + 1;
+  std::vector<std::string> host_by_id(n_hosts);
+  for (auto &h : hosts) host_by_id[h.second] = h.first;
+
+  // rules
+  std::vector<DevRule> drules(rs->rules.size());
+  std::vector<uint16_t> trans;
+  std::vector<uint8_t> ae, ascii(rs->rules.size() * 128), lits;
+  std::vector<uint32_t> nonascii;
+  for (size_t i = 0; i < rs->rules.size(); ++i) {
+    const auto &r = rs->rules[i];
+    DevRule &d = drules[i];
+    memset(&d, 0, sizeof d);
+    d.trans_off = (uint32_t)trans.size();
+    trans.insert(trans.end(), r.rx.trans.begin(), r.rx.trans.end());
+    d.ae_off = (uint32_t)ae.size();
+    ae.insert(ae.end(), r.rx.accept_end.begin(), r.rx.accept_end.end());
+    d.na_off = (uint32_t)(nonascii.size() / 2);
+    for (auto &p : r.rx.nonascii) { nonascii.push_back(p.first); nonascii.push_back(p.second); }
+    d.n_na = (uint16_t)r.rx.nonascii.size();
+    d.ncls = (uint16_t)r.rx.ncls;
+    d.start = r.rx.start;
+    d.flags = (uint16_t)r.rx.flags;
+    memcpy(&ascii[i * 128], r.rx.ascii_cls, 128);
+    d.name_id = intern_name(e, r.name);
+    d.decision = r.decision;
+    d.lit_off = (uint32_t)lits.size();
+    d.lit_len = (int32_t)r.rx.required_literal.size();
+    lits.insert(lits.end(), r.rx.required_literal.begin(), r.rx.required_literal.end());
+    d.interval_ns = r.interval_ns;
+    d.hits = r.hits;
+  }
+  std::vector<uint32_t> global_rules(rs->n_global);
+  for (uint32_t i = 0; i < rs->n_global; ++i) global_rules[i] = i;
+  std::vector<uint32_t> site_off(n_hosts + 1, 0), site_rules;
+  std::vector<std::vector<uint32_t>> per_host(n_hosts);
+  for (auto &s : rs->sites) per_host[hosts[s.first]] = s.second;
+  uint32_t max_app = rs->n_global;
+  for (uint32_t h = 0; h < n_hosts; ++h) {
+    site_off[h] = (uint32_t)site_rules.size();
+    site_rules.insert(site_rules.end(), per_host[h].begin(), per_host[h].end());
+    max_app = std::max<uint32_t>(max_app, (uint32_t)per_host[h].size() + rs->n_global);
+  }
+  site_off[n_hosts] = (uint32_t)site_rules.size();
+  // host dict sorted by hash
+  std::vector<std::pair<uint64_t, uint32_t>> hd;
+  for (uint32_t h = 0; h < n_hosts; ++h)
+    hd.push_back({hash_bytes(reinterpret_cast<const uint8_t *>(host_by_id[h].data()), (uint32_t)host_by_id[h].size()), h});
+  std::sort(hd.begin(), hd.end());
+  std::vector<uint64_t> hd_hash;
+  std::vector<uint32_t> hd_id, hd_off, hd_len;
+  std::vector<uint8_t> hd_bytes;
+  for (auto &p : hd) {
+    hd_hash.push_back(p.first);
+    hd_id.push_back(p.second);
+    hd_off.push_back((uint32_t)hd_bytes.size());
+    hd_len.push_back((uint32_t)host_by_id[p.second].size());
+    hd_bytes.insert(hd_bytes.end(), host_by_id[p.second].begin(), host_by_id[p.second].end());
+  }
+  std::vector<int32_t> host_scope(n_hosts, -1);
+  for (auto &s : scope_of_site) host_scope[hosts[s.first]] = s.second;
+  std::vector<uint64_t> skip;
+  for (size_t i = 0; i < rs->rules.size(); ++i)
+    for (auto &h : rs->rules[i].skip_hosts) skip.push_back(((uint64_t)i << 32) | hosts[h]);
+  std::sort(skip.begin(), skip.end());
+  skip.erase(std::unique(skip.begin(), skip.end()), skip.end());
+
+  // allow scopes (decision.go:278-374): exact maps are last-writer-wins in
+  // config order; Allow IPFilters hold every allow entry
+  std::vector<std::vector<std::array<uint8_t, 16>>> sc_addrs(n_scopes);
+  std::vector<std::vector<Subnet>> sc_subs(n_scopes);
+  std::vector<std::map<std::string, int32_t>> sc_exact(n_scopes);
+  bool any_allow = false;
+  for (auto &d : e->decisions) {
+    const int sc = d.global ? 0 : scope_of_site[d.site];
+    if (d.ip.find('/') == std::string::npos) sc_exact[sc][d.ip] = d.decision;
+    if (d.decision == BJX_ALLOW) {
+      any_allow = true;
+      parse_allow_entry(d.ip, sc_addrs[sc], sc_subs[sc]);
+    }
+  }
+  std::vector<uint32_t> sc_addr_off(n_scopes + 1, 0), sc_sub_off(n_scopes + 1, 0), sc_str_off(n_scopes + 1, 0);
+  std::vector<uint64_t> sc_addr, sc_str_hash;
+  std::vector<Subnet> sc_sub;
+  std::vector<uint32_t> sc_str_boff, sc_str_len;
+  std::vector<uint8_t> sc_str_bytes;
+  for (uint32_t sc = 0; sc < n_scopes; ++sc) {
+    auto &v = sc_addrs[sc];
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    sc_addr_off[sc] = (uint32_t)(sc_addr.size() / 2);
+    for (auto &a : v) { sc_addr.push_back(be64_host(a.data())); sc_addr.push_back(be64_host(a.data() + 8)); }
+    sc_sub_off[sc] = (uint32_t)sc_sub.size();
+    sc_sub.insert(sc_sub.end(), sc_subs[sc].begin(), sc_subs[sc].end());
+    sc_str_off[sc] = (uint32_t)sc_str_hash.size();
+    std::vector<std::pair<uint64_t, std::string>> strs;
+    for (auto &kv : sc_exact[sc]) {
+      if (kv.second != BJX_ALLOW) continue;
+      uint8_t a[16];
+      bool is4;
+      if (go_parse_addr(reinterpret_cast<const uint8_t *>(kv.first.data()), (uint32_t)kv.first.size(), a, &is4)) continue;
+      strs.push_back({hash_bytes(reinterpret_cast<const uint8_t *>(kv.first.data()), (uint32_t)kv.first.size()), kv.first});
+      any_allow = true;
+    }
+    std::sort(strs.begin(), strs.end());
+    for (auto &p : strs) {
+      sc_str_hash.push_back(p.first);
+      sc_str_boff.push_back((uint32_t)sc_str_bytes.size());
+      sc_str_len.push_back((uint32_t)p.second.size());
+      sc_str_bytes.insert(sc_str_bytes.end(), p.second.begin(), p.second.end());
+    }
+  }
+  sc_addr_off[n_scopes] = (uint32_t)(sc_addr.size() / 2);
+  sc_sub_off[n_scopes] = (uint32_t)sc_sub.size();
+  sc_str_off[n_scopes] = (uint32_t)sc_str_hash.size();
+
+  BlobBuilder bb;
+  size_t o_rules = bb.add(drules), o_trans = bb.add(trans), o_ae = bb.add(ae), o_ascii = bb.add(ascii),
+         o_na = bb.add(nonascii), o_lits = bb.add(lits), o_glob = bb.add(global_rules), o_soff = bb.add(site_off),
+         o_srules = bb.add(site_rules), o_hdh = bb.add(hd_hash), o_hdid = bb.add(hd_id), o_hdoff = bb.add(hd_off),
+         o_hdlen = bb.add(hd_len), o_hdb = bb.add(hd_bytes), o_hsc = bb.add(host_scope), o_skip = bb.add(skip),
+         o_sao = bb.add(sc_addr_off), o_sa = bb.add(sc_addr), o_sso = bb.add(sc_sub_off), o_ss = bb.add(sc_sub),
+         o_sto = bb.add(sc_str_off), o_sth = bb.add(sc_str_hash), o_stb = bb.add(sc_str_boff), o_stl = bb.add(sc_str_len),
+         o_stbytes = bb.add(sc_str_bytes);
+  e->bind_blob.ensure(bb.bytes.size());
+  HIP_OK(hipMemcpy(e->bind_blob.p, bb.bytes.data(), bb.bytes.size(), hipMemcpyHostToDevice));
+  uint8_t *base = e->bind_blob.p;
+  Bind &B = e->bind;
+  B.rules = reinterpret_cast<const DevRule *>(base + o_rules);
+  B.trans = reinterpret_cast<const uint16_t *>(base + o_trans);
+  B.accept_end = base + o_ae;
+  B.ascii_cls = base + o_ascii;
+  B.nonascii = reinterpret_cast<const uint32_t *>(base + o_na);
+  B.lits = base + o_lits;
+  B.global_rules = reinterpret_cast<const uint32_t *>(base + o_glob);
+  B.site_off = reinterpret_cast<const uint32_t *>(base + o_soff);
+  B.site_rules = reinterpret_cast<const uint32_t *>(base + o_srules);
+  B.hd_hash = reinterpret_cast<const uint64_t *>(base + o_hdh);
+  B.hd_id = reinterpret_cast<const uint32_t *>(base + o_hdid);
+  B.hd_off = reinterpret_cast<const uint32_t *>(base + o_hdoff);
+  B.hd_len = reinterpret_cast<const uint32_t *>(base + o_hdlen);
+  B.hd_bytes = base + o_hdb;
+  B.host_scope = reinterpret_cast<const int32_t *>(base + o_hsc);
+  B.skip_keys = reinterpret_cast<const uint64_t *>(base + o_skip);
+  B.sc_addr_off = reinterpret_cast<const uint32_t *>(base + o_sao);
+  B.sc_addr = reinterpret_cast<const uint64_t *>(base + o_sa);
+  B.sc_sub_off = reinterpret_cast<const uint32_t *>(base + o_sso);
+  B.sc_sub = reinterpret_cast<const Subnet *>(base + o_ss);
+  B.sc_str_off = reinterpret_cast<const uint32_t *>(base + o_sto);
+  B.sc_str_hash = reinterpret_cast<const uint64_t *>(base + o_sth);
+  B.sc_str_boff = reinterpret_cast<const uint32_t *>(base + o_stb);
+  B.sc_str_len = reinterpret_cast<const uint32_t *>(base + o_stl);
+  B.sc_str_bytes = base + o_stbytes;
+  B.n_rules = (uint32_t)rs->rules.size();
+  B.n_global = rs->n_global;
+  B.n_hosts = n_hosts;
+  B.n_hd = (uint32_t)hd.size();
+  B.n_skip = (uint32_t)skip.size();
+  B.n_scopes = n_scopes;
+  B.any_allow = any_allow ? 1 : 0;
+  B.mask_words = std::max<uint32_t>(1, (max_app + 63) / 64);
+  e->host_rules = drules;
+  e->bound_uid = rs->uid;
+  e->bound_dec_version = e->decisions_version;
+}
+
+void alloc_state(bjx_engine *e, uint64_t ip_cap, uint64_t st_cap, uint64_t arena_cap) {
+  State &S = e->S;
+  HIP_OK(hipMalloc(&S.ip_slot_hash, ip_cap * 8));
+  HIP_OK(hipMalloc(&S.ip_slot_id, ip_cap * 4));
+  HIP_OK(hipMalloc(&S.ip_off, ip_cap * 8));
+  HIP_OK(hipMalloc(&S.ip_len, ip_cap * 4));
+  HIP_OK(hipMalloc(&S.arena, arena_cap));
+  HIP_OK(hipMalloc(&S.st_key, st_cap * 8));
+  HIP_OK(hipMalloc(&S.st_hits, st_cap * 8));
+  HIP_OK(hipMalloc(&S.st_start, st_cap * 8));
+  HIP_OK(hipMalloc(&S.counters, 64));
+  HIP_OK(hipMemset(S.ip_slot_hash, 0, ip_cap * 8));
+  HIP_OK(hipMemset(S.st_key, 0, st_cap * 8));
+  HIP_OK(hipMemset(S.counters, 0, 64));
+  S.ip_mask = ip_cap - 1;
+  S.st_mask = st_cap - 1;
+  S.arena_cap = arena_cap;
+  e->ip_cap = ip_cap;
+  e->st_cap = st_cap;
+  e->max_ips = ip_cap - ip_cap / 4;
+}
+
+void free_state(bjx_engine *e) {
+  State &S = e->S;
+  for (void *p : {(void *)S.ip_slot_hash, (void *)S.ip_slot_id, (void *)S.ip_off, (void *)S.ip_len, (void *)S.arena,
+                  (void *)S.st_key, (void *)S.st_hits, (void *)S.st_start, (void *)S.counters})
+    if (p) (void)hipFree(p);
+  S = State{};
+}
+
+void read_counters(bjx_engine *e) {
+  HIP_OK(hipMemcpyAsync(e->host_counters, e->S.counters, 24, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+}
+
+// grow tables so that `new_ips` more IPs, `new_bytes` more arena bytes and
+// `new_states` more states fit under a 3/4 load factor
+void ensure_capacity(bjx_engine *e, uint64_t new_ips, uint64_t new_bytes, uint64_t new_states) {
+  read_counters(e);
+  State &S = e->S;
+  const uint64_t n_ips = e->host_counters[0], used = e->host_counters[1], n_st = e->host_counters[2];
+  if ((n_ips + new_ips) * 4 > e->ip_cap * 3) {
+    uint64_t cap = next_pow2((n_ips + new_ips) * 2 + 1024);
+    uint64_t *nh; uint32_t *nid; uint64_t *noff; uint32_t *nlen;
+    HIP_OK(hipMalloc(&nh, cap * 8));
+    HIP_OK(hipMalloc(&nid, cap * 4));
+    HIP_OK(hipMalloc(&noff, cap * 8));
+    HIP_OK(hipMalloc(&nlen, cap * 4));
+    HIP_OK(hipMemsetAsync(nh, 0, cap * 8, e->stream));
+    HIP_OK(hipMemcpyAsync(noff, S.ip_off, n_ips * 8, hipMemcpyDeviceToDevice, e->stream));
+    HIP_OK(hipMemcpyAsync(nlen, S.ip_len, n_ips * 4, hipMemcpyDeviceToDevice, e->stream));
+    hipLaunchKernelGGL(k_rehash_ip, dim3(grid_for(e->ip_cap)), dim3(kBlock), 0, e->stream, e->ip_cap, S.ip_slot_hash,
+                       S.ip_slot_id, nh, nid, cap - 1);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(e->stream));
+    (void)hipFree(S.ip_slot_hash); (void)hipFree(S.ip_slot_id); (void)hipFree(S.ip_off); (void)hipFree(S.ip_len);
+    S.ip_slot_hash = nh; S.ip_slot_id = nid; S.ip_off = noff; S.ip_len = nlen;
+    S.ip_mask = cap - 1;
+    e->ip_cap = cap;
+    e->max_ips = cap - cap / 4;
+  }
+  if (used + new_bytes > S.arena_cap) {
+    uint64_t cap = std::max<uint64_t>(S.arena_cap * 2, used + new_bytes + (1 << 20));
+    uint8_t *na;
+    HIP_OK(hipMalloc(&na, cap));
+    HIP_OK(hipMemcpyAsync(na, S.arena, used, hipMemcpyDeviceToDevice, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    (void)hipFree(S.arena);
+    S.arena = na;
+    S.arena_cap = cap;
+  }
+  if ((n_st + new_states) * 4 > e->st_cap * 3) {
+    uint64_t cap = next_pow2((n_st + new_states) * 2 + 1024);
+    uint64_t *nk; int64_t *nh, *ns;
+    HIP_OK(hipMalloc(&nk, cap * 8));
+    HIP_OK(hipMalloc(&nh, cap * 8));
+    HIP_OK(hipMalloc(&ns, cap * 8));
+    HIP_OK(hipMemsetAsync(nk, 0, cap * 8, e->stream));
+    hipLaunchKernelGGL(k_rehash_st, dim3(grid_for(e->st_cap)), dim3(kBlock), 0, e->stream, e->st_cap, S.st_key,
+                       S.st_hits, S.st_start, nk, nh, ns, cap - 1);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(e->stream));
+    (void)hipFree(S.st_key); (void)hipFree(S.st_hits); (void)hipFree(S.st_start);
+    S.st_key = nk; S.st_hits = nh; S.st_start = ns;
+    S.st_mask = cap - 1;
+    e->st_cap = cap;
+  }
+}
+
+template <typename F>
+void cub_call(bjx_engine *e, F f) {
+  size_t bytes = 0;
+  HIP_OK(f((void *)nullptr, bytes));
+  e->cub_tmp.ensure(bytes + 16);
+  HIP_OK(f((void *)e->cub_tmp.p, bytes));
+}
+
+int bit_width(uint64_t x) {
+  int b = 0;
+  while (x) { ++b; x >>= 1; }
+  return b;
+}
+
+}  // namespace
+
+extern "C" int bjx_engine_create(int device, const bjx_engine_options *opts, bjx_engine **out, char *err, size_t err_len) {
+  if (!out) return BJX_ERR_ARG;
+  *out = nullptr;
+  auto e = std::make_unique<bjx_engine>();
+  try {
+    int n = 0;
+    HIP_OK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) throw BjxError(BJX_ERR_DEVICE, "no such HIP device");
+    e->device = device;
+    HIP_OK(hipSetDevice(device));
+    HIP_OK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    HIP_OK(hipEventCreate(&e->ev0));
+    HIP_OK(hipEventCreate(&e->ev1));
+    HIP_OK(hipEventCreate(&e->evm0));
+    HIP_OK(hipEventCreate(&e->evm1));
+    uint64_t ipc = opts && opts->ip_capacity ? next_pow2(opts->ip_capacity) : (1ull << 20);
+    uint64_t stc = opts && opts->state_capacity ? next_pow2(opts->state_capacity) : (1ull << 22);
+    uint64_t ar = opts && opts->ip_arena_bytes ? opts->ip_arena_bytes : (64ull << 20);
+    alloc_state(e.get(), ipc, stc, ar);
+    *out = e.release();
+    return BJX_OK;
+  } catch (const BjxError &x) {
+    set_err(err, err_len, x.what());
+    return x.code;
+  }
+}
+
+extern "C" void bjx_engine_destroy(bjx_engine *e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  (void)hipStreamSynchronize(e->stream);
+  free_state(e);
+  for (auto *b : {&e->staging, &e->l_flags, &e->head_flag, &e->rl_out, &e->processed, &e->trip_flag, &e->bind_blob,
+                  &e->cub_tmp, &e->q_ip})
+    b->release();
+  e->tile_counts.release(); e->tile_base.release(); e->nl.release(); e->l_ts.release(); e->l_iph.release();
+  e->l_counts.release(); e->l_offs.release(); e->l_masks.release(); e->l_ipoff.release(); e->l_iplen.release();
+  e->l_hoff.release(); e->l_hlen.release(); e->l_roff.release(); e->slow_list.release(); e->l_hid.release();
+  e->scalars.release(); e->res_seq.release(); e->res_rule.release(); e->ev_key.release(); e->ev_res.release();
+  e->ev_key2.release(); e->ev_res2.release(); e->heads.release(); e->trip_idx.release(); e->d_trips.release();
+  e->d_results.release(); e->q_out.release();
+  (void)hipEventDestroy(e->ev0); (void)hipEventDestroy(e->ev1); (void)hipEventDestroy(e->evm0); (void)hipEventDestroy(e->evm1);
+  (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+extern "C" const char *bjx_engine_last_error(bjx_engine *e) { return e ? e->last_error.c_str() : "no engine"; }
+
+extern "C" int bjx_engine_set_decision_lists(bjx_engine *e, const bjx_decision_entry *entries, size_t n) {
+  if (!e || (n && !entries)) return BJX_ERR_ARG;
+  std::lock_guard<std::mutex> g(e->mu);
+  std::vector<bjx_engine::Entry> v;
+  for (size_t i = 0; i < n; ++i) {
+    if (entries[i].decision < BJX_ALLOW || entries[i].decision > BJX_IPTABLES_BLOCK) return BJX_ERR_DECISION;
+    bjx_engine::Entry x;
+    x.global = entries[i].site.ptr == nullptr;
+    if (!x.global) x.site.assign(entries[i].site.ptr, entries[i].site.len);
+    x.decision = entries[i].decision;
+    x.ip.assign(entries[i].ip.ptr ? entries[i].ip.ptr : "", entries[i].ip.len);
+    v.push_back(std::move(x));
+  }
+  e->decisions.swap(v);
+  e->decisions_version++;
+  return BJX_OK;
+}
+
+static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns, uint32_t flags,
+                      bjx_batch_result *out) {
+  HIP_OK(hipSetDevice(e->device));
+  bind_ruleset(e, rs);
+  const Bind &B = e->bind;
+  hipStream_t st = e->stream;
+  memset(out, 0, sizeof *out);
+  e->trips.clear();
+  e->results.clear();
+  e->line_flags.clear();
+  if (n == 0) return;
+
+  const uint8_t *buf = bytes;
+  if (!(flags & BJX_INPUT_DEVICE) || (reinterpret_cast<uintptr_t>(bytes) & 15)) {
+    e->staging.ensure(n + 16);
+    HIP_OK(hipMemcpyAsync(e->staging.p, bytes, n, (flags & BJX_INPUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+    buf = e->staging.p;
+  }
+  HIP_OK(hipEventRecord(e->ev0, st));
+
+  // ---- framing
+  const uint64_t n_tiles = (n + kTile - 1) / kTile;
+  e->tile_counts.ensure(n_tiles);
+  e->tile_base.ensure(n_tiles + 1);
+  hipLaunchKernelGGL(k_nl_count, dim3((unsigned)n_tiles), dim3(kBlock), 0, st, buf, (uint64_t)n, e->tile_counts.p);
+  HIP_OK(hipGetLastError());
+  {
+    uint32_t *in = e->tile_counts.p;
+    uint64_t *o = e->tile_base.p;
+    cub_call(e, [&](void *tmp, size_t &bytes) {
+      return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)n_tiles, st);
+    });
+  }
+  uint64_t last_base = 0;
+  uint32_t last_cnt = 0;
+  HIP_OK(hipMemcpyAsync(&last_base, e->tile_base.p + (n_tiles - 1), 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(&last_cnt, e->tile_counts.p + (n_tiles - 1), 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  const uint64_t n_lines = last_base + last_cnt;
+  out->n_lines = n_lines;
+  if (n_lines == 0) return;
+  e->nl.ensure(n_lines);
+  hipLaunchKernelGGL(k_nl_write, dim3((unsigned)n_tiles), dim3(kBlock), 0, st, buf, (uint64_t)n, e->tile_base.p, e->nl.p);
+  HIP_OK(hipGetLastError());
+  uint64_t last_nl = 0;
+  HIP_OK(hipMemcpyAsync(&last_nl, e->nl.p + (n_lines - 1), 8, hipMemcpyDeviceToHost, st));
+
+  // ---- per-line arrays
+  e->l_ts.ensure(n_lines); e->l_iph.ensure(n_lines); e->l_counts.ensure(n_lines + 1); e->l_offs.ensure(n_lines + 1);
+  e->l_masks.ensure(n_lines * B.mask_words);
+  e->l_ipoff.ensure(n_lines); e->l_iplen.ensure(n_lines); e->l_hoff.ensure(n_lines); e->l_hlen.ensure(n_lines);
+  e->l_roff.ensure(n_lines); e->l_hid.ensure(n_lines); e->l_flags.ensure(n_lines); e->slow_list.ensure(n_lines);
+  e->scalars.ensure(8);
+  Lines L;
+  L.ts = e->l_ts.p; L.ip_hash = e->l_iph.p; L.ip_off = e->l_ipoff.p; L.ip_len = e->l_iplen.p; L.host_off = e->l_hoff.p;
+  L.host_len = e->l_hlen.p; L.rest_off = e->l_roff.p; L.host_id = e->l_hid.p; L.flags = e->l_flags.p;
+  L.counts = e->l_counts.p; L.masks = e->l_masks.p;
+  HIP_OK(hipMemsetAsync(e->scalars.p, 0, 8 * sizeof(unsigned long long), st));
+
+  // ---- parse + match (the hot kernel)
+  HIP_OK(hipEventRecord(e->evm0, st));
+  hipLaunchKernelGGL(k_parse_match<false>, dim3(grid_for(n_lines)), dim3(kBlock), 0, st, B, buf, e->nl.p, n_lines,
+                     (const uint32_t *)nullptr, now_ns, L, e->slow_list.p, e->scalars.p);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(e->evm1, st));
+  unsigned long long n_slow = 0;
+  HIP_OK(hipMemcpyAsync(&n_slow, e->scalars.p, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  out->consumed_bytes = last_nl + 1;
+  if (n_slow) {
+    hipLaunchKernelGGL(k_parse_match<true>, dim3(grid_for(n_slow)), dim3(kBlock), 0, st, B, buf, e->nl.p, (uint64_t)n_slow,
+                       e->slow_list.p, now_ns, L, e->slow_list.p, e->scalars.p);
+    HIP_OK(hipGetLastError());
+  }
+
+  // ---- RuleResults + events in reference order
+  HIP_OK(hipMemsetAsync(e->l_counts.p + n_lines, 0, 8, st));
+  {
+    uint64_t *in = e->l_counts.p, *o = e->l_offs.p;
+    cub_call(e, [&](void *tmp, size_t &bytes) {
+      return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)(n_lines + 1), st);
+    });
+  }
+  uint64_t tot = 0;
+  HIP_OK(hipMemcpyAsync(&tot, e->l_offs.p + n_lines, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  const uint64_t n_res = tot >> 32, n_ev = tot & 0xFFFFFFFFull;
+  out->n_results = n_res;
+  out->n_events = n_ev;
+  e->res_seq.ensure(n_res + 1); e->res_rule.ensure(n_res + 1); e->rl_out.ensure(n_res + 1);
+  e->ev_key.ensure(n_ev + 1); e->ev_res.ensure(n_ev + 1); e->ev_key2.ensure(n_ev + 1); e->ev_res2.ensure(n_ev + 1);
+  if (n_res) {
+    hipLaunchKernelGGL(k_emit, dim3(grid_for(n_lines)), dim3(kBlock), 0, st, B, n_lines, L, e->l_offs.p, e->res_seq.p,
+                       e->res_rule.p, e->ev_key.p, e->ev_res.p);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemsetAsync(e->rl_out.p, 0, n_res, st));
+  }
+
+  // ---- rate limiting: group events per IP (stable), one thread per IP
+  uint64_t n_trips = 0;
+  if (n_ev) {
+    {
+      uint32_t *ki = e->ev_key.p, *ko = e->ev_key2.p, *vi = e->ev_res.p, *vo = e->ev_res2.p;
+      cub_call(e, [&](void *tmp, size_t &bytes) {
+        return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)n_ev, 0, 32, st);
+      });
+    }
+    e->head_flag.ensure(n_ev); e->heads.ensure(n_ev + 1); e->processed.ensure(n_ev);
+    HIP_OK(hipMemsetAsync(e->scalars.p + 1, 0, 3 * 8, st));
+    hipLaunchKernelGGL(k_heads, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_key2.p, e->ev_res2.p, e->res_seq.p,
+                       L, e->head_flag.p, e->scalars.p + 1);
+    HIP_OK(hipGetLastError());
+    {
+      hipcub::CountingInputIterator<uint32_t> it(0);
+      uint8_t *fl = e->head_flag.p;
+      uint32_t *o = e->heads.p;
+      unsigned long long *ns = e->scalars.p + 3;
+      cub_call(e, [&](void *tmp, size_t &bytes) {
+        return hipcub::DeviceSelect::Flagged(tmp, bytes, it, fl, o, ns, (int)n_ev, st);
+      });
+    }
+    unsigned long long sc[3] = {0, 0, 0};
+    HIP_OK(hipMemcpyAsync(sc, e->scalars.p + 1, 24, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    const uint64_t n_seg = sc[2];
+    if (n_seg == 0) throw BjxError(BJX_ERR_DEVICE, "internal: no event segments");
+    ensure_capacity(e, sc[0] + 1024, sc[1] + 4096, n_ev);
+    HIP_OK(hipMemsetAsync(e->processed.p, 0, n_ev, st));
+    hipLaunchKernelGGL(k_ratelimit, dim3(grid_for(n_seg)), dim3(kBlock), 0, st, n_seg, n_ev, e->heads.p, e->ev_res2.p,
+                       e->res_seq.p, e->res_rule.p, e->nl.p, buf, L, B.rules, e->S, e->rl_out.p, e->processed.p);
+    HIP_OK(hipGetLastError());
+    // trips in reference order
+    e->trip_flag.ensure(n_res); e->trip_idx.ensure(n_res + 1);
+    hipLaunchKernelGGL(k_flag_trips, dim3(grid_for(n_res)), dim3(kBlock), 0, st, n_res, e->rl_out.p, e->trip_flag.p);
+    {
+      hipcub::CountingInputIterator<uint32_t> it(0);
+      uint8_t *fl = e->trip_flag.p;
+      uint32_t *o = e->trip_idx.p;
+      unsigned long long *ns = e->scalars.p + 4;
+      cub_call(e, [&](void *tmp, size_t &bytes) {
+        return hipcub::DeviceSelect::Flagged(tmp, bytes, it, fl, o, ns, (int)n_res, st);
+      });
+    }
+    unsigned long long nt = 0;
+    HIP_OK(hipMemcpyAsync(&nt, e->scalars.p + 4, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    n_trips = nt;
+    if (n_trips) {
+      e->d_trips.ensure(n_trips);
+      hipLaunchKernelGGL(k_build_trips, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_idx.p, e->res_seq.p,
+                         e->res_rule.p, e->nl.p, L, B.rules, e->d_trips.p);
+      HIP_OK(hipGetLastError());
+      e->trips.resize(n_trips);
+      HIP_OK(hipMemcpyAsync(e->trips.data(), e->d_trips.p, n_trips * sizeof(bjx_trip), hipMemcpyDeviceToHost, st));
+    }
+  }
+  HIP_OK(hipEventRecord(e->ev1, st));
+  if (flags & BJX_COPY_RESULTS) {
+    hipLaunchKernelGGL(k_final_flags, dim3(grid_for(n_lines)), dim3(kBlock), 0, st, n_lines, e->l_flags.p);
+    e->line_flags.resize(n_lines);
+    HIP_OK(hipMemcpyAsync(e->line_flags.data(), e->l_flags.p, n_lines, hipMemcpyDeviceToHost, st));
+    if (n_res) {
+      e->d_results.ensure(n_res);
+      hipLaunchKernelGGL(k_build_results, dim3(grid_for(n_res)), dim3(kBlock), 0, st, n_res, e->res_seq.p, e->res_rule.p,
+                         e->rl_out.p, e->d_results.p);
+      e->results.resize(n_res);
+      HIP_OK(hipMemcpyAsync(e->results.data(), e->d_results.p, n_res * sizeof(bjx_rule_result), hipMemcpyDeviceToHost, st));
+    }
+  }
+  HIP_OK(hipStreamSynchronize(st));
+  float ms = 0, mms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
+  HIP_OK(hipEventElapsedTime(&mms, e->evm0, e->evm1));
+  out->device_ms = ms;
+  out->match_kernel_ms = mms;
+  out->n_trips = n_trips;
+  out->trips = e->trips.empty() ? nullptr : e->trips.data();
+  out->results = e->results.empty() ? nullptr : e->results.data();
+  out->line_flags = e->line_flags.empty() ? nullptr : e->line_flags.data();
+}
+
+extern "C" int bjx_process_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns,
+                                 uint32_t flags, bjx_batch_result *out) {
+  if (!e || !rs || !out || (n && !bytes)) return BJX_ERR_ARG;
+  std::lock_guard<std::mutex> g(e->mu);
+  try {
+    run_batch(e, rs, bytes, n, now_ns, flags, out);
+    return BJX_OK;
+  } catch (const BjxError &x) {
+    e->last_error = x.what();
+    return x.code;
+  } catch (const std::bad_alloc &) {
+    e->last_error = "host out of memory";
+    return BJX_ERR_NOMEM;
+  }
+}
+
+extern "C" int bjx_state_get(bjx_engine *e, const char *ip, size_t ip_len, const char *name, size_t name_len,
+                             int64_t *num_hits, int64_t *start_ns) {
+  if (!e || (ip_len && !ip)) return BJX_ERR_ARG;
+  std::lock_guard<std::mutex> g(e->mu);
+  try {
+    HIP_OK(hipSetDevice(e->device));
+    auto it = e->name_ids.find(std::string(name ? name : "", name_len));
+    if (it == e->name_ids.end()) return 0;
+    e->q_ip.ensure(ip_len + 1);
+    e->q_out.ensure(4);
+    if (ip_len) HIP_OK(hipMemcpyAsync(e->q_ip.p, ip, ip_len, hipMemcpyHostToDevice, e->stream));
+    const uint64_t h = hash_bytes(reinterpret_cast<const uint8_t *>(ip), (uint32_t)ip_len);
+    hipLaunchKernelGGL(k_state_get, dim3(1), dim3(1), 0, e->stream, e->S, h, e->q_ip.p, (uint32_t)ip_len, it->second, e->q_out.p);
+    HIP_OK(hipGetLastError());
+    int64_t o[3];
+    HIP_OK(hipMemcpyAsync(o, e->q_out.p, 24, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    if (o[0] != 2) return 0;
+    if (num_hits) *num_hits = o[1];
+    if (start_ns) *start_ns = o[2];
+    return 1;
+  } catch (const BjxError &x) {
+    e->last_error = x.what();
+    return x.code;
+  }
+}
+
+extern "C" int64_t bjx_state_len(bjx_engine *e) {
+  if (!e) return BJX_ERR_ARG;
+  std::lock_guard<std::mutex> g(e->mu);
+  try {
+    HIP_OK(hipSetDevice(e->device));
+    read_counters(e);
+    return (int64_t)e->host_counters[0];
+  } catch (const BjxError &x) {
+    e->last_error = x.what();
+    return x.code;
+  }
+}
+
+extern "C" int bjx_state_clear(bjx_engine *e) {
+  if (!e) return BJX_ERR_ARG;
+  std::lock_guard<std::mutex> g(e->mu);
+  try {
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipMemsetAsync(e->S.ip_slot_hash, 0, e->ip_cap * 8, e->stream));
+    HIP_OK(hipMemsetAsync(e->S.st_key, 0, e->st_cap * 8, e->stream));
+    HIP_OK(hipMemsetAsync(e->S.counters, 0, 64, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    return BJX_OK;
+  } catch (const BjxError &x) {
+    e->last_error = x.what();
+    return x.code;
+  }
+}
+
+extern "C" size_t bjx_state_dump(bjx_engine *e, char *out, size_t cap) {
+  if (!e) return 0;
+  std::lock_guard<std::mutex> g(e->mu);
+  try {
+    HIP_OK(hipSetDevice(e->device));
+    read_counters(e);
+    const uint64_t n_ips = e->host_counters[0], used = e->host_counters[1];
+    std::vector<uint64_t> off(n_ips), keys(e->st_cap);
+    std::vector<uint32_t> len(n_ips);
+    std::vector<int64_t> hits(e->st_cap), start(e->st_cap);
+    std::vector<uint8_t> arena(used);
+    HIP_OK(hipMemcpy(off.data(), e->S.ip_off, n_ips * 8, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(len.data(), e->S.ip_len, n_ips * 4, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(arena.data(), e->S.arena, used, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(keys.data(), e->S.st_key, e->st_cap * 8, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(hits.data(), e->S.st_hits, e->st_cap * 8, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(start.data(), e->S.st_start, e->st_cap * 8, hipMemcpyDeviceToHost));
+    std::vector<std::vector<std::pair<uint32_t, uint64_t>>> per_ip(n_ips);
+    for (uint64_t i = 0; i < e->st_cap; ++i)
+      if (keys[i]) per_ip[(keys[i] >> 24) - 1].push_back({(uint32_t)(keys[i] & 0xFFFFFF), i});
+    std::string s;
+    char buf[96];
+    for (uint64_t id = 0; id < n_ips; ++id) {
+      s.append(reinterpret_cast<const char *>(arena.data() + off[id]), len[id]);
+      s += ":\n";
+      std::sort(per_ip[id].begin(), per_ip[id].end(),
+                [&](const std::pair<uint32_t, uint64_t> &a, const std::pair<uint32_t, uint64_t> &b) {
+                  return e->names[a.first] < e->names[b.first];
+                });
+      for (auto &p : per_ip[id]) {
+        s += "\t" + e->names[p.first] + ":\n";
+        snprintf(buf, sizeof buf, "\t\t{%lld %lld}\n", (long long)hits[p.second], (long long)start[p.second]);
+        s += buf;
+      }
+      s += "\n";
+    }
+    if (out && cap) memcpy(out, s.data(), std::min(cap, s.size()));
+    return s.size();
+  } catch (const BjxError &x) {
+    e->last_error = x.what();
+    return 0;
+  }
+}
+
+// ------------------------------------------------------------ self-test hooks
+#include "../../include/banjax_gpu_debug.h"
+
+extern "C" int bjx_debug_rule_match_host(const bjx_ruleset *rs, size_t i, const uint8_t *text, size_t n) {
+  if (!rs || i >= rs->rules.size() || (n && !text)) return BJX_ERR_ARG;
+  return dfa_match_host(rs->rules[i].rx, text, n) ? 1 : 0;
+}
+extern "C" size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t i, char *out, size_t cap) {
+  if (!rs || i >= rs->rules.size()) return 0;
+  const std::string &l = rs->rules[i].rx.required_literal;
+  if (out && cap) memcpy(out, l.data(), std::min(cap, l.size()));
+  return l.size();
+}

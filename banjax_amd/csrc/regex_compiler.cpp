@@ -1,0 +1,1219 @@
+// Rule compiler for the MI355X engine: Go regexp syntax -> rune-class DFA.
+//
+// Parsing follows Go 1.25 regexp/syntax (parse.go, published algorithm) with
+// the flags regexp.Compile uses (syntax.Perl = ClassNL|OneLine|PerlX|
+// UnicodeGroups), so that the set of accepted patterns, their meaning and the
+// error texts match the reference's config load (internal/config.go:110-113).
+// Matching semantics are those of (*Regexp).Match on []byte (reference
+// internal/regex_rate_limiter.go:234): unanchored, boolean, over runes decoded
+// with Go's utf8.DecodeRune (an invalid byte is U+FFFD of width 1), with
+// empty-width assertions evaluated by syntax.EmptyOpContext.
+//
+// The automaton built here is a DFA over *rune classes* (a per-rule partition
+// of [0, 0x10FFFF]); \b, \B, ^ and $ are handled by carrying the category of
+// the previous rune (word / newline / start-of-text) in the DFA state, and the
+// unanchored search by re-seeding the NFA start at every rune boundary.
+// Accepting is absorbing (boolean match), so the device loop stops at the
+// first ACCEPT or DEAD state.
+#include "regex_compiler.h"
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <unordered_map>
+
+#include "../../include/banjax_gpu.h"
+#include "../../third_party/unicode/fold_orbits.h"
+
+namespace bjx {
+namespace {
+
+constexpr int32_t kMaxRune = 0x10FFFF;
+constexpr int32_t kRuneError = 0xFFFD;
+
+// ---------------------------------------------------------------- runes
+
+int32_t decode_rune(const uint8_t *s, size_t n, int *width) {
+  if (n == 0) { *width = 0; return -1; }
+  uint8_t b0 = s[0];
+  if (b0 < 0x80) { *width = 1; return b0; }
+  int need; uint8_t lo = 0x80, hi = 0xBF; int32_t r;
+  if (b0 >= 0xC2 && b0 <= 0xDF) { need = 1; r = b0 & 0x1F; }
+  else if (b0 == 0xE0) { need = 2; lo = 0xA0; r = b0 & 0x0F; }
+  else if ((b0 >= 0xE1 && b0 <= 0xEC) || b0 == 0xEE || b0 == 0xEF) { need = 2; r = b0 & 0x0F; }
+  else if (b0 == 0xED) { need = 2; hi = 0x9F; r = b0 & 0x0F; }
+  else if (b0 == 0xF0) { need = 3; lo = 0x90; r = b0 & 0x07; }
+  else if (b0 >= 0xF1 && b0 <= 0xF3) { need = 3; r = b0 & 0x07; }
+  else if (b0 == 0xF4) { need = 3; hi = 0x8F; r = b0 & 0x07; }
+  else { *width = 1; return kRuneError; }
+  if (n < static_cast<size_t>(need) + 1 || s[1] < lo || s[1] > hi) { *width = 1; return kRuneError; }
+  r = (r << 6) | (s[1] & 0x3F);
+  for (int k = 2; k <= need; ++k) {
+    if (s[k] < 0x80 || s[k] > 0xBF) { *width = 1; return kRuneError; }
+    r = (r << 6) | (s[k] & 0x3F);
+  }
+  *width = need + 1;
+  return r;
+}
+
+int32_t simple_fold(int32_t r) {
+  const uint32_t *b = bjx_fold_from, *e = bjx_fold_from + BJX_FOLD_N;
+  const uint32_t *it = std::lower_bound(b, e, static_cast<uint32_t>(r));
+  if (it != e && *it == static_cast<uint32_t>(r)) return static_cast<int32_t>(bjx_fold_to[it - b]);
+  return r;
+}
+
+bool is_word_rune(int32_t r) {
+  return r >= 0 && r < 0x80 && ((r >= '0' && r <= '9') || (r >= 'A' && r <= 'Z') || (r >= 'a' && r <= 'z') || r == '_');
+}
+bool is_alnum(int c) { return (c >= '0' && c <= '9') || (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z'); }
+
+using Ranges = std::vector<std::pair<int32_t, int32_t>>;
+
+void clean(Ranges &r) {
+  std::sort(r.begin(), r.end());
+  Ranges o;
+  for (auto &p : r) {
+    if (!o.empty() && p.first <= o.back().second + 1) o.back().second = std::max(o.back().second, p.second);
+    else o.push_back(p);
+  }
+  r.swap(o);
+}
+void negate(Ranges &r) {  // r clean
+  Ranges o;
+  int32_t next = 0;
+  for (auto &p : r) {
+    if (p.first > next) o.push_back({next, p.first - 1});
+    next = p.second + 1;
+  }
+  if (next <= kMaxRune) o.push_back({next, kMaxRune});
+  r.swap(o);
+}
+void add_folded(Ranges &r, int32_t lo, int32_t hi) {
+  const int32_t min_fold = 0x41, max_fold = static_cast<int32_t>(bjx_fold_from[BJX_FOLD_N - 1]);
+  if ((lo <= min_fold && hi >= max_fold) || hi < min_fold || lo > max_fold) { r.push_back({lo, hi}); return; }
+  if (lo < min_fold) { r.push_back({lo, min_fold - 1}); lo = min_fold; }
+  if (hi > max_fold) { r.push_back({max_fold + 1, hi}); hi = max_fold; }
+  for (int32_t c = lo; c <= hi; ++c) {
+    r.push_back({c, c});
+    for (int32_t f = simple_fold(c); f != c; f = simple_fold(f)) r.push_back({f, f});
+  }
+}
+
+// ------------------------------------------------------------------ AST
+
+enum Op : uint8_t {
+  kNoMatch = 1, kEmpty, kLit, kClass, kAnyNotNL, kAnyChar, kBOL, kEOL, kBOT, kEOT, kWB, kNWB,
+  kCap, kStar, kPlus, kQuest, kRepeat, kConcat, kAlt,
+  kPseudo = 100, kLParen, kVBar
+};
+enum Flag : uint32_t { kFold = 1, kClassNL = 2, kDotNL = 4, kOneLine = 8, kNonGreedy = 16, kPerlX = 32 };
+
+struct Re {
+  Op op;
+  uint32_t flags;
+  int min = 0, max = 0, cap = 0;
+  int32_t rune = 0;
+  Ranges cls;
+  std::vector<std::unique_ptr<Re>> sub;
+  Re(Op o, uint32_t f) : op(o), flags(f) {}
+};
+using ReP = std::unique_ptr<Re>;
+
+struct ParseError {
+  std::string code, expr;
+};
+
+const char *kErrInvalidCharRange = "invalid character class range";
+const char *kErrInvalidEscape = "invalid escape sequence";
+const char *kErrInvalidNamedCapture = "invalid named capture";
+const char *kErrInvalidPerlOp = "invalid or unsupported Perl syntax";
+const char *kErrInvalidRepeatOp = "invalid nested repetition operator";
+const char *kErrInvalidRepeatSize = "invalid repeat count";
+const char *kErrInvalidUTF8 = "invalid UTF-8";
+const char *kErrMissingBracket = "missing closing ]";
+const char *kErrMissingParen = "missing closing )";
+const char *kErrMissingRepeatArg = "missing argument to repetition operator";
+const char *kErrTrailingBackslash = "trailing backslash at end of expression";
+const char *kErrUnexpectedParen = "unexpected )";
+const char *kErrNestingDepth = "expression nests too deeply";
+
+struct Group { const char *name; int sign; std::vector<int32_t> r; };
+const std::vector<Group> &perl_groups() {
+  static const std::vector<Group> g = {
+    {"\\d", 1, {'0', '9'}}, {"\\D", -1, {'0', '9'}},
+    {"\\s", 1, {'\t', '\n', '\f', '\r', ' ', ' '}}, {"\\S", -1, {'\t', '\n', '\f', '\r', ' ', ' '}},
+    {"\\w", 1, {'0', '9', 'A', 'Z', '_', '_', 'a', 'z'}}, {"\\W", -1, {'0', '9', 'A', 'Z', '_', '_', 'a', 'z'}},
+  };
+  return g;
+}
+const std::vector<Group> &posix_groups() {
+  static std::vector<Group> g;
+  if (g.empty()) {
+    struct B { const char *n; std::vector<int32_t> r; };
+    std::vector<B> base = {
+      {"alnum", {'0', '9', 'A', 'Z', 'a', 'z'}}, {"alpha", {'A', 'Z', 'a', 'z'}}, {"ascii", {0, 0x7F}},
+      {"blank", {'\t', '\t', ' ', ' '}}, {"cntrl", {0, 0x1F, 0x7F, 0x7F}}, {"digit", {'0', '9'}},
+      {"graph", {'!', '~'}}, {"lower", {'a', 'z'}}, {"print", {' ', '~'}},
+      {"punct", {'!', '/', ':', '@', '[', '`', '{', '~'}}, {"space", {'\t', '\r', ' ', ' '}},
+      {"upper", {'A', 'Z'}}, {"word", {'0', '9', 'A', 'Z', '_', '_', 'a', 'z'}}, {"xdigit", {'0', '9', 'A', 'F', 'a', 'f'}},
+    };
+    static std::vector<std::string> names;
+    names.reserve(base.size() * 2);
+    for (auto &b : base) {
+      names.push_back(std::string("[:") + b.n + ":]");
+      names.push_back(std::string("[:^") + b.n + ":]");
+    }
+    for (size_t i = 0; i < base.size(); ++i) {
+      g.push_back({names[2 * i].c_str(), 1, base[i].r});
+      g.push_back({names[2 * i + 1].c_str(), -1, base[i].r});
+    }
+  }
+  return g;
+}
+
+class Parser {
+ public:
+  Parser(const std::string &s) : whole_(s) {}
+
+  ReP parse() {
+    const char *t = whole_.data(), *end = whole_.data() + whole_.size();
+    const char *last_repeat = nullptr;
+    while (t < end) {
+      const char *repeat = nullptr;
+      switch (*t) {
+        case '(':
+          if ((flags_ & kPerlX) && end - t >= 2 && t[1] == '?') { t = perl_flags(t, end); break; }
+          ++ncap_;
+          push_paren(ncap_);
+          ++t;
+          break;
+        case '|':
+          concat();
+          if (!swap_vbar()) push(std::make_unique<Re>(kVBar, flags_));
+          ++t;
+          break;
+        case ')': {
+          concat();
+          if (swap_vbar()) stack_.pop_back();
+          alternate();
+          size_t n = stack_.size();
+          if (n < 2) throw ParseError{kErrUnexpectedParen, whole_};
+          ReP re1 = std::move(stack_[n - 1]);
+          ReP re2 = std::move(stack_[n - 2]);
+          stack_.resize(n - 2);
+          if (re2->op != kLParen) throw ParseError{kErrUnexpectedParen, whole_};
+          flags_ = re2->flags;
+          if (re2->cap == 0) push(std::move(re1));
+          else { auto c = std::make_unique<Re>(kCap, re1->flags); c->cap = re2->cap; c->sub.push_back(std::move(re1)); push(std::move(c)); }
+          ++t;
+          break;
+        }
+        case '^': push(std::make_unique<Re>((flags_ & kOneLine) ? kBOT : kBOL, flags_)); ++t; break;
+        case '$': push(std::make_unique<Re>((flags_ & kOneLine) ? kEOT : kEOL, flags_)); ++t; break;
+        case '.': push(std::make_unique<Re>((flags_ & kDotNL) ? kAnyChar : kAnyNotNL, flags_)); ++t; break;
+        case '[': t = parse_class(t, end); break;
+        case '*': case '+': case '?': {
+          Op op = *t == '*' ? kStar : (*t == '+' ? kPlus : kQuest);
+          const char *before = t;
+          t = apply_repeat(op, 0, 0, before, t + 1, end, last_repeat);
+          repeat = before;
+          break;
+        }
+        case '{': {
+          const char *before = t, *after;
+          int mn, mx;
+          if (!parse_repeat(t, end, &mn, &mx, &after)) { literal('{'); ++t; break; }
+          if (mn < 0 || mn > 1000 || mx > 1000 || (mx >= 0 && mn > mx))
+            throw ParseError{kErrInvalidRepeatSize, std::string(before, after)};
+          t = apply_repeat(kRepeat, mn, mx, before, after, end, last_repeat);
+          repeat = before;
+          break;
+        }
+        case '\\': t = parse_backslash(t, end); break;
+        default: {
+          int w;
+          int32_t c = next_rune(t, end, &w);
+          literal(c);
+          t += w;
+        }
+      }
+      last_repeat = repeat;
+    }
+    concat();
+    if (swap_vbar()) stack_.pop_back();
+    alternate();
+    if (stack_.size() != 1) throw ParseError{kErrMissingParen, whole_};
+    ReP root = std::move(stack_[0]);
+    if (height(root.get()) > 1000) throw ParseError{kErrNestingDepth, whole_};
+    return root;
+  }
+
+ private:
+  const std::string &whole_;
+  uint32_t flags_ = kClassNL | kOneLine | kPerlX;
+  int ncap_ = 0;
+  std::vector<ReP> stack_;
+
+  static int height(const Re *r) {
+    int h = 0;
+    for (auto &s : r->sub) h = std::max(h, height(s.get()));
+    return h + 1;
+  }
+
+  int32_t next_rune(const char *t, const char *end, int *w) {
+    int32_t c = decode_rune(reinterpret_cast<const uint8_t *>(t), static_cast<size_t>(end - t), w);
+    if (c == kRuneError && *w == 1) throw ParseError{kErrInvalidUTF8, std::string(t, end)};
+    return c;
+  }
+
+  void push(ReP r) { stack_.push_back(std::move(r)); }
+  void push_paren(int cap) {
+    auto p = std::make_unique<Re>(kLParen, flags_);
+    p->cap = cap;
+    push(std::move(p));
+  }
+  void literal(int32_t r) {
+    auto n = std::make_unique<Re>(kLit, flags_);
+    n->rune = r;
+    push(std::move(n));
+  }
+  size_t top_items() const {
+    size_t i = stack_.size();
+    while (i > 0 && stack_[i - 1]->op < kPseudo) --i;
+    return i;
+  }
+  void concat() {
+    size_t i = top_items();
+    ReP n;
+    if (stack_.size() - i == 0) n = std::make_unique<Re>(kEmpty, flags_);
+    else if (stack_.size() - i == 1) n = std::move(stack_[i]);
+    else {
+      n = std::make_unique<Re>(kConcat, flags_);
+      for (size_t k = i; k < stack_.size(); ++k) n->sub.push_back(std::move(stack_[k]));
+    }
+    stack_.resize(i);
+    push(std::move(n));
+  }
+  void alternate() {
+    size_t i = top_items();
+    ReP n;
+    if (stack_.size() - i == 0) n = std::make_unique<Re>(kNoMatch, flags_);
+    else if (stack_.size() - i == 1) n = std::move(stack_[i]);
+    else {
+      n = std::make_unique<Re>(kAlt, flags_);
+      for (size_t k = i; k < stack_.size(); ++k) n->sub.push_back(std::move(stack_[k]));
+    }
+    stack_.resize(i);
+    push(std::move(n));
+  }
+  // swapVerticalBar: [.. VBAR x] -> [.. x VBAR]
+  bool swap_vbar() {
+    size_t n = stack_.size();
+    if (n >= 2 && stack_[n - 2]->op == kVBar) { std::swap(stack_[n - 1], stack_[n - 2]); return true; }
+    return false;
+  }
+
+  static bool repeat_valid(const Re *re, int n) {
+    if (re->op == kRepeat) {
+      int m = re->max;
+      if (m == 0) return true;
+      if (m < 0) m = re->min;
+      if (m > n) return false;
+      if (m > 0) n /= m;
+    }
+    for (auto &s : re->sub)
+      if (!repeat_valid(s.get(), n)) return false;
+    return true;
+  }
+
+  const char *apply_repeat(Op op, int mn, int mx, const char *before, const char *after, const char *end,
+                           const char *last_repeat) {
+    uint32_t f = flags_;
+    if (after < end && *after == '?') { ++after; f ^= kNonGreedy; }
+    if (last_repeat) throw ParseError{kErrInvalidRepeatOp, std::string(last_repeat, after)};
+    if (stack_.empty() || stack_.back()->op >= kPseudo) throw ParseError{kErrMissingRepeatArg, std::string(before, after)};
+    auto n = std::make_unique<Re>(op, f);
+    n->min = mn;
+    n->max = mx;
+    n->sub.push_back(std::move(stack_.back()));
+    stack_.back() = std::move(n);
+    if (op == kRepeat && (mn >= 2 || mx >= 2) && !repeat_valid(stack_.back().get(), 1000))
+      throw ParseError{kErrInvalidRepeatSize, std::string(before, after)};
+    return after;
+  }
+
+  static bool parse_int(const char **s, const char *end, int *out) {
+    const char *t = *s;
+    if (t >= end || *t < '0' || *t > '9') return false;
+    if (end - t >= 2 && t[0] == '0' && t[1] >= '0' && t[1] <= '9') return false;
+    const char *q = t;
+    while (q < end && *q >= '0' && *q <= '9') ++q;
+    int n = 0;
+    for (const char *c = t; c < q; ++c) {
+      if (n >= 100000000) { n = -1; break; }
+      n = n * 10 + (*c - '0');
+    }
+    *out = n;
+    *s = q;
+    return true;
+  }
+  static bool parse_repeat(const char *s, const char *end, int *mn, int *mx, const char **rest) {
+    if (s >= end || *s != '{') return false;
+    ++s;
+    if (!parse_int(&s, end, mn)) return false;
+    if (s >= end) return false;
+    if (*s != ',') *mx = *mn;
+    else {
+      ++s;
+      if (s >= end) return false;
+      if (*s == '}') *mx = -1;
+      else if (!parse_int(&s, end, mx)) return false;
+      else if (*mx < 0) *mn = -1;
+    }
+    if (s >= end || *s != '}') return false;
+    *rest = s + 1;
+    return true;
+  }
+
+  static int unhex(int32_t c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  }
+
+  int32_t parse_escape(const char *s, const char *end, const char **rest) {
+    const char *t = s + 1;
+    if (t >= end) throw ParseError{kErrTrailingBackslash, ""};
+    int w;
+    int32_t c = next_rune(t, end, &w);
+    t += w;
+    switch (c) {
+      case '1': case '2': case '3': case '4': case '5': case '6': case '7':
+        if (t >= end || *t < '0' || *t > '7') break;
+        [[fallthrough]];
+      case '0': {
+        int32_t r = c - '0';
+        for (int i = 1; i < 3; ++i) {
+          if (t >= end || *t < '0' || *t > '7') break;
+          r = r * 8 + (*t - '0');
+          ++t;
+        }
+        *rest = t;
+        return r;
+      }
+      case 'x': {
+        if (t >= end) break;
+        c = next_rune(t, end, &w);
+        t += w;
+        if (c == '{') {
+          int nhex = 0;
+          int64_t r = 0;
+          for (;;) {
+            if (t >= end) goto bad;
+            c = next_rune(t, end, &w);
+            t += w;
+            if (c == '}') break;
+            int v = unhex(c);
+            if (v < 0) goto bad;
+            r = r * 16 + v;
+            if (r > kMaxRune) goto bad;
+            ++nhex;
+          }
+          if (nhex == 0) goto bad;
+          *rest = t;
+          return static_cast<int32_t>(r);
+        }
+        int x = unhex(c), y = -1;
+        if (t < end) { c = next_rune(t, end, &w); t += w; y = unhex(c); }
+        if (x < 0 || y < 0) break;
+        *rest = t;
+        return x * 16 + y;
+      }
+      case 'a': *rest = t; return 7;
+      case 'f': *rest = t; return 12;
+      case 'n': *rest = t; return 10;
+      case 'r': *rest = t; return 13;
+      case 't': *rest = t; return 9;
+      case 'v': *rest = t; return 11;
+      default:
+        if (c < 0x80 && !is_alnum(c)) { *rest = t; return c; }
+    }
+  bad:
+    throw ParseError{kErrInvalidEscape, std::string(s, t)};
+  }
+
+  void append_group(Ranges &cls, const Group &g) {
+    Ranges tmp;
+    for (size_t i = 0; i < g.r.size(); i += 2) {
+      if (flags_ & kFold) add_folded(tmp, g.r[i], g.r[i + 1]);
+      else tmp.push_back({g.r[i], g.r[i + 1]});
+    }
+    clean(tmp);
+    if (g.sign < 0) negate(tmp);
+    cls.insert(cls.end(), tmp.begin(), tmp.end());
+  }
+  const Group *perl_class_escape(const char *s, const char *end) {
+    if (!(flags_ & kPerlX) || end - s < 2 || s[0] != '\\') return nullptr;
+    for (auto &g : perl_groups())
+      if (g.name[1] == s[1]) return &g;
+    return nullptr;
+  }
+  void reject_unicode_class(const char *s, const char *end) {
+    if (end - s >= 2 && s[0] == '\\' && (s[1] == 'p' || s[1] == 'P'))
+      throw ParseError{"unsupported Unicode class (\\p) in this build", std::string(s, std::min(end, s + 8))};
+  }
+
+  const char *parse_class(const char *s, const char *end) {
+    const char *t = s + 1;
+    auto re = std::make_unique<Re>(kClass, flags_);
+    int sign = 1;
+    if (t < end && *t == '^') {
+      sign = -1;
+      ++t;
+      if (!(flags_ & kClassNL)) re->cls.push_back({'\n', '\n'});
+    }
+    bool first = true;
+    while (t >= end || *t != ']' || first) {
+      first = false;
+      if (end - t > 2 && t[0] == '[' && t[1] == ':') {
+        const char *q = nullptr;
+        for (const char *c = t + 2; c + 1 < end; ++c)
+          if (c[0] == ':' && c[1] == ']') { q = c; break; }
+        if (q) {
+          std::string name(t, q + 2);
+          const Group *g = nullptr;
+          for (auto &pg : posix_groups())
+            if (name == pg.name) g = &pg;
+          if (!g) throw ParseError{kErrInvalidCharRange, name};
+          append_group(re->cls, *g);
+          t = q + 2;
+          continue;
+        }
+      }
+      reject_unicode_class(t, end);
+      if (const Group *g = perl_class_escape(t, end)) { append_group(re->cls, *g); t += 2; continue; }
+      const char *rng = t;
+      int32_t lo, hi;
+      if (t >= end) throw ParseError{kErrMissingBracket, std::string(s, end)};
+      if (*t == '\\') lo = parse_escape(t, end, &t);
+      else { int w; lo = next_rune(t, end, &w); t += w; }
+      hi = lo;
+      if (end - t >= 2 && t[0] == '-' && t[1] != ']') {
+        ++t;
+        if (*t == '\\') hi = parse_escape(t, end, &t);
+        else { int w; hi = next_rune(t, end, &w); t += w; }
+        if (hi < lo) throw ParseError{kErrInvalidCharRange, std::string(rng, t)};
+      }
+      if (flags_ & kFold) add_folded(re->cls, lo, hi);
+      else re->cls.push_back({lo, hi});
+    }
+    ++t;
+    clean(re->cls);
+    if (sign < 0) negate(re->cls);
+    push(std::move(re));
+    return t;
+  }
+
+  const char *perl_flags(const char *s, const char *end) {
+    const char *t = s;
+    size_t off = 0;
+    if (end - t > 4 && t[2] == 'P' && t[3] == '<') off = 4;
+    else if (end - t > 3 && t[2] == '<') off = 3;
+    if (off) {
+      const char *gt = static_cast<const char *>(memchr(t, '>', static_cast<size_t>(end - t)));
+      if (!gt) {
+        for (const char *c = t; c < end;) { int w; next_rune(c, end, &w); c += w; }  // checkUTF8
+        throw ParseError{kErrInvalidNamedCapture, std::string(s, end)};
+      }
+      std::string name(t + off, gt);
+      bool ok = !name.empty();
+      for (char ch : name)
+        if (!(is_alnum(static_cast<unsigned char>(ch)) || ch == '_')) ok = false;
+      if (!ok) {
+        for (const char *c = t + off; c < gt;) { int w; next_rune(c, gt, &w); c += w; }
+        throw ParseError{kErrInvalidNamedCapture, std::string(s, gt + 1)};
+      }
+      ++ncap_;
+      push_paren(ncap_);
+      return gt + 1;
+    }
+    t += 2;
+    uint32_t f = flags_;
+    int sign = 1;
+    bool saw = false;
+    while (t < end) {
+      int w;
+      int32_t c = next_rune(t, end, &w);
+      t += w;
+      switch (c) {
+        case 'i': f |= kFold; saw = true; continue;
+        case 'm': f &= ~kOneLine; saw = true; continue;
+        case 's': f |= kDotNL; saw = true; continue;
+        case 'U': f |= kNonGreedy; saw = true; continue;
+        case '-':
+          if (sign < 0) goto bad;
+          sign = -1;
+          f = ~f;
+          saw = false;
+          continue;
+        case ':': case ')':
+          if (sign < 0) {
+            if (!saw) goto bad;
+            f = ~f;
+          }
+          if (c == ':') push_paren(0);
+          flags_ = f;
+          return t;
+        default:
+          goto bad;
+      }
+    }
+  bad:
+    throw ParseError{kErrInvalidPerlOp, std::string(s, t)};
+  }
+
+  const char *parse_backslash(const char *t, const char *end) {
+    if ((flags_ & kPerlX) && end - t >= 2) {
+      switch (t[1]) {
+        case 'A': push(std::make_unique<Re>(kBOT, flags_)); return t + 2;
+        case 'b': push(std::make_unique<Re>(kWB, flags_)); return t + 2;
+        case 'B': push(std::make_unique<Re>(kNWB, flags_)); return t + 2;
+        case 'C': throw ParseError{kErrInvalidEscape, std::string(t, t + 2)};
+        case 'Q': {
+          const char *q = t + 2, *e = nullptr;
+          for (const char *c = q; c + 1 < end; ++c)
+            if (c[0] == '\\' && c[1] == 'E') { e = c; break; }
+          const char *lend = e ? e : end;
+          while (q < lend) { int w; int32_t c = next_rune(q, lend, &w); literal(c); q += w; }
+          return e ? e + 2 : end;
+        }
+        case 'z': push(std::make_unique<Re>(kEOT, flags_)); return t + 2;
+        default: break;
+      }
+    }
+    reject_unicode_class(t, end);
+    if (const Group *g = perl_class_escape(t, end)) {
+      auto re = std::make_unique<Re>(kClass, flags_);
+      append_group(re->cls, *g);
+      clean(re->cls);
+      push(std::move(re));
+      return t + 2;
+    }
+    const char *rest;
+    int32_t c = parse_escape(t, end, &rest);
+    literal(c);
+    return rest;
+  }
+};
+
+// ------------------------------------------------------------------ NFA
+
+enum NK : uint8_t { NK_CHAR, NK_EPS, NK_SPLIT, NK_ASSERT, NK_MATCH };
+enum Cond : uint8_t { C_BOL = 1, C_EOL = 2, C_BOT = 4, C_EOT = 8, C_WB = 16, C_NWB = 32 };
+
+struct NNode {
+  NK k;
+  uint8_t cond = 0;
+  int32_t out = -1, out1 = -1;
+  int32_t set = -1;  // NK_CHAR: index into Nfa::sets
+};
+
+struct Nfa {
+  std::vector<NNode> nodes;
+  std::vector<Ranges> sets;
+  std::map<Ranges, int32_t> set_ids;
+  int32_t start = -1;
+  uint8_t conds = 0;  // union of assertion kinds present
+  size_t limit = 2000000;
+
+  int32_t node(NK k) {
+    if (nodes.size() >= limit) throw ParseError{"", ""};
+    nodes.push_back(NNode{k});
+    return static_cast<int32_t>(nodes.size() - 1);
+  }
+  int32_t set_id(const Ranges &r) {
+    auto it = set_ids.find(r);
+    if (it != set_ids.end()) return it->second;
+    sets.push_back(r);
+    return set_ids[r] = static_cast<int32_t>(sets.size() - 1);
+  }
+};
+
+struct Frag {
+  int32_t start;
+  std::vector<int64_t> holes;  // (node << 1) | which
+};
+
+class NfaBuilder {
+ public:
+  explicit NfaBuilder(Nfa &n) : n_(n) {}
+  Frag build(const Re *r) {
+    switch (r->op) {
+      case kNoMatch: { int32_t i = n_.node(NK_CHAR); n_.nodes[i].set = n_.set_id({}); return {i, {}}; }
+      case kEmpty: return empty();
+      case kLit: {
+        Ranges v{{r->rune, r->rune}};
+        if (r->flags & kFold)
+          for (int32_t f = simple_fold(r->rune); f != r->rune; f = simple_fold(f)) v.push_back({f, f});
+        clean(v);
+        return chr(v);
+      }
+      case kClass: return chr(r->cls);
+      case kAnyChar: return chr({{0, kMaxRune}});
+      case kAnyNotNL: return chr({{0, '\n' - 1}, {'\n' + 1, kMaxRune}});
+      case kBOL: return assert_(C_BOL);
+      case kEOL: return assert_(C_EOL);
+      case kBOT: return assert_(C_BOT);
+      case kEOT: return assert_(C_EOT);
+      case kWB: return assert_(C_WB);
+      case kNWB: return assert_(C_NWB);
+      case kCap: return build(r->sub[0].get());
+      case kStar: return star(build(r->sub[0].get()));
+      case kPlus: {
+        Frag b = build(r->sub[0].get());
+        int32_t s = n_.node(NK_SPLIT);
+        n_.nodes[s].out = b.start;
+        patch(b, s);
+        return {b.start, {(int64_t(s) << 1) | 1}};
+      }
+      case kQuest: return quest(build(r->sub[0].get()));
+      case kRepeat: {
+        const Re *x = r->sub[0].get();
+        int mn = r->min, mx = r->max;
+        if (mx == 0) return empty();
+        Frag acc{-1, {}};
+        bool have = false;
+        for (int i = 0; i < mn; ++i) {
+          Frag c = build(x);
+          acc = have ? cat(acc, c) : c;
+          have = true;
+        }
+        if (mx < 0) {
+          Frag s = star(build(x));
+          return have ? cat(acc, s) : s;
+        }
+        if (mx > mn) {
+          Frag opt = quest(build(x));
+          for (int i = mn + 1; i < mx; ++i) opt = quest(cat(build(x), opt));
+          return have ? cat(acc, opt) : opt;
+        }
+        return acc;
+      }
+      case kConcat: {
+        Frag acc = build(r->sub[0].get());
+        for (size_t i = 1; i < r->sub.size(); ++i) acc = cat(acc, build(r->sub[i].get()));
+        return acc;
+      }
+      case kAlt: {
+        Frag acc = build(r->sub.back().get());
+        for (int i = static_cast<int>(r->sub.size()) - 2; i >= 0; --i) {
+          Frag a = build(r->sub[i].get());
+          int32_t s = n_.node(NK_SPLIT);
+          n_.nodes[s].out = a.start;
+          n_.nodes[s].out1 = acc.start;
+          a.holes.insert(a.holes.end(), acc.holes.begin(), acc.holes.end());
+          acc = {s, std::move(a.holes)};
+        }
+        return acc;
+      }
+      default: return empty();
+    }
+  }
+  void patch(Frag &f, int32_t target) {
+    for (int64_t h : f.holes) {
+      NNode &nd = n_.nodes[static_cast<size_t>(h >> 1)];
+      if (h & 1) nd.out1 = target; else nd.out = target;
+    }
+    f.holes.clear();
+  }
+
+ private:
+  Nfa &n_;
+  Frag empty() { int32_t i = n_.node(NK_EPS); return {i, {int64_t(i) << 1}}; }
+  Frag chr(const Ranges &r) {
+    int32_t i = n_.node(NK_CHAR);
+    n_.nodes[i].set = n_.set_id(r);
+    return {i, {int64_t(i) << 1}};
+  }
+  Frag assert_(uint8_t c) {
+    int32_t i = n_.node(NK_ASSERT);
+    n_.nodes[i].cond = c;
+    n_.conds |= c;
+    return {i, {int64_t(i) << 1}};
+  }
+  Frag star(Frag b) {
+    int32_t s = n_.node(NK_SPLIT);
+    n_.nodes[s].out = b.start;
+    patch(b, s);
+    return {s, {(int64_t(s) << 1) | 1}};
+  }
+  Frag quest(Frag b) {
+    int32_t s = n_.node(NK_SPLIT);
+    n_.nodes[s].out = b.start;
+    b.holes.push_back((int64_t(s) << 1) | 1);
+    return {s, std::move(b.holes)};
+  }
+  Frag cat(Frag a, Frag b) {
+    patch(a, b.start);
+    return {a.start, std::move(b.holes)};
+  }
+};
+
+// --------------------------------------------------- literal analysis
+
+struct LitInfo {
+  bool exact = false;
+  std::string exact_s;  // valid if exact
+  std::string req;      // every match contains req
+};
+
+LitInfo lit_info(const Re *r) {
+  LitInfo o;
+  auto ascii_lit = [](const Re *x, char *c) {
+    if (x->op == kLit && !(x->flags & kFold) && x->rune < 0x80) { *c = static_cast<char>(x->rune); return true; }
+    if (x->op == kClass && x->cls.size() == 1 && x->cls[0].first == x->cls[0].second && x->cls[0].first < 0x80) {
+      *c = static_cast<char>(x->cls[0].first);
+      return true;
+    }
+    return false;
+  };
+  char c;
+  if (ascii_lit(r, &c)) { o.exact = true; o.exact_s = std::string(1, c); o.req = o.exact_s; return o; }
+  switch (r->op) {
+    case kEmpty: case kBOL: case kEOL: case kBOT: case kEOT: case kWB: case kNWB:
+      o.exact = true;
+      return o;
+    case kCap: return lit_info(r->sub[0].get());
+    case kPlus: { LitInfo s = lit_info(r->sub[0].get()); o.req = s.req; return o; }
+    case kRepeat: {
+      LitInfo s = lit_info(r->sub[0].get());
+      if (r->min >= 1) o.req = s.req;
+      if (s.exact && r->min == r->max && s.exact_s.size() * static_cast<size_t>(r->min) <= 256) {
+        o.exact = true;
+        for (int i = 0; i < r->min; ++i) o.exact_s += s.exact_s;
+        if (o.exact_s.size() > o.req.size()) o.req = o.exact_s;
+      }
+      return o;
+    }
+    case kConcat: {
+      std::string run;
+      bool all_exact = true;
+      std::string all;
+      for (auto &s : r->sub) {
+        LitInfo si = lit_info(s.get());
+        if (si.exact) {
+          run += si.exact_s;
+          all += si.exact_s;
+        } else {
+          all_exact = false;
+          if (run.size() > o.req.size()) o.req = run;
+          run.clear();
+        }
+        if (si.req.size() > o.req.size()) o.req = si.req;
+      }
+      if (run.size() > o.req.size()) o.req = run;
+      if (all_exact) { o.exact = true; o.exact_s = all; }
+      return o;
+    }
+    default: return o;
+  }
+}
+
+bool is_dotstar(const Re *r) {
+  return r->op == kStar && (r->sub[0]->op == kAnyNotNL || r->sub[0]->op == kAnyChar);
+}
+
+// match <=> contains L when the pattern is (.*)* L (.*)* with L exact ASCII
+bool literal_equivalent(const Re *r, const std::string &lit) {
+  while (r->op == kCap) r = r->sub[0].get();
+  if (lit.empty()) return false;
+  if (r->op != kConcat) {
+    LitInfo li = lit_info(r);
+    return li.exact && li.exact_s == lit && r->op != kBOT;
+  }
+  size_t i = 0, n = r->sub.size();
+  while (i < n && is_dotstar(r->sub[i].get())) ++i;
+  std::string mid;
+  size_t j = i;
+  for (; j < n; ++j) {
+    const Re *x = r->sub[j].get();
+    if (is_dotstar(x)) break;
+    LitInfo li = lit_info(x);
+    if (!li.exact) return false;
+    // assertions inside would change meaning
+    if (x->op == kBOL || x->op == kEOL || x->op == kBOT || x->op == kEOT || x->op == kWB || x->op == kNWB) return false;
+    mid += li.exact_s;
+  }
+  for (; j < n; ++j)
+    if (!is_dotstar(r->sub[j].get())) return false;
+  return mid == lit;
+}
+
+// ------------------------------------------------------------------ DFA
+
+enum Ctx : uint8_t { X_OTHER = 0, X_WORD = 1, X_NL = 2, X_START = 3 };
+
+uint8_t empty_flags(uint8_t ctx, int nextcat /*0 other,1 word,2 nl,3 end*/) {
+  uint8_t op = C_NWB;
+  int boundary = 0;
+  if (ctx == X_WORD) boundary = 1;
+  else if (ctx == X_NL) op |= C_BOL;
+  else if (ctx == X_START) op |= C_BOT | C_BOL;
+  if (nextcat == 1) boundary ^= 1;
+  else if (nextcat == 2) op |= C_EOL;
+  else if (nextcat == 3) op |= C_EOT | C_EOL;
+  if (boundary) op ^= (C_WB | C_NWB);
+  return op;
+}
+
+struct KeyHash {
+  size_t operator()(const std::string &s) const { return std::hash<std::string>()(s); }
+};
+
+class DfaBuilder {
+ public:
+  DfaBuilder(const Nfa &nfa, uint32_t max_states) : n_(nfa), max_states_(max_states) {}
+
+  int build(CompiledRegex *out) {
+    make_classes();
+    if (ncls_ > 255) return BJX_ERR_TOO_COMPLEX;
+    track_word_ = (n_.conds & (C_WB | C_NWB)) != 0;
+    track_nl_ = (n_.conds & C_BOL) != 0;
+    track_start_ = (n_.conds & (C_BOT | C_BOL)) != 0;
+    mark_.assign(n_.nodes.size(), 0);
+    // state 0 = DEAD placeholder, 1 = ACCEPT
+    rows_.assign(2 * ncls_, 0);
+    for (uint32_t c = 0; c < ncls_; ++c) { rows_[c] = kDead; rows_[ncls_ + c] = kAccept; }
+    acc_end_ = {0, 1};
+    std::vector<int32_t> seed{n_.start};
+    std::vector<int32_t> s0 = closure0(seed);
+    uint32_t start = has_match(s0) ? kAccept : intern(s0, track_start_ ? X_START : X_OTHER);
+    while (!work_.empty()) {
+      uint32_t sid = work_.back();
+      work_.pop_back();
+      if (sid >= max_states_) return BJX_ERR_TOO_COMPLEX;
+      expand(sid);
+    }
+    finish(start, out);
+    return 0;
+  }
+
+ private:
+  const Nfa &n_;
+  uint32_t max_states_;
+  uint32_t ncls_ = 0;
+  std::vector<std::pair<int32_t, uint32_t>> intervals_;  // (lo, class) over [0, max]
+  std::vector<std::vector<uint8_t>> member_;             // set -> class -> in
+  std::vector<int> cls_cat_;                             // class -> 0 other / 1 word / 2 nl
+  bool track_word_ = false, track_nl_ = false, track_start_ = false;
+  std::unordered_map<std::string, uint32_t, KeyHash> ids_;
+  std::vector<std::pair<std::vector<int32_t>, uint8_t>> states_;  // by id (index id-2)
+  std::vector<uint32_t> work_;
+  std::vector<uint16_t> rows_;
+  std::vector<uint8_t> acc_end_;
+  std::vector<uint32_t> mark_;
+  uint32_t gen_ = 0;
+
+  void make_classes() {
+    std::vector<int32_t> b{0, kMaxRune + 1, 0x80};
+    for (auto &s : n_.sets)
+      for (auto &p : s) { b.push_back(p.first); b.push_back(p.second + 1); }
+    if (n_.conds & (C_WB | C_NWB))
+      for (int32_t x : {int32_t('0'), int32_t('9' + 1), int32_t('A'), int32_t('Z' + 1), int32_t('_'), int32_t('_' + 1),
+                        int32_t('a'), int32_t('z' + 1)})
+        b.push_back(x);
+    if (n_.conds & (C_BOL | C_EOL)) { b.push_back('\n'); b.push_back('\n' + 1); }
+    std::sort(b.begin(), b.end());
+    b.erase(std::unique(b.begin(), b.end()), b.end());
+    // signature per elementary interval
+    std::map<std::vector<uint8_t>, uint32_t> sig_ids;
+    const size_t nsets = n_.sets.size();
+    std::vector<std::vector<uint8_t>> cls_sig;
+    for (size_t i = 0; i + 1 < b.size(); ++i) {
+      int32_t lo = b[i];
+      std::vector<uint8_t> sig(nsets + 1, 0);
+      for (size_t s = 0; s < nsets; ++s) {
+        const Ranges &r = n_.sets[s];
+        auto it = std::upper_bound(r.begin(), r.end(), std::make_pair(lo, kMaxRune + 1));
+        if (it != r.begin() && std::prev(it)->second >= lo) sig[s] = 1;
+      }
+      int cat = 0;
+      if ((n_.conds & (C_WB | C_NWB)) && is_word_rune(lo)) cat = 1;
+      else if ((n_.conds & (C_BOL | C_EOL)) && lo == '\n') cat = 2;
+      sig[nsets] = static_cast<uint8_t>(cat);
+      auto it = sig_ids.find(sig);
+      uint32_t cid;
+      if (it == sig_ids.end()) {
+        cid = static_cast<uint32_t>(sig_ids.size());
+        sig_ids.emplace(sig, cid);
+        cls_sig.push_back(sig);
+        cls_cat_.push_back(cat);
+      } else cid = it->second;
+      intervals_.push_back({lo, cid});
+    }
+    ncls_ = static_cast<uint32_t>(sig_ids.size());
+    member_.assign(nsets, std::vector<uint8_t>(ncls_, 0));
+    for (uint32_t c = 0; c < ncls_; ++c)
+      for (size_t s = 0; s < nsets; ++s) member_[s][c] = cls_sig[c][s];
+  }
+
+  // closure through EPS/SPLIT (not through assertions): CHAR, ASSERT, MATCH nodes
+  std::vector<int32_t> closure0(const std::vector<int32_t> &seeds) {
+    ++gen_;
+    std::vector<int32_t> st(seeds.rbegin(), seeds.rend()), out;
+    while (!st.empty()) {
+      int32_t i = st.back();
+      st.pop_back();
+      if (i < 0 || mark_[i] == gen_) continue;
+      mark_[i] = gen_;
+      const NNode &nd = n_.nodes[i];
+      switch (nd.k) {
+        case NK_EPS: st.push_back(nd.out); break;
+        case NK_SPLIT: st.push_back(nd.out1); st.push_back(nd.out); break;
+        default: out.push_back(i);
+      }
+    }
+    std::sort(out.begin(), out.end());
+    return out;
+  }
+  // continue through assertions satisfied by flags; returns CHAR nodes, sets *match
+  std::vector<int32_t> closure_flags(const std::vector<int32_t> &seeds, uint8_t flags, bool *match) {
+    ++gen_;
+    std::vector<int32_t> st(seeds.rbegin(), seeds.rend()), out;
+    *match = false;
+    while (!st.empty()) {
+      int32_t i = st.back();
+      st.pop_back();
+      if (i < 0 || mark_[i] == gen_) continue;
+      mark_[i] = gen_;
+      const NNode &nd = n_.nodes[i];
+      switch (nd.k) {
+        case NK_EPS: st.push_back(nd.out); break;
+        case NK_SPLIT: st.push_back(nd.out1); st.push_back(nd.out); break;
+        case NK_ASSERT: if ((nd.cond & ~flags) == 0) st.push_back(nd.out); break;
+        case NK_MATCH: *match = true; break;
+        case NK_CHAR: out.push_back(i); break;
+      }
+    }
+    return out;
+  }
+  bool has_match(const std::vector<int32_t> &s) const {
+    for (int32_t i : s)
+      if (n_.nodes[i].k == NK_MATCH) return true;
+    return false;
+  }
+  bool has_assert(const std::vector<int32_t> &s) const {
+    for (int32_t i : s)
+      if (n_.nodes[i].k == NK_ASSERT) return true;
+    return false;
+  }
+  uint8_t mask_ctx(uint8_t ctx) const {
+    if (ctx == X_WORD && !track_word_) return X_OTHER;
+    if (ctx == X_NL && !track_nl_) return X_OTHER;
+    if (ctx == X_START && !track_start_) return X_OTHER;
+    return ctx;
+  }
+  uint32_t intern(const std::vector<int32_t> &set, uint8_t ctx) {
+    if (!has_assert(set)) ctx = X_OTHER;
+    ctx = mask_ctx(ctx);
+    std::string key(reinterpret_cast<const char *>(set.data()), set.size() * sizeof(int32_t));
+    key.push_back(static_cast<char>(ctx));
+    auto it = ids_.find(key);
+    if (it != ids_.end()) return it->second;
+    uint32_t id = static_cast<uint32_t>(states_.size() + 2);
+    ids_.emplace(std::move(key), id);
+    states_.push_back({set, ctx});
+    rows_.resize(static_cast<size_t>(id + 1) * ncls_, 0);
+    acc_end_.push_back(0);
+    work_.push_back(id);
+    return id;
+  }
+  void expand(uint32_t sid) {
+    // copy: states_ may grow during expansion
+    std::vector<int32_t> set = states_[sid - 2].first;
+    uint8_t ctx = states_[sid - 2].second;
+    bool m;
+    closure_flags(set, empty_flags(ctx, 3), &m);
+    acc_end_[sid] = m ? 1 : 0;
+    for (uint32_t c = 0; c < ncls_; ++c) {
+      uint8_t f = empty_flags(ctx, cls_cat_[c]);
+      std::vector<int32_t> chars = closure_flags(set, f, &m);
+      uint32_t next;
+      if (m) next = kAccept;
+      else {
+        std::vector<int32_t> seeds;
+        for (int32_t i : chars) {
+          const NNode &nd = n_.nodes[i];
+          if (member_[nd.set][c]) seeds.push_back(nd.out);
+        }
+        seeds.push_back(n_.start);
+        std::vector<int32_t> nx = closure0(seeds);
+        if (has_match(nx)) next = kAccept;
+        else {
+          uint8_t nctx = cls_cat_[c] == 1 ? X_WORD : (cls_cat_[c] == 2 ? X_NL : X_OTHER);
+          next = intern(nx, nctx);
+          if (next >= max_states_) { rows_[static_cast<size_t>(sid) * ncls_ + c] = 0; work_.push_back(next); return; }
+        }
+      }
+      rows_[static_cast<size_t>(sid) * ncls_ + c] = static_cast<uint16_t>(next);
+    }
+  }
+
+  void finish(uint32_t start, CompiledRegex *out) {
+    const uint32_t n = static_cast<uint32_t>(states_.size() + 2);
+    // live = can reach ACCEPT or an accept_end state
+    std::vector<std::vector<uint32_t>> rev(n);
+    for (uint32_t s = 2; s < n; ++s)
+      for (uint32_t c = 0; c < ncls_; ++c) rev[rows_[static_cast<size_t>(s) * ncls_ + c]].push_back(s);
+    std::vector<uint8_t> live(n, 0);
+    std::vector<uint32_t> st;
+    live[kAccept] = 1;
+    st.push_back(kAccept);
+    for (uint32_t s = 2; s < n; ++s)
+      if (acc_end_[s]) { live[s] = 1; st.push_back(s); }
+    while (!st.empty()) {
+      uint32_t s = st.back();
+      st.pop_back();
+      for (uint32_t p : rev[s])
+        if (!live[p]) { live[p] = 1; st.push_back(p); }
+    }
+    // Moore minimisation over live states; dead -> 0
+    std::vector<uint32_t> block(n, 0);
+    block[kDead] = 0;
+    block[kAccept] = 1;
+    for (uint32_t s = 2; s < n; ++s) block[s] = live[s] ? (acc_end_[s] ? 2 : 3) : 0;
+    uint32_t nblocks = 0;
+    for (;;) {
+      std::map<std::vector<uint32_t>, uint32_t> sig;
+      std::vector<uint32_t> nb(n);
+      // keep DEAD = 0 and ACCEPT = 1 fixed
+      sig[{0xFFFFFFFFu, 0}] = 0;
+      sig[{0xFFFFFFFFu, 1}] = 1;
+      nb[kDead] = 0;
+      nb[kAccept] = 1;
+      for (uint32_t s = 2; s < n; ++s) {
+        if (block[s] == 0) { nb[s] = 0; continue; }
+        std::vector<uint32_t> k;
+        k.reserve(ncls_ + 1);
+        k.push_back(block[s]);
+        for (uint32_t c = 0; c < ncls_; ++c) k.push_back(block[rows_[static_cast<size_t>(s) * ncls_ + c]]);
+        auto it = sig.find(k);
+        if (it == sig.end()) it = sig.emplace(k, static_cast<uint32_t>(sig.size())).first;
+        nb[s] = it->second;
+      }
+      uint32_t cnt = static_cast<uint32_t>(sig.size());
+      block.swap(nb);
+      if (cnt == nblocks) break;
+      nblocks = cnt;
+    }
+    // renumber: BFS from start over blocks
+    std::vector<int64_t> newid(nblocks + 2, -1);
+    std::vector<uint32_t> rep(nblocks + 2, 0);
+    for (uint32_t s = n; s-- > 2;) rep[block[s]] = s;
+    newid[0] = kDead;
+    newid[1] = kAccept;
+    std::vector<uint32_t> order;
+    uint32_t next_id = 2;
+    uint32_t sb = block[start];
+    if (newid[sb] < 0) { newid[sb] = next_id++; order.push_back(sb); }
+    for (size_t qi = 0; qi < order.size(); ++qi) {
+      uint32_t s = rep[order[qi]];
+      for (uint32_t c = 0; c < ncls_; ++c) {
+        uint32_t t = block[rows_[static_cast<size_t>(s) * ncls_ + c]];
+        if (newid[t] < 0) { newid[t] = next_id++; order.push_back(t); }
+      }
+    }
+    out->nstates = next_id;
+    out->ncls = ncls_;
+    out->start = static_cast<uint16_t>(newid[sb]);
+    out->trans.assign(static_cast<size_t>(next_id) * ncls_, 0);
+    out->accept_end.assign(next_id, 0);
+    out->accept_end[kAccept] = 1;
+    for (uint32_t c = 0; c < ncls_; ++c) { out->trans[c] = kDead; out->trans[ncls_ + c] = kAccept; }
+    for (uint32_t b : order) {
+      uint32_t s = rep[b];
+      uint32_t id = static_cast<uint32_t>(newid[b]);
+      out->accept_end[id] = acc_end_[s];
+      for (uint32_t c = 0; c < ncls_; ++c)
+        out->trans[static_cast<size_t>(id) * ncls_ + c] =
+            static_cast<uint16_t>(newid[block[rows_[static_cast<size_t>(s) * ncls_ + c]]]);
+    }
+    // rune -> class tables
+    for (auto &iv : intervals_) {
+      int32_t lo = iv.first;
+      if (lo < 0x80) {
+        auto it = std::upper_bound(intervals_.begin(), intervals_.end(), std::make_pair(lo, 0xFFFFFFFFu));
+        int32_t hi = (it == intervals_.end()) ? 0x80 : std::min<int32_t>(it->first, 0x80);
+        for (int32_t r = lo; r < hi; ++r) out->ascii_cls[r] = static_cast<uint8_t>(iv.second);
+      } else {
+        if (out->nonascii.empty() || out->nonascii.back().second != iv.second)
+          out->nonascii.push_back({static_cast<uint32_t>(lo), iv.second});
+      }
+    }
+    bool always = out->accept_end[out->start] != 0;
+    for (uint32_t c = 0; c < ncls_ && always; ++c)
+      if (out->trans[static_cast<size_t>(out->start) * ncls_ + c] != kAccept) always = false;
+    if (out->start == kAccept) always = true;
+    out->flags = 0;
+    if (always) out->flags |= kRuleAlways;
+    if (out->start == kDead) out->flags |= kRuleNever;
+  }
+};
+
+}  // namespace
+
+int compile_regex(const std::string &pattern, CompiledRegex *out, std::string *err, uint32_t max_dfa_states) {
+  ReP root;
+  try {
+    Parser p(pattern);
+    root = p.parse();
+  } catch (const ParseError &e) {
+    if (err) *err = "error parsing regexp: " + e.code + ": `" + e.expr + "`";
+    return BJX_ERR_REGEX;
+  }
+  Nfa nfa;
+  try {
+    NfaBuilder b(nfa);
+    Frag f = b.build(root.get());
+    int32_t m = nfa.node(NK_MATCH);
+    b.patch(f, m);
+    nfa.start = f.start;
+  } catch (const ParseError &) {
+    if (err) *err = "rule too complex for the automaton compiler (NFA size)";
+    return BJX_ERR_TOO_COMPLEX;
+  }
+  *out = CompiledRegex();
+  DfaBuilder d(nfa, std::min<uint32_t>(max_dfa_states, 65000));
+  int rc = d.build(out);
+  if (rc != 0) {
+    if (err) *err = "rule too complex for the DFA engine (state or class limit)";
+    return rc;
+  }
+  LitInfo li = lit_info(root.get());
+  out->required_literal = li.req;
+  out->literal_equivalent = literal_equivalent(root.get(), li.req);
+  return 0;
+}
+
+bool dfa_match_host(const CompiledRegex &rx, const uint8_t *text, size_t n) {
+  uint32_t st = rx.start;
+  size_t p = 0;
+  while (p < n && st > kAccept) {
+    int w;
+    int32_t r = decode_rune(text + p, n - p, &w);
+    uint32_t c;
+    if (r < 0x80) c = rx.ascii_cls[r];
+    else {
+      auto it = std::upper_bound(rx.nonascii.begin(), rx.nonascii.end(), std::make_pair(static_cast<uint32_t>(r), 0xFFFFFFFFu));
+      c = std::prev(it)->second;
+    }
+    st = rx.trans[static_cast<size_t>(st) * rx.ncls + c];
+    p += static_cast<size_t>(w);
+  }
+  return rx.accept_end[st] != 0;
+}
+
+}  // namespace bjx

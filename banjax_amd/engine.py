@@ -1,0 +1,104 @@
+"""One MI355X engine (bjx_engine): persistent rate-limit state in HBM plus the
+batch pipeline of include/banjax_gpu.h."""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Iterable, List, Optional, Tuple
+
+from . import _lib
+from .config import Config, Ruleset
+
+
+class BatchOutput:
+    """Host view of one bjx_process_batch."""
+
+    def __init__(self, res: _lib.BatchResult, copy_results: bool):
+        self.n_lines = res.n_lines
+        self.consumed_bytes = res.consumed_bytes
+        self.n_results = res.n_results
+        self.n_events = res.n_events
+        self.n_trips = res.n_trips
+        self.device_ms = res.device_ms
+        self.match_kernel_ms = res.match_kernel_ms
+        self.trips = [res.trips[i] for i in range(res.n_trips)] if res.n_trips else []
+        if copy_results:
+            self.line_flags = bytes(C.string_at(res.line_flags, res.n_lines)) if res.n_lines else b""
+            self.results = [res.results[i] for i in range(res.n_results)] if res.n_results else []
+        else:
+            self.line_flags = None
+            self.results = None
+
+
+class Engine:
+    def __init__(self, device: int = 0, ip_capacity: int = 0, state_capacity: int = 0, ip_arena_bytes: int = 0):
+        L = _lib.lib()
+        h = C.c_void_p()
+        err = C.create_string_buffer(512)
+        opts = _lib.EngineOptions(ip_capacity, state_capacity, ip_arena_bytes)
+        rc = L.bjx_engine_create(device, C.byref(opts), C.byref(h), err, 512)
+        if rc != _lib.OK:
+            raise _lib.BanjaxGpuError(rc, "bjx_engine_create: " + err.value.decode(errors="replace"))
+        self._h = h
+        self.device = device
+
+    def _check(self, rc, what):
+        if rc < 0:
+            msg = _lib.lib().bjx_engine_last_error(self._h)
+            raise _lib.BanjaxGpuError(rc, "%s: %s" % (what, (msg or b"").decode(errors="replace")))
+        return rc
+
+    def set_decision_lists(self, entries: Iterable[Tuple[Optional[str], int, str]]):
+        """StaticDecisionLists from config (decision.go:278-374)."""
+        entries = list(entries)
+        arr = (_lib.DecisionEntry * max(1, len(entries)))()
+        keep = []
+        for i, (site, dec, ip) in enumerate(entries):
+            s = _lib.Str(None, 0) if site is None else _lib.mkstr(site)
+            ipb = _lib.mkstr(ip)
+            keep.append((s, ipb))
+            arr[i] = _lib.DecisionEntry(s, dec, ipb)
+        self._check(_lib.lib().bjx_engine_set_decision_lists(self._h, arr, len(entries)), "set_decision_lists")
+
+    def process(self, rs: Ruleset, data, now_ns: int, copy_results: bool = False, device_ptr: Optional[int] = None,
+                nbytes: Optional[int] = None) -> BatchOutput:
+        """consumeLine over every complete line of `data` (bytes) or of a device
+        buffer (device_ptr, nbytes) already resident in HBM."""
+        res = _lib.BatchResult()
+        flags = _lib.COPY_RESULTS if copy_results else 0
+        if device_ptr is not None:
+            rc = _lib.lib().bjx_process_batch(self._h, rs.handle, C.c_void_p(device_ptr), nbytes, now_ns,
+                                              flags | _lib.INPUT_DEVICE, C.byref(res))
+        else:
+            buf = _lib.b(data)
+            rc = _lib.lib().bjx_process_batch(self._h, rs.handle, C.c_char_p(buf), len(buf), now_ns, flags,
+                                              C.byref(res))
+        self._check(rc, "process_batch")
+        return BatchOutput(res, copy_results)
+
+    def state_get(self, ip, name):
+        hits, start = C.c_int64(), C.c_int64()
+        ipb, nb = _lib.b(ip), _lib.b(name)
+        rc = self._check(_lib.lib().bjx_state_get(self._h, ipb, len(ipb), nb, len(nb), C.byref(hits), C.byref(start)),
+                         "state_get")
+        return (hits.value, start.value) if rc == 1 else None
+
+    def state_len(self) -> int:
+        return self._check(_lib.lib().bjx_state_len(self._h), "state_len")
+
+    def state_clear(self):
+        self._check(_lib.lib().bjx_state_clear(self._h), "state_clear")
+
+    def state_dump(self) -> str:
+        n = _lib.lib().bjx_state_dump(self._h, None, 0)
+        buf = C.create_string_buffer(n + 1)
+        _lib.lib().bjx_state_dump(self._h, buf, n)
+        return buf.raw[:n].decode(errors="replace")
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h and _lib._lib is not None:
+            _lib._lib.bjx_engine_destroy(h)
+        self._h = None
+
+    def __del__(self):
+        self.close()

@@ -1,0 +1,189 @@
+/*
+ * banjax_gpu.h — C ABI of libbanjax_gpu.so, the MI355X engine behind banjax's
+ * regex rate-limiting log tailer.
+ *
+ * Drop-in boundary: a Go host keeps banjax's surface (YAML schema,
+ * consumeLine/RunLogTailer, RegexRateLimitStates, BannerInterface, decision
+ * lists) and calls these entry points through cgo (binding: INTEGRATION.md).
+ * Plain pointers and sizes only; no GPU or torch types cross the boundary.
+ *
+ * Reference interfaces replaced (deflect-ca/banjax):
+ *   bjx_ruleset_compile     RegexWithRate.UnmarshalYAML        internal/config.go:96-131
+ *                           (regexp.Compile per rule, config.go:110; reload: config_holder.go:55-66)
+ *   bjx_engine_set_decision_lists  newStaticDecisionListsFromConfig  internal/decision.go:278-374
+ *   bjx_process_batch       consumeLine + applyRegexToLog per line
+ *                           internal/regex_rate_limiter.go:113-269, fed by RunLogTailer :21-78
+ *   bjx_state_get           RegexRateLimitStates.Get           internal/rate_limit.go:81-96
+ *   bjx_state_len           RegexRateLimitStates.Len           internal/rate_limit.go:30-35
+ *   bjx_state_dump          RegexRateLimitStates.String        internal/rate_limit.go:98-103,204-220
+ *
+ * Ownership: input buffers are borrowed for the duration of a call.  Result
+ * arrays are engine-owned and valid until the next bjx_process_batch on the
+ * same engine.  Rulesets are immutable; a reload compiles a new one (state is
+ * keyed by rule *name* and survives, as in the reference).
+ * Threading: one bjx_process_batch at a time per engine; bjx_state_* may be
+ * called from other threads (they serialise on the engine lock, as the
+ * reference's mutex does, rate_limit.go:19).
+ * Errors: int status (BJX_OK = 0, negative code) + a caller buffer for the
+ * message.  Malformed log lines are data (BJX_LINE_ERROR), never API errors.
+ */
+#ifndef BANJAX_GPU_H
+#define BANJAX_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BJX_ABI_VERSION 1
+
+enum bjx_status {
+  BJX_OK = 0,
+  BJX_ERR_REGEX = -1,       /* a rule's regex does not compile (Go error text in err) */
+  BJX_ERR_ARG = -2,
+  BJX_ERR_DEVICE = -3,      /* HIP runtime failure / no GPU */
+  BJX_ERR_NOMEM = -4,
+  BJX_ERR_TOO_COMPLEX = -5, /* rule exceeds the engine's automaton limits */
+  BJX_ERR_CAPACITY = -6,    /* state tables full (raise bjx_engine_options) */
+  BJX_ERR_DECISION = -7     /* unknown decision string / value */
+};
+
+/* Decision, reference internal/decision.go:20-28 */
+enum bjx_decision { BJX_ALLOW = 1, BJX_CHALLENGE = 2, BJX_NGINX_BLOCK = 3, BJX_IPTABLES_BLOCK = 4 };
+/* RateLimitMatchType, reference internal/rate_limit.go:175-181 */
+enum bjx_match_type { BJX_FIRST_TIME = 0, BJX_OUTSIDE_INTERVAL = 1, BJX_INSIDE_INTERVAL = 2 };
+/* ConsumeLineResult.{Error,OldLine,Exempted}, reference regex_rate_limiter.go:80-85 */
+enum bjx_line_flag { BJX_LINE_ERROR = 1, BJX_LINE_OLD = 2, BJX_LINE_EXEMPTED = 4 };
+
+typedef struct bjx_str {
+  const char *ptr;
+  size_t len;
+} bjx_str;
+
+/* One RegexWithRate (config.go:87-94), already decoded from YAML by the host. */
+typedef struct bjx_rule_spec {
+  bjx_str name;               /* Rule */
+  bjx_str regex;              /* RE2 / Go regexp syntax */
+  int64_t interval_ns;        /* time.Duration(interval * 1e9), computed by the host (config.go:116) */
+  int64_t hits_per_interval;  /* HitsPerInterval (Go int) */
+  int32_t decision;           /* enum bjx_decision (ParseDecision, decision.go:30-43) */
+  const bjx_str *hosts_to_skip; /* HostsToSkip keys whose value is true */
+  size_t n_hosts_to_skip;
+} bjx_rule_spec;
+
+/* per_site_regexes_with_rates[host] (config.go:19) */
+typedef struct bjx_site_rules {
+  bjx_str host;
+  const bjx_rule_spec *rules;
+  size_t n_rules;
+} bjx_site_rules;
+
+typedef struct bjx_ruleset bjx_ruleset;
+typedef struct bjx_engine bjx_engine;
+
+/* Compile every rule (regexp.Compile semantics, syntax.Perl flags).  Rule
+   indices: global rules 0..n_global-1, then each site's rules in order.  On a
+   compile error returns BJX_ERR_REGEX, *err_rule = failing index and the Go
+   error text ("error parsing regexp: ...") in err, and no ruleset. */
+int bjx_ruleset_compile(const bjx_rule_spec *global_rules, size_t n_global, const bjx_site_rules *per_site,
+                        size_t n_sites, bjx_ruleset **out, int64_t *err_rule, char *err, size_t err_len);
+void bjx_ruleset_release(bjx_ruleset *rs);
+size_t bjx_ruleset_num_rules(const bjx_ruleset *rs);
+/* Per-rule automaton statistics (DFA states, rune classes) for diagnostics. */
+int bjx_ruleset_rule_info(const bjx_ruleset *rs, size_t rule_idx, uint32_t *dfa_states, uint32_t *classes,
+                          uint32_t *flags);
+
+typedef struct bjx_engine_options {
+  uint64_t ip_capacity;       /* distinct IPs kept (reference never evicts, rate_limit.go:45-67); 0 = default */
+  uint64_t state_capacity;    /* distinct (ip, rule name) states; 0 = default */
+  uint64_t ip_arena_bytes;    /* bytes of IP strings; 0 = default */
+} bjx_engine_options;
+
+/* One engine per GPU (device index as HIP sees it).  opts may be NULL. */
+int bjx_engine_create(int device, const bjx_engine_options *opts, bjx_engine **out, char *err, size_t err_len);
+void bjx_engine_destroy(bjx_engine *e);
+
+/* Static decision lists used by CheckIsAllowed (decision.go:185-216): one
+   entry per IP/CIDR string of global_decision_lists (site.ptr == NULL) or
+   per_site_decision_lists[site], in config order.  Replaces previous lists
+   (StaticDecisionLists.UpdateFromConfig on reload, banjax.go:113). */
+typedef struct bjx_decision_entry {
+  bjx_str site;     /* ptr == NULL: global */
+  int32_t decision; /* enum bjx_decision */
+  bjx_str ip;       /* IP or CIDR text */
+} bjx_decision_entry;
+int bjx_engine_set_decision_lists(bjx_engine *e, const bjx_decision_entry *entries, size_t n);
+
+/* RuleResult of one matched (line, rule) pair, reference regex_rate_limiter.go:87-93.
+   RegexMatch is implied (only matches are reported, as consumeLine does, :189,208). */
+typedef struct bjx_rule_result {
+  uint64_t line_idx;
+  uint32_t rule_idx;  /* ruleset rule index */
+  uint16_t rule_pos;  /* position in the line's evaluation order (per-site rules, then global) */
+  uint8_t skip_host;
+  uint8_t seen_ip;
+  uint8_t match_type; /* enum bjx_match_type */
+  uint8_t exceeded;
+  uint8_t _pad[2];
+} bjx_rule_result;
+
+/* A rate-limit trip (RateLimitResult.Exceeded): the host replays
+   Banner.BanOrChallengeIp then Banner.LogRegexBan for it, in the order given
+   (regex_rate_limiter.go:254-266).  Offsets are relative to the line start in
+   the caller's buffer. */
+typedef struct bjx_trip {
+  uint64_t line_idx;
+  uint64_t line_offset; /* byte offset of the line in the batch */
+  uint32_t line_len;    /* without '\n' */
+  uint32_t rule_idx;
+  int64_t ts_ns;        /* parsed line timestamp (LogRegexBan logTime) */
+  uint32_t ip_off, ip_len;
+  uint32_t host_off, host_len;
+  uint32_t rest_off;    /* timeIpRest[2]: rest runs to line_len */
+  int32_t decision;
+} bjx_trip;
+
+enum bjx_batch_flags {
+  BJX_INPUT_DEVICE = 1,   /* bytes is a device pointer already resident in HBM */
+  BJX_COPY_RESULTS = 2    /* also copy per-line flags and RuleResults to host memory */
+};
+
+typedef struct bjx_batch_result {
+  uint64_t n_lines;        /* complete ('\n'-terminated) lines processed */
+  uint64_t consumed_bytes; /* offset after the last '\n' (the caller carries the rest) */
+  uint64_t n_results;      /* RuleResults (matched rules) */
+  uint64_t n_events;       /* RuleResults that reached RegexRateLimitStates.Apply */
+  uint64_t n_trips;
+  const uint8_t *line_flags;        /* host, n_lines entries, if BJX_COPY_RESULTS */
+  const bjx_rule_result *results;   /* host, n_results entries in reference order, if BJX_COPY_RESULTS */
+  const bjx_trip *trips;            /* host, n_trips entries in reference order */
+  double device_ms;                 /* device time of the batch (HIP events) */
+  double match_kernel_ms;           /* device time of the match kernel alone */
+} bjx_batch_result;
+
+/* consumeLine for every complete line of bytes[0..n) with injected clock
+   now_ns (time.Now(), used for OldLine). */
+int bjx_process_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns,
+                      uint32_t flags, bjx_batch_result *out);
+
+/* RegexRateLimitStates.Get(ip)[name]: 1 found (num_hits, start_ns set), 0 not found, <0 error. */
+int bjx_state_get(bjx_engine *e, const char *ip, size_t ip_len, const char *name, size_t name_len,
+                  int64_t *num_hits, int64_t *interval_start_ns);
+/* RegexRateLimitStates.Len(): number of distinct IPs with state. */
+int64_t bjx_state_len(bjx_engine *e);
+/* Drop every rate-limit state (a fresh RegexRateLimitStates). */
+int bjx_state_clear(bjx_engine *e);
+/* RegexRateLimitStates.String(): "ip:\n\trule:\n\t\t{hits start}\n" blocks, IPs in
+   first-seen order.  Returns the full length (writes at most cap bytes). */
+size_t bjx_state_dump(bjx_engine *e, char *out, size_t cap);
+
+/* Last error message of an engine call. */
+const char *bjx_engine_last_error(bjx_engine *e);
+int bjx_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BANJAX_GPU_H */

@@ -1,0 +1,24 @@
+/*
+ * banjax_gpu_debug.h — self-test hooks of libbanjax_gpu.so (not part of the
+ * drop-in boundary; never used by bjx_process_batch).
+ *
+ * bjx_debug_rule_match_host evaluates one compiled rule's DFA tables on the
+ * host, so the rule compiler can be checked against the oracle on machines
+ * without a GPU.  The product matches on the GPU only.
+ */
+#ifndef BANJAX_GPU_DEBUG_H
+#define BANJAX_GPU_DEBUG_H
+#include <stddef.h>
+#include <stdint.h>
+#include "banjax_gpu.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* 1 match, 0 no match, <0 error */
+int bjx_debug_rule_match_host(const bjx_ruleset *rs, size_t rule_idx, const uint8_t *text, size_t n);
+/* required literal the prefilter uses for a rule (bytes written, full length returned) */
+size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t rule_idx, char *out, size_t cap);
+#ifdef __cplusplus
+}
+#endif
+#endif

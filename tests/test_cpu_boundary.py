@@ -1,0 +1,101 @@
+"""CPU-side checks of the drop-in boundary (no GPU compute): the C-ABI library
+loads and exports every symbol include/banjax_gpu.h declares, the host rule
+compiler agrees with the oracle (compile errors and matching, via the
+compiler self-test hook), and the config schema mirrors config.go."""
+import ctypes as C
+import random
+import re
+
+import pytest
+
+from banjax_amd import Config, ConfigError, Ruleset, _lib, parse_decision
+from oracle import oracle as O
+
+HEADER = "include/banjax_gpu.h"
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    text = open(HEADER).read()
+    declared = set(re.findall(r"^(?:const\s+)?[a-z_0-9]+\s*\*?\s*(bjx_[a-z_0-9]+)\s*\(", text, re.M))
+    assert declared == set(_lib.EXPORTS), declared ^ set(_lib.EXPORTS)
+    for name in declared:
+        assert hasattr(L, name), name
+    assert L.bjx_abi_version() == 1
+
+
+def test_regex_with_rate_unmarshal():
+    """config_test.go:47-72 TestRegexWithRate."""
+    cfg = Config.from_yaml("""
+regexes_with_rates:
+  - decision: nginx_block
+    hits_per_interval: 800
+    interval: 30
+    regex: .*
+    rule: "All sites/methods: 800 req/30 sec"
+    hosts_to_skip:
+      localhost: true
+""")
+    r = cfg.regexes_with_rates[0]
+    assert r.decision == 3 and r.hits_per_interval == 800 and r.interval == 30 * 10 ** 9
+    assert r.regex == ".*" and r.rule == "All sites/methods: 800 req/30 sec"
+    assert r.hosts_to_skip == {"localhost": True}
+    assert len(Ruleset(cfg)) == 1
+
+
+def test_decisions_and_bad_config():
+    assert [parse_decision(s) for s in ("allow", "challenge", "nginx_block", "iptables_block")] == [1, 2, 3, 4]
+    with pytest.raises(ConfigError):
+        parse_decision("ban")
+    bad = "regexes_with_rates:\n  - {rule: x, regex: '(?invalid', interval: 1, hits_per_interval: 0, decision: allow}\n"
+    with pytest.raises(ConfigError) as ei:
+        Ruleset(Config.from_yaml(bad))
+    assert str(ei.value) == "error parsing regexp: invalid or unsupported Perl syntax: `(?in`"
+
+
+def _one_rule_ruleset(pat):
+    y = "regexes_with_rates:\n  - {rule: r, regex: '%s', interval: 1, hits_per_interval: 0, decision: allow}\n" % (
+        pat.replace("'", "''"))
+    return Ruleset(Config.from_yaml(y))
+
+
+PATTERNS = [r"a|b", r"(ab)*c", r"a.b", r"[^a]b", r"\ba", r"a\b", r"^a", r"a$", r"(?m)^a$", r"\Ba\B", r"a{2}",
+            r"(a|ab)(c|bcd)(d*)", r"(?s)a.", r"[[:space:]]x", r"(?i)A", r"\x{FFFD}", r"(?U)a+?b", r"a?$", r"^$",
+            r"\B", r"(?m)$\n^", r"(?i)straße", r"[\d\s]+", r"\W\w", r"(?i)k", r"[^\n]", r".*blockme.*",
+            r"GET \S+ GET \/wp-login\.php HTTP\/[0-2.]+ .*", r"(?i)(ahrefs|semrush)bot", r"\.(php|asp)\?.*=(\.\.\/)+",
+            r"x{3,}", r"(x|y){0,2}z", r"\Q.*\E", r"[a-c-e]", r"[]a]", r"\pL", r"a**", r"(?P<n>x)y", r"[[:^alpha:]]"]
+
+
+def test_compiler_matches_oracle_regexp():
+    rnd = random.Random(3)
+    alpha = [b"a", b"b", b"c", b"d", b"A", b"K", b"k", b"x", b"y", b"z", b"1", b" ", b"\n", b"_", b".", b"?", b"=",
+             b"/", b"\xc3\xa9", b"\xc3\x9f", b"\xff", b"\xe2\x84\xaa", b"\xc3", b"-", b"]"]
+    L = _lib.lib()
+    for pat in PATTERNS:
+        oerr = O.compile_error(pat)
+        try:
+            rs = _one_rule_ruleset(pat)
+            perr = None
+        except ConfigError as e:
+            perr = str(e)
+        assert perr == oerr, (pat, perr, oerr)
+        if perr:
+            continue
+        ore = O.Regex(pat)
+        for _ in range(400):
+            t = b"".join(rnd.choice(alpha) for _ in range(rnd.randrange(0, 10)))
+            got = L.bjx_debug_rule_match_host(rs.handle, 0, t, len(t))
+            assert got == int(ore.match(t)), (pat, t)
+
+
+def test_python_re_cross_check_of_oracle():
+    """Independent cross-check of the oracle's regexp on the subset where Go and
+    Python agree (ASCII text without newline; no \\s/\\d/$ differences)."""
+    rnd = random.Random(9)
+    pats = [r"a|bc", r"(ab)+c", r"a.b", r"[^a]b", r"\ba", r"a\b", r"^a", r"x{2,3}", r"(?i)ab", r"[a-c]+z", r"\w+\W",
+            r"(a|ab)(c|bcd)", r"a?b?c?$"]
+    for p in pats:
+        ore, pre = O.Regex(p), re.compile(p)
+        for _ in range(300):
+            t = "".join(rnd.choice("abcxyzAB _.") for _ in range(rnd.randrange(0, 9)))
+            assert ore.match(t) == (pre.search(t) is not None), (p, t)

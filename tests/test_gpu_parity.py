@@ -1,0 +1,294 @@
+"""GPU parity: the HIP engine (through the C ABI) against the oracle, bit-exact.
+
+Restates the reference's hot-path tests (internal/regex_rate_limiter_test.go)
+through the engine, then checks every BASELINE.json workload shape at sizes
+the oracle finishes in seconds, edge-case lines, and size-independent
+properties at larger sizes.
+"""
+import random
+
+import pytest
+
+import workloads as W
+from banjax_amd import Config, Engine, MockBanner, RegexRateLimiter, consume_line
+from oracle import oracle as O
+from tests.parity import Pair
+
+pytestmark = pytest.mark.gpu
+S = 1_000_000_000
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = Engine()
+    yield e
+    e.close()
+
+
+TEST_CONSUME_LINE_CFG = r"""
+regexes_with_rates:
+  - decision: nginx_block
+    rule: 'rule1'
+    regex: 'GET example\.com GET .*'
+    interval: 5
+    hits_per_interval: 2
+  - decision: challenge
+    rule: 'rule2'
+    regex: 'POST .*'
+    interval: 5
+    hits_per_interval: 1
+per_site_regexes_with_rates:
+  per-site.com:
+    - decision: nginx_block
+      hits_per_interval: 0
+      interval: 1
+      regex: .*blockme.*
+      rule: "instant block"
+"""
+
+
+def test_consume_line_sequence(engine):
+    """regex_rate_limiter_test.go:77-260 TestConsumeLine, through the GPU."""
+    engine.state_clear()
+    lim = RegexRateLimiter(Config.from_yaml(TEST_CONSUME_LINE_CFG), engine=engine, banner=MockBanner())
+    t0 = 1700000000.123456
+    now = int(t0 * 1e9)
+    ua = "AppleWebKit/537.36 (KHTML, like Gecko) Chrome/51.0.2704.103 Safari/537.36 -"
+    get = " 1.2.3.4 GET example.com GET /whatever HTTP/1.1 " + ua
+    post = " 1.2.3.4 POST example.com POST /whatever HTTP/1.1 " + ua
+    consume_line(lim, "%f" % t0 + get, now)
+    assert lim.states.get("1.2.3.4")["rule1"][0] == 1 and lim.banner.banned_ip == ""
+    consume_line(lim, "%f" % (t0 + 4) + get, now)
+    assert lim.states.get("1.2.3.4")["rule1"][0] == 2 and lim.banner.banned_ip == ""
+    consume_line(lim, "%f" % (t0 + 5.5) + get, now)
+    assert lim.states.get("1.2.3.4")["rule1"][0] == 1 and lim.banner.banned_ip == ""
+    consume_line(lim, "%f" % (t0 + 6.5) + post, now)
+    st = lim.states.get("1.2.3.4")
+    assert st["rule1"][0] == 1 and st["rule2"][0] == 1 and lim.banner.banned_ip == ""
+    r = consume_line(lim, "%f" % (t0 + 7.0) + post, now)
+    st = lim.states.get("1.2.3.4")
+    assert st["rule1"][0] == 1 and st["rule2"][0] == 0 and lim.banner.banned_ip == "1.2.3.4"
+    assert [x.rule_name for x in r.rule_results] == ["rule2"] and r.rule_results[0].rate_limit_result.exceeded
+    consume_line(lim, "%f 1.6.6.6 GET per-site.com GET /blockme/?a HTTP/1.1 %s" % (t0 + 20, ua), now)
+    assert lim.states.get("1.6.6.6") is not None
+    consume_line(lim, "%f 1.6.6.7 GET no-per-site.com GET /blockme/?a HTTP/1.1 %s" % (t0 + 22, ua), now)
+    assert lim.states.get("1.6.6.7") is None
+
+
+def test_consume_line_hosts_to_skip(engine):
+    """regex_rate_limiter_test.go:262-297 TestConsumeLineHostsToSkip."""
+    engine.state_clear()
+    cfg = Config.from_yaml(r"""
+regexes_with_rates:
+  - decision: nginx_block
+    rule: 'rule1'
+    regex: '^GET https?:\/\/\.*'
+    interval: 5
+    hits_per_interval: 2
+    hosts_to_skip:
+      skiphost.com: true
+""")
+    lim = RegexRateLimiter(cfg, engine=engine, banner=MockBanner())
+    t = 1700000000.5
+    consume_line(lim, "%f 1.2.3.4 GET skiphost.com GET /whatever HTTP/1.1 x" % t, int(t * 1e9))
+    assert lim.states.get("1.2.3.4") is None
+    r = consume_line(lim, "%f 1.2.3.4 GET skiphost.com GET http://x HTTP/1.1 x" % t, int(t * 1e9))
+    assert lim.states.get("1.2.3.4") is None
+    assert len(r.rule_results) == 0
+
+
+def test_per_site_regex_stress(engine):
+    """regex_rate_limiter_test.go:299-365 TestPerSiteRegexStress (10,000 global
+    rules, every line trips its own rule), seeded."""
+    rnd = random.Random(11)
+    n = 10000
+    doms, paths, rules = [], [], ["regexes_with_rates:"]
+    for i in range(n):
+        d = "%s%d.%s" % (rnd.choice(["acme", "shop", "news", "blog"]), i, rnd.choice(["com", "org", "net"]))
+        p = "/%s/%d" % (rnd.choice(["a", "img", "api"]), rnd.randrange(10 ** 6))
+        rules.append("  - decision: nginx_block\n    rule: 'rule%d'\n    regex: 'GET %s GET \\%s HTTP\\/[0-2.]+ .*'\n"
+                     "    interval: 1\n    hits_per_interval: 0" % (i, d.replace(".", "\\."), p))
+        doms.append(d)
+        paths.append(p)
+    pair = Pair("\n".join(rules) + "\n", engine)
+    base = 1700000000
+    lines, ips = [], []
+    for j in range(n):
+        ip = "%d.%d.%d.%d" % (rnd.randrange(1, 255), rnd.randrange(256), rnd.randrange(256), rnd.randrange(256))
+        ips.append(ip)
+        lines.append("%f %s GET %s GET %s HTTP/2.0 Mozilla/5.0 (X11)\n" % (float(base + j), ip, doms[j], paths[j]))
+    data = "".join(lines).encode()
+    out = pair.feed(data, (base + n) * S)
+    assert out.n_trips == n
+    for j in range(0, n, 997):
+        assert pair.engine.state_get(ips[j], "rule%d" % j) == (0, (base + j) * S)
+    pair.compare_state(ips[:50])
+
+
+@pytest.mark.parametrize("name,n_lines,batches", [
+    ("cfg1", 200_000, 3), ("cfg2", 40_000, 2), ("cfg3", 100_000, 3), ("cfg4", 1_500, 2), ("cfg5", 60_000, 2)])
+def test_workload_parity(engine, name, n_lines, batches):
+    """Every BASELINE.json config shape, oracle-sized, split into batches so the
+    HBM state carries across bjx_process_batch calls."""
+    w = W.scaled(W.ALL[name], n_lines, n_ips=min(W.ALL[name].n_ips, n_lines // 3 + 1))
+    pair = Pair(w.rules_yaml, engine)
+    per = (n_lines + batches - 1) // batches
+    ips = set()
+    for b in range(batches):
+        first, cnt = b * per, min(per, n_lines - b * per)
+        data = w.host_lines(first, cnt)
+        for ln in data.split(b"\n")[:200]:
+            parts = ln.split(b" ")
+            if len(parts) > 2:
+                ips.add(parts[1].decode())
+        pair.feed(data, w.now_ns(first, cnt))
+    pair.compare_state(sorted(ips)[:100])
+
+
+EDGE_CFG = r"""
+global_decision_lists:
+  allow:
+    - 20.20.20.20
+    - 2001:db8::/32
+    - 10.0.0.0/8
+    - not-an-ip
+    - ::ffff:5.6.7.8
+  challenge:
+    - 8.8.8.8
+per_site_decision_lists:
+  "h.com":
+    allow:
+      - 171.171.171.0/24
+      - 01.2.3.4
+      - ::ffff:9.9.0.0/112
+regexes_with_rates:
+  - rule: "all"
+    regex: '.*'
+    interval: 2
+    hits_per_interval: 1
+    decision: challenge
+  - rule: "wb"
+    regex: '\bx\b'
+    interval: 1
+    hits_per_interval: 0
+    decision: nginx_block
+  - rule: "anch"
+    regex: '^GET \S+ GET /$'
+    interval: 10
+    hits_per_interval: 0
+    decision: iptables_block
+  - rule: "utf"
+    regex: '(?i)straße|\x{FFFD}k'
+    interval: 1
+    hits_per_interval: 0
+    decision: nginx_block
+  - rule: "neg"
+    regex: '[^\x00-\x7f]'
+    interval: 100
+    hits_per_interval: 3
+    decision: challenge
+per_site_regexes_with_rates:
+  "h.com":
+    - rule: "all"
+      regex: 'POST'
+      interval: 0.5
+      hits_per_interval: -1
+      decision: nginx_block
+expiring_decision_ttl_seconds: 7
+"""
+
+
+def edge_lines(t):
+    L = []
+    add = L.append
+    add(b"")
+    add(b"garbage")
+    add(b"1.5 1.2.3.4")
+    add(b"%d 1.2.3.4 GET" % t)
+    add(b"%d 1.2.3.4 GET h.com" % t)
+    add(b"%d 1.2.3.4 GET h.com GET / HTTP/1.1 ua" % t)
+    add(b"%d.5 1.2.3.4 GET h.com GET / x" % (t - 11))
+    add(b"%d.5 1.2.3.4 GET h.com GET / x" % (t - 9))
+    for ts in [b"1e9", b"1_700_000_000.25", b"0x1.95p30", b"+1700000000", b"-5", b"inf", b"NaN", b"1e400", b"1e-400",
+               b".5", b"5.", b"1700000000.123456789012345678901", b"00001700000000", b"1.2.3", b"", b"0x", b"1__0",
+               b"170000000000000000000000000000", b"1700000000.000000000000000000000000001"]:
+        add(ts + b" 3.3.3.3 GET h.com GET /x HTTP/1.1 ua")
+    for ip in [b"20.20.20.20", b"2001:db8::7", b"10.9.8.7", b"not-an-ip", b"5.6.7.8", b"::ffff:20.20.20.20",
+               b"171.171.171.5", b"01.2.3.4", b"9.9.1.1", b"9.9.0.1", b"::ffff:9.9.0.7", b"1.2.3.4%eth0", b"",
+               b"256.1.1.1", b"::", b"2001:db9::1", b"8.8.8.8"]:
+        add(b"%d " % t + ip + b" GET h.com GET / HTTP/1.1 ua")
+        add(b"%d " % t + ip + b" POST other.com POST / HTTP/1.1 ua")
+    add(b"%d 4.4.4.4 GET h.com GET x y\r" % t)
+    add(b"%d 4.4.4.4 GET h.com GET / x STRASSE" % t)
+    add(b"%d 4.4.4.4 GET h.com GET / x stra\xc3\x9fe" % t)
+    add(b"%d 4.4.4.4 GET h.com GET / x \xffk" % t)
+    add(b"%d 4.4.4.4 GET h.com GET / x \xe2\x84\xaak" % t)
+    add(b"%d 4.4.4.4 GET h.com GET / x \xc3" % t)
+    add(b"%d 4.4.4.4 GET h.com GET / x x" % t)
+    add(b"%d 4.4.4.4 GET h.com GET / x_x" % t)
+    add(b"%d 4.4.4.4  h.com GET / " % t)
+    add(b"%d 4.4.4.4 GET  GET / x" % t)
+    add(b"%d  GET h.com GET / x" % t)
+    add(b"%d 4.4.4.4 GET h.com GET /" % t)
+    return b"\n".join(L) + b"\npartial-line-without-newline"
+
+
+def test_edge_lines(engine):
+    t = 1700000000
+    pair = Pair(EDGE_CFG, engine)
+    data = edge_lines(t)
+    pair.feed(data, t * S)
+    pair.feed(data, (t + 1) * S)  # replay: carried state, trips, escalations
+    pair.compare_state(["1.2.3.4", "3.3.3.3", "4.4.4.4", "8.8.8.8", "", "::", "not-an-ip"])
+
+
+def test_regex_corpus(engine):
+    """Random rules x random texts, GPU engine vs oracle regexp."""
+    rnd = random.Random(5)
+    atoms = [r"a", r"b", r"\d", r"\w", r"\W", r"\s", r".", r"[a-c]", r"[^ab]", r"(?i:K)", r"\b", r"\B", r"^", r"$",
+             r"é", r"\x{FFFD}", r"(a|bc)", r"x?", r"y+", r"z*", r"[[:upper:]]", r"\.", r" "]
+    pats = []
+    for _ in range(60):
+        p = "".join(rnd.choice(atoms) for _ in range(rnd.randrange(1, 5)))
+        if rnd.random() < 0.3:
+            p = p + "{1,3}" if not p.endswith(("?", "+", "*", "}")) else p
+        if O.compile_error(p) is None:
+            pats.append(p)
+    yaml_rules = ["regexes_with_rates:"]
+    for i, p in enumerate(pats):
+        yaml_rules.append("  - rule: 'r%d'\n    regex: '%s'\n    interval: 1\n    hits_per_interval: 1000000\n"
+                          "    decision: challenge" % (i, p.replace("'", "''")))
+    pair = Pair("\n".join(yaml_rules) + "\n", engine)
+    alpha = [b"a", b"b", b"c", b"K", b"k", b"1", b" ", b"_", b".", b"\xc3\xa9", b"\xff", b"\xe2\x84\xaa", b"-", b"x",
+             b"y", b"z", b"\r"]
+    lines = []
+    for j in range(3000):
+        body = b"".join(rnd.choice(alpha) for _ in range(rnd.randrange(0, 12)))
+        lines.append(b"1700000000 9.9.9.%d GET h%d.com " % (j % 250, j % 7) + body)
+    pair.feed(b"\n".join(lines) + b"\n", 1700000000 * S)
+
+
+def test_batching_is_associative(engine):
+    """Size-independent property at a larger size: one batch == four batches
+    (same trips in the same order, same final state)."""
+    w = W.scaled(W.CFG3, 2_000_000, n_ips=50_000)
+    data = w.host_lines()
+    now = w.now_ns()
+    engine.state_clear()
+    rs_cfg = Config.from_yaml(w.rules_yaml)
+    lim = RegexRateLimiter(rs_cfg, engine=engine, banner=MockBanner())
+    _, one = lim.consume_lines(data, now, want_results=False)
+    trips_one = [(t.line_idx, t.rule_idx) for t in one.trips]
+    dump_one = engine.state_dump()
+    engine.state_clear()
+    lim2 = RegexRateLimiter(rs_cfg, engine=engine, banner=MockBanner())
+    lines = data.split(b"\n")[:-1]
+    q = len(lines) // 4
+    trips_four, base = [], 0
+    for k in range(4):
+        chunk = b"\n".join(lines[k * q:(k + 1) * q if k < 3 else len(lines)]) + b"\n"
+        _, o = lim2.consume_lines(chunk, now, want_results=False)
+        trips_four += [(t.line_idx + base, t.rule_idx) for t in o.trips]
+        base += o.n_lines
+    assert trips_one == trips_four
+    assert sorted(dump_one.split("\n\n")) == sorted(engine.state_dump().split("\n\n"))
