@@ -112,6 +112,10 @@ def lib():
     L.bjx_debug_rule_match_host.argtypes = [vp, sz, C.c_char_p, sz]
     L.bjx_debug_rule_literal.restype = sz
     L.bjx_debug_rule_literal.argtypes = [vp, sz, C.c_char_p, sz]
+    L.bjx_debug_phase_ms.restype = sz
+    L.bjx_debug_phase_ms.argtypes = [vp, C.POINTER(C.c_double), sz]
+    L.bjx_debug_scan_stats.restype = sz
+    L.bjx_debug_scan_stats.argtypes = [vp, C.POINTER(C.c_uint64), sz]
     L.bjx_engine_last_error.restype = C.c_char_p
     L.bjx_engine_last_error.argtypes = [vp]
     _lib = L

@@ -84,6 +84,25 @@ __global__ __launch_bounds__(kBlock) void k_nl_count(const uint8_t *__restrict__
   if (threadIdx.x == 0) tile_counts[blockIdx.x] = tot;
 }
 
+// pass A of the v2 pipeline: '\n' count per 8 KB scan tile (32 B per lane)
+__global__ __launch_bounds__(kBlock) void k_nl_count8(const uint8_t *__restrict__ buf, uint64_t n,
+                                                      uint32_t *__restrict__ tile_counts) {
+  typedef hipcub::BlockReduce<uint32_t, kBlock> BR;
+  __shared__ typename BR::TempStorage tmp;
+  const uint64_t base = (uint64_t)blockIdx.x * 8192u + threadIdx.x * 32u;
+  uint32_t cnt = 0;
+  if (base + 32 <= n) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(buf + base);
+    const uint4 a = src[0], b = src[1];
+    cnt = __popc(nl_mask_word(a.x)) + __popc(nl_mask_word(a.y)) + __popc(nl_mask_word(a.z)) + __popc(nl_mask_word(a.w)) +
+          __popc(nl_mask_word(b.x)) + __popc(nl_mask_word(b.y)) + __popc(nl_mask_word(b.z)) + __popc(nl_mask_word(b.w));
+  } else {
+    for (uint64_t k = base; k < n && k < base + 32; ++k) cnt += buf[k] == '\n';
+  }
+  const uint32_t tot = BR(tmp).Sum(cnt);
+  if (threadIdx.x == 0) tile_counts[blockIdx.x] = tot;
+}
+
 __global__ __launch_bounds__(kBlock) void k_nl_write(const uint8_t *__restrict__ buf, uint64_t n,
                                                      const uint64_t *__restrict__ tile_base, uint64_t *__restrict__ nl) {
   typedef hipcub::BlockScan<uint32_t, kBlock> BS;
@@ -267,23 +286,21 @@ __device__ void parse_and_match(const Bind &B, const uint8_t *__restrict__ p, ui
   int32_t hid;
   bool exempt;
   double f;
+  hid = host_lookup(B, p + host_off, host_len);
+  exempt = B.any_allow && check_is_allowed(B, hid, p + ip_off, ip_len);
+  L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
+  L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
+  L.host_id[j] = hid;
+  L.ip_hash[j] = hash_bytes(p + ip_off, ip_len);
   if (!SLOW) {
-    hid = host_lookup(B, p + host_off, host_len);
-    exempt = B.any_allow && check_is_allowed(B, hid, p + ip_off, ip_len);
-    L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
-    L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
-    L.host_id[j] = hid;
-    L.ip_hash[j] = hash_bytes(p + ip_off, ip_len);
     if (parse_float_fast(p, sp1, &f) != 0) {
       // rare: exotic timestamp token -> general ParseFloat kernel
-      L.flags[j] = kLineSlowTs | (exempt ? kLineExemptPending : 0);
+      L.flags[j] = kLineSlowTs;
       unsigned long long k = atomicAdd(slow_count, 1ull);
       slow_list[k] = (uint32_t)j;
       return;
     }
   } else {
-    hid = L.host_id[j];
-    exempt = (L.flags[j] & kLineExemptPending) != 0;
     Decimal dec;
     if (go_parse_float(p, sp1, &f, &dec) != 0) { L.flags[j] = kLineError; return; }
   }
@@ -297,7 +314,7 @@ __device__ void parse_and_match(const Bind &B, const uint8_t *__restrict__ p, ui
   // per-site rules first, then global rules, in YAML order (regex_rate_limiter.go:175-211)
   const uint8_t *rest = p + rest_off;
   const uint32_t rest_len = n - rest_off;
-  uint64_t *mask = L.masks + j * B.mask_words;
+  uint64_t *mask = L.masks + (size_t)j * B.mask_words;
   uint64_t word = 0;
   uint32_t pos = 0, wi = 0, nres = 0, nev = 0;
   uint32_t s_begin = 0, s_end = 0;
@@ -328,6 +345,327 @@ __global__ __launch_bounds__(kBlock) void k_parse_match(Bind B, const uint8_t *_
   const uint64_t s = j ? nl[j - 1] + 1 : 0;
   const uint32_t n = (uint32_t)(nl[j] - s);
   parse_and_match<SLOW>(B, buf + s, n, j, now_ns, L, slow_list, slow_count);
+}
+
+// =====================================================================
+//   v2 pipeline: byte-parallel scan pass + per-line resolve pass
+// =====================================================================
+
+constexpr uint32_t kScanTile = 8192;  // 256 lanes x 32 B
+constexpr uint32_t kScanHalo = 512;   // bytes past the tile kept for headers / anchored rules
+
+struct ScanArgs {
+  const uint8_t *buf;
+  uint64_t n;
+  uint64_t n_tiles;
+  uint64_t n_lines;
+  const uint64_t *tile_base;  // newlines before each 8 KB tile (pass A)
+  uint64_t *nl;
+  Lines L;
+  int64_t now_ns;
+  uint32_t *slow_list;
+  unsigned long long *slow_count;
+  unsigned long long *stats;  // [0] gram-table probes, [1] candidates
+};
+
+__device__ __forceinline__ void fallback_line(const ScanArgs &A, uint64_t j) {
+  A.L.flags[j] = kLineSlowTs;
+  const unsigned long long k = atomicAdd(A.slow_count, 1ull);
+  A.slow_list[k] = (uint32_t)j;
+}
+
+// Anchored rule over rest held in LDS: 1 match, 0 no match, -1 undecided
+// within the window (k_resolve finishes it from HBM).
+__device__ int anchored_lds(const Bind &B, uint32_t r, const uint8_t *s, uint32_t i, uint32_t lim) {
+  const DevRule R = B.rules[r];
+  const uint16_t *tr = B.trans + R.trans_off;
+  const uint8_t *ac = B.ascii_cls + (size_t)r * 128;
+  uint32_t st = R.start;
+  for (;;) {
+    if (i >= lim) return -1;
+    const uint8_t b = s[i];
+    if (b == '\n') return B.accept_end[R.ae_off + st];  // end of the line = end of text
+    uint32_t c;
+    if (b < 0x80) {
+      c = ac[b];
+      ++i;
+    } else {
+      // decode only with the whole sequence (or the line end) inside the window
+      uint32_t avail = 0;
+      while (avail < 4 && i + avail < lim && s[i + avail] != '\n') ++avail;
+      if (avail < 4 && i + avail >= lim) return -1;
+      int w;
+      const int32_t rune = decode_rune_hd(s + i, avail, &w);
+      i += (uint32_t)w;
+      const uint32_t *na = B.nonascii + 2 * R.na_off;
+      uint32_t lo = 0, hi = R.n_na;
+      while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (na[2 * m] <= (uint32_t)rune) lo = m; else hi = m;
+      }
+      c = na[2 * lo + 1];
+    }
+    st = tr[st * R.ncls + c];
+    if (st <= 1) return st;
+  }
+}
+
+// Header of line j starting at LDS offset o (SplitN x2, ParseFloat fast path,
+// host lookup, CheckIsAllowed, OldLine) plus the anchored rules.
+__device__ void scan_line_header(const Bind &B, const ScanArgs &A, const uint8_t *s, uint32_t o, uint32_t lim,
+                                 uint64_t j) {
+  const Lines &L = A.L;
+  L.counts[j] = 0;
+  uint32_t sp[4];
+  int ns = 0;
+  uint32_t i = o;
+  bool eol = false;
+  while (i < lim) {
+    const uint8_t c = s[i];
+    if (c == '\n') { eol = true; break; }
+    if (c == ' ') { sp[ns++] = i; if (ns == 4) break; }
+    ++i;
+  }
+  if (ns < 4) {
+    if (eol) L.flags[j] = kLineError;
+    else fallback_line(A, j);  // header longer than the window
+    return;
+  }
+  double f;
+  if (parse_float_fast(s + o, sp[0] - o, &f) != 0) { fallback_line(A, j); return; }
+  const uint32_t ip_off = sp[0] + 1 - o, ip_len = sp[1] - sp[0] - 1;
+  const uint32_t rest_off = sp[1] + 1 - o, host_off = sp[2] + 1 - o, host_len = sp[3] - sp[2] - 1;
+  const int32_t hid = host_lookup(B, s + o + host_off, host_len);
+  const bool exempt = B.any_allow && check_is_allowed(B, hid, s + o + ip_off, ip_len);
+  L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
+  L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
+  L.host_id[j] = hid;
+  L.ip_hash[j] = hash_bytes(s + o + ip_off, ip_len);
+  const int64_t ts = ns_from_seconds(f);
+  L.ts[j] = ts;
+  uint8_t fl = 0;
+  if (go_sub(A.now_ns, ts) > 10000000000LL) fl = kLineOld;
+  else if (exempt) fl = kLineExempt;
+  L.flags[j] = fl;
+  if (fl || !B.any_anchored) { L.amask[j] = 0; L.ares[j] = 0; return; }
+  uint32_t s_begin = 0, s_end = 0;
+  if (hid >= 0) { s_begin = B.site_off[hid]; s_end = B.site_off[hid + 1]; }
+  const uint32_t nsite = s_end - s_begin, napp = nsite + B.n_global;
+  uint64_t am = 0, ar = 0;
+  for (uint32_t k = 0; k < napp; ++k) {
+    const uint32_t r = k < nsite ? B.site_rules[s_begin + k] : B.global_rules[k - nsite];
+    if (B.rules[r].mode != kModeAnchored) continue;
+    if (k >= 63) { ar |= 1ull << 63; continue; }
+    const int m = anchored_lds(B, r, s, o + rest_off, lim);
+    if (m < 0) ar |= 1ull << k;
+    else if (m) am |= 1ull << k;
+  }
+  L.amask[j] = am;
+  L.ares[j] = ar;
+}
+
+__device__ __forceinline__ uint8_t tile_byte(const uint8_t *s, int32_t l, uint32_t prev) {
+  return l >= 0 ? s[l] : (uint8_t)(prev >> (8 * (4 + l)));
+}
+
+// Pass B: one pass over the bytes, 32 per lane, coalesced; persistent blocks
+// walk 8 KB tiles.  Writes '\n' positions, parses every header (from LDS),
+// decides anchored rules, and runs the 4-gram prefilter (bitset in LDS) whose
+// exact hits become per-line literal candidates.
+__global__ __launch_bounds__(kBlock) void k_scan(Bind B, ScanArgs A) {
+  __shared__ uint32_t s_bits[kGramWords];
+  __shared__ __attribute__((aligned(16))) uint8_t s_tile[kScanTile + kScanHalo];
+  __shared__ uint32_t s_prev;
+  typedef hipcub::BlockScan<uint32_t, kBlock> BS;
+  __shared__ typename BS::TempStorage scan_tmp;
+  const uint32_t tid = threadIdx.x;
+  if (B.any_prefilter)
+    for (uint32_t i = tid; i < kGramWords; i += kBlock) s_bits[i] = B.gram_bits[i];
+  for (uint64_t t = blockIdx.x; t < A.n_tiles; t += gridDim.x) {
+    const uint64_t tstart = t * kScanTile;
+    const uint32_t lim = (uint32_t)min<uint64_t>(kScanTile + kScanHalo, A.n - tstart);
+    __syncthreads();
+    // ---- stage the tile (+ halo) in LDS; keep my 32 bytes in registers
+    uint32_t d[8];
+    const uint64_t mine = tstart + tid * 32u;
+    if (mine + 32 <= A.n) {
+      const uint4 *src = reinterpret_cast<const uint4 *>(A.buf + mine);
+      const uint4 a = src[0], b = src[1];
+      d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+    } else {
+      for (int w = 0; w < 8; ++w) {
+        uint32_t v = 0;
+        for (int k = 0; k < 4; ++k) {
+          const uint64_t pos = mine + 4 * w + k;
+          if (pos < A.n) v |= (uint32_t)A.buf[pos] << (8 * k);
+        }
+        d[w] = v;
+      }
+    }
+    uint4 *dst = reinterpret_cast<uint4 *>(s_tile + tid * 32u);
+    dst[0] = make_uint4(d[0], d[1], d[2], d[3]);
+    dst[1] = make_uint4(d[4], d[5], d[6], d[7]);
+    if (tid < kScanHalo / 16) {
+      const uint64_t h = tstart + kScanTile + tid * 16u;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (h + 16 <= A.n) v = *reinterpret_cast<const uint4 *>(A.buf + h);
+      else if (h < A.n) {
+        uint32_t w4[4] = {0, 0, 0, 0};
+        for (int k = 0; k < 16 && h + k < A.n; ++k) w4[k >> 2] |= (uint32_t)A.buf[h + k] << (8 * (k & 3));
+        v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      }
+      *reinterpret_cast<uint4 *>(s_tile + kScanTile + tid * 16u) = v;
+    }
+    if (tid == 0) s_prev = tstart >= 4 ? *reinterpret_cast<const uint32_t *>(A.buf + tstart - 4) : 0u;
+    // ---- newlines: positions and this lane's first line index
+    uint32_t nlm = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      const uint32_t x = d[w] ^ 0x0A0A0A0Au;
+      const uint32_t hb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+      nlm |= ((hb >> 7) & 1u) << (4 * w) | ((hb >> 15) & 1u) << (4 * w + 1) | ((hb >> 23) & 1u) << (4 * w + 2) |
+             ((hb >> 31) & 1u) << (4 * w + 3);
+    }
+    if (mine + 32 > A.n) nlm &= mine >= A.n ? 0u : ((1u << (A.n - mine)) - 1u);
+    uint32_t off;
+    BS(scan_tmp).ExclusiveSum((uint32_t)__popc(nlm), off);
+    __syncthreads();  // s_tile / s_prev visible
+    const uint64_t line0 = A.tile_base[t] + off;  // line containing my first byte
+    {
+      uint32_t x = nlm;
+      uint64_t r = line0;
+      while (x) {
+        const int k = __ffs(x) - 1;
+        x &= x - 1;
+        A.nl[r++] = mine + k;
+      }
+    }
+    // ---- line starts owned by this lane
+    if (tid == 0 && line0 < A.n_lines && (t == 0 || (s_prev >> 24) == '\n'))
+      scan_line_header(B, A, s_tile, 0, lim, line0);
+    {
+      uint32_t x = nlm;
+      uint64_t r = line0;
+      while (x) {
+        const int k = __ffs(x) - 1;
+        x &= x - 1;
+        ++r;  // the line after this newline
+        const uint32_t o = tid * 32u + (uint32_t)k + 1u;
+        if (o < kScanTile && r < A.n_lines) scan_line_header(B, A, s_tile, o, lim, r);
+      }
+    }
+    // ---- 4-gram prefilter over my 32 positions
+    if (!B.any_prefilter) continue;
+    const uint32_t dp = tid ? *reinterpret_cast<const uint32_t *>(s_tile + tid * 32u - 4u) : s_prev;
+    uint32_t hits = 0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int st = k - 3;
+      uint32_t g;
+      if (st < 0) g = __builtin_amdgcn_alignbyte(d[0], dp, (uint32_t)(4 + st));
+      else if ((st & 3) == 0) g = d[st >> 2];
+      else g = __builtin_amdgcn_alignbyte(d[(st >> 2) + 1], d[st >> 2], (uint32_t)(st & 3));
+      const uint32_t h = gram_hash(g);
+      hits |= ((s_bits[h >> 5] >> (h & 31)) & 1u) << k;
+    }
+    if (mine + 32 > A.n) hits &= mine >= A.n ? 0u : ((1u << (A.n - mine)) - 1u);
+    while (hits) {
+      const int k = __ffs(hits) - 1;
+      hits &= hits - 1;
+      const int32_t l0 = (int32_t)(tid * 32u) + k - 3;
+      const uint32_t g = (uint32_t)tile_byte(s_tile, l0, s_prev) | (uint32_t)tile_byte(s_tile, l0 + 1, s_prev) << 8 |
+                         (uint32_t)tile_byte(s_tile, l0 + 2, s_prev) << 16 | (uint32_t)tile_byte(s_tile, l0 + 3, s_prev) << 24;
+      atomicAdd(&A.stats[0], 1ull);
+      uint32_t slot = (uint32_t)mix64(g) & B.gt_mask;
+      while (B.gt_len[slot] && B.gt_key[slot] != g) slot = (slot + 1) & B.gt_mask;
+      if (!B.gt_len[slot]) continue;
+      const uint64_t line = line0 + __popc(nlm & ((1u << k) - 1u));
+      if (line >= A.n_lines) continue;
+      const int64_t gpos = (int64_t)(mine + k) - 3;
+      for (uint32_t e = 0; e < B.gt_len[slot]; ++e) {
+        const uint32_t lit = B.gt_entries[2 * (B.gt_off[slot] + e)];
+        const int64_t q = gpos - (int64_t)B.gt_entries[2 * (B.gt_off[slot] + e) + 1];
+        if (q < 0) continue;
+        const uint32_t c = atomicAdd(&A.L.cand_cnt[line], 1u);
+        atomicAdd(&A.stats[1], 1ull);
+        if (c < kCandSlots) A.L.cand[line * kCandSlots + c] = ((uint64_t)q << 24) | lit;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ bool literal_at(const Bind &B, uint32_t lit, const uint8_t *p) {
+  const uint32_t off = B.lit_off[lit], len = B.lit_len[lit];
+  for (uint32_t i = 0; i < len; ++i) {
+    const uint8_t t = p[i], l = B.lit_bytes[off + i];
+    if (B.lit_ci[off + i] ? ((t | 0x20) != l) : (t != l)) return false;
+  }
+  return true;
+}
+
+// Pass C: per line, decide every applicable rule from the scan pass's
+// anchored verdicts and literal candidates; DFA only where needed.
+__global__ __launch_bounds__(kBlock) void k_resolve(Bind B, const uint8_t *__restrict__ buf,
+                                                    const uint64_t *__restrict__ nl, uint64_t n_lines, Lines L) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_lines || L.flags[j] != 0) return;
+  const uint64_t s = j ? nl[j - 1] + 1 : 0;
+  const uint32_t n = (uint32_t)(nl[j] - s);
+  const uint8_t *p = buf + s;
+  const uint32_t rest_off = L.rest_off[j];
+  const uint8_t *rest = p + rest_off;
+  const uint32_t rest_len = n - rest_off;
+  const int32_t hid = L.host_id[j];
+  uint32_t cand_lit[kCandSlots];
+  uint32_t nc = 0;
+  bool ovf = false;
+  if (B.any_prefilter) {
+    const uint32_t cc = L.cand_cnt[j];
+    ovf = cc > (uint32_t)kCandSlots;
+    for (uint32_t c = 0; c < cc && c < (uint32_t)kCandSlots; ++c) {
+      const uint64_t v = L.cand[j * kCandSlots + c];
+      const uint32_t lit = (uint32_t)(v & 0xFFFFFF);
+      const uint64_t q = v >> 24;
+      if (q >= s + rest_off && q + B.lit_len[lit] <= s + n && literal_at(B, lit, buf + q)) cand_lit[nc++] = lit;
+    }
+  }
+  const uint64_t am = B.any_anchored ? L.amask[j] : 0, ar = B.any_anchored ? L.ares[j] : 0;
+  uint64_t *mask = L.masks + (size_t)j * B.mask_words;
+  uint64_t word = 0;
+  uint32_t pos = 0, wi = 0, nres = 0, nev = 0;
+  uint32_t s_begin = 0, s_end = 0;
+  if (hid >= 0) { s_begin = B.site_off[hid]; s_end = B.site_off[hid + 1]; }
+  const uint32_t nsite = s_end - s_begin;
+  const uint32_t napp = nsite + B.n_global;
+  for (uint32_t k = 0; k < napp; ++k) {
+    const uint32_t r = k < nsite ? B.site_rules[s_begin + k] : B.global_rules[k - nsite];
+    const uint8_t mode = B.rules[r].mode;
+    bool m;
+    if (mode == kModeAlways) m = true;
+    else if (mode == kModeNever) m = false;
+    else if (mode == kModeAnchored) {
+      if (k < 63 && !((ar >> k) & 1)) m = (am >> k) & 1;
+      else m = rule_match(B, r, rest, rest_len);
+    } else if (mode == kModePrefilter && !ovf) {
+      const DevRule &R = B.rules[r];
+      bool hit = false;
+      for (uint32_t c = 0; c < nc && !hit; ++c)
+        for (uint32_t e = 0; e < R.lits_len; ++e)
+          if (B.rule_lits[R.lits_off + e] == cand_lit[c]) { hit = true; break; }
+      m = hit && (R.equiv || rule_match(B, r, rest, rest_len));
+    } else {
+      m = rule_match(B, r, rest, rest_len);
+    }
+    if (m) {
+      word |= 1ull << (pos & 63);
+      ++nres;
+      nev += is_skip(B, r, hid) ? 0u : 1u;
+    }
+    ++pos;
+    if ((pos & 63) == 0) { mask[wi++] = word; word = 0; }
+  }
+  if (pos & 63) mask[wi] = word;
+  L.counts[j] = ((uint64_t)nres << 32) | nev;
 }
 
 // RuleResults (reference order) and rate-limit events from the per-line masks.
@@ -714,7 +1052,7 @@ extern "C" int bjx_ruleset_rule_info(const bjx_ruleset *rs, size_t i, uint32_t *
   const auto &rx = rs->rules[i].rx;
   if (states) *states = rx.nstates;
   if (classes) *classes = rx.ncls;
-  if (flags) *flags = rx.flags | (rx.literal_equivalent ? 0x100u : 0u);
+  if (flags) *flags = rx.flags | ((uint32_t)rx.mode << 8) | (rx.pref_equivalent ? 0x10000u : 0u) | ((uint32_t)rx.pref.size() << 20);
   return BJX_OK;
 }
 
@@ -726,6 +1064,10 @@ struct bjx_engine {
   std::string last_error;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evm0 = nullptr, evm1 = nullptr;
+  static constexpr int kPhases = 8;
+  hipEvent_t ph[kPhases + 1] = {};
+  double phase_ms[kPhases] = {};
+  bool phase_rec[kPhases + 1] = {};
 
   // decision lists (config order)
   struct Entry { bool global; std::string site; int32_t decision; std::string ip; };
@@ -755,6 +1097,10 @@ struct bjx_engine {
   DevBuf<uint64_t> l_iph, l_counts, l_offs, l_masks;
   DevBuf<uint32_t> l_ipoff, l_iplen, l_hoff, l_hlen, l_roff, slow_list;
   DevBuf<int32_t> l_hid;
+  DevBuf<uint64_t> l_amask, l_ares, l_cand;
+  DevBuf<uint32_t> l_ccnt;
+  unsigned long long scan_stats[2] = {0, 0};
+  uint64_t last_slow = 0;
   DevBuf<uint8_t> l_flags;
   DevBuf<unsigned long long> scalars;  // [0] slow count, [1..2] bounds, [3] selected
   DevBuf<uint64_t> res_seq;
@@ -887,6 +1233,10 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs) {
   std::vector<uint16_t> trans;
   std::vector<uint8_t> ae, ascii(rs->rules.size() * 128), lits;
   std::vector<uint32_t> nonascii;
+  std::map<std::pair<std::string, std::string>, uint32_t> lit_ids;
+  std::vector<uint8_t> lit_bytes, lit_ci;
+  std::vector<uint32_t> lit_off, lit_len, lit_gram, rule_lits;
+  bool any_anchored = false;
   for (size_t i = 0; i < rs->rules.size(); ++i) {
     const auto &r = rs->rules[i];
     DevRule &d = drules[i];
@@ -904,12 +1254,63 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs) {
     memcpy(&ascii[i * 128], r.rx.ascii_cls, 128);
     d.name_id = intern_name(e, r.name);
     d.decision = r.decision;
-    d.lit_off = (uint32_t)lits.size();
-    d.lit_len = (int32_t)r.rx.required_literal.size();
-    lits.insert(lits.end(), r.rx.required_literal.begin(), r.rx.required_literal.end());
+    d.mode = (uint8_t)r.rx.mode;
+    d.equiv = r.rx.pref_equivalent ? 1 : 0;
+    d.lits_off = (uint32_t)rule_lits.size();
+    if (r.rx.mode == kModePrefilter) {
+      for (auto &pl : r.rx.pref) {
+        auto key = std::make_pair(pl.s, pl.ci);
+        auto it = lit_ids.find(key);
+        uint32_t id;
+        if (it != lit_ids.end()) id = it->second;
+        else {
+          id = (uint32_t)lit_off.size();
+          lit_ids.emplace(key, id);
+          lit_off.push_back((uint32_t)lit_bytes.size());
+          lit_len.push_back((uint32_t)pl.s.size());
+          lit_gram.push_back(pl.gram_off);
+          lit_bytes.insert(lit_bytes.end(), pl.s.begin(), pl.s.end());
+          lit_ci.insert(lit_ci.end(), pl.ci.begin(), pl.ci.end());
+        }
+        rule_lits.push_back(id);
+      }
+    }
+    d.lits_len = (uint16_t)(rule_lits.size() - d.lits_off);
+    any_anchored = any_anchored || r.rx.mode == kModeAnchored;
     d.interval_ns = r.interval_ns;
     d.hits = r.hits;
   }
+  // gram filter: each literal's chosen 4-byte window, every ASCII case variant
+  // of its case-insensitive bytes, -> bitset bit + exact table entry
+  std::map<uint32_t, std::vector<std::pair<uint32_t, uint32_t>>> gmap;
+  for (uint32_t id = 0; id < lit_off.size(); ++id) {
+    const uint32_t o = lit_off[id] + lit_gram[id];
+    for (uint32_t v = 0; v < 16; ++v) {
+      uint32_t g = 0;
+      bool ok = true;
+      for (int k = 0; k < 4; ++k) {
+        uint8_t c = lit_bytes[o + k];
+        if (lit_ci[o + k]) c = ((v >> k) & 1) ? (uint8_t)(c & ~0x20) : c;
+        else if ((v >> k) & 1) ok = false;
+        g |= (uint32_t)c << (8 * k);
+      }
+      if (ok) gmap[g].push_back({id, lit_gram[id]});
+    }
+  }
+  std::vector<uint32_t> gram_bits(kGramWords, 0);
+  const uint32_t gt_cap = (uint32_t)next_pow2(gmap.size() * 2 + 16);
+  std::vector<uint32_t> gt_key(gt_cap, 0), gt_off(gt_cap, 0), gt_len(gt_cap, 0), gt_entries;
+  for (auto &kv : gmap) {
+    const uint32_t h = gram_hash(kv.first);
+    gram_bits[h >> 5] |= 1u << (h & 31);
+    uint32_t slot = (uint32_t)mix64(kv.first) & (gt_cap - 1);
+    while (gt_len[slot]) slot = (slot + 1) & (gt_cap - 1);
+    gt_key[slot] = kv.first;
+    gt_off[slot] = (uint32_t)(gt_entries.size() / 2);
+    gt_len[slot] = (uint32_t)kv.second.size();
+    for (auto &e : kv.second) { gt_entries.push_back(e.first); gt_entries.push_back(e.second); }
+  }
+  if (lit_bytes.empty()) { lit_bytes.push_back(0); lit_ci.push_back(0); }
   std::vector<uint32_t> global_rules(rs->n_global);
   for (uint32_t i = 0; i < rs->n_global; ++i) global_rules[i] = i;
   std::vector<uint32_t> site_off(n_hosts + 1, 0), site_rules;
@@ -1001,7 +1402,9 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs) {
          o_hdlen = bb.add(hd_len), o_hdb = bb.add(hd_bytes), o_hsc = bb.add(host_scope), o_skip = bb.add(skip),
          o_sao = bb.add(sc_addr_off), o_sa = bb.add(sc_addr), o_sso = bb.add(sc_sub_off), o_ss = bb.add(sc_sub),
          o_sto = bb.add(sc_str_off), o_sth = bb.add(sc_str_hash), o_stb = bb.add(sc_str_boff), o_stl = bb.add(sc_str_len),
-         o_stbytes = bb.add(sc_str_bytes);
+         o_stbytes = bb.add(sc_str_bytes), o_gbits = bb.add(gram_bits), o_gtk = bb.add(gt_key), o_gto = bb.add(gt_off),
+         o_gtl = bb.add(gt_len), o_gte = bb.add(gt_entries), o_lb = bb.add(lit_bytes), o_lci = bb.add(lit_ci),
+         o_lo = bb.add(lit_off), o_ll = bb.add(lit_len), o_rl = bb.add(rule_lits);
   e->bind_blob.ensure(bb.bytes.size());
   HIP_OK(hipMemcpy(e->bind_blob.p, bb.bytes.data(), bb.bytes.size(), hipMemcpyHostToDevice));
   uint8_t *base = e->bind_blob.p;
@@ -1039,6 +1442,20 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs) {
   B.n_scopes = n_scopes;
   B.any_allow = any_allow ? 1 : 0;
   B.mask_words = std::max<uint32_t>(1, (max_app + 63) / 64);
+  B.gram_bits = reinterpret_cast<const uint32_t *>(base + o_gbits);
+  B.gt_key = reinterpret_cast<const uint32_t *>(base + o_gtk);
+  B.gt_off = reinterpret_cast<const uint32_t *>(base + o_gto);
+  B.gt_len = reinterpret_cast<const uint32_t *>(base + o_gtl);
+  B.gt_entries = reinterpret_cast<const uint32_t *>(base + o_gte);
+  B.lit_bytes = base + o_lb;
+  B.lit_ci = base + o_lci;
+  B.lit_off = reinterpret_cast<const uint32_t *>(base + o_lo);
+  B.lit_len = reinterpret_cast<const uint32_t *>(base + o_ll);
+  B.rule_lits = reinterpret_cast<const uint32_t *>(base + o_rl);
+  B.gt_mask = gt_cap - 1;
+  B.n_lits = (uint32_t)lit_off.size();
+  B.any_anchored = any_anchored ? 1 : 0;
+  B.any_prefilter = lit_off.empty() ? 0 : 1;
   e->host_rules = drules;
   e->bound_uid = rs->uid;
   e->bound_dec_version = e->decisions_version;
@@ -1164,6 +1581,7 @@ extern "C" int bjx_engine_create(int device, const bjx_engine_options *opts, bjx
     HIP_OK(hipEventCreate(&e->ev1));
     HIP_OK(hipEventCreate(&e->evm0));
     HIP_OK(hipEventCreate(&e->evm1));
+    for (auto &x : e->ph) HIP_OK(hipEventCreate(&x));
     uint64_t ipc = opts && opts->ip_capacity ? next_pow2(opts->ip_capacity) : (1ull << 20);
     uint64_t stc = opts && opts->state_capacity ? next_pow2(opts->state_capacity) : (1ull << 22);
     uint64_t ar = opts && opts->ip_arena_bytes ? opts->ip_arena_bytes : (64ull << 20);
@@ -1190,7 +1608,9 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   e->scalars.release(); e->res_seq.release(); e->res_rule.release(); e->ev_key.release(); e->ev_res.release();
   e->ev_key2.release(); e->ev_res2.release(); e->heads.release(); e->trip_idx.release(); e->d_trips.release();
   e->d_results.release(); e->q_out.release();
+  e->l_amask.release(); e->l_ares.release(); e->l_cand.release(); e->l_ccnt.release();
   (void)hipEventDestroy(e->ev0); (void)hipEventDestroy(e->ev1); (void)hipEventDestroy(e->evm0); (void)hipEventDestroy(e->evm1);
+  for (auto &x : e->ph) (void)hipEventDestroy(x);
   (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -1215,6 +1635,13 @@ extern "C" int bjx_engine_set_decision_lists(bjx_engine *e, const bjx_decision_e
   return BJX_OK;
 }
 
+// phase boundaries: 0 start, 1 counted (pass A), 2 scanned (pass B), 3 resolved
+// (pass C + fallback), 4 emitted, 5 sorted, 6 segmented, 7 rate-limited, 8 trips
+static void mark(bjx_engine *e, int k) {
+  HIP_OK(hipEventRecord(e->ph[k], e->stream));
+  e->phase_rec[k] = true;
+}
+
 static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns, uint32_t flags,
                       bjx_batch_result *out) {
   HIP_OK(hipSetDevice(e->device));
@@ -1234,12 +1661,14 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
     buf = e->staging.p;
   }
   HIP_OK(hipEventRecord(e->ev0, st));
+  for (auto &r : e->phase_rec) r = false;
+  mark(e, 0);
 
-  // ---- framing
-  const uint64_t n_tiles = (n + kTile - 1) / kTile;
+  // ---- pass A: '\n' count per 8 KB tile, exclusive scan -> line index of each tile
+  const uint64_t n_tiles = (n + kScanTile - 1) / kScanTile;
   e->tile_counts.ensure(n_tiles);
   e->tile_base.ensure(n_tiles + 1);
-  hipLaunchKernelGGL(k_nl_count, dim3((unsigned)n_tiles), dim3(kBlock), 0, st, buf, (uint64_t)n, e->tile_counts.p);
+  hipLaunchKernelGGL(k_nl_count8, dim3((unsigned)n_tiles), dim3(kBlock), 0, st, buf, (uint64_t)n, e->tile_counts.p);
   HIP_OK(hipGetLastError());
   {
     uint32_t *in = e->tile_counts.p;
@@ -1256,39 +1685,53 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
   const uint64_t n_lines = last_base + last_cnt;
   out->n_lines = n_lines;
   if (n_lines == 0) return;
-  e->nl.ensure(n_lines);
-  hipLaunchKernelGGL(k_nl_write, dim3((unsigned)n_tiles), dim3(kBlock), 0, st, buf, (uint64_t)n, e->tile_base.p, e->nl.p);
-  HIP_OK(hipGetLastError());
-  uint64_t last_nl = 0;
-  HIP_OK(hipMemcpyAsync(&last_nl, e->nl.p + (n_lines - 1), 8, hipMemcpyDeviceToHost, st));
 
   // ---- per-line arrays
+  e->nl.ensure(n_lines);
   e->l_ts.ensure(n_lines); e->l_iph.ensure(n_lines); e->l_counts.ensure(n_lines + 1); e->l_offs.ensure(n_lines + 1);
   e->l_masks.ensure(n_lines * B.mask_words);
   e->l_ipoff.ensure(n_lines); e->l_iplen.ensure(n_lines); e->l_hoff.ensure(n_lines); e->l_hlen.ensure(n_lines);
   e->l_roff.ensure(n_lines); e->l_hid.ensure(n_lines); e->l_flags.ensure(n_lines); e->slow_list.ensure(n_lines);
-  e->scalars.ensure(8);
+  e->l_amask.ensure(n_lines); e->l_ares.ensure(n_lines); e->l_ccnt.ensure(n_lines);
+  e->l_cand.ensure(B.any_prefilter ? n_lines * kCandSlots : 1);
+  e->scalars.ensure(16);
   Lines L;
   L.ts = e->l_ts.p; L.ip_hash = e->l_iph.p; L.ip_off = e->l_ipoff.p; L.ip_len = e->l_iplen.p; L.host_off = e->l_hoff.p;
   L.host_len = e->l_hlen.p; L.rest_off = e->l_roff.p; L.host_id = e->l_hid.p; L.flags = e->l_flags.p;
-  L.counts = e->l_counts.p; L.masks = e->l_masks.p;
-  HIP_OK(hipMemsetAsync(e->scalars.p, 0, 8 * sizeof(unsigned long long), st));
+  L.counts = e->l_counts.p; L.masks = e->l_masks.p; L.amask = e->l_amask.p; L.ares = e->l_ares.p;
+  L.cand_cnt = e->l_ccnt.p; L.cand = e->l_cand.p;
+  HIP_OK(hipMemsetAsync(e->scalars.p, 0, 16 * sizeof(unsigned long long), st));
+  if (B.any_prefilter) HIP_OK(hipMemsetAsync(e->l_ccnt.p, 0, n_lines * 4, st));
+  mark(e, 1);
 
-  // ---- parse + match (the hot kernel)
+  // ---- pass B: the scan kernel (the hot, HBM-bound kernel)
+  ScanArgs A;
+  A.buf = buf; A.n = n; A.n_tiles = n_tiles; A.n_lines = n_lines; A.tile_base = e->tile_base.p; A.nl = e->nl.p;
+  A.L = L; A.now_ns = now_ns; A.slow_list = e->slow_list.p; A.slow_count = e->scalars.p; A.stats = e->scalars.p + 8;
   HIP_OK(hipEventRecord(e->evm0, st));
-  hipLaunchKernelGGL(k_parse_match<false>, dim3(grid_for(n_lines)), dim3(kBlock), 0, st, B, buf, e->nl.p, n_lines,
-                     (const uint32_t *)nullptr, now_ns, L, e->slow_list.p, e->scalars.p);
+  const unsigned scan_grid = (unsigned)std::min<uint64_t>(n_tiles, 256 * 8);
+  hipLaunchKernelGGL(k_scan, dim3(scan_grid), dim3(kBlock), 0, st, B, A);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e->evm1, st));
+  mark(e, 2);
+  uint64_t last_nl = 0;
   unsigned long long n_slow = 0;
+  HIP_OK(hipMemcpyAsync(&last_nl, e->nl.p + (n_lines - 1), 8, hipMemcpyDeviceToHost, st));
   HIP_OK(hipMemcpyAsync(&n_slow, e->scalars.p, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(e->scan_stats, e->scalars.p + 8, 16, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
   out->consumed_bytes = last_nl + 1;
+
+  // ---- pass C: per-line rule decisions; per-line fallback for rare lines
+  hipLaunchKernelGGL(k_resolve, dim3(grid_for(n_lines)), dim3(kBlock), 0, st, B, buf, e->nl.p, n_lines, L);
+  HIP_OK(hipGetLastError());
   if (n_slow) {
     hipLaunchKernelGGL(k_parse_match<true>, dim3(grid_for(n_slow)), dim3(kBlock), 0, st, B, buf, e->nl.p, (uint64_t)n_slow,
                        e->slow_list.p, now_ns, L, e->slow_list.p, e->scalars.p);
     HIP_OK(hipGetLastError());
   }
+  e->last_slow = n_slow;
+  mark(e, 3);
 
   // ---- RuleResults + events in reference order
   HIP_OK(hipMemsetAsync(e->l_counts.p + n_lines, 0, 8, st));
@@ -1312,6 +1755,7 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemsetAsync(e->rl_out.p, 0, n_res, st));
   }
+  mark(e, 4);
 
   // ---- rate limiting: group events per IP (stable), one thread per IP
   uint64_t n_trips = 0;
@@ -1322,6 +1766,7 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
         return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)n_ev, 0, 32, st);
       });
     }
+    mark(e, 5);
     e->head_flag.ensure(n_ev); e->heads.ensure(n_ev + 1); e->processed.ensure(n_ev);
     HIP_OK(hipMemsetAsync(e->scalars.p + 1, 0, 3 * 8, st));
     hipLaunchKernelGGL(k_heads, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_key2.p, e->ev_res2.p, e->res_seq.p,
@@ -1343,9 +1788,11 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
     if (n_seg == 0) throw BjxError(BJX_ERR_DEVICE, "internal: no event segments");
     ensure_capacity(e, sc[0] + 1024, sc[1] + 4096, n_ev);
     HIP_OK(hipMemsetAsync(e->processed.p, 0, n_ev, st));
+    mark(e, 6);
     hipLaunchKernelGGL(k_ratelimit, dim3(grid_for(n_seg)), dim3(kBlock), 0, st, n_seg, n_ev, e->heads.p, e->ev_res2.p,
                        e->res_seq.p, e->res_rule.p, e->nl.p, buf, L, B.rules, e->S, e->rl_out.p, e->processed.p);
     HIP_OK(hipGetLastError());
+    mark(e, 7);
     // trips in reference order
     e->trip_flag.ensure(n_res); e->trip_idx.ensure(n_res + 1);
     hipLaunchKernelGGL(k_flag_trips, dim3(grid_for(n_res)), dim3(kBlock), 0, st, n_res, e->rl_out.p, e->trip_flag.p);
@@ -1372,6 +1819,7 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
     }
   }
   HIP_OK(hipEventRecord(e->ev1, st));
+  mark(e, 8);
   if (flags & BJX_COPY_RESULTS) {
     hipLaunchKernelGGL(k_final_flags, dim3(grid_for(n_lines)), dim3(kBlock), 0, st, n_lines, e->l_flags.p);
     e->line_flags.resize(n_lines);
@@ -1390,6 +1838,16 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
   HIP_OK(hipEventElapsedTime(&mms, e->evm0, e->evm1));
   out->device_ms = ms;
   out->match_kernel_ms = mms;
+  for (int k = 0; k < bjx_engine::kPhases; ++k) {
+    e->phase_ms[k] = 0;
+    if (!e->phase_rec[k]) continue;
+    int j = k + 1;
+    while (j <= bjx_engine::kPhases && !e->phase_rec[j]) ++j;
+    if (j > bjx_engine::kPhases) continue;
+    float x = 0;
+    HIP_OK(hipEventElapsedTime(&x, e->ph[k], e->ph[j]));
+    e->phase_ms[k] = x;
+  }
   out->n_trips = n_trips;
   out->trips = e->trips.empty() ? nullptr : e->trips.data();
   out->results = e->results.empty() ? nullptr : e->results.data();
@@ -1518,6 +1976,17 @@ extern "C" size_t bjx_state_dump(bjx_engine *e, char *out, size_t cap) {
 extern "C" int bjx_debug_rule_match_host(const bjx_ruleset *rs, size_t i, const uint8_t *text, size_t n) {
   if (!rs || i >= rs->rules.size() || (n && !text)) return BJX_ERR_ARG;
   return dfa_match_host(rs->rules[i].rx, text, n) ? 1 : 0;
+}
+extern "C" size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap) {
+  if (!e) return 0;
+  for (size_t k = 0; k < cap && k < (size_t)bjx_engine::kPhases; ++k) out[k] = e->phase_ms[k];
+  return bjx_engine::kPhases;
+}
+extern "C" size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap) {
+  if (!e) return 0;
+  const uint64_t v[3] = {e->scan_stats[0], e->scan_stats[1], e->last_slow};
+  for (size_t k = 0; k < cap && k < 3; ++k) out[k] = v[k];
+  return 3;
 }
 extern "C" size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t i, char *out, size_t cap) {
   if (!rs || i >= rs->rules.size()) return 0;

@@ -15,11 +15,19 @@ struct DevRule {
   uint16_t flags;       // kRuleAlways / kRuleNever
   uint32_t name_id;     // engine-wide interned rule name (state key, rate_limit.go:54)
   int32_t decision;
-  int32_t lit_len;      // required literal (prefilter), 0 = none
-  uint32_t lit_off;
+  uint32_t lits_off;     // prefilter literal ids: rule_lits[lits_off .. + lits_len)
+  uint16_t lits_len;
+  uint8_t mode;          // RuleMode
+  uint8_t equiv;         // match <=> one of its literals occurs in rest
   int64_t interval_ns;
   int64_t hits;
 };
+
+// Prefilter gram bitset: one bit per hash of a 4-byte window (LDS resident).
+constexpr uint32_t kGramLog2 = 18;
+constexpr uint32_t kGramWords = (1u << kGramLog2) / 32;
+__host__ __device__ inline uint32_t gram_hash(uint32_t g) { return (g * 0x9E3779B1u) >> (32 - kGramLog2); }
+constexpr int kCandSlots = 4;
 
 struct Subnet {
   uint8_t net[16];
@@ -64,6 +72,21 @@ struct Bind {
   uint32_t n_scopes;
   uint32_t any_allow;
   uint32_t mask_words;         // ceil(max applicable rules per line / 64)
+  // prefilter
+  const uint32_t *gram_bits;   // kGramWords
+  const uint32_t *gt_key;      // open-addressing gram table (gt_mask + 1 slots)
+  const uint32_t *gt_off;      // entries offset (pairs lit, gram offset)
+  const uint32_t *gt_len;      // 0 = empty slot
+  const uint32_t *gt_entries;
+  const uint8_t *lit_bytes;
+  const uint8_t *lit_ci;
+  const uint32_t *lit_off;
+  const uint32_t *lit_len;
+  const uint32_t *rule_lits;
+  uint32_t gt_mask;
+  uint32_t n_lits;
+  uint32_t any_anchored;
+  uint32_t any_prefilter;
 };
 
 // Per-line SoA arrays (batch workspace).
@@ -75,6 +98,10 @@ struct Lines {
   uint8_t *flags;
   uint64_t *counts;    // (n_results << 32) | n_events per line, then scanned in place
   uint64_t *masks;     // mask_words per line
+  uint64_t *amask;     // anchored rules decided in the scan pass (positions < 64)
+  uint64_t *ares;      // anchored rules left unresolved by the scan pass
+  uint32_t *cand_cnt;  // prefilter candidates per line
+  uint64_t *cand;      // kCandSlots per line: (start position << 24) | literal id
 };
 
 // Persistent rate-limit state (RegexRateLimitStates, rate_limit.go:17-21),
@@ -96,8 +123,9 @@ struct State {
 
 enum LineFlagBits : uint8_t {
   kLineError = 1, kLineOld = 2, kLineExempt = 4,
-  kLineSlowTs = 0x40,     // timestamp needs the general ParseFloat kernel
+  kLineSlowTs = 0x40,     // per-line fallback kernel (timestamp / long header)
   kLineExemptPending = 0x20,
+  kLineAnchoredHigh = 0x10, // anchored rules at positions >= 64: resolve in k_resolve
 };
 
 }  // namespace bjx

@@ -763,62 +763,227 @@ class NfaBuilder {
 };
 
 // --------------------------------------------------- literal analysis
+//
+// Prefilter extraction (RE2-style "required literals"): for every node,
+// `exact` = the finite set of strings the node can match (when small), and
+// `req` = an OR-set such that every match contains one of its strings.  A
+// string is ASCII bytes with a per-byte case-insensitivity flag; runes whose
+// fold orbit leaves ASCII (k, s, non-ASCII) break strings, so an ASCII
+// case-insensitive compare is always a *necessary* condition for a match.
 
-struct LitInfo {
+struct LStr {
+  std::string s, ci;
+};
+using LSet = std::vector<LStr>;
+
+struct LInfo {
   bool exact = false;
-  std::string exact_s;  // valid if exact
-  std::string req;      // every match contains req
+  LSet ex;
+  bool pure = true;  // no empty-width assertions inside
+  bool has_req = false;
+  LSet req;
 };
 
-LitInfo lit_info(const Re *r) {
-  LitInfo o;
-  auto ascii_lit = [](const Re *x, char *c) {
-    if (x->op == kLit && !(x->flags & kFold) && x->rune < 0x80) { *c = static_cast<char>(x->rune); return true; }
-    if (x->op == kClass && x->cls.size() == 1 && x->cls[0].first == x->cls[0].second && x->cls[0].first < 0x80) {
-      *c = static_cast<char>(x->cls[0].first);
-      return true;
+constexpr size_t kMaxSet = 32, kMaxLen = 96;
+
+bool cross(const LSet &a, const LSet &b, LSet *out) {
+  if (a.size() * b.size() > kMaxSet) return false;
+  LSet o;
+  for (auto &x : a)
+    for (auto &y : b) {
+      if (x.s.size() + y.s.size() > kMaxLen) return false;
+      o.push_back({x.s + y.s, x.ci + y.ci});
     }
-    return false;
+  *out = std::move(o);
+  return true;
+}
+
+bool nonempty_all(const LSet &s) {
+  if (s.empty()) return false;
+  for (auto &x : s)
+    if (x.s.empty()) return false;
+  return true;
+}
+
+int byte_weight(unsigned char c) {
+  static const char *common = "etaoinsrhldcumwfgypbvkxjqz";
+  if (c >= 'a' && c <= 'z') {
+    const char *p = strchr(common, c);
+    return 26 - (int)(p - common);
+  }
+  if (c >= 'A' && c <= 'Z') return strchr("GETPOSHTML", c) ? 12 : 6;
+  if (c >= '0' && c <= '9') return 10;
+  switch (c) {
+    case ' ': return 30;
+    case '/': case '.': return 20;
+    case ':': case '|': return 10;
+    case '-': case ';': case '(': case ')': case ',': return 8;
+    default: return 4;
+  }
+}
+
+// lower = rarer; windows over case-insensitive bytes cost their variants
+int window_score(const LStr &l, size_t o) {
+  int sc = 0, ci = 0;
+  for (size_t i = o; i < o + 4; ++i) {
+    unsigned char c = (unsigned char)l.s[i];
+    sc += byte_weight(l.ci[i] ? (unsigned char)(c | 0x20) : c);
+    ci += l.ci[i] ? 1 : 0;
+  }
+  return sc + 3 * ci;
+}
+
+int string_score(const LStr &l) {
+  if (l.s.size() < 4) return 1 << 20;
+  int best = 1 << 20;
+  for (size_t o = 0; o + 4 <= l.s.size(); ++o) best = std::min(best, window_score(l, o));
+  return best;
+}
+
+// score of an OR-set: the worst member dominates (every member is probed)
+int set_score(const LSet &s) {
+  if (!nonempty_all(s)) return 1 << 22;
+  int worst = 0;
+  for (auto &x : s) worst = std::max(worst, string_score(x));
+  return worst + 2 * (int)s.size();
+}
+
+void consider(LInfo &o, const LSet &cand) {
+  if (!nonempty_all(cand)) return;
+  if (!o.has_req || set_score(cand) < set_score(o.req)) {
+    o.req = cand;
+    o.has_req = true;
+  }
+}
+
+bool lit_char(const Re *x, LStr *out) {
+  auto cs = [&](int32_t r) {
+    out->s = std::string(1, (char)r);
+    out->ci = std::string(1, '\0');
+    return true;
   };
-  char c;
-  if (ascii_lit(r, &c)) { o.exact = true; o.exact_s = std::string(1, c); o.req = o.exact_s; return o; }
+  auto ci_letter = [&](int32_t r) {
+    int32_t lo = r | 0x20;
+    if (lo == 'k' || lo == 's') return false;  // folds to U+212A / U+017F
+    out->s = std::string(1, (char)lo);
+    out->ci = std::string(1, '\1');
+    return true;
+  };
+  auto is_letter = [](int32_t r) { return (r >= 'a' && r <= 'z') || (r >= 'A' && r <= 'Z'); };
+  if (x->op == kLit) {
+    if (x->rune >= 0x80) return false;
+    if ((x->flags & kFold) && is_letter(x->rune)) return ci_letter(x->rune);
+    return cs(x->rune);
+  }
+  if (x->op == kClass) {
+    const Ranges &c = x->cls;
+    if (c.size() == 1 && c[0].first == c[0].second && c[0].first < 0x80) return cs(c[0].first);
+    if (c.size() == 2 && c[0].first == c[0].second && c[1].first == c[1].second && c[1].first < 0x80 &&
+        is_letter(c[0].first) && (c[0].first | 0x20) == c[1].first && c[1].first - c[0].first == 0x20)
+      return ci_letter(c[0].first);
+  }
+  return false;
+}
+
+LInfo analyze(const Re *r) {
+  LInfo o;
+  LStr ch;
+  if (lit_char(r, &ch)) {
+    o.exact = true;
+    o.ex = {ch};
+    o.has_req = true;
+    o.req = o.ex;
+    return o;
+  }
   switch (r->op) {
-    case kEmpty: case kBOL: case kEOL: case kBOT: case kEOT: case kWB: case kNWB:
+    case kEmpty:
       o.exact = true;
+      o.ex = {LStr{}};
       return o;
-    case kCap: return lit_info(r->sub[0].get());
-    case kPlus: { LitInfo s = lit_info(r->sub[0].get()); o.req = s.req; return o; }
+    case kBOL: case kEOL: case kBOT: case kEOT: case kWB: case kNWB:
+      o.exact = true;
+      o.ex = {LStr{}};
+      o.pure = false;
+      return o;
+    case kCap: return analyze(r->sub[0].get());
+    case kPlus: {
+      LInfo c = analyze(r->sub[0].get());
+      if (c.exact && nonempty_all(c.ex)) consider(o, c.ex);
+      if (c.has_req) consider(o, c.req);
+      o.pure = c.pure;
+      return o;
+    }
     case kRepeat: {
-      LitInfo s = lit_info(r->sub[0].get());
-      if (r->min >= 1) o.req = s.req;
-      if (s.exact && r->min == r->max && s.exact_s.size() * static_cast<size_t>(r->min) <= 256) {
-        o.exact = true;
-        for (int i = 0; i < r->min; ++i) o.exact_s += s.exact_s;
-        if (o.exact_s.size() > o.req.size()) o.req = o.exact_s;
+      LInfo c = analyze(r->sub[0].get());
+      o.pure = c.pure;
+      if (r->min < 1) return o;
+      if (c.exact && nonempty_all(c.ex)) consider(o, c.ex);
+      if (c.has_req) consider(o, c.req);
+      if (c.exact && r->min == r->max) {
+        LSet acc{LStr{}};
+        bool ok = true;
+        for (int i = 0; i < r->min && ok; ++i) ok = cross(acc, c.ex, &acc);
+        if (ok) {
+          o.exact = true;
+          o.ex = acc;
+          consider(o, acc);
+        }
       }
       return o;
     }
     case kConcat: {
-      std::string run;
-      bool all_exact = true;
-      std::string all;
-      for (auto &s : r->sub) {
-        LitInfo si = lit_info(s.get());
-        if (si.exact) {
-          run += si.exact_s;
-          all += si.exact_s;
+      LSet run{LStr{}};
+      bool all_exact = true, run_ok = true;
+      LSet full{LStr{}};
+      for (auto &sp : r->sub) {
+        LInfo c = analyze(sp.get());
+        o.pure = o.pure && c.pure;
+        if (c.exact) {
+          LSet nr;
+          if (run_ok && cross(run, c.ex, &nr)) run = std::move(nr);
+          else {
+            consider(o, run);
+            run = c.ex;
+            run_ok = true;
+          }
+          if (all_exact && !cross(full, c.ex, &full)) all_exact = false;
         } else {
           all_exact = false;
-          if (run.size() > o.req.size()) o.req = run;
-          run.clear();
+          consider(o, run);
+          run = {LStr{}};
+          if (c.has_req) consider(o, c.req);
         }
-        if (si.req.size() > o.req.size()) o.req = si.req;
       }
-      if (run.size() > o.req.size()) o.req = run;
-      if (all_exact) { o.exact = true; o.exact_s = all; }
+      consider(o, run);
+      if (all_exact) {
+        o.exact = true;
+        o.ex = full;
+      }
       return o;
     }
-    default: return o;
+    case kAlt: {
+      bool all_exact = true, all_req = true;
+      LSet ex, req;
+      for (auto &sp : r->sub) {
+        LInfo c = analyze(sp.get());
+        o.pure = o.pure && c.pure;
+        if (c.exact) ex.insert(ex.end(), c.ex.begin(), c.ex.end());
+        else all_exact = false;
+        const LSet *best = nullptr;
+        if (c.exact && nonempty_all(c.ex)) best = &c.ex;
+        if (c.has_req && (!best || set_score(c.req) < set_score(*best))) best = &c.req;
+        if (best) req.insert(req.end(), best->begin(), best->end());
+        else all_req = false;
+      }
+      if (all_exact && ex.size() <= kMaxSet) {
+        o.exact = true;
+        o.ex = ex;
+      }
+      if (all_req && req.size() <= kMaxSet) consider(o, req);
+      return o;
+    }
+    default:
+      return o;
   }
 }
 
@@ -826,30 +991,42 @@ bool is_dotstar(const Re *r) {
   return r->op == kStar && (r->sub[0]->op == kAnyNotNL || r->sub[0]->op == kAnyChar);
 }
 
-// match <=> contains L when the pattern is (.*)* L (.*)* with L exact ASCII
-bool literal_equivalent(const Re *r, const std::string &lit) {
+// Anchored at rest[0]: the pattern begins with \A / ^ (OneLine).
+bool anchored_start(const Re *r) {
   while (r->op == kCap) r = r->sub[0].get();
-  if (lit.empty()) return false;
+  if (r->op == kBOT) return true;
+  if (r->op == kConcat && !r->sub.empty()) return anchored_start(r->sub[0].get());
+  return false;
+}
+
+// match <=> text contains one of S, when the pattern is (.*)* X (.*)* with X
+// pure and exact (S = X's strings), since .* can always match empty.
+bool prefilter_equivalent(const Re *r, const LSet &chosen) {
+  while (r->op == kCap) r = r->sub[0].get();
+  LSet x;
   if (r->op != kConcat) {
-    LitInfo li = lit_info(r);
-    return li.exact && li.exact_s == lit && r->op != kBOT;
+    LInfo li = analyze(r);
+    if (!li.exact || !li.pure) return false;
+    x = li.ex;
+  } else {
+    size_t i = 0, n = r->sub.size();
+    while (i < n && is_dotstar(r->sub[i].get())) ++i;
+    size_t j = n;
+    while (j > i && is_dotstar(r->sub[j - 1].get())) --j;
+    x = {LStr{}};
+    for (size_t k = i; k < j; ++k) {
+      LInfo li = analyze(r->sub[k].get());
+      if (!li.exact || !li.pure || !cross(x, li.ex, &x)) return false;
+    }
   }
-  size_t i = 0, n = r->sub.size();
-  while (i < n && is_dotstar(r->sub[i].get())) ++i;
-  std::string mid;
-  size_t j = i;
-  for (; j < n; ++j) {
-    const Re *x = r->sub[j].get();
-    if (is_dotstar(x)) break;
-    LitInfo li = lit_info(x);
-    if (!li.exact) return false;
-    // assertions inside would change meaning
-    if (x->op == kBOL || x->op == kEOL || x->op == kBOT || x->op == kEOT || x->op == kWB || x->op == kNWB) return false;
-    mid += li.exact_s;
-  }
-  for (; j < n; ++j)
-    if (!is_dotstar(r->sub[j].get())) return false;
-  return mid == lit;
+  if (!nonempty_all(x) || x.size() != chosen.size()) return false;
+  auto key = [](const LSet &s) {
+    std::vector<std::string> v;
+    for (auto &e : s) v.push_back(e.s + '\0' + e.ci);
+    std::sort(v.begin(), v.end());
+    return v;
+  };
+  return key(x) == key(chosen);
 }
 
 // ------------------------------------------------------------------ DFA
@@ -1192,9 +1369,32 @@ int compile_regex(const std::string &pattern, CompiledRegex *out, std::string *e
     if (err) *err = "rule too complex for the DFA engine (state or class limit)";
     return rc;
   }
-  LitInfo li = lit_info(root.get());
-  out->required_literal = li.req;
-  out->literal_equivalent = literal_equivalent(root.get(), li.req);
+  if (out->flags & kRuleAlways) out->mode = kModeAlways;
+  else if (out->flags & kRuleNever) out->mode = kModeNever;
+  else if (anchored_start(root.get())) out->mode = kModeAnchored;
+  else {
+    LInfo li = analyze(root.get());
+    LSet best;
+    bool have = false;
+    if (li.exact && nonempty_all(li.ex)) { best = li.ex; have = true; }
+    if (li.has_req && (!have || set_score(li.req) < set_score(best))) { best = li.req; have = true; }
+    if (have && set_score(best) < (1 << 20)) {
+      out->mode = kModePrefilter;
+      for (auto &x : best) {
+        PrefLit pl{x.s, x.ci, 0};
+        int bs = 1 << 30;
+        for (size_t o = 0; o + 4 <= x.s.size(); ++o) {
+          int sc = window_score(x, o);
+          if (sc < bs) { bs = sc; pl.gram_off = (uint32_t)o; }
+        }
+        out->pref.push_back(pl);
+      }
+      out->pref_equivalent = prefilter_equivalent(root.get(), best);
+      out->required_literal = best[0].s;
+    } else {
+      out->mode = kModeScan;
+    }
+  }
   return 0;
 }
 

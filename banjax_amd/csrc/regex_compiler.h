@@ -19,6 +19,24 @@ enum RuleFlags : uint32_t {
   kRuleNever = 2,   // matches nothing
 };
 
+// How the device decides a rule on a line.
+enum RuleMode : uint8_t {
+  kModeAlways = 0,     // matches every text
+  kModeNever = 1,      // matches nothing
+  kModeAnchored = 2,   // every match starts at rest[0]: DFA from the start, dies early
+  kModePrefilter = 3,  // every match contains one of `pref` literals: candidates from the
+                       // byte-parallel gram filter, then literal check (+ DFA unless equivalent)
+  kModeScan = 4,       // no usable literal: full DFA scan of rest
+};
+
+// A prefilter literal: ASCII bytes; ci[i] = 1 if byte i matches ASCII-case-insensitively
+// (only letters whose Go simple-fold orbit is ASCII-only, i.e. not k or s).
+struct PrefLit {
+  std::string s;
+  std::string ci;
+  uint32_t gram_off = 0;  // start of the 4-byte window probed by the gram filter
+};
+
 struct CompiledRegex {
   uint32_t nstates = 0;  // including DEAD and ACCEPT
   uint32_t ncls = 0;     // rune classes
@@ -29,10 +47,11 @@ struct CompiledRegex {
   uint8_t ascii_cls[128] = {};      // rune < 0x80 -> class
   // rune >= 0x80: sorted (lo, class) interval starts covering [0x80, 0x10FFFF]
   std::vector<std::pair<uint32_t, uint32_t>> nonascii;
-  // Longest literal every match must contain (byte string, case-sensitive), or
-  // empty; used by the device prefilter.  Only set when the literal is pure ASCII.
-  std::string required_literal;
-  bool literal_equivalent = false;  // match <=> text contains required_literal
+  RuleMode mode = kModeScan;
+  // every match contains at least one of these (kModePrefilter); each >= 4 bytes
+  std::vector<PrefLit> pref;
+  bool pref_equivalent = false;  // match <=> text contains one of `pref`
+  std::string required_literal;  // diagnostics: the first prefilter literal
 };
 
 // Returns 0 on success; otherwise a negative bjx_status with *err set to the

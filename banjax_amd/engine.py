@@ -75,6 +75,18 @@ class Engine:
         self._check(rc, "process_batch")
         return BatchOutput(res, copy_results)
 
+    PHASES = ("count", "scan", "resolve", "emit", "event_sort", "segment", "rate_limit", "trips")
+
+    def scan_stats(self):
+        out = (C.c_uint64 * 3)()
+        _lib.lib().bjx_debug_scan_stats(self._h, out, 3)
+        return {"gram_probes": out[0], "candidates": out[1], "fallback_lines": out[2]}
+
+    def phase_ms(self):
+        out = (C.c_double * 8)()
+        _lib.lib().bjx_debug_phase_ms(self._h, out, 8)
+        return {k: round(out[i], 3) for i, k in enumerate(self.PHASES)}
+
     def state_get(self, ip, name):
         hits, start = C.c_int64(), C.c_int64()
         ipb, nb = _lib.b(ip), _lib.b(name)

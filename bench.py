@@ -100,6 +100,7 @@ def main():
     match_ms = sum(o.match_kernel_ms for o in outs) / len(outs)
     dev_ms = sum(o.device_ms for o in outs) / len(outs)
     o = outs[-1]
+    phases = eng.phase_ms()
     total_lines = n_lines * world
     value = total_lines / (elapsed / args.steps)
     achieved = nbytes / (match_ms / 1000.0) / 1e9
@@ -127,6 +128,7 @@ def main():
                 "rate_limit_events_per_step": o.n_events,
                 "trips_per_step": o.n_trips,
                 "device_ms_per_step": round(dev_ms, 3),
+                "phase_ms_last_step": phases,
                 "parallelism": "dp%d: chunk-sharded lines" % world,
             },
             "roofline": {

@@ -18,6 +18,11 @@ extern "C" {
 int bjx_debug_rule_match_host(const bjx_ruleset *rs, size_t rule_idx, const uint8_t *text, size_t n);
 /* required literal the prefilter uses for a rule (bytes written, full length returned) */
 size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t rule_idx, char *out, size_t cap);
+/* device ms of the last batch's phases: framing, match, slow timestamps, emit,
+   event sort, segmenting, rate limit, trips (returns the phase count) */
+size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap);
+/* last batch: gram-table probes, literal candidates, lines sent to the per-line fallback */
+size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap);
 #ifdef __cplusplus
 }
 #endif

@@ -41,7 +41,8 @@ class Pair:
         self.n_rules = len(self.cfg.all_rules())
 
     def feed(self, data: bytes, now_ns: int, check=True):
-        oflags, ores, oconsumed = self.ost.consume(self.ocfg, data, now_ns)
+        oflags, ores, oconsumed = self.ost.consume(self.ocfg, data, now_ns,
+                                                   cap=(data.count(b"\n") + 1) * (self.n_rules + 1))
         results, out = self.lim.consume_lines(data, now_ns, want_results=True)
         if check:
             compare_batch(oflags, ores, oconsumed, out)

@@ -92,10 +92,10 @@ class Workload:
         return t, int(need)
 
     def now_ns(self, first_line=0, n_lines=None) -> int:
-        """Injected clock: the batch's last timestamp (OldLine never fires)."""
-        n = self.n_lines if n_lines is None else n_lines
-        last = first_line + max(n - 1, 0)
-        return (T0_MS * 1000 + last * self.us_per_line) // 1000 * 1_000_000
+        """Injected clock (time.Now() of consumeLine): the batch's first timestamp,
+        so no line is more than 10 s old and OldLine never fires; later lines are
+        in the future, as in the reference's own tests."""
+        return (T0_MS * 1000 + first_line * self.us_per_line) // 1000 * 1_000_000
 
 
 # --------------------------------------------------------------- rule sets
