@@ -82,6 +82,13 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise BanjaxGpuError(ERR_DEVICE, "libbanjax_gpu.so not built (run __graft_entry__.build()); "
                                          "there is no CPU fallback")
+    # torch wheels bundle their own libamdhip64.so.7 (same soname as
+    # /opt/rocm's): load torch first so the process has ONE HIP runtime and
+    # device buffers/streams pass freely between torch and the engine.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, sz = C.c_void_p, C.c_size_t
     L.bjx_abi_version.restype = C.c_int

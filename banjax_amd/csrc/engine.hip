@@ -479,6 +479,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(Bind B, ScanArgs A) {
   typedef hipcub::BlockScan<uint32_t, kBlock> BS;
   __shared__ typename BS::TempStorage scan_tmp;
   const uint32_t tid = threadIdx.x;
+  uint32_t n_probe = 0, n_cand = 0;  // per-lane stats, one atomic per wave at the end
   if (B.any_prefilter)
     for (uint32_t i = tid; i < kGramWords; i += kBlock) s_bits[i] = B.gram_bits[i];
   for (uint64_t t = blockIdx.x; t < A.n_tiles; t += gridDim.x) {
@@ -575,7 +576,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(Bind B, ScanArgs A) {
       const int32_t l0 = (int32_t)(tid * 32u) + k - 3;
       const uint32_t g = (uint32_t)tile_byte(s_tile, l0, s_prev) | (uint32_t)tile_byte(s_tile, l0 + 1, s_prev) << 8 |
                          (uint32_t)tile_byte(s_tile, l0 + 2, s_prev) << 16 | (uint32_t)tile_byte(s_tile, l0 + 3, s_prev) << 24;
-      atomicAdd(&A.stats[0], 1ull);
+      ++n_probe;
       uint32_t slot = (uint32_t)mix64(g) & B.gt_mask;
       while (B.gt_len[slot] && B.gt_key[slot] != g) slot = (slot + 1) & B.gt_mask;
       if (!B.gt_len[slot]) continue;
@@ -587,10 +588,18 @@ __global__ __launch_bounds__(kBlock) void k_scan(Bind B, ScanArgs A) {
         const int64_t q = gpos - (int64_t)B.gt_entries[2 * (B.gt_off[slot] + e) + 1];
         if (q < 0) continue;
         const uint32_t c = atomicAdd(&A.L.cand_cnt[line], 1u);
-        atomicAdd(&A.stats[1], 1ull);
+        ++n_cand;
         if (c < kCandSlots) A.L.cand[line * kCandSlots + c] = ((uint64_t)q << 24) | lit;
       }
     }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    n_probe += __shfl_xor(n_probe, o);
+    n_cand += __shfl_xor(n_cand, o);
+  }
+  if ((tid & 63) == 0 && (n_probe | n_cand)) {
+    atomicAdd(&A.stats[0], (unsigned long long)n_probe);
+    atomicAdd(&A.stats[1], (unsigned long long)n_cand);
   }
 }
 
@@ -951,6 +960,33 @@ struct DevBuf {
   }
 };
 
+// Pinned host array for batch outputs (D2H at full PCIe rate, no zero-fill).
+template <typename T>
+struct HostBuf {
+  T *p = nullptr;
+  size_t n = 0, cap = 0;
+  void resize(size_t want) {
+    if (want > cap) {
+      if (p) (void)hipHostFree(p);
+      p = nullptr;
+      cap = 0;
+      const size_t c = want < 1024 ? 1024 : want + want / 4;
+      HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&p), c * sizeof(T), hipHostMallocDefault));
+      cap = c;
+    }
+    n = want;
+  }
+  void clear() { n = 0; }
+  bool empty() const { return n == 0; }
+  T *data() { return p; }
+  size_t size() const { return n; }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = cap = 0;
+  }
+};
+
 inline unsigned grid_for(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 uint64_t next_pow2(uint64_t x) {
@@ -1113,9 +1149,9 @@ struct bjx_engine {
   DevBuf<uint8_t> q_ip;
 
   // host copies of the last batch
-  std::vector<bjx_trip> trips;
-  std::vector<bjx_rule_result> results;
-  std::vector<uint8_t> line_flags;
+  HostBuf<bjx_trip> trips;
+  HostBuf<bjx_rule_result> results;
+  HostBuf<uint8_t> line_flags;
 };
 
 namespace {
@@ -1201,7 +1237,65 @@ bool parse_allow_entry(const std::string &s, std::vector<std::array<uint8_t, 16>
   return false;
 }
 
-void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs) {
+// 4-byte value of literal window [o, o+4) in ASCII-case variant v (bit k set =
+// upper-case byte k); false if v flips a case-sensitive byte.
+static bool window_variant(const uint8_t *s, const uint8_t *ci, uint32_t v, uint32_t *g) {
+  uint32_t x = 0;
+  for (int k = 0; k < 4; ++k) {
+    uint8_t c = s[k];
+    if (ci[k]) c = ((v >> k) & 1) ? (uint8_t)(c & ~0x20) : c;
+    else if ((v >> k) & 1) return false;
+    x |= (uint32_t)c << (8 * k);
+  }
+  *g = x;
+  return true;
+}
+
+// Gram calibration: for each literal pick the 4-byte window (all its ASCII-case
+// variants) that occurs least often in a sample of the traffic being bound,
+// ties going to the compiler's static choice.  Any window of a literal is a
+// necessary condition for it, so the choice changes speed, never results.
+static void calibrate_grams(const std::vector<uint8_t> &lit_bytes, const std::vector<uint8_t> &lit_ci,
+                            const std::vector<uint32_t> &lit_off, const std::vector<uint32_t> &lit_len,
+                            std::vector<uint32_t> &lit_gram, const uint8_t *sample, size_t n) {
+  if (n < 4 || lit_off.empty()) return;
+  std::unordered_map<uint32_t, uint32_t> cnt;
+  std::vector<uint64_t> seen(1u << 14, 0);  // 2^20-bit presence filter
+  auto fh = [](uint32_t g) { return (g * 0x9E3779B1u) >> 12; };
+  for (size_t id = 0; id < lit_off.size(); ++id)
+    for (uint32_t o = 0; o + 4 <= lit_len[id]; ++o)
+      for (uint32_t v = 0; v < 16; ++v) {
+        uint32_t g;
+        if (!window_variant(&lit_bytes[lit_off[id] + o], &lit_ci[lit_off[id] + o], v, &g)) continue;
+        cnt.emplace(g, 0);
+        seen[fh(g) >> 6] |= 1ull << (fh(g) & 63);
+      }
+  uint32_t g = 0;
+  for (size_t i = 0; i < n; ++i) {
+    g = (g >> 8) | ((uint32_t)sample[i] << 24);
+    if (i < 3) continue;
+    const uint32_t h = fh(g);
+    if (!((seen[h >> 6] >> (h & 63)) & 1)) continue;
+    auto it = cnt.find(g);
+    if (it != cnt.end()) ++it->second;
+  }
+  for (size_t id = 0; id < lit_off.size(); ++id) {
+    uint64_t best = ~0ull;
+    uint32_t best_o = lit_gram[id];
+    for (uint32_t o = 0; o + 4 <= lit_len[id]; ++o) {
+      uint64_t c = 0;
+      for (uint32_t v = 0; v < 16; ++v) {
+        uint32_t x;
+        if (window_variant(&lit_bytes[lit_off[id] + o], &lit_ci[lit_off[id] + o], v, &x)) c += cnt[x];
+      }
+      c = 2 * c + (o == lit_gram[id] ? 0 : 1);
+      if (c < best) { best = c; best_o = o; }
+    }
+    lit_gram[id] = best_o;
+  }
+}
+
+void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, size_t sample_n) {
   if (e->bound_uid == rs->uid && e->bound_dec_version == e->decisions_version) return;
   // host dictionary: per-site hosts, skip hosts, allow-list sites
   std::map<std::string, uint32_t> hosts;
@@ -1280,21 +1374,15 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs) {
     d.interval_ns = r.interval_ns;
     d.hits = r.hits;
   }
+  calibrate_grams(lit_bytes, lit_ci, lit_off, lit_len, lit_gram, sample, sample_n);
   // gram filter: each literal's chosen 4-byte window, every ASCII case variant
   // of its case-insensitive bytes, -> bitset bit + exact table entry
   std::map<uint32_t, std::vector<std::pair<uint32_t, uint32_t>>> gmap;
   for (uint32_t id = 0; id < lit_off.size(); ++id) {
     const uint32_t o = lit_off[id] + lit_gram[id];
     for (uint32_t v = 0; v < 16; ++v) {
-      uint32_t g = 0;
-      bool ok = true;
-      for (int k = 0; k < 4; ++k) {
-        uint8_t c = lit_bytes[o + k];
-        if (lit_ci[o + k]) c = ((v >> k) & 1) ? (uint8_t)(c & ~0x20) : c;
-        else if ((v >> k) & 1) ok = false;
-        g |= (uint32_t)c << (8 * k);
-      }
-      if (ok) gmap[g].push_back({id, lit_gram[id]});
+      uint32_t g;
+      if (window_variant(&lit_bytes[o], &lit_ci[o], v, &g)) gmap[g].push_back({id, lit_gram[id]});
     }
   }
   std::vector<uint32_t> gram_bits(kGramWords, 0);
@@ -1599,6 +1687,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   (void)hipSetDevice(e->device);
   (void)hipStreamSynchronize(e->stream);
   free_state(e);
+  e->trips.release(); e->results.release(); e->line_flags.release();
   for (auto *b : {&e->staging, &e->l_flags, &e->head_flag, &e->rl_out, &e->processed, &e->trip_flag, &e->bind_blob,
                   &e->cub_tmp, &e->q_ip})
     b->release();
@@ -1645,7 +1734,18 @@ static void mark(bjx_engine *e, int k) {
 static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns, uint32_t flags,
                       bjx_batch_result *out) {
   HIP_OK(hipSetDevice(e->device));
-  bind_ruleset(e, rs);
+  if (e->bound_uid != rs->uid || e->bound_dec_version != e->decisions_version) {
+    // (re)binding: calibrate the gram filter on the head of this batch
+    const size_t sn = std::min<size_t>(n, 4u << 20);
+    std::vector<uint8_t> sample;
+    const uint8_t *sp = bytes;
+    if (flags & BJX_INPUT_DEVICE) {
+      sample.resize(sn);
+      if (sn) HIP_OK(hipMemcpy(sample.data(), bytes, sn, hipMemcpyDeviceToHost));
+      sp = sample.data();
+    }
+    bind_ruleset(e, rs, sp, sn);
+  }
   const Bind &B = e->bind;
   hipStream_t st = e->stream;
   memset(out, 0, sizeof *out);
@@ -1990,7 +2090,14 @@ extern "C" size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap)
 }
 extern "C" size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t i, char *out, size_t cap) {
   if (!rs || i >= rs->rules.size()) return 0;
-  const std::string &l = rs->rules[i].rx.required_literal;
+  // "<mode> <equiv>" then per literal "\n<gram_off> <ci mask as 0/1> <bytes>"
+  const CompiledRegex &rx = rs->rules[i].rx;
+  std::string l = std::to_string((int)rx.mode) + " " + std::to_string((int)rx.pref_equivalent);
+  for (const PrefLit &pl : rx.pref) {
+    l += "\n" + std::to_string(pl.gram_off) + " ";
+    for (char c : pl.ci) l += c ? '1' : '0';
+    l += " " + pl.s;
+  }
   if (out && cap) memcpy(out, l.data(), std::min(cap, l.size()));
   return l.size();
 }

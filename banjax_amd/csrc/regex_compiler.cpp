@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <strings.h>
 #include <map>
 #include <memory>
 #include <unordered_map>
@@ -811,7 +812,7 @@ int byte_weight(unsigned char c) {
     const char *p = strchr(common, c);
     return 26 - (int)(p - common);
   }
-  if (c >= 'A' && c <= 'Z') return strchr("GETPOSHTML", c) ? 12 : 6;
+  if (c >= 'A' && c <= 'Z') return strchr("GETPOSHTML", c) ? 24 : 6;
   if (c >= '0' && c <= '9') return 10;
   switch (c) {
     case ' ': return 30;
@@ -822,8 +823,22 @@ int byte_weight(unsigned char c) {
   }
 }
 
+// 4-grams present in nearly every access-log line (method, protocol, common
+// host / user-agent tokens): a window equal to one of these is never chosen
+// while a rarer one exists.
+bool common_log_gram(const char *g) {
+  static const char *kCommon[] = {"GET ", "POST", "OST ", "HTTP", "TTP/", "TP/1", "P/1.", "/1.1", "/2.0", "P/2.",
+                                  "HEAD", "EAD ", ".com", "www.", "Mozi", "ozil", "zill", "illa", "lla/", "a/5.",
+                                  "/5.0", ".php", "html", ".htm", "http", "ttp:", "tp:/", "p://", "://w", "//ww",
+                                  "/ww.", "Wind", "indo", "ndow", "dows", "Geck", "ecko", "Appl", "pple", "ebKi"};
+  for (const char *c : kCommon)
+    if (strncasecmp(c, g, 4) == 0) return true;
+  return false;
+}
+
 // lower = rarer; windows over case-insensitive bytes cost their variants
 int window_score(const LStr &l, size_t o) {
+  if (common_log_gram(l.s.data() + o)) return 1000;
   int sc = 0, ci = 0;
   for (size_t i = o; i < o + 4; ++i) {
     unsigned char c = (unsigned char)l.s[i];

@@ -10,7 +10,10 @@ from .config import Config, Ruleset
 
 
 class BatchOutput:
-    """Host view of one bjx_process_batch."""
+    """Host view of one bjx_process_batch.  The arrays live in engine-owned
+    pinned memory valid until the next process(); `trips` / `results` are
+    materialized as Python records only when read (trips_array() gives the
+    zero-copy numpy view the Banner replay iterates)."""
 
     def __init__(self, res: _lib.BatchResult, copy_results: bool):
         self.n_lines = res.n_lines
@@ -20,13 +23,33 @@ class BatchOutput:
         self.n_trips = res.n_trips
         self.device_ms = res.device_ms
         self.match_kernel_ms = res.match_kernel_ms
-        self.trips = [res.trips[i] for i in range(res.n_trips)] if res.n_trips else []
-        if copy_results:
-            self.line_flags = bytes(C.string_at(res.line_flags, res.n_lines)) if res.n_lines else b""
-            self.results = [res.results[i] for i in range(res.n_results)] if res.n_results else []
-        else:
-            self.line_flags = None
-            self.results = None
+        self._res = res
+        self._trips = None
+        self._results = None
+        self._copy = copy_results
+        self.line_flags = (bytes(C.string_at(res.line_flags, res.n_lines)) if res.n_lines else b"") \
+            if copy_results else None
+
+    @property
+    def trips(self):
+        if self._trips is None:
+            self._trips = [self._res.trips[i] for i in range(self.n_trips)] if self.n_trips else []
+        return self._trips
+
+    def trips_array(self):
+        import numpy as np
+        if not self.n_trips:
+            return np.zeros(0, dtype=np.dtype(_lib.Trip))
+        buf = (_lib.Trip * self.n_trips).from_address(C.addressof(self._res.trips.contents))
+        return np.ctypeslib.as_array(buf)
+
+    @property
+    def results(self):
+        if not self._copy:
+            return None
+        if self._results is None:
+            self._results = [self._res.results[i] for i in range(self.n_results)] if self.n_results else []
+        return self._results
 
 
 class Engine:
