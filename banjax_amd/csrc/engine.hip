@@ -22,6 +22,7 @@
 #include <array>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -348,333 +349,619 @@ __global__ __launch_bounds__(kBlock) void k_parse_match(Bind B, const uint8_t *_
 }
 
 // =====================================================================
-//   v2 pipeline: byte-parallel scan pass + per-line resolve pass
+//   match pipeline: wave-tiled scan pass (+ long-line resolve)
 // =====================================================================
+//
+// Every wave owns 4 KB tiles of the batch (64 lanes x 64 B, coalesced 16 B
+// loads, next tile prefetched into registers) plus a 512 B halo, staged in a
+// wave-private LDS region; no block barrier after the table preload, so a
+// wave busy with per-line work never stalls the others.  Per tile:
+//   1. '\n' bitmasks -> line positions (nl[]) and the lines that START in the
+//      tile (their ends in the tile or the halo),
+//   2. 4-byte gram of every position -> LDS bitset -> exact gram table (LDS)
+//      -> literal verified against the LDS bytes -> per-line hit slots (LDS);
+//      hits on lines that do not fit the window go to global slots,
+//   3. one lane per line: header (SplitN x2, ParseFloat fast path), host
+//      lookup, CheckIsAllowed, OldLine, then the applicable rules decided from
+//      the per-host ALWAYS mask, the anchored / no-literal rules' DFAs and the
+//      rules required by the line's verified literals (DFA only when the
+//      literal is not sufficient).
+// Lines that cannot be decided in the window (longer than the halo, more than
+// kLineCap lines in a tile, header past the window, exotic timestamp, more
+// than 128 applicable rules) go to k_resolve_long or the per-line fallback.
 
-constexpr uint32_t kScanTile = 8192;  // 256 lanes x 32 B
-constexpr uint32_t kScanHalo = 512;   // bytes past the tile kept for headers / anchored rules
+constexpr uint32_t kWT = 4096;        // bytes per wave tile
+constexpr uint32_t kHalo = 512;
+constexpr uint32_t kLineCap = 128;    // lines starting in one tile decided from LDS
+constexpr uint32_t kHitSlots = 4;     // verified literal hits kept per line
+constexpr int kScanWaves = 16;        // waves per block (one block per CU)
+constexpr uint32_t kTileLds = kWT + kHalo + 16;
+constexpr uint32_t kWaveJobs = 64;   // DFA jobs staged per wave before one global append
+constexpr uint32_t kWaveLds = kTileLds + kLineCap * (2 + 2 + 4 + 4 * kHitSlots) + kWaveJobs * 8 + 16;
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kScanLdsMax = 160 * 1024;  // gfx950 LDS per CU (one scan block per CU)
 
 struct ScanArgs {
   const uint8_t *buf;
   uint64_t n;
   uint64_t n_tiles;
   uint64_t n_lines;
-  const uint64_t *tile_base;  // newlines before each 8 KB tile (pass A)
+  const uint64_t *tile_base;  // newlines before each wave tile (pass A)
   uint64_t *nl;
   Lines L;
   int64_t now_ns;
   uint32_t *slow_list;
   unsigned long long *slow_count;
-  unsigned long long *stats;  // [0] gram-table probes, [1] candidates
+  uint32_t *long_list;
+  unsigned long long *long_count;
+  unsigned long long *stats;  // [0] bitset hits, [1] recorded literal hits
+  uint2 *jobs;                // DFA jobs: (line, rule | position << 24)
+  unsigned long long *job_count;
+  uint64_t job_cap;
+  uint32_t shared_bytes;      // per-wave LDS regions start here
 };
 
-__device__ __forceinline__ void fallback_line(const ScanArgs &A, uint64_t j) {
-  A.L.flags[j] = kLineSlowTs;
-  const unsigned long long k = atomicAdd(A.slow_count, 1ull);
-  A.slow_list[k] = (uint32_t)j;
+// pass A: '\n' count per wave tile
+__global__ __launch_bounds__(kBlock) void k_nl_count_wt(const uint8_t *__restrict__ buf, uint64_t n, uint64_t n_tiles,
+                                                        uint32_t *__restrict__ counts) {
+  const uint64_t t = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (t >= n_tiles) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t base = t * kWT + lane * 64u;
+  uint32_t c = 0;
+  if (base + 64 <= n) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(buf + base);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 v = src[k];
+      c += __popc(nl_mask_word(v.x)) + __popc(nl_mask_word(v.y)) + __popc(nl_mask_word(v.z)) + __popc(nl_mask_word(v.w));
+    }
+  } else {
+    for (uint64_t k = base; k < n && k < base + 64; ++k) c += buf[k] == '\n';
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if (lane == 0) counts[t] = c;
 }
 
-// Anchored rule over rest held in LDS: 1 match, 0 no match, -1 undecided
-// within the window (k_resolve finishes it from HBM).
-__device__ int anchored_lds(const Bind &B, uint32_t r, const uint8_t *s, uint32_t i, uint32_t lim) {
-  const DevRule R = B.rules[r];
-  const uint16_t *tr = B.trans + R.trans_off;
-  const uint8_t *ac = B.ascii_cls + (size_t)r * 128;
-  uint32_t st = R.start;
+__device__ __forceinline__ void push_list(uint32_t *list, unsigned long long *count, uint64_t j) {
+  const unsigned long long k = atomicAdd(count, 1ull);
+  list[k] = (uint32_t)j;
+}
+
+// lookup image viewed from LDS (scan pass) or HBM (other kernels)
+struct Tabs {
+  const uint32_t *gt, *ge, *ht;
+  const uint64_t *hrec;
+  const uint32_t *hid;
+  const uint8_t *hbytes;
+  const uint32_t *lrec;
+  const uint8_t *lbytes;
+  const uint32_t *lci;
+};
+__device__ __forceinline__ Tabs make_tabs(const uint8_t *base, const ImgLayout &il) {
+  Tabs t;
+  t.gt = reinterpret_cast<const uint32_t *>(base + il.gt);
+  t.ge = reinterpret_cast<const uint32_t *>(base + il.ge);
+  t.ht = reinterpret_cast<const uint32_t *>(base + il.ht);
+  t.hrec = reinterpret_cast<const uint64_t *>(base + il.hrec);
+  t.hid = reinterpret_cast<const uint32_t *>(base + il.hid);
+  t.hbytes = base + il.hbytes;
+  t.lrec = reinterpret_cast<const uint32_t *>(base + il.lrec);
+  t.lbytes = base + il.lbytes;
+  t.lci = reinterpret_cast<const uint32_t *>(base + il.lci);
+  return t;
+}
+
+// host id from the open-addressing host table
+__device__ int32_t host_lookup_ht(const Bind &B, const Tabs &T, const uint8_t *h, uint32_t n) {
+  if (B.n_hd == 0) return -1;
+  const uint64_t hh = hash_bytes(h, n);
+  const uint32_t tag = (uint32_t)(hh >> 32) | 1u;
+  uint32_t s = (uint32_t)hh & (B.ht_cap - 1);
   for (;;) {
-    if (i >= lim) return -1;
-    const uint8_t b = s[i];
-    if (b == '\n') return B.accept_end[R.ae_off + st];  // end of the line = end of text
-    uint32_t c;
-    if (b < 0x80) {
-      c = ac[b];
-      ++i;
-    } else {
-      // decode only with the whole sequence (or the line end) inside the window
-      uint32_t avail = 0;
-      while (avail < 4 && i + avail < lim && s[i + avail] != '\n') ++avail;
-      if (avail < 4 && i + avail >= lim) return -1;
-      int w;
-      const int32_t rune = decode_rune_hd(s + i, avail, &w);
-      i += (uint32_t)w;
-      const uint32_t *na = B.nonascii + 2 * R.na_off;
-      uint32_t lo = 0, hi = R.n_na;
-      while (hi - lo > 1) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (na[2 * m] <= (uint32_t)rune) lo = m; else hi = m;
-      }
-      c = na[2 * lo + 1];
+    const uint32_t k = T.ht[2 * s];
+    if (k == 0) return -1;
+    if (k == tag) {
+      const uint32_t i = T.ht[2 * s + 1];
+      const uint64_t rec = T.hrec[i];
+      if ((uint32_t)(rec & 0xFFFFFFFFu) == n && bytes_eq(T.hbytes + (rec >> 32), h, n)) return (int32_t)T.hid[i];
     }
-    st = tr[st * R.ncls + c];
-    if (st <= 1) return st;
+    s = (s + 1) & (B.ht_cap - 1);
   }
 }
 
-// Header of line j starting at LDS offset o (SplitN x2, ParseFloat fast path,
-// host lookup, CheckIsAllowed, OldLine) plus the anchored rules.
-__device__ void scan_line_header(const Bind &B, const ScanArgs &A, const uint8_t *s, uint32_t o, uint32_t lim,
-                                 uint64_t j) {
-  const Lines &L = A.L;
-  L.counts[j] = 0;
-  uint32_t sp[4];
-  int ns = 0;
-  uint32_t i = o;
-  bool eol = false;
-  while (i < lim) {
-    const uint8_t c = s[i];
-    if (c == '\n') { eol = true; break; }
-    if (c == ' ') { sp[ns++] = i; if (ns == 4) break; }
-    ++i;
-  }
-  if (ns < 4) {
-    if (eol) L.flags[j] = kLineError;
-    else fallback_line(A, j);  // header longer than the window
-    return;
-  }
-  double f;
-  if (parse_float_fast(s + o, sp[0] - o, &f) != 0) { fallback_line(A, j); return; }
-  const uint32_t ip_off = sp[0] + 1 - o, ip_len = sp[1] - sp[0] - 1;
-  const uint32_t rest_off = sp[1] + 1 - o, host_off = sp[2] + 1 - o, host_len = sp[3] - sp[2] - 1;
-  const int32_t hid = host_lookup(B, s + o + host_off, host_len);
-  const bool exempt = B.any_allow && check_is_allowed(B, hid, s + o + ip_off, ip_len);
-  L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
-  L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
-  L.host_id[j] = hid;
-  L.ip_hash[j] = hash_bytes(s + o + ip_off, ip_len);
-  const int64_t ts = ns_from_seconds(f);
-  L.ts[j] = ts;
-  uint8_t fl = 0;
-  if (go_sub(A.now_ns, ts) > 10000000000LL) fl = kLineOld;
-  else if (exempt) fl = kLineExempt;
-  L.flags[j] = fl;
-  if (fl || !B.any_anchored) { L.amask[j] = 0; L.ares[j] = 0; return; }
-  uint32_t s_begin = 0, s_end = 0;
-  if (hid >= 0) { s_begin = B.site_off[hid]; s_end = B.site_off[hid + 1]; }
-  const uint32_t nsite = s_end - s_begin, napp = nsite + B.n_global;
-  uint64_t am = 0, ar = 0;
-  for (uint32_t k = 0; k < napp; ++k) {
-    const uint32_t r = k < nsite ? B.site_rules[s_begin + k] : B.global_rules[k - nsite];
-    if (B.rules[r].mode != kModeAnchored) continue;
-    if (k >= 63) { ar |= 1ull << 63; continue; }
-    const int m = anchored_lds(B, r, s, o + rest_off, lim);
-    if (m < 0) ar |= 1ull << k;
-    else if (m) am |= 1ull << k;
-  }
-  L.amask[j] = am;
-  L.ares[j] = ar;
-}
+__device__ __forceinline__ uint32_t lit_len_of(const Tabs &T, uint32_t lit) { return T.lrec[lit] & 0xFF; }
 
-__device__ __forceinline__ uint8_t tile_byte(const uint8_t *s, int32_t l, uint32_t prev) {
-  return l >= 0 ? s[l] : (uint8_t)(prev >> (8 * (4 + l)));
-}
-
-// Pass B: one pass over the bytes, 32 per lane, coalesced; persistent blocks
-// walk 8 KB tiles.  Writes '\n' positions, parses every header (from LDS),
-// decides anchored rules, and runs the 4-gram prefilter (bitset in LDS) whose
-// exact hits become per-line literal candidates.
-__global__ __launch_bounds__(kBlock) void k_scan(Bind B, ScanArgs A) {
-  __shared__ uint32_t s_bits[kGramWords];
-  __shared__ __attribute__((aligned(16))) uint8_t s_tile[kScanTile + kScanHalo];
-  __shared__ uint32_t s_prev;
-  typedef hipcub::BlockScan<uint32_t, kBlock> BS;
-  __shared__ typename BS::TempStorage scan_tmp;
-  const uint32_t tid = threadIdx.x;
-  uint32_t n_probe = 0, n_cand = 0;  // per-lane stats, one atomic per wave at the end
-  if (B.any_prefilter)
-    for (uint32_t i = tid; i < kGramWords; i += kBlock) s_bits[i] = B.gram_bits[i];
-  for (uint64_t t = blockIdx.x; t < A.n_tiles; t += gridDim.x) {
-    const uint64_t tstart = t * kScanTile;
-    const uint32_t lim = (uint32_t)min<uint64_t>(kScanTile + kScanHalo, A.n - tstart);
-    __syncthreads();
-    // ---- stage the tile (+ halo) in LDS; keep my 32 bytes in registers
-    uint32_t d[8];
-    const uint64_t mine = tstart + tid * 32u;
-    if (mine + 32 <= A.n) {
-      const uint4 *src = reinterpret_cast<const uint4 *>(A.buf + mine);
-      const uint4 a = src[0], b = src[1];
-      d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
-    } else {
-      for (int w = 0; w < 8; ++w) {
-        uint32_t v = 0;
-        for (int k = 0; k < 4; ++k) {
-          const uint64_t pos = mine + 4 * w + k;
-          if (pos < A.n) v |= (uint32_t)A.buf[pos] << (8 * k);
-        }
-        d[w] = v;
-      }
-    }
-    uint4 *dst = reinterpret_cast<uint4 *>(s_tile + tid * 32u);
-    dst[0] = make_uint4(d[0], d[1], d[2], d[3]);
-    dst[1] = make_uint4(d[4], d[5], d[6], d[7]);
-    if (tid < kScanHalo / 16) {
-      const uint64_t h = tstart + kScanTile + tid * 16u;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (h + 16 <= A.n) v = *reinterpret_cast<const uint4 *>(A.buf + h);
-      else if (h < A.n) {
-        uint32_t w4[4] = {0, 0, 0, 0};
-        for (int k = 0; k < 16 && h + k < A.n; ++k) w4[k >> 2] |= (uint32_t)A.buf[h + k] << (8 * (k & 3));
-        v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-      }
-      *reinterpret_cast<uint4 *>(s_tile + kScanTile + tid * 16u) = v;
-    }
-    if (tid == 0) s_prev = tstart >= 4 ? *reinterpret_cast<const uint32_t *>(A.buf + tstart - 4) : 0u;
-    // ---- newlines: positions and this lane's first line index
-    uint32_t nlm = 0;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-      const uint32_t x = d[w] ^ 0x0A0A0A0Au;
-      const uint32_t hb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
-      nlm |= ((hb >> 7) & 1u) << (4 * w) | ((hb >> 15) & 1u) << (4 * w + 1) | ((hb >> 23) & 1u) << (4 * w + 2) |
-             ((hb >> 31) & 1u) << (4 * w + 3);
-    }
-    if (mine + 32 > A.n) nlm &= mine >= A.n ? 0u : ((1u << (A.n - mine)) - 1u);
-    uint32_t off;
-    BS(scan_tmp).ExclusiveSum((uint32_t)__popc(nlm), off);
-    __syncthreads();  // s_tile / s_prev visible
-    const uint64_t line0 = A.tile_base[t] + off;  // line containing my first byte
-    {
-      uint32_t x = nlm;
-      uint64_t r = line0;
-      while (x) {
-        const int k = __ffs(x) - 1;
-        x &= x - 1;
-        A.nl[r++] = mine + k;
-      }
-    }
-    // ---- line starts owned by this lane
-    if (tid == 0 && line0 < A.n_lines && (t == 0 || (s_prev >> 24) == '\n'))
-      scan_line_header(B, A, s_tile, 0, lim, line0);
-    {
-      uint32_t x = nlm;
-      uint64_t r = line0;
-      while (x) {
-        const int k = __ffs(x) - 1;
-        x &= x - 1;
-        ++r;  // the line after this newline
-        const uint32_t o = tid * 32u + (uint32_t)k + 1u;
-        if (o < kScanTile && r < A.n_lines) scan_line_header(B, A, s_tile, o, lim, r);
-      }
-    }
-    // ---- 4-gram prefilter over my 32 positions
-    if (!B.any_prefilter) continue;
-    const uint32_t dp = tid ? *reinterpret_cast<const uint32_t *>(s_tile + tid * 32u - 4u) : s_prev;
-    uint32_t hits = 0;
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const int st = k - 3;
-      uint32_t g;
-      if (st < 0) g = __builtin_amdgcn_alignbyte(d[0], dp, (uint32_t)(4 + st));
-      else if ((st & 3) == 0) g = d[st >> 2];
-      else g = __builtin_amdgcn_alignbyte(d[(st >> 2) + 1], d[st >> 2], (uint32_t)(st & 3));
-      const uint32_t h = gram_hash(g);
-      hits |= ((s_bits[h >> 5] >> (h & 31)) & 1u) << k;
-    }
-    if (mine + 32 > A.n) hits &= mine >= A.n ? 0u : ((1u << (A.n - mine)) - 1u);
-    while (hits) {
-      const int k = __ffs(hits) - 1;
-      hits &= hits - 1;
-      const int32_t l0 = (int32_t)(tid * 32u) + k - 3;
-      const uint32_t g = (uint32_t)tile_byte(s_tile, l0, s_prev) | (uint32_t)tile_byte(s_tile, l0 + 1, s_prev) << 8 |
-                         (uint32_t)tile_byte(s_tile, l0 + 2, s_prev) << 16 | (uint32_t)tile_byte(s_tile, l0 + 3, s_prev) << 24;
-      ++n_probe;
-      uint32_t slot = (uint32_t)mix64(g) & B.gt_mask;
-      while (B.gt_len[slot] && B.gt_key[slot] != g) slot = (slot + 1) & B.gt_mask;
-      if (!B.gt_len[slot]) continue;
-      const uint64_t line = line0 + __popc(nlm & ((1u << k) - 1u));
-      if (line >= A.n_lines) continue;
-      const int64_t gpos = (int64_t)(mine + k) - 3;
-      for (uint32_t e = 0; e < B.gt_len[slot]; ++e) {
-        const uint32_t lit = B.gt_entries[2 * (B.gt_off[slot] + e)];
-        const int64_t q = gpos - (int64_t)B.gt_entries[2 * (B.gt_off[slot] + e) + 1];
-        if (q < 0) continue;
-        const uint32_t c = atomicAdd(&A.L.cand_cnt[line], 1u);
-        ++n_cand;
-        if (c < kCandSlots) A.L.cand[line * kCandSlots + c] = ((uint64_t)q << 24) | lit;
-      }
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    n_probe += __shfl_xor(n_probe, o);
-    n_cand += __shfl_xor(n_cand, o);
-  }
-  if ((tid & 63) == 0 && (n_probe | n_cand)) {
-    atomicAdd(&A.stats[0], (unsigned long long)n_probe);
-    atomicAdd(&A.stats[1], (unsigned long long)n_cand);
-  }
-}
-
-__device__ __forceinline__ bool literal_at(const Bind &B, uint32_t lit, const uint8_t *p) {
-  const uint32_t off = B.lit_off[lit], len = B.lit_len[lit];
+__device__ __forceinline__ bool literal_at(const Tabs &T, uint32_t lit, const uint8_t *p) {
+  const uint32_t rec = T.lrec[lit];
+  const uint32_t off = rec >> 8, len = rec & 0xFF;
   for (uint32_t i = 0; i < len; ++i) {
-    const uint8_t t = p[i], l = B.lit_bytes[off + i];
-    if (B.lit_ci[off + i] ? ((t | 0x20) != l) : (t != l)) return false;
+    const uint32_t q = off + i;
+    const uint8_t t = p[i], l = T.lbytes[q];
+    const bool ci = (T.lci[q >> 5] >> (q & 31)) & 1u;
+    if (ci ? ((t | 0x20) != l) : (t != l)) return false;
   }
   return true;
 }
 
-// Pass C: per line, decide every applicable rule from the scan pass's
-// anchored verdicts and literal candidates; DFA only where needed.
-__global__ __launch_bounds__(kBlock) void k_resolve(Bind B, const uint8_t *__restrict__ buf,
-                                                    const uint64_t *__restrict__ nl, uint64_t n_lines, Lines L) {
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n_lines || L.flags[j] != 0) return;
-  const uint64_t s = j ? nl[j - 1] + 1 : 0;
-  const uint32_t n = (uint32_t)(nl[j] - s);
-  const uint8_t *p = buf + s;
-  const uint32_t rest_off = L.rest_off[j];
-  const uint8_t *rest = p + rest_off;
-  const uint32_t rest_len = n - rest_off;
-  const int32_t hid = L.host_id[j];
-  uint32_t cand_lit[kCandSlots];
-  uint32_t nc = 0;
-  bool ovf = false;
-  if (B.any_prefilter) {
-    const uint32_t cc = L.cand_cnt[j];
-    ovf = cc > (uint32_t)kCandSlots;
-    for (uint32_t c = 0; c < cc && c < (uint32_t)kCandSlots; ++c) {
-      const uint64_t v = L.cand[j * kCandSlots + c];
-      const uint32_t lit = (uint32_t)(v & 0xFFFFFF);
-      const uint64_t q = v >> 24;
-      if (q >= s + rest_off && q + B.lit_len[lit] <= s + n && literal_at(B, lit, buf + q)) cand_lit[nc++] = lit;
+
+__device__ __forceinline__ void set_pos(uint64_t &m0, uint64_t &m1, uint32_t pos) {
+  if (pos < 64) m0 |= 1ull << pos; else m1 |= 1ull << (pos - 64);
+}
+__device__ __forceinline__ bool has_pos(uint64_t m0, uint64_t m1, uint32_t pos) {
+  return ((pos < 64 ? m0 >> pos : m1 >> (pos - 64)) & 1) != 0;
+}
+
+// DFA work found by the scan pass: staged per wave in LDS, appended to HBM
+// with one atomic per wave tile (overflow goes straight to HBM).
+struct JobSink {
+  uint2 *lds;
+  uint32_t *cnt;
+  uint2 *jobs;
+  unsigned long long *count;
+  uint64_t cap;
+};
+__device__ __forceinline__ void emit_job(const JobSink &S, uint64_t j, uint32_t r, uint32_t pos) {
+  const uint2 v = make_uint2((uint32_t)j, r | (pos << 24));
+  const uint32_t c = atomicAdd(S.cnt, 1u);
+  if (c < kWaveJobs) { S.lds[c] = v; return; }
+  const unsigned long long g = atomicAdd(S.count, 1ull);
+  if (g < S.cap) S.jobs[g] = v;
+}
+
+// One rule whose decision needs its automaton: an anchored prefix may decide
+// it first; otherwise run the DFA here (EMIT = false) or hand it to k_dfa.
+template <bool EMIT>
+__device__ __forceinline__ void dfa_rule(const Bind &B, const Tabs &T, uint32_t r, uint32_t pos, bool anchored,
+                                         const uint8_t *rest, uint32_t rest_len, uint64_t &m0, uint64_t &m1, uint64_t j,
+                                         const JobSink &S) {
+  if (anchored) {
+    const DevRule &R = B.rules[r];
+    if (R.anc_len) {
+      bool any = false;
+      for (uint32_t i = 0; i < R.anc_len && !any; ++i) {
+        const uint32_t lit = B.rule_lits[R.anc_off + i];
+        any = lit_len_of(T, lit) <= rest_len && literal_at(T, lit, rest);
+      }
+      if (!any) return;
+      if (R.anc_equiv) { set_pos(m0, m1, pos); return; }
     }
   }
-  const uint64_t am = B.any_anchored ? L.amask[j] : 0, ar = B.any_anchored ? L.ares[j] : 0;
-  uint64_t *mask = L.masks + (size_t)j * B.mask_words;
-  uint64_t word = 0;
-  uint32_t pos = 0, wi = 0, nres = 0, nev = 0;
+  if (EMIT) emit_job(S, j, r, pos);
+  else if (rule_match(B, r, rest, rest_len)) set_pos(m0, m1, pos);
+}
+
+// The applicable rules of one line (per-site[host] then global, YAML order;
+// regex_rate_limiter.go:175-211) decided from the line's verified literal
+// hits.  Writes the match mask (positions < 128) and the result/event counts
+// of the rules decided here; rules left to k_dfa add theirs atomically.
+// lits: up to 4 literal ids packed 16 bits each.
+template <bool EMIT>
+__device__ void decide_rules(const Bind &B, const Tabs &T, const uint8_t *rest, uint32_t rest_len, int32_t hid,
+                             uint64_t lits, uint32_t nlit, bool ovf, uint64_t j, const Lines &L, const JobSink &S) {
+  const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
   uint32_t s_begin = 0, s_end = 0;
   if (hid >= 0) { s_begin = B.site_off[hid]; s_end = B.site_off[hid + 1]; }
   const uint32_t nsite = s_end - s_begin;
-  const uint32_t napp = nsite + B.n_global;
-  for (uint32_t k = 0; k < napp; ++k) {
-    const uint32_t r = k < nsite ? B.site_rules[s_begin + k] : B.global_rules[k - nsite];
-    const uint8_t mode = B.rules[r].mode;
-    bool m;
-    if (mode == kModeAlways) m = true;
-    else if (mode == kModeNever) m = false;
-    else if (mode == kModeAnchored) {
-      if (k < 63 && !((ar >> k) & 1)) m = (am >> k) & 1;
-      else m = rule_match(B, r, rest, rest_len);
-    } else if (mode == kModePrefilter && !ovf) {
-      const DevRule &R = B.rules[r];
-      bool hit = false;
-      for (uint32_t c = 0; c < nc && !hit; ++c)
-        for (uint32_t e = 0; e < R.lits_len; ++e)
-          if (B.rule_lits[R.lits_off + e] == cand_lit[c]) { hit = true; break; }
-      m = hit && (R.equiv || rule_match(B, r, rest, rest_len));
-    } else {
-      m = rule_match(B, r, rest, rest_len);
+  uint64_t m0 = B.sc_always[2 * sc], m1 = B.sc_always[2 * sc + 1];
+  // anchored / no-literal rules: every line
+  if (hid >= 0)
+    for (uint32_t i = B.dfa_site_off[hid]; i < B.dfa_site_off[hid + 1]; ++i) {
+      const uint2 e = B.dfa_site[i];
+      dfa_rule<EMIT>(B, T, e.x, e.y, true, rest, rest_len, m0, m1, j, S);
     }
-    if (m) {
-      word |= 1ull << (pos & 63);
-      ++nres;
-      nev += is_skip(B, r, hid) ? 0u : 1u;
-    }
-    ++pos;
-    if ((pos & 63) == 0) { mask[wi++] = word; word = 0; }
+  for (uint32_t i = 0; i < B.n_dfa_glob; ++i) {
+    const uint2 e = B.dfa_glob[i];
+    dfa_rule<EMIT>(B, T, e.x, nsite + e.y, true, rest, rest_len, m0, m1, j, S);
   }
-  if (pos & 63) mask[wi] = word;
+  if (ovf) {
+    // more hits than slots: every literal rule by its DFA (exact, slower)
+    if (hid >= 0)
+      for (uint32_t i = B.pref_site_off[hid]; i < B.pref_site_off[hid + 1]; ++i) {
+        const uint2 e = B.pref_site[i];
+        dfa_rule<EMIT>(B, T, e.x, e.y, false, rest, rest_len, m0, m1, j, S);
+      }
+    for (uint32_t i = 0; i < B.n_pref_glob; ++i) {
+      const uint2 e = B.pref_glob[i];
+      dfa_rule<EMIT>(B, T, e.x, nsite + e.y, false, rest, rest_len, m0, m1, j, S);
+    }
+  } else {
+    uint64_t t0 = 0, t1 = 0;  // literal rules already decided
+    for (uint32_t c = 0; c < nlit; ++c) {
+      const uint32_t lit = (uint32_t)(lits >> (16 * c)) & 0xFFFF;
+      bool dup = false;
+      for (uint32_t d = 0; d < c; ++d) dup = dup || ((uint32_t)(lits >> (16 * d)) & 0xFFFF) == lit;
+      if (dup) continue;
+      const uint32_t b = B.lr_off[lit], g = B.lr_gend[lit], e = B.lr_off[lit + 1];
+      for (uint32_t i = b; i < g; ++i) {
+        const uint2 x = B.lr_ent[i];
+        const uint32_t pos = nsite + x.y;
+        if (has_pos(t0, t1, pos)) continue;
+        set_pos(t0, t1, pos);
+        if (x.x >> 31) set_pos(m0, m1, pos);
+        else dfa_rule<EMIT>(B, T, x.x, pos, false, rest, rest_len, m0, m1, j, S);
+      }
+      if (hid < 0 || g == e) continue;
+      uint32_t lo = g, hi = e;  // first site entry of this host
+      while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (B.lr_host[m] < hid) lo = m + 1; else hi = m;
+      }
+      for (uint32_t i = lo; i < e && B.lr_host[i] == hid; ++i) {
+        const uint2 x = B.lr_ent[i];
+        if (has_pos(t0, t1, x.y)) continue;
+        set_pos(t0, t1, x.y);
+        if (x.x >> 31) set_pos(m0, m1, x.y);
+        else dfa_rule<EMIT>(B, T, x.x, x.y, false, rest, rest_len, m0, m1, j, S);
+      }
+    }
+  }
+  uint64_t *mask = L.masks + j * B.mask_words;
+  mask[0] = m0;
+  if (B.mask_words > 1) mask[1] = m1;
+  const uint64_t k0 = B.sc_skip[2 * sc], k1 = B.sc_skip[2 * sc + 1];
+  const uint32_t nres = __popcll(m0) + __popcll(m1);
+  const uint32_t nev = __popcll(m0 & ~k0) + __popcll(m1 & ~k1);
   L.counts[j] = ((uint64_t)nres << 32) | nev;
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+
+template <bool IMG_LDS>
+__global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_scan(Bind B, ScanArgs A) {
+  // ---- block-shared tables (read-only after this barrier): gram bitset, then
+  // the lookup image when it fits
+  uint32_t *s_bits = reinterpret_cast<uint32_t *>(s_dyn);
+  uint8_t *s_img = s_dyn + kGramWords * 4;
+  for (uint32_t i = threadIdx.x; i < kGramWords / 4; i += blockDim.x)
+    reinterpret_cast<uint4 *>(s_bits)[i] = reinterpret_cast<const uint4 *>(B.gram_bits)[i];
+  if (IMG_LDS)
+    for (uint32_t i = threadIdx.x; i < B.img_bytes / 16; i += blockDim.x)
+      reinterpret_cast<uint4 *>(s_img)[i] = reinterpret_cast<const uint4 *>(B.img)[i];
+  __syncthreads();
+  const Tabs TB = make_tabs(IMG_LDS ? s_img : B.img, B.il);
+  const uint32_t *gt = TB.gt, *ge = TB.ge;
+
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint8_t *T = s_dyn + A.shared_bytes + wave * kWaveLds;
+  uint16_t *ls = reinterpret_cast<uint16_t *>(T + kTileLds);
+  uint16_t *le = ls + kLineCap;
+  uint32_t *hc = reinterpret_cast<uint32_t *>(le + kLineCap);
+  uint32_t *hs = hc + kLineCap;
+  JobSink S;
+  S.lds = reinterpret_cast<uint2 *>(hs + kLineCap * kHitSlots);
+  S.cnt = reinterpret_cast<uint32_t *>(S.lds + kWaveJobs);
+  S.jobs = A.jobs;
+  S.count = A.job_count;
+  S.cap = A.job_cap;
+  if (lane == 0) *S.cnt = 0;
+  wave_sync();
+  const Lines &L = A.L;
+  uint32_t n_probe = 0, n_hit = 0;
+
+  const uint64_t nw = (uint64_t)gridDim.x * kScanWaves;
+  uint64_t t = (uint64_t)blockIdx.x * kScanWaves + wave;
+  uint4 q[4];
+  auto load_tile = [&](uint64_t tt) {
+    const uint64_t base = tt * kWT + lane * 64u;
+    if (base + 64 <= A.n) {
+      const uint4 *src = reinterpret_cast<const uint4 *>(A.buf + base);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q[k] = src[k];
+    } else {
+      uint32_t w[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = 0;
+      for (uint32_t k = 0; k < 64 && base + k < A.n; ++k) w[k >> 2] |= (uint32_t)A.buf[base + k] << (8 * (k & 3));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+    }
+  };
+  if (t < A.n_tiles) load_tile(t);
+  for (; t < A.n_tiles; t += nw) {
+    const uint64_t ts0 = t * kWT;
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { w[4 * k] = q[k].x; w[4 * k + 1] = q[k].y; w[4 * k + 2] = q[k].z; w[4 * k + 3] = q[k].w; }
+    if (t + nw < A.n_tiles) load_tile(t + nw);  // prefetch
+    // halo (8 B per lane) and the byte before the tile
+    uint2 hv = make_uint2(0, 0);
+    {
+      const uint64_t h = ts0 + kWT + lane * 8u;
+      if (h + 8 <= A.n) hv = *reinterpret_cast<const uint2 *>(A.buf + h);
+      else if (h < A.n) {
+        uint32_t a = 0, b = 0;
+        for (uint32_t k = 0; k < 8 && h + k < A.n; ++k) {
+          if (k < 4) a |= (uint32_t)A.buf[h + k] << (8 * k); else b |= (uint32_t)A.buf[h + k] << (8 * (k - 4));
+        }
+        hv = make_uint2(a, b);
+      }
+    }
+    const uint32_t prevb = ts0 ? (uint32_t)A.buf[ts0 - 1] : (uint32_t)'\n';
+    uint4 *dst = reinterpret_cast<uint4 *>(T + lane * 64u);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+    *reinterpret_cast<uint2 *>(T + kWT + lane * 8u) = hv;
+    if (lane < 4) reinterpret_cast<uint32_t *>(T + kWT + kHalo)[lane] = 0;
+
+    // ---- '\n' bitmask of my 64 bytes (bytes past the batch end are 0)
+    uint64_t nlm = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t hb = nl_mask_word(w[k]);
+      nlm |= (uint64_t)(((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u)) << (4 * k);
+    }
+    const uint32_t cnt = __popcll(nlm);
+    uint32_t pre = cnt;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(pre, o);
+      if (lane >= (uint32_t)o) pre += v;
+    }
+    const uint32_t tot = __shfl(pre, 63);
+    pre -= cnt;
+    const uint64_t tb = A.tile_base[t];
+    const bool head = prevb == '\n';
+    const uint32_t nh = head ? 0u : 1u;
+    const bool last_nl = (__shfl((uint32_t)(nlm >> 63), 63) & 1u) != 0;
+    const uint32_t n_st = (head ? 1u : 0u) + tot - (last_nl ? 1u : 0u);
+    // first '\n' in the tile and in the halo
+    const uint64_t any_nl = __ballot(cnt != 0);
+    uint32_t p0 = kNone;
+    if (any_nl) {
+      const uint32_t fl = (uint32_t)__ffsll((unsigned long long)any_nl) - 1;
+      const uint64_t fm = __shfl(nlm, fl);
+      p0 = fl * 64u + (uint32_t)__ffsll((unsigned long long)fm) - 1;
+    }
+    uint32_t hmask;
+    {
+      const uint32_t a = nl_mask_word(hv.x), b = nl_mask_word(hv.y);
+      hmask = ((a >> 7) & 1u) | ((a >> 14) & 2u) | ((a >> 21) & 4u) | ((a >> 28) & 8u) |
+              (((b >> 7) & 1u) | ((b >> 14) & 2u) | ((b >> 21) & 4u) | ((b >> 28) & 8u)) << 4;
+    }
+    if (ts0 + kWT + lane * 8u >= A.n) hmask = 0;
+    const uint64_t any_h = __ballot(hmask != 0);
+    uint32_t hfirst = kNone;
+    if (any_h) {
+      const uint32_t fl = (uint32_t)__ffsll((unsigned long long)any_h) - 1;
+      hfirst = kWT + fl * 8u + (uint32_t)__ffs(__shfl(hmask, fl)) - 1;
+    }
+    // ---- nl[] and line start/end positions (tile-relative)
+    {
+      uint64_t x = nlm;
+      uint32_t r = pre;
+      while (x) {
+        const uint32_t b = (uint32_t)__ffsll((unsigned long long)x) - 1;
+        x &= x - 1;
+        const uint32_t p = lane * 64u + b;
+        if (tb + r < A.n_lines) A.nl[tb + r] = ts0 + p;
+        const int32_t lk = (int32_t)r - (int32_t)nh;  // started line this '\n' ends
+        if (lk >= 0 && lk < (int32_t)kLineCap) le[lk] = (uint16_t)p;
+        if (p + 1 < kWT && lk + 1 < (int32_t)kLineCap) ls[lk + 1] = (uint16_t)(p + 1);
+        ++r;
+      }
+    }
+    if (lane == 0 && head) ls[0] = 0;
+    const bool last_in_halo = n_st && !last_nl && hfirst != kNone;
+    const bool last_long = n_st && !last_nl && hfirst == kNone;
+    if (lane == 0 && last_in_halo && n_st - 1 < kLineCap) le[n_st - 1] = (uint16_t)hfirst;
+    // the line open at the tile start is long iff it started before the previous
+    // tile (that tile has no '\n') or runs past the previous tile's halo
+    const bool open_long = !head && (p0 == kNone || p0 >= kHalo || tb == A.tile_base[t - 1]);
+    for (uint32_t k = lane; k < kLineCap; k += 64) hc[k] = 0;
+    wave_sync();
+
+    // ---- 4-gram prefilter: positions [64 lane, 64 lane + 64) and the last line's halo part
+    if (B.any_prefilter) {
+      const uint32_t nxt = *reinterpret_cast<const uint32_t *>(T + lane * 64u + 64u);
+      uint64_t hits = 0;
+#pragma unroll
+      for (int k = 0; k < 64; ++k) {
+        const uint32_t lo = w[k >> 2], hi = (k >> 2) < 15 ? w[(k >> 2) + 1] : nxt;
+        const uint32_t g = (k & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3)) : lo;
+        const uint32_t h = gram_hash(g);
+        hits |= (uint64_t)((s_bits[h >> 5] >> (h & 31)) & 1u) << k;
+      }
+      if (ts0 + lane * 64u + 64u > A.n) hits &= (ts0 + lane * 64u >= A.n) ? 0ull : ((1ull << (A.n - ts0 - lane * 64u)) - 1ull);
+      uint32_t hh = 0;  // halo positions of the last started line
+      const uint32_t hend = last_in_halo ? hfirst : kWT;
+      if (lane * 8u + kWT < hend) {
+        for (uint32_t k = 0; k < 8 && kWT + lane * 8u + k < hend; ++k) {
+          const uint32_t p = kWT + lane * 8u + k;
+          const uint32_t gg = (uint32_t)T[p] | (uint32_t)T[p + 1] << 8 | (uint32_t)T[p + 2] << 16 | (uint32_t)T[p + 3] << 24;
+          const uint32_t h = gram_hash(gg);
+          hh |= ((s_bits[h >> 5] >> (h & 31)) & 1u) << k;
+        }
+      }
+      n_probe += __popcll(hits) + __popc(hh);
+      for (int part = 0; part < 2; ++part) {
+        uint64_t x = part == 0 ? hits : (uint64_t)hh;
+        while (x) {
+          const uint32_t k = (uint32_t)__ffsll((unsigned long long)x) - 1;
+          x &= x - 1;
+          const uint32_t p = part == 0 ? lane * 64u + k : kWT + lane * 8u + k;
+          if (T[p] == '\n') continue;
+          const uint32_t g = (uint32_t)T[p] | (uint32_t)T[p + 1] << 8 | (uint32_t)T[p + 2] << 16 | (uint32_t)T[p + 3] << 24;
+          uint32_t slot = (uint32_t)mix64(g) & (B.gt2_cap - 1);
+          uint32_t key, ol;
+          for (;;) {
+            key = gt[2 * slot];
+            ol = gt[2 * slot + 1];
+            if ((ol & 0xFFFF) == 0 || key == g) break;
+            slot = (slot + 1) & (B.gt2_cap - 1);
+          }
+          if ((ol & 0xFFFF) == 0) continue;
+          // owning line: started-line index lk, or the open line (lk < 0)
+          int32_t lk;
+          uint64_t gline;
+          if (part == 0) {
+            const uint32_t before = pre + (uint32_t)__popcll(nlm & ((1ull << k) - 1ull));
+            gline = tb + before;
+            lk = (int32_t)before - (int32_t)nh;
+          } else {
+            lk = (int32_t)n_st - 1;
+            gline = tb + tot;
+          }
+          const bool is_long = lk < 0 ? open_long : (lk == (int32_t)n_st - 1 && last_long);
+          if (lk < 0 && !open_long) continue;  // decided by the previous tile
+          for (uint32_t ei = 0; ei < (ol & 0xFFFF); ++ei) {
+            const uint32_t en = ge[(ol >> 16) + ei];
+            const uint32_t lit = en >> 8, goff = en & 0xFF;
+            if (is_long) {
+              const int64_t q0 = (int64_t)(ts0 + p) - (int64_t)goff;
+              if (q0 < 0 || gline >= A.n_lines) continue;
+              const uint32_t c = atomicAdd(&L.cand_cnt[gline], 1u);
+              if (c < (uint32_t)kCandSlots) L.cand[gline * kCandSlots + c] = ((uint64_t)q0 << 24) | lit;
+              ++n_hit;
+            } else if (lk < (int32_t)kLineCap) {
+              const int32_t s0 = (int32_t)p - (int32_t)goff;
+              const uint32_t len = lit_len_of(TB, lit);
+              if (s0 < (int32_t)ls[lk] || (uint32_t)s0 + len > le[lk]) continue;
+              if (!literal_at(TB, lit, T + s0)) continue;
+              const uint32_t c = atomicAdd(&hc[lk], 1u);
+              if (c < kHitSlots) hs[lk * kHitSlots + c] = ((uint32_t)s0 << 16) | lit;
+              ++n_hit;
+            }
+          }
+        }
+      }
+      wave_sync();
+    }
+
+    // ---- one lane per line starting in this tile
+    for (uint32_t k = lane; k < n_st; k += 64) {
+      const uint64_t j = tb + k + nh;
+      if (j >= A.n_lines) break;
+      if (k >= kLineCap) { L.flags[j] = kLineSlowTs; push_list(A.slow_list, A.slow_count, j); continue; }
+      const bool is_long = k == n_st - 1 && last_long;
+      const uint32_t s = ls[k];
+      const uint32_t e = is_long ? kWT + kHalo : le[k];
+      L.counts[j] = 0;
+      // first four spaces, 4 bytes at a time (aligned LDS words)
+      uint32_t sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0, ns = 0;
+      for (uint32_t i = s & ~3u; i < e && ns < 4; i += 4) {
+        const uint32_t x = *reinterpret_cast<const uint32_t *>(T + i) ^ 0x20202020u;
+        uint32_t m = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+        while (m && ns < 4) {
+          const uint32_t p = i + (((uint32_t)__ffs(m) - 1) >> 3);
+          m &= m - 1;
+          if (p < s || p >= e) continue;
+          if (ns == 0) sp0 = p; else if (ns == 1) sp1 = p; else if (ns == 2) sp2 = p; else sp3 = p;
+          ++ns;
+        }
+      }
+      if (ns < 4) {  // SplitN short: Error, or the header runs past the window
+        if (!is_long) L.flags[j] = kLineError;
+        else { L.flags[j] = kLineSlowTs; push_list(A.slow_list, A.slow_count, j); }
+        continue;
+      }
+      double f;
+      if (parse_float_fast(T + s, sp0 - s, &f) != 0) {
+        L.flags[j] = kLineSlowTs;
+        push_list(A.slow_list, A.slow_count, j);
+        continue;
+      }
+      const uint32_t ip_off = sp0 + 1 - s, ip_len = sp1 - sp0 - 1;
+      const uint32_t rest_off = sp1 + 1 - s, host_off = sp2 + 1 - s, host_len = sp3 - sp2 - 1;
+      const int32_t hid = host_lookup_ht(B, TB, T + s + host_off, host_len);
+      const uint32_t napp = (hid >= 0 ? B.site_off[hid + 1] - B.site_off[hid] : 0u) + B.n_global;
+      if (napp > 128) { L.flags[j] = kLineSlowTs; push_list(A.slow_list, A.slow_count, j); continue; }
+      const bool exempt = B.any_allow && check_is_allowed(B, hid, T + s + ip_off, ip_len);
+      L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
+      L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
+      L.host_id[j] = hid;
+      L.ip_hash[j] = hash_bytes(T + s + ip_off, ip_len);
+      const int64_t tsn = ns_from_seconds(f);
+      L.ts[j] = tsn;
+      uint8_t fl = 0;
+      if (go_sub(A.now_ns, tsn) > 10000000000LL) fl = kLineOld;
+      else if (exempt) fl = kLineExempt;
+      if (fl) { L.flags[j] = fl; continue; }
+      if (is_long) { L.flags[j] = kLineLong; push_list(A.long_list, A.long_count, j); continue; }
+      L.flags[j] = 0;
+      uint64_t lits = 0;
+      const uint32_t nhit = hc[k];
+      uint32_t nlit = 0;
+      const uint32_t rs = s + rest_off;
+      for (uint32_t c = 0; c < nhit && c < kHitSlots; ++c) {
+        const uint32_t v = hs[k * kHitSlots + c];
+        if ((v >> 16) >= rs) lits |= (uint64_t)(v & 0xFFFF) << (16 * nlit++);
+      }
+      decide_rules<true>(B, TB, T + rs, e - rs, hid, lits, nlit, nhit > kHitSlots, j, L, S);
+    }
+    // ---- append this tile's DFA jobs (one global atomic per wave tile)
+    wave_sync();
+    const uint32_t nj = min(*S.cnt, kWaveJobs);
+    if (nj) {
+      unsigned long long base = 0;
+      if (lane == 0) base = atomicAdd(A.job_count, (unsigned long long)nj);
+      base = __shfl(base, 0);
+      for (uint32_t i = lane; i < nj; i += 64)
+        if (base + i < A.job_cap) A.jobs[base + i] = S.lds[i];
+    }
+    wave_sync();
+    if (lane == 0) *S.cnt = 0;
+    wave_sync();
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    n_probe += __shfl_xor(n_probe, o);
+    n_hit += __shfl_xor(n_hit, o);
+  }
+  if (lane == 0 && (n_probe | n_hit)) {
+    atomicAdd(&A.stats[0], (unsigned long long)n_probe);
+    atomicAdd(&A.stats[1], (unsigned long long)n_hit);
+  }
+}
+
+// Long lines (past the scan window): header already parsed by k_scan; decide
+// the rules from the globally recorded literal hits, bytes from HBM.
+__global__ __launch_bounds__(kBlock) void k_resolve_long(Bind B, const uint8_t *__restrict__ buf,
+                                                         const uint64_t *__restrict__ nl, const uint32_t *__restrict__ list,
+                                                         uint64_t n, Lines L) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint64_t j = list[t];
+  const uint64_t s = j ? nl[j - 1] + 1 : 0;
+  const uint64_t e = nl[j];
+  const uint64_t rs = s + L.rest_off[j];
+  const uint32_t cc = L.cand_cnt[j];
+  const Tabs TB = make_tabs(B.img, B.il);
+  uint64_t lits = 0;
+  uint32_t nlit = 0;
+  for (uint32_t c = 0; c < cc && c < (uint32_t)kCandSlots; ++c) {
+    const uint64_t v = L.cand[j * kCandSlots + c];
+    const uint32_t lit = (uint32_t)(v & 0xFFFFFF);
+    const uint64_t q = v >> 24;
+    if (q >= rs && q + lit_len_of(TB, lit) <= e && literal_at(TB, lit, buf + q)) lits |= (uint64_t)lit << (16 * nlit++);
+  }
+  L.flags[j] = 0;
+  JobSink S{};
+  decide_rules<false>(B, TB, buf + rs, (uint32_t)(e - rs), L.host_id[j], lits, nlit, cc > (uint32_t)kCandSlots, j, L, S);
+}
+
+// DFA jobs from the scan pass: one (line, rule) per lane; a match sets the
+// rule's bit and adds to the line's result / event counts.
+__global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restrict__ buf, const uint64_t *__restrict__ nl,
+                                                const uint2 *__restrict__ jobs, uint64_t n, Lines L) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint2 v = jobs[t];
+  const uint64_t j = v.x;
+  const uint32_t r = v.y & 0xFFFFFF, pos = v.y >> 24;
+  const uint64_t s = j ? nl[j - 1] + 1 : 0;
+  const uint64_t rs = s + L.rest_off[j];
+  if (!rule_match(B, r, buf + rs, (uint32_t)(nl[j] - rs))) return;
+  const int32_t hid = L.host_id[j];
+  const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
+  const bool skip = (B.sc_skip[2 * sc + (pos >> 6)] >> (pos & 63)) & 1;
+  atomicOr(reinterpret_cast<unsigned long long *>(L.masks + j * B.mask_words + (pos >> 6)), 1ull << (pos & 63));
+  atomicAdd(reinterpret_cast<unsigned long long *>(L.counts + j), (1ull << 32) | (skip ? 0ull : 1ull));
 }
 
 // RuleResults (reference order) and rate-limit events from the per-line masks.
@@ -1133,9 +1420,13 @@ struct bjx_engine {
   DevBuf<uint64_t> l_iph, l_counts, l_offs, l_masks;
   DevBuf<uint32_t> l_ipoff, l_iplen, l_hoff, l_hlen, l_roff, slow_list;
   DevBuf<int32_t> l_hid;
-  DevBuf<uint64_t> l_amask, l_ares, l_cand;
+  DevBuf<uint64_t> l_cand;
+  DevBuf<uint32_t> long_list;
+  DevBuf<uint2> jobs;
+  uint64_t last_jobs = 0;
+  uint32_t scan_lds[2] = {0, 0};
   DevBuf<uint32_t> l_ccnt;
-  unsigned long long scan_stats[2] = {0, 0};
+  unsigned long long scan_stats[5] = {0, 0, 0, 0, 0};
   uint64_t last_slow = 0;
   DevBuf<uint8_t> l_flags;
   DevBuf<unsigned long long> scalars;  // [0] slow count, [1..2] bounds, [3] selected
@@ -1330,6 +1621,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   std::map<std::pair<std::string, std::string>, uint32_t> lit_ids;
   std::vector<uint8_t> lit_bytes, lit_ci;
   std::vector<uint32_t> lit_off, lit_len, lit_gram, rule_lits;
+  std::vector<uint8_t> lit_pref;
   bool any_anchored = false;
   for (size_t i = 0; i < rs->rules.size(); ++i) {
     const auto &r = rs->rules[i];
@@ -1350,26 +1642,33 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     d.decision = r.decision;
     d.mode = (uint8_t)r.rx.mode;
     d.equiv = r.rx.pref_equivalent ? 1 : 0;
-    d.lits_off = (uint32_t)rule_lits.size();
-    if (r.rx.mode == kModePrefilter) {
-      for (auto &pl : r.rx.pref) {
-        auto key = std::make_pair(pl.s, pl.ci);
-        auto it = lit_ids.find(key);
-        uint32_t id;
-        if (it != lit_ids.end()) id = it->second;
-        else {
-          id = (uint32_t)lit_off.size();
-          lit_ids.emplace(key, id);
-          lit_off.push_back((uint32_t)lit_bytes.size());
-          lit_len.push_back((uint32_t)pl.s.size());
-          lit_gram.push_back(pl.gram_off);
-          lit_bytes.insert(lit_bytes.end(), pl.s.begin(), pl.s.end());
-          lit_ci.insert(lit_ci.end(), pl.ci.begin(), pl.ci.end());
-        }
-        rule_lits.push_back(id);
+    auto intern_lit = [&](const PrefLit &pl, bool pref) {
+      auto key = std::make_pair(pl.s, pl.ci);
+      auto it = lit_ids.find(key);
+      uint32_t id;
+      if (it != lit_ids.end()) id = it->second;
+      else {
+        id = (uint32_t)lit_off.size();
+        lit_ids.emplace(key, id);
+        lit_off.push_back((uint32_t)lit_bytes.size());
+        lit_len.push_back((uint32_t)pl.s.size());
+        lit_gram.push_back(pl.gram_off);
+        lit_pref.push_back(0);
+        lit_bytes.insert(lit_bytes.end(), pl.s.begin(), pl.s.end());
+        lit_ci.insert(lit_ci.end(), pl.ci.begin(), pl.ci.end());
       }
-    }
+      if (pref) { lit_pref[id] = 1; lit_gram[id] = pl.gram_off; }
+      return id;
+    };
+    d.lits_off = (uint32_t)rule_lits.size();
+    if (r.rx.mode == kModePrefilter)
+      for (auto &pl : r.rx.pref) rule_lits.push_back(intern_lit(pl, true));
     d.lits_len = (uint16_t)(rule_lits.size() - d.lits_off);
+    d.anc_off = (uint32_t)rule_lits.size();
+    if (r.rx.mode == kModeAnchored)
+      for (auto &pl : r.rx.anchor) rule_lits.push_back(intern_lit(pl, false));
+    d.anc_len = (uint16_t)(rule_lits.size() - d.anc_off);
+    d.anc_equiv = r.rx.anchor_equivalent ? 1 : 0;
     any_anchored = any_anchored || r.rx.mode == kModeAnchored;
     d.interval_ns = r.interval_ns;
     d.hits = r.hits;
@@ -1379,25 +1678,30 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   // of its case-insensitive bytes, -> bitset bit + exact table entry
   std::map<uint32_t, std::vector<std::pair<uint32_t, uint32_t>>> gmap;
   for (uint32_t id = 0; id < lit_off.size(); ++id) {
+    if (!lit_pref[id]) continue;
     const uint32_t o = lit_off[id] + lit_gram[id];
     for (uint32_t v = 0; v < 16; ++v) {
       uint32_t g;
       if (window_variant(&lit_bytes[o], &lit_ci[o], v, &g)) gmap[g].push_back({id, lit_gram[id]});
     }
   }
+  // exact gram table: slot (key, entries offset << 16 | count), entries (lit << 8 | window offset)
+  size_t n_gent = 0;
+  for (auto &kv : gmap) n_gent += kv.second.size();
+  const bool use_pref = n_gent > 0 && n_gent < 65536 && lit_off.size() < 65536;
   std::vector<uint32_t> gram_bits(kGramWords, 0);
-  const uint32_t gt_cap = (uint32_t)next_pow2(gmap.size() * 2 + 16);
-  std::vector<uint32_t> gt_key(gt_cap, 0), gt_off(gt_cap, 0), gt_len(gt_cap, 0), gt_entries;
-  for (auto &kv : gmap) {
-    const uint32_t h = gram_hash(kv.first);
-    gram_bits[h >> 5] |= 1u << (h & 31);
-    uint32_t slot = (uint32_t)mix64(kv.first) & (gt_cap - 1);
-    while (gt_len[slot]) slot = (slot + 1) & (gt_cap - 1);
-    gt_key[slot] = kv.first;
-    gt_off[slot] = (uint32_t)(gt_entries.size() / 2);
-    gt_len[slot] = (uint32_t)kv.second.size();
-    for (auto &e : kv.second) { gt_entries.push_back(e.first); gt_entries.push_back(e.second); }
-  }
+  const uint32_t gt2_cap = (uint32_t)next_pow2((use_pref ? gmap.size() : 0) * 2 + 16);
+  std::vector<uint32_t> gt2(2 * gt2_cap, 0), gt2_ent;
+  if (use_pref)
+    for (auto &kv : gmap) {
+      const uint32_t h = gram_hash(kv.first);
+      gram_bits[h >> 5] |= 1u << (h & 31);
+      uint32_t slot = (uint32_t)mix64(kv.first) & (gt2_cap - 1);
+      while (gt2[2 * slot + 1] & 0xFFFF) slot = (slot + 1) & (gt2_cap - 1);
+      gt2[2 * slot] = kv.first;
+      gt2[2 * slot + 1] = ((uint32_t)gt2_ent.size() << 16) | (uint32_t)kv.second.size();
+      for (auto &en : kv.second) gt2_ent.push_back((en.first << 8) | en.second);
+    }
   if (lit_bytes.empty()) { lit_bytes.push_back(0); lit_ci.push_back(0); }
   std::vector<uint32_t> global_rules(rs->n_global);
   for (uint32_t i = 0; i < rs->n_global; ++i) global_rules[i] = i;
@@ -1411,7 +1715,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     max_app = std::max<uint32_t>(max_app, (uint32_t)per_host[h].size() + rs->n_global);
   }
   site_off[n_hosts] = (uint32_t)site_rules.size();
-  // host dict sorted by hash
+  // host dict sorted by hash (+ open-addressing table over it for the scan pass)
   std::vector<std::pair<uint64_t, uint32_t>> hd;
   for (uint32_t h = 0; h < n_hosts; ++h)
     hd.push_back({hash_bytes(reinterpret_cast<const uint8_t *>(host_by_id[h].data()), (uint32_t)host_by_id[h].size()), h});
@@ -1426,6 +1730,14 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     hd_len.push_back((uint32_t)host_by_id[p.second].size());
     hd_bytes.insert(hd_bytes.end(), host_by_id[p.second].begin(), host_by_id[p.second].end());
   }
+  const uint32_t ht_cap = (uint32_t)next_pow2(std::max<size_t>(64, 2 * hd.size()));
+  std::vector<uint32_t> ht(2 * ht_cap, 0);
+  for (uint32_t i = 0; i < hd.size(); ++i) {
+    uint32_t slot = (uint32_t)hd[i].first & (ht_cap - 1);
+    while (ht[2 * slot]) slot = (slot + 1) & (ht_cap - 1);
+    ht[2 * slot] = (uint32_t)(hd[i].first >> 32) | 1u;
+    ht[2 * slot + 1] = i;
+  }
   std::vector<int32_t> host_scope(n_hosts, -1);
   for (auto &s : scope_of_site) host_scope[hosts[s.first]] = s.second;
   std::vector<uint64_t> skip;
@@ -1433,6 +1745,72 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     for (auto &h : rs->rules[i].skip_hosts) skip.push_back(((uint64_t)i << 32) | hosts[h]);
   std::sort(skip.begin(), skip.end());
   skip.erase(std::unique(skip.begin(), skip.end()), skip.end());
+
+  // scan-pass rule tables: per scope (host, or n_hosts = none) ALWAYS / skip
+  // masks over applicable positions < 128; rules needing a DFA on every line;
+  // literal rules; and literal -> rules requiring it
+  auto mode_of = [&](uint32_t r) {
+    const RuleMode m = rs->rules[r].rx.mode;
+    return (m == kModePrefilter && !use_pref) ? kModeScan : m;
+  };
+  auto equiv_of = [&](uint32_t r) { return rs->rules[r].rx.pref_equivalent ? 0x80000000u : 0u; };
+  std::vector<uint64_t> sc_always(2 * (n_hosts + 1), 0), sc_skipm(2 * (n_hosts + 1), 0);
+  for (uint32_t sc = 0; sc <= n_hosts; ++sc) {
+    const uint32_t nsite = sc < n_hosts ? (uint32_t)per_host[sc].size() : 0;
+    for (uint32_t pos = 0; pos < nsite + rs->n_global && pos < 128; ++pos) {
+      const uint32_t r = pos < nsite ? per_host[sc][pos] : pos - nsite;
+      if (mode_of(r) == kModeAlways) sc_always[2 * sc + pos / 64] |= 1ull << (pos % 64);
+      if (sc < n_hosts && std::binary_search(skip.begin(), skip.end(), ((uint64_t)r << 32) | sc))
+        sc_skipm[2 * sc + pos / 64] |= 1ull << (pos % 64);
+    }
+  }
+  std::vector<uint32_t> dfa_site_off(n_hosts + 1, 0), pref_site_off(n_hosts + 1, 0);
+  std::vector<uint2> dfa_site, pref_site, dfa_glob, pref_glob;
+  for (uint32_t h = 0; h < n_hosts; ++h) {
+    dfa_site_off[h] = (uint32_t)dfa_site.size();
+    pref_site_off[h] = (uint32_t)pref_site.size();
+    for (uint32_t k = 0; k < per_host[h].size(); ++k) {
+      const uint32_t r = per_host[h][k];
+      const RuleMode m = mode_of(r);
+      if (m == kModeAnchored || m == kModeScan) dfa_site.push_back(make_uint2(r, k));
+      else if (m == kModePrefilter) pref_site.push_back(make_uint2(r, k));
+    }
+  }
+  dfa_site_off[n_hosts] = (uint32_t)dfa_site.size();
+  pref_site_off[n_hosts] = (uint32_t)pref_site.size();
+  for (uint32_t g = 0; g < rs->n_global; ++g) {
+    const RuleMode m = mode_of(g);
+    if (m == kModeAnchored || m == kModeScan) dfa_glob.push_back(make_uint2(g, g));
+    else if (m == kModePrefilter) pref_glob.push_back(make_uint2(g, g));
+  }
+  const uint32_t n_lit = (uint32_t)lit_off.size();
+  std::vector<std::vector<uint2>> lr_g(n_lit);
+  std::vector<std::vector<std::pair<int32_t, uint2>>> lr_s(n_lit);
+  if (use_pref) {
+    for (uint32_t g = 0; g < rs->n_global; ++g)
+      if (mode_of(g) == kModePrefilter)
+        for (uint32_t i = drules[g].lits_off; i < drules[g].lits_off + drules[g].lits_len; ++i)
+          lr_g[rule_lits[i]].push_back(make_uint2(g | equiv_of(g), g));
+    for (uint32_t h = 0; h < n_hosts; ++h)
+      for (uint32_t k = 0; k < per_host[h].size(); ++k) {
+        const uint32_t r = per_host[h][k];
+        if (mode_of(r) != kModePrefilter) continue;
+        for (uint32_t i = drules[r].lits_off; i < drules[r].lits_off + drules[r].lits_len; ++i)
+          lr_s[rule_lits[i]].push_back({(int32_t)h, make_uint2(r | equiv_of(r), k)});
+      }
+  }
+  std::vector<uint32_t> lr_off(n_lit + 1, 0), lr_gend(std::max<uint32_t>(1, n_lit), 0);
+  std::vector<uint2> lr_ent;
+  std::vector<int32_t> lr_host;
+  for (uint32_t l = 0; l < n_lit; ++l) {
+    lr_off[l] = (uint32_t)lr_ent.size();
+    for (auto &x : lr_g[l]) { lr_ent.push_back(x); lr_host.push_back(-1); }
+    lr_gend[l] = (uint32_t)lr_ent.size();
+    std::stable_sort(lr_s[l].begin(), lr_s[l].end(),
+                     [](const std::pair<int32_t, uint2> &a, const std::pair<int32_t, uint2> &b) { return a.first < b.first; });
+    for (auto &x : lr_s[l]) { lr_ent.push_back(x.second); lr_host.push_back(x.first); }
+  }
+  lr_off[n_lit] = (uint32_t)lr_ent.size();
 
   // allow scopes (decision.go:278-374): exact maps are last-writer-wins in
   // config order; Allow IPFilters hold every allow entry
@@ -1483,6 +1861,32 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   sc_sub_off[n_scopes] = (uint32_t)sc_sub.size();
   sc_str_off[n_scopes] = (uint32_t)sc_str_hash.size();
 
+  // lookup image (LDS-resident in the scan pass when it fits)
+  std::vector<uint8_t> img;
+  auto put = [&](const void *p, size_t nbytes) {
+    const size_t off = (img.size() + 15) & ~size_t(15);
+    img.resize(off + nbytes + 4, 0);
+    if (nbytes) memcpy(img.data() + off, p, nbytes);
+    return (uint32_t)off;
+  };
+  std::vector<uint64_t> hrec(hd.size());
+  for (size_t i = 0; i < hd.size(); ++i) hrec[i] = ((uint64_t)hd_off[i] << 32) | hd_len[i];
+  std::vector<uint32_t> lrec(lit_off.size()), lci((lit_bytes.size() + 31) / 32 + 1, 0);
+  for (size_t i = 0; i < lit_off.size(); ++i) lrec[i] = (lit_off[i] << 8) | lit_len[i];
+  for (size_t q = 0; q < lit_ci.size(); ++q)
+    if (lit_ci[q]) lci[q >> 5] |= 1u << (q & 31);
+  ImgLayout il;
+  il.gt = put(gt2.data(), gt2.size() * 4);
+  il.ge = put(gt2_ent.data(), gt2_ent.size() * 4);
+  il.ht = put(ht.data(), ht.size() * 4);
+  il.hrec = put(hrec.data(), hrec.size() * 8);
+  il.hid = put(hd_id.data(), hd_id.size() * 4);
+  il.hbytes = put(hd_bytes.data(), hd_bytes.size());
+  il.lrec = put(lrec.data(), lrec.size() * 4);
+  il.lbytes = put(lit_bytes.data(), lit_bytes.size());
+  il.lci = put(lci.data(), lci.size() * 4);
+  img.resize((img.size() + 15) & ~size_t(15), 0);
+
   BlobBuilder bb;
   size_t o_rules = bb.add(drules), o_trans = bb.add(trans), o_ae = bb.add(ae), o_ascii = bb.add(ascii),
          o_na = bb.add(nonascii), o_lits = bb.add(lits), o_glob = bb.add(global_rules), o_soff = bb.add(site_off),
@@ -1490,9 +1894,11 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
          o_hdlen = bb.add(hd_len), o_hdb = bb.add(hd_bytes), o_hsc = bb.add(host_scope), o_skip = bb.add(skip),
          o_sao = bb.add(sc_addr_off), o_sa = bb.add(sc_addr), o_sso = bb.add(sc_sub_off), o_ss = bb.add(sc_sub),
          o_sto = bb.add(sc_str_off), o_sth = bb.add(sc_str_hash), o_stb = bb.add(sc_str_boff), o_stl = bb.add(sc_str_len),
-         o_stbytes = bb.add(sc_str_bytes), o_gbits = bb.add(gram_bits), o_gtk = bb.add(gt_key), o_gto = bb.add(gt_off),
-         o_gtl = bb.add(gt_len), o_gte = bb.add(gt_entries), o_lb = bb.add(lit_bytes), o_lci = bb.add(lit_ci),
-         o_lo = bb.add(lit_off), o_ll = bb.add(lit_len), o_rl = bb.add(rule_lits);
+         o_stbytes = bb.add(sc_str_bytes), o_gbits = bb.add(gram_bits),
+         o_rl = bb.add(rule_lits), o_img = bb.add(img), o_lro = bb.add(lr_off), o_lrg = bb.add(lr_gend),
+         o_lre = bb.add(lr_ent), o_lrh = bb.add(lr_host), o_sca = bb.add(sc_always), o_scs = bb.add(sc_skipm),
+         o_dso = bb.add(dfa_site_off), o_ds = bb.add(dfa_site), o_dg = bb.add(dfa_glob), o_pso = bb.add(pref_site_off),
+         o_ps = bb.add(pref_site), o_pg = bb.add(pref_glob);
   e->bind_blob.ensure(bb.bytes.size());
   HIP_OK(hipMemcpy(e->bind_blob.p, bb.bytes.data(), bb.bytes.size(), hipMemcpyHostToDevice));
   uint8_t *base = e->bind_blob.p;
@@ -1531,19 +1937,31 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.any_allow = any_allow ? 1 : 0;
   B.mask_words = std::max<uint32_t>(1, (max_app + 63) / 64);
   B.gram_bits = reinterpret_cast<const uint32_t *>(base + o_gbits);
-  B.gt_key = reinterpret_cast<const uint32_t *>(base + o_gtk);
-  B.gt_off = reinterpret_cast<const uint32_t *>(base + o_gto);
-  B.gt_len = reinterpret_cast<const uint32_t *>(base + o_gtl);
-  B.gt_entries = reinterpret_cast<const uint32_t *>(base + o_gte);
-  B.lit_bytes = base + o_lb;
-  B.lit_ci = base + o_lci;
-  B.lit_off = reinterpret_cast<const uint32_t *>(base + o_lo);
-  B.lit_len = reinterpret_cast<const uint32_t *>(base + o_ll);
   B.rule_lits = reinterpret_cast<const uint32_t *>(base + o_rl);
-  B.gt_mask = gt_cap - 1;
-  B.n_lits = (uint32_t)lit_off.size();
+  B.n_lits = n_lit;
   B.any_anchored = any_anchored ? 1 : 0;
-  B.any_prefilter = lit_off.empty() ? 0 : 1;
+  B.any_prefilter = use_pref ? 1 : 0;
+  B.img = base + o_img;
+  B.img_bytes = (uint32_t)img.size();
+  B.il = il;
+  B.gt2_cap = gt2_cap;
+  B.gt2_nent = (uint32_t)gt2_ent.size();
+  B.ht_cap = ht_cap;
+  B.max_app = max_app;
+  B.lr_off = reinterpret_cast<const uint32_t *>(base + o_lro);
+  B.lr_gend = reinterpret_cast<const uint32_t *>(base + o_lrg);
+  B.lr_ent = reinterpret_cast<const uint2 *>(base + o_lre);
+  B.lr_host = reinterpret_cast<const int32_t *>(base + o_lrh);
+  B.sc_always = reinterpret_cast<const uint64_t *>(base + o_sca);
+  B.sc_skip = reinterpret_cast<const uint64_t *>(base + o_scs);
+  B.dfa_site_off = reinterpret_cast<const uint32_t *>(base + o_dso);
+  B.dfa_site = reinterpret_cast<const uint2 *>(base + o_ds);
+  B.dfa_glob = reinterpret_cast<const uint2 *>(base + o_dg);
+  B.n_dfa_glob = (uint32_t)dfa_glob.size();
+  B.pref_site_off = reinterpret_cast<const uint32_t *>(base + o_pso);
+  B.pref_site = reinterpret_cast<const uint2 *>(base + o_ps);
+  B.pref_glob = reinterpret_cast<const uint2 *>(base + o_pg);
+  B.n_pref_glob = (uint32_t)pref_glob.size();
   e->host_rules = drules;
   e->bound_uid = rs->uid;
   e->bound_dec_version = e->decisions_version;
@@ -1697,7 +2115,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   e->scalars.release(); e->res_seq.release(); e->res_rule.release(); e->ev_key.release(); e->ev_res.release();
   e->ev_key2.release(); e->ev_res2.release(); e->heads.release(); e->trip_idx.release(); e->d_trips.release();
   e->d_results.release(); e->q_out.release();
-  e->l_amask.release(); e->l_ares.release(); e->l_cand.release(); e->l_ccnt.release();
+  e->long_list.release(); e->jobs.release(); e->l_cand.release(); e->l_ccnt.release();
   (void)hipEventDestroy(e->ev0); (void)hipEventDestroy(e->ev1); (void)hipEventDestroy(e->evm0); (void)hipEventDestroy(e->evm1);
   for (auto &x : e->ph) (void)hipEventDestroy(x);
   (void)hipStreamDestroy(e->stream);
@@ -1726,9 +2144,18 @@ extern "C" int bjx_engine_set_decision_lists(bjx_engine *e, const bjx_decision_e
 
 // phase boundaries: 0 start, 1 counted (pass A), 2 scanned (pass B), 3 resolved
 // (pass C + fallback), 4 emitted, 5 sorted, 6 segmented, 7 rate-limited, 8 trips
+static bool trace_on() {
+  static const bool on = getenv("BJX_TRACE") != nullptr;
+  return on;
+}
+
 static void mark(bjx_engine *e, int k) {
   HIP_OK(hipEventRecord(e->ph[k], e->stream));
   e->phase_rec[k] = true;
+  if (trace_on()) {  // debugging aid: drain the stream at every phase boundary
+    HIP_OK(hipStreamSynchronize(e->stream));
+    fprintf(stderr, "[bjx] phase %d done\n", k);
+  }
 }
 
 static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns, uint32_t flags,
@@ -1764,11 +2191,12 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
   for (auto &r : e->phase_rec) r = false;
   mark(e, 0);
 
-  // ---- pass A: '\n' count per 8 KB tile, exclusive scan -> line index of each tile
-  const uint64_t n_tiles = (n + kScanTile - 1) / kScanTile;
+  // ---- pass A: '\n' count per 4 KB wave tile, exclusive scan -> line index of each tile
+  const uint64_t n_tiles = (n + kWT - 1) / kWT;
   e->tile_counts.ensure(n_tiles);
   e->tile_base.ensure(n_tiles + 1);
-  hipLaunchKernelGGL(k_nl_count8, dim3((unsigned)n_tiles), dim3(kBlock), 0, st, buf, (uint64_t)n, e->tile_counts.p);
+  hipLaunchKernelGGL(k_nl_count_wt, dim3((unsigned)((n_tiles + 3) / 4)), dim3(kBlock), 0, st, buf, (uint64_t)n, n_tiles,
+                     e->tile_counts.p);
   HIP_OK(hipGetLastError());
   {
     uint32_t *in = e->tile_counts.p;
@@ -1792,39 +2220,70 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
   e->l_masks.ensure(n_lines * B.mask_words);
   e->l_ipoff.ensure(n_lines); e->l_iplen.ensure(n_lines); e->l_hoff.ensure(n_lines); e->l_hlen.ensure(n_lines);
   e->l_roff.ensure(n_lines); e->l_hid.ensure(n_lines); e->l_flags.ensure(n_lines); e->slow_list.ensure(n_lines);
-  e->l_amask.ensure(n_lines); e->l_ares.ensure(n_lines); e->l_ccnt.ensure(n_lines);
+  e->long_list.ensure(n_lines); e->l_ccnt.ensure(n_lines);
   e->l_cand.ensure(B.any_prefilter ? n_lines * kCandSlots : 1);
   e->scalars.ensure(16);
   Lines L;
   L.ts = e->l_ts.p; L.ip_hash = e->l_iph.p; L.ip_off = e->l_ipoff.p; L.ip_len = e->l_iplen.p; L.host_off = e->l_hoff.p;
   L.host_len = e->l_hlen.p; L.rest_off = e->l_roff.p; L.host_id = e->l_hid.p; L.flags = e->l_flags.p;
-  L.counts = e->l_counts.p; L.masks = e->l_masks.p; L.amask = e->l_amask.p; L.ares = e->l_ares.p;
+  L.counts = e->l_counts.p; L.masks = e->l_masks.p;
   L.cand_cnt = e->l_ccnt.p; L.cand = e->l_cand.p;
-  HIP_OK(hipMemsetAsync(e->scalars.p, 0, 16 * sizeof(unsigned long long), st));
-  if (B.any_prefilter) HIP_OK(hipMemsetAsync(e->l_ccnt.p, 0, n_lines * 4, st));
-  mark(e, 1);
-
-  // ---- pass B: the scan kernel (the hot, HBM-bound kernel)
-  ScanArgs A;
-  A.buf = buf; A.n = n; A.n_tiles = n_tiles; A.n_lines = n_lines; A.tile_base = e->tile_base.p; A.nl = e->nl.p;
-  A.L = L; A.now_ns = now_ns; A.slow_list = e->slow_list.p; A.slow_count = e->scalars.p; A.stats = e->scalars.p + 8;
-  HIP_OK(hipEventRecord(e->evm0, st));
-  const unsigned scan_grid = (unsigned)std::min<uint64_t>(n_tiles, 256 * 8);
-  hipLaunchKernelGGL(k_scan, dim3(scan_grid), dim3(kBlock), 0, st, B, A);
-  HIP_OK(hipGetLastError());
-  HIP_OK(hipEventRecord(e->evm1, st));
-  mark(e, 2);
+  e->jobs.ensure(std::max<uint64_t>(e->jobs.n, n_lines + (1u << 20)));
   uint64_t last_nl = 0;
-  unsigned long long n_slow = 0;
-  HIP_OK(hipMemcpyAsync(&last_nl, e->nl.p + (n_lines - 1), 8, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipMemcpyAsync(&n_slow, e->scalars.p, 8, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipMemcpyAsync(e->scan_stats, e->scalars.p + 8, 16, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
-  out->consumed_bytes = last_nl + 1;
+  unsigned long long sc4[5] = {0, 0, 0, 0, 0};
+  for (int attempt = 0;; ++attempt) {
+    HIP_OK(hipMemsetAsync(e->scalars.p, 0, 16 * sizeof(unsigned long long), st));
+    if (B.any_prefilter) HIP_OK(hipMemsetAsync(e->l_ccnt.p, 0, n_lines * 4, st));
+    mark(e, 1);
 
-  // ---- pass C: per-line rule decisions; per-line fallback for rare lines
-  hipLaunchKernelGGL(k_resolve, dim3(grid_for(n_lines)), dim3(kBlock), 0, st, B, buf, e->nl.p, n_lines, L);
-  HIP_OK(hipGetLastError());
+    // ---- the scan kernel (the hot, HBM-bound kernel)
+    ScanArgs A;
+    A.buf = buf; A.n = n; A.n_tiles = n_tiles; A.n_lines = n_lines; A.tile_base = e->tile_base.p; A.nl = e->nl.p;
+    A.L = L; A.now_ns = now_ns; A.slow_list = e->slow_list.p; A.slow_count = e->scalars.p;
+    A.long_list = e->long_list.p; A.long_count = e->scalars.p + 10; A.stats = e->scalars.p + 8;
+    A.jobs = e->jobs.p; A.job_count = e->scalars.p + 11; A.job_cap = e->jobs.n;
+    // block-shared LDS: gram bitset, the lookup image when it fits, then 16 wave regions
+    const uint32_t fixed = kGramWords * 4 + kScanWaves * kWaveLds;
+    const bool img_lds = fixed + B.img_bytes <= kScanLdsMax;
+    A.shared_bytes = kGramWords * 4 + (img_lds ? B.img_bytes : 0);
+    const uint32_t lds = A.shared_bytes + kScanWaves * kWaveLds;
+    const void *kfn = img_lds ? reinterpret_cast<const void *>(&k_scan<true>) : reinterpret_cast<const void *>(&k_scan<false>);
+    if (lds != e->scan_lds[img_lds]) {
+      HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      e->scan_lds[img_lds] = lds;
+    }
+    HIP_OK(hipEventRecord(e->evm0, st));
+    const unsigned grid = (unsigned)std::min<uint64_t>((n_tiles + kScanWaves - 1) / kScanWaves, 256);
+    if (img_lds) hipLaunchKernelGGL(k_scan<true>, dim3(grid), dim3(kScanWaves * 64), lds, st, B, A);
+    else hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kScanWaves * 64), lds, st, B, A);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(e->evm1, st));
+    mark(e, 2);
+    HIP_OK(hipMemcpyAsync(&last_nl, e->nl.p + (n_lines - 1), 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(sc4, e->scalars.p + 8, 32, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(sc4 + 4, e->scalars.p, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (sc4[3] <= e->jobs.n) break;
+    // more DFA jobs than the buffer holds: grow it and redo the (idempotent) scan
+    if (attempt > 0) throw BjxError(BJX_ERR_DEVICE, "internal: DFA job buffer overflow");
+    e->jobs.ensure(sc4[3] + (1u << 20));
+  }
+  out->consumed_bytes = last_nl + 1;
+  const unsigned long long n_slow = sc4[4], n_long = sc4[2], n_jobs = sc4[3];
+  e->last_jobs = n_jobs;
+  if (n_jobs) {
+    hipLaunchKernelGGL(k_dfa, dim3(grid_for(n_jobs)), dim3(kBlock), 0, st, B, buf, e->nl.p, e->jobs.p, (uint64_t)n_jobs, L);
+    HIP_OK(hipGetLastError());
+  }
+  e->scan_stats[0] = sc4[0]; e->scan_stats[1] = sc4[1]; e->scan_stats[2] = n_slow; e->scan_stats[3] = n_long;
+  e->scan_stats[4] = n_jobs;
+
+  // ---- long lines from HBM; per-line fallback for rare lines
+  if (n_long) {
+    hipLaunchKernelGGL(k_resolve_long, dim3(grid_for(n_long)), dim3(kBlock), 0, st, B, buf, e->nl.p, e->long_list.p,
+                       (uint64_t)n_long, L);
+    HIP_OK(hipGetLastError());
+  }
   if (n_slow) {
     hipLaunchKernelGGL(k_parse_match<true>, dim3(grid_for(n_slow)), dim3(kBlock), 0, st, B, buf, e->nl.p, (uint64_t)n_slow,
                        e->slow_list.p, now_ns, L, e->slow_list.p, e->scalars.p);
@@ -2084,9 +2543,8 @@ extern "C" size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap) {
 }
 extern "C" size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap) {
   if (!e) return 0;
-  const uint64_t v[3] = {e->scan_stats[0], e->scan_stats[1], e->last_slow};
-  for (size_t k = 0; k < cap && k < 3; ++k) out[k] = v[k];
-  return 3;
+  for (size_t k = 0; k < 5 && k < cap; ++k) out[k] = e->scan_stats[k];
+  return 5;
 }
 extern "C" size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t i, char *out, size_t cap) {
   if (!rs || i >= rs->rules.size()) return 0;
@@ -2095,6 +2553,11 @@ extern "C" size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t i, char *
   std::string l = std::to_string((int)rx.mode) + " " + std::to_string((int)rx.pref_equivalent);
   for (const PrefLit &pl : rx.pref) {
     l += "\n" + std::to_string(pl.gram_off) + " ";
+    for (char c : pl.ci) l += c ? '1' : '0';
+    l += " " + pl.s;
+  }
+  for (const PrefLit &pl : rx.anchor) {
+    l += std::string("\n^") + (rx.anchor_equivalent ? "=" : "~") + " ";
     for (char c : pl.ci) l += c ? '1' : '0';
     l += " " + pl.s;
   }

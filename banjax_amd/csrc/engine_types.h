@@ -19,21 +19,33 @@ struct DevRule {
   uint16_t lits_len;
   uint8_t mode;          // RuleMode
   uint8_t equiv;         // match <=> one of its literals occurs in rest
+  uint32_t anc_off;      // anchored rules: prefix literal ids rule_lits[anc_off .. + anc_len)
+  uint16_t anc_len;
+  uint8_t anc_equiv;     // match <=> rest starts with one of them
+  uint8_t _pad;
   int64_t interval_ns;
   int64_t hits;
 };
 
 // Prefilter gram bitset: one bit per hash of a 4-byte window (LDS resident).
-constexpr uint32_t kGramLog2 = 18;
+// Full-rate hash (24-bit multiply after folding the top byte in).
+constexpr uint32_t kGramLog2 = 16;
 constexpr uint32_t kGramWords = (1u << kGramLog2) / 32;
-__host__ __device__ inline uint32_t gram_hash(uint32_t g) { return (g * 0x9E3779B1u) >> (32 - kGramLog2); }
-constexpr int kCandSlots = 4;
+__host__ __device__ inline uint32_t gram_hash(uint32_t g) {
+  const uint32_t x = g ^ (g >> 15);
+  return ((x & 0xFFFFFFu) * 0x2C1B3Bu >> 8) & ((1u << kGramLog2) - 1);
+}
+constexpr int kCandSlots = 4;  // literal hits kept per long line (more = overflow: every rule by DFA)
 
 struct Subnet {
   uint8_t net[16];
   uint8_t mask[16];
   uint32_t netlen;  // 4 (IPv4 compare, To4 semantics) or 16
   uint32_t _pad;
+};
+
+struct ImgLayout {
+  uint32_t gt, ge, ht, hrec, hid, hbytes, lrec, lbytes, lci;
 };
 
 // Everything the per-line kernels need about the current (ruleset, decision
@@ -74,19 +86,43 @@ struct Bind {
   uint32_t mask_words;         // ceil(max applicable rules per line / 64)
   // prefilter
   const uint32_t *gram_bits;   // kGramWords
-  const uint32_t *gt_key;      // open-addressing gram table (gt_mask + 1 slots)
-  const uint32_t *gt_off;      // entries offset (pairs lit, gram offset)
-  const uint32_t *gt_len;      // 0 = empty slot
-  const uint32_t *gt_entries;
-  const uint8_t *lit_bytes;
-  const uint8_t *lit_ci;
-  const uint32_t *lit_off;
-  const uint32_t *lit_len;
   const uint32_t *rule_lits;
-  uint32_t gt_mask;
   uint32_t n_lits;
   uint32_t any_anchored;
   uint32_t any_prefilter;
+  ImgLayout il;
+  // Lookup image for the scan pass (one blob, copied whole to LDS when it
+  // fits; ImgLayout gives the offsets):
+  //   gram table  gt2_cap slots of (key, entries offset << 16 | count),
+  //               entries (lit << 8 | window offset)
+  //   host table  ht_cap slots of (hash tag, hd index); host records
+  //               (bytes offset << 32 | len) and ids; host bytes
+  //   literals    (bytes offset << 8 | len); bytes; ASCII-ci bits
+  const uint8_t *img;
+  uint32_t img_bytes;
+  uint32_t gt2_cap, gt2_nent;
+  uint32_t ht_cap;
+  uint32_t max_app;            // most rules applicable to one line (<= 128 on the scan path)
+  // literal -> rules that require it: [lr_off[l], lr_gend[l]) global rules,
+  // [lr_gend[l], lr_off[l+1]) site rules sorted by host (lr_host)
+  const uint32_t *lr_off;
+  const uint32_t *lr_gend;
+  const uint2 *lr_ent;         // (rule | equiv << 31, index in its site / global list)
+  const int32_t *lr_host;
+  // per scope (host id, or n_hosts = no per-site rules): 2-word masks over the
+  // applicable-rule positions of ALWAYS rules and of hosts_to_skip hits
+  const uint64_t *sc_always;
+  const uint64_t *sc_skip;
+  // rules that need a DFA on every line (anchored / no literal), and rules
+  // with literals (used when a line overflows its hit slots)
+  const uint32_t *dfa_site_off;  // n_hosts + 1
+  const uint2 *dfa_site;         // (rule, index)
+  const uint2 *dfa_glob;
+  uint32_t n_dfa_glob;
+  const uint32_t *pref_site_off;
+  const uint2 *pref_site;
+  const uint2 *pref_glob;
+  uint32_t n_pref_glob;
 };
 
 // Per-line SoA arrays (batch workspace).
@@ -98,10 +134,8 @@ struct Lines {
   uint8_t *flags;
   uint64_t *counts;    // (n_results << 32) | n_events per line, then scanned in place
   uint64_t *masks;     // mask_words per line
-  uint64_t *amask;     // anchored rules decided in the scan pass (positions < 64)
-  uint64_t *ares;      // anchored rules left unresolved by the scan pass
-  uint32_t *cand_cnt;  // prefilter candidates per line
-  uint64_t *cand;      // kCandSlots per line: (start position << 24) | literal id
+  uint32_t *cand_cnt;  // long lines: literal hits recorded by the scan pass
+  uint64_t *cand;      // kCandSlots per line: (literal start << 24) | literal id
 };
 
 // Persistent rate-limit state (RegexRateLimitStates, rate_limit.go:17-21),
@@ -124,8 +158,7 @@ struct State {
 enum LineFlagBits : uint8_t {
   kLineError = 1, kLineOld = 2, kLineExempt = 4,
   kLineSlowTs = 0x40,     // per-line fallback kernel (timestamp / long header)
-  kLineExemptPending = 0x20,
-  kLineAnchoredHigh = 0x10, // anchored rules at positions >= 64: resolve in k_resolve
+  kLineLong = 0x80,       // line ends past the scan window: rules decided by k_resolve_long
 };
 
 }  // namespace bjx

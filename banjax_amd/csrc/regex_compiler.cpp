@@ -1014,6 +1014,31 @@ bool anchored_start(const Re *r) {
   return false;
 }
 
+// Anchored rules: the exact strings every match starts with (the longest run
+// of exact, assertion-free pieces after \A), and whether the rest of the
+// pattern can match anything (only .* left), so that the prefix decides alone.
+bool anchored_prefix(const Re *r, LSet *pre, bool *equiv) {
+  while (r->op == kCap) r = r->sub[0].get();
+  if (r->op != kConcat || r->sub.empty()) return false;
+  const Re *first = r->sub[0].get();
+  while (first->op == kCap) first = first->sub[0].get();
+  if (first->op != kBOT) return false;
+  LSet run{LStr{}};
+  size_t k = 1;
+  for (; k < r->sub.size(); ++k) {
+    LInfo c = analyze(r->sub[k].get());
+    LSet nr;
+    if (!c.exact || !c.pure || !cross(run, c.ex, &nr)) break;
+    run = std::move(nr);
+  }
+  if (!nonempty_all(run)) return false;
+  bool rest_any = true;
+  for (size_t i = k; i < r->sub.size(); ++i) rest_any = rest_any && is_dotstar(r->sub[i].get());
+  *pre = std::move(run);
+  *equiv = rest_any;
+  return true;
+}
+
 // match <=> text contains one of S, when the pattern is (.*)* X (.*)* with X
 // pure and exact (S = X's strings), since .* can always match empty.
 bool prefilter_equivalent(const Re *r, const LSet &chosen) {
@@ -1386,7 +1411,15 @@ int compile_regex(const std::string &pattern, CompiledRegex *out, std::string *e
   }
   if (out->flags & kRuleAlways) out->mode = kModeAlways;
   else if (out->flags & kRuleNever) out->mode = kModeNever;
-  else if (anchored_start(root.get())) out->mode = kModeAnchored;
+  else if (anchored_start(root.get())) {
+    out->mode = kModeAnchored;
+    LSet pre;
+    bool eq = false;
+    if (anchored_prefix(root.get(), &pre, &eq)) {
+      for (auto &x : pre) out->anchor.push_back(PrefLit{x.s, x.ci, 0});
+      out->anchor_equivalent = eq;
+    }
+  }
   else {
     LInfo li = analyze(root.get());
     LSet best;

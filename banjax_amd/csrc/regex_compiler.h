@@ -51,6 +51,9 @@ struct CompiledRegex {
   // every match contains at least one of these (kModePrefilter); each >= 4 bytes
   std::vector<PrefLit> pref;
   bool pref_equivalent = false;  // match <=> text contains one of `pref`
+  // kModeAnchored: every match starts with one of these (exact, ASCII-ci as above)
+  std::vector<PrefLit> anchor;
+  bool anchor_equivalent = false;  // match <=> text starts with one of `anchor`
   std::string required_literal;  // diagnostics: the first prefilter literal
 };
 

@@ -101,9 +101,10 @@ class Engine:
     PHASES = ("count", "scan", "resolve", "emit", "event_sort", "segment", "rate_limit", "trips")
 
     def scan_stats(self):
-        out = (C.c_uint64 * 3)()
-        _lib.lib().bjx_debug_scan_stats(self._h, out, 3)
-        return {"gram_probes": out[0], "candidates": out[1], "fallback_lines": out[2]}
+        out = (C.c_uint64 * 5)()
+        _lib.lib().bjx_debug_scan_stats(self._h, out, 5)
+        return {"gram_bitset_hits": out[0], "literal_hits": out[1], "fallback_lines": out[2], "long_lines": out[3],
+                "dfa_jobs": out[4]}
 
     def phase_ms(self):
         out = (C.c_double * 8)()

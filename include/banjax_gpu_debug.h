@@ -21,7 +21,8 @@ size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t rule_idx, char *out,
 /* device ms of the last batch's phases: framing, match, slow timestamps, emit,
    event sort, segmenting, rate limit, trips (returns the phase count) */
 size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap);
-/* last batch: gram-table probes, literal candidates, lines sent to the per-line fallback */
+/* last batch: gram bitset hits, recorded literal hits, lines sent to the per-line
+   fallback, lines decided by the long-line pass, DFA jobs */
 size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap);
 #ifdef __cplusplus
 }

@@ -770,12 +770,12 @@ int orc_decision_get(orc_state *s, const char *ip, size_t il, int *decision, int
   Expiring *e = sl->v;
   *decision = e->decision; *expires = e->expires;
   if (domain && cap) { size_t k = e->dl < cap - 1 ? e->dl : cap - 1; memcpy(domain, e->domain, k); domain[k] = 0; }
-  return 1;
+  return (int)e->dl + 1;  /* found: domain length + 1 (caller re-asks with a larger buffer) */
 }
 int64_t orc_decision_len(orc_state *s) { return (int64_t)s->decisions.n; }
 size_t orc_last_banned_ip(orc_state *s, char *out, size_t cap) {
   size_t k = s->banned_len < cap ? s->banned_len : cap;
-  if (s->banned_ip) memcpy(out, s->banned_ip, k);
+  if (s->banned_ip && out) memcpy(out, s->banned_ip, k);
   return s->banned_len;
 }
 size_t orc_ban_log(orc_state *s, char *out, size_t cap) {

@@ -197,18 +197,24 @@ class State:
 
     def decision(self, ip):
         d, e = C.c_int(), C.c_int64()
-        dom = C.create_string_buffer(512)
         ib = _b(ip)
-        if lib().orc_decision_get(self._h, ib, len(ib), C.byref(d), C.byref(e), dom, 512):
-            return d.value, e.value, dom.value.decode(errors="replace")
-        return None
+        cap = 512
+        while True:
+            dom = C.create_string_buffer(cap)
+            r = lib().orc_decision_get(self._h, ib, len(ib), C.byref(d), C.byref(e), dom, cap)
+            if r == 0:
+                return None
+            if r <= cap:
+                return d.value, e.value, dom.raw[:r - 1].decode(errors="replace")
+            cap = r
 
     def decisions_len(self):
         return lib().orc_decision_len(self._h)
 
     def banned_ip(self):
-        buf = C.create_string_buffer(512)
-        n = lib().orc_last_banned_ip(self._h, buf, 512)
+        n = lib().orc_last_banned_ip(self._h, None, 0)
+        buf = C.create_string_buffer(n + 1)
+        lib().orc_last_banned_ip(self._h, buf, n + 1)
         return buf.raw[:n].decode(errors="replace")
 
     def ban_log(self):

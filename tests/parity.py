@@ -80,11 +80,11 @@ def compare_batch(oflags, ores, oconsumed, out):
         bad = [i for i in range(len(oflags)) if gflags[i] != oflags[i]][:10]
         raise AssertionError("line flags differ at %s: gpu=%s oracle=%s" %
                              (bad, [gflags[i] for i in bad], [oflags[i] for i in bad]))
-    assert out.n_results == len(ores), (out.n_results, len(ores))
     for k, (g, o) in enumerate(zip(out.results, ores)):
         gt = (g.line_idx, g.rule_idx, g.rule_pos, g.skip_host, g.seen_ip, g.match_type, g.exceeded)
         ot = (o.line_idx, o.rule_id, o.rule_pos, o.skip_host, o.seen_ip, o.match_type, o.exceeded)
         if gt != ot:
             raise AssertionError("RuleResult %d differs: gpu=%s oracle=%s" % (k, gt, ot))
+    assert out.n_results == len(ores), (out.n_results, len(ores))
     trips = [(o.line_idx, o.rule_id) for o in ores if o.exceeded]
     assert [(t.line_idx, t.rule_idx) for t in out.trips] == trips

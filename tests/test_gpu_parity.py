@@ -292,3 +292,106 @@ def test_batching_is_associative(engine):
         base += o.n_lines
     assert trips_one == trips_four
     assert sorted(dump_one.split("\n\n")) == sorted(engine.state_dump().split("\n\n"))
+
+
+GEOM_CFG = r"""
+regexes_with_rates:
+  - rule: "all"
+    regex: '.*'
+    interval: 5
+    hits_per_interval: 50
+    decision: challenge
+  - rule: "equiv"
+    regex: 'needle'
+    interval: 1
+    hits_per_interval: 2
+    decision: nginx_block
+  - rule: "nonequiv"
+    regex: 'haystack[0-9]+x'
+    interval: 1
+    hits_per_interval: 1
+    decision: challenge
+  - rule: "ci"
+    regex: '(?i)foobar'
+    interval: 1
+    hits_per_interval: 3
+    decision: challenge
+  - rule: "anch"
+    regex: '^GET \S+ GET /a'
+    interval: 1
+    hits_per_interval: 4
+    decision: challenge
+  - rule: "scan"
+    regex: '[0-9]{3}z'
+    interval: 1
+    hits_per_interval: 0
+    decision: nginx_block
+  - rule: "alt"
+    regex: 'alpha(beta|gamma)delta|omega{2,}'
+    interval: 2
+    hits_per_interval: 1
+    decision: challenge
+per_site_regexes_with_rates:
+  "h.com":
+    - rule: "site"
+      regex: 'sitelit'
+      interval: 1
+      hits_per_interval: 0
+      decision: nginx_block
+    - rule: "equiv"
+      regex: 'needle\d'
+      interval: 1
+      hits_per_interval: 1
+      decision: challenge
+expiring_decision_ttl_seconds: 10
+"""
+
+
+def geom_lines(t, seed, n=3000):
+    """Lines of every length class against the scan geometry (4 KB wave
+    tiles + 512 B halo, <= 128 lines decided per tile): runs of tiny lines,
+    halo-edge lengths, multi-tile lines, literals at random offsets (so they
+    straddle tile and halo edges), long headers."""
+    import random
+    rnd = random.Random(seed)
+    toks = [b"needle", b"haystack123x", b"haystack12", b"FooBar", b"fOOBAR", b"sitelit", b"123z", b"alphagammadelta",
+            b"omegaa", b"needle7", b"GET /a"]
+    out = []
+    i = 0
+    while i < n:
+        kind = rnd.random()
+        if kind < 0.05:  # a run of tiny lines (> 128 per tile)
+            for _ in range(rnd.randint(150, 400)):
+                out.append(b"%d 9.9.9.%d G h G /a" % (t, rnd.randint(0, 9)))
+            i += 1
+            continue
+        if kind < 0.5:
+            size = rnd.randint(40, 300)
+        elif kind < 0.75:
+            size = rnd.randint(300, 800)
+        elif kind < 0.95:
+            size = rnd.randint(800, 9000)
+        else:
+            size = rnd.randint(4000, 12000)
+        host = rnd.choice([b"h.com", b"x.org", b"h.com", b"y" * rnd.randint(1, 700)])
+        m = rnd.choice([b"GET", b"POST"])
+        head = b"%d 10.0.%d.%d %s %s %s /a" % (t, rnd.randint(0, 3), rnd.randint(0, 50), m, host, m)
+        body = bytearray(rnd.choice(b"abcdefghij klmnop0123456789/") for _ in range(max(0, size - len(head))))
+        for _ in range(rnd.randint(0, 4)):
+            tok = rnd.choice(toks)
+            p = rnd.randint(0, max(0, len(body) - len(tok)))
+            body[p:p + len(tok)] = tok
+        out.append(head + bytes(body))
+        i += 1
+    return b"\n".join(out) + b"\n"
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_tile_geometry(engine, seed):
+    t = 1700000000
+    pair = Pair(GEOM_CFG, engine)
+    data = geom_lines(t, seed)
+    pair.feed(data, t * S)
+    # same bytes shifted by a few bytes: every literal lands on other tile offsets
+    pair.feed(b"\n" * (seed * 7) + data, t * S)
+    pair.compare_state(["10.0.0.1", "10.0.1.2", "9.9.9.1"])

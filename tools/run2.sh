@@ -1,3 +1,3 @@
 tools/gpu_session.sh \
- "stats|400|python tools/scan_stats.py cfg3 20000000 3 && python tools/scan_stats.py cfg2 20000000 2 && python tools/scan_stats.py cfg4 2000000 2 && python tools/scan_stats.py cfg5 20000000 2 && python tools/scan_stats.py cfg1 1000000 2" \
- "bench_full|500|python bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+ "pytest_gpu|400|python -m pytest tests -m gpu -v -p no:cacheprovider --timeout 120" \
+ "prof|600|tools/prof_scan.sh cfg3v3 cfg3 10000000"
