@@ -53,18 +53,44 @@ BJX_HD uint64_t mix64(uint64_t x) {
   x ^= x >> 33;
   return x;
 }
-// 64-bit hash of a byte string; never returns 0 or ~0 (table sentinels).
+// 4 little-endian bytes at p, any alignment.  Device: two aligned 32-bit
+// loads + v_alignbyte (LDS and HBM alike); the aligned word may extend up to 3
+// bytes past p + 3, so callers keep 4 readable bytes of slack (all scan
+// buffers and tables are padded).  Host: memcpy.
+inline uint32_t ld4(const uint8_t *p) {
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);
+  return v;
+}
+#ifdef __HIPCC__
+__device__ __forceinline__ uint32_t ld4(const uint8_t *p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  return sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
+}
+#endif
+
+BJX_HD uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+// 64-bit hash of a byte string (engine-internal: host dictionary, IP state
+// keys); 4 bytes per step in two 32-bit lanes, murmur3-style finalizer.
+// Never returns 0 or ~0 (table sentinels).
 BJX_HD uint64_t hash_bytes(const uint8_t *p, uint32_t n) {
-  uint64_t h = 0x9E3779B97F4A7C15ULL ^ (uint64_t)n;
+  uint32_t a = 0x9E3779B9u ^ n, b = 0x7F4A7C15u + n * 0x85EBCA6Bu;
   uint32_t i = 0;
-  for (; i + 8 <= n; i += 8) {
-    uint64_t w = 0;
-    for (int k = 0; k < 8; ++k) w |= (uint64_t)p[i + k] << (8 * k);
-    h = mix64(h ^ w) + 0x632BE59BD9B4E019ULL;
+  for (; i + 4 <= n; i += 4) {
+    const uint32_t w = ld4(p + i);
+    a = rotl32(a ^ w, 7) * 0x27D4EB2Du;
+    b = rotl32(b + w, 13) * 0x165667B1u;
   }
-  uint64_t w = 0;
-  for (int k = 0; i + k < n; ++k) w |= (uint64_t)p[i + k] << (8 * k);
-  h = mix64(h ^ w ^ 0xA0761D6478BD642FULL);
+  uint32_t t = 0;
+  for (uint32_t k = 0; i + k < n; ++k) t |= (uint32_t)p[i + k] << (8 * k);
+  a = rotl32(a ^ t ^ 0xA5A5A5A5u, 7) * 0x27D4EB2Du;
+  b = rotl32(b + t, 13) * 0x165667B1u;
+  a ^= b >> 16; a *= 0x85EBCA6Bu; a ^= a >> 13; a *= 0xC2B2AE35u; a ^= a >> 16;
+  b ^= a >> 15; b *= 0x2C1B3C6Du; b ^= b >> 12; b *= 0x297A2D39u; b ^= b >> 15;
+  uint64_t h = ((uint64_t)a << 32) | b;
   if (h == 0 || h == ~0ULL) h = 0x1234567ULL;
   return h;
 }

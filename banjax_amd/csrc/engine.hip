@@ -140,7 +140,10 @@ __device__ __forceinline__ uint32_t find_space(const uint8_t *p, uint32_t i, uin
 }
 
 __device__ __forceinline__ bool bytes_eq(const uint8_t *a, const uint8_t *b, uint32_t n) {
-  for (uint32_t k = 0; k < n; ++k)
+  uint32_t k = 0;
+  for (; k + 4 <= n; k += 4)
+    if (ld4(a + k) != ld4(b + k)) return false;
+  for (; k < n; ++k)
     if (a[k] != b[k]) return false;
   return true;
 }
@@ -377,9 +380,10 @@ constexpr uint32_t kHitSlots = 4;     // verified literal hits kept per line
 constexpr int kScanWaves = 16;        // waves per block (one block per CU)
 constexpr uint32_t kTileLds = kWT + kHalo + 16;
 constexpr uint32_t kWaveJobs = 64;   // DFA jobs staged per wave before one global append
-constexpr uint32_t kWaveLds = kTileLds + kLineCap * (2 + 2 + 4 + 4 * kHitSlots) + kWaveJobs * 8 + 16;
+constexpr uint32_t kWaveLds = kTileLds + kLineCap * (2 + 2);
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kScanLdsMax = 160 * 1024;  // gfx950 LDS per CU (one scan block per CU)
+constexpr uint32_t kLinesImgMax = 32 * 1024;  // k_lines copies the lookup image to LDS up to this size
 
 struct ScanArgs {
   const uint8_t *buf;
@@ -389,16 +393,9 @@ struct ScanArgs {
   const uint64_t *tile_base;  // newlines before each wave tile (pass A)
   uint64_t *nl;
   Lines L;
-  int64_t now_ns;
-  uint32_t *slow_list;
-  unsigned long long *slow_count;
-  uint32_t *long_list;
-  unsigned long long *long_count;
   unsigned long long *stats;  // [0] bitset hits, [1] recorded literal hits
-  uint2 *jobs;                // DFA jobs: (line, rule | position << 24)
-  unsigned long long *job_count;
-  uint64_t job_cap;
   uint32_t shared_bytes;      // per-wave LDS regions start here
+  uint32_t debug_skip;        // timing experiments only (BJX_DEBUG_SKIP): 1 gram phase
 };
 
 // pass A: '\n' count per wave tile
@@ -436,7 +433,8 @@ struct Tabs {
   const uint8_t *hbytes;
   const uint32_t *lrec;
   const uint8_t *lbytes;
-  const uint32_t *lci;
+  const uint8_t *lcim;
+  const uint8_t *lchk;
 };
 __device__ __forceinline__ Tabs make_tabs(const uint8_t *base, const ImgLayout &il) {
   Tabs t;
@@ -448,7 +446,8 @@ __device__ __forceinline__ Tabs make_tabs(const uint8_t *base, const ImgLayout &
   t.hbytes = base + il.hbytes;
   t.lrec = reinterpret_cast<const uint32_t *>(base + il.lrec);
   t.lbytes = base + il.lbytes;
-  t.lci = reinterpret_cast<const uint32_t *>(base + il.lci);
+  t.lcim = base + il.lcim;
+  t.lchk = base + il.lchk;
   return t;
 }
 
@@ -472,14 +471,21 @@ __device__ int32_t host_lookup_ht(const Bind &B, const Tabs &T, const uint8_t *h
 
 __device__ __forceinline__ uint32_t lit_len_of(const Tabs &T, uint32_t lit) { return T.lrec[lit] & 0xFF; }
 
+// literal `lit` at p: 4 bytes per step, (text | case mask) == literal
+// (literals are stored lower-case, 4-byte aligned, zero padded); the literal's
+// rarest other window is compared first, so most failing checks cost one step
 __device__ __forceinline__ bool literal_at(const Tabs &T, uint32_t lit, const uint8_t *p) {
   const uint32_t rec = T.lrec[lit];
   const uint32_t off = rec >> 8, len = rec & 0xFF;
-  for (uint32_t i = 0; i < len; ++i) {
-    const uint32_t q = off + i;
-    const uint8_t t = p[i], l = T.lbytes[q];
-    const bool ci = (T.lci[q >> 5] >> (q & 31)) & 1u;
-    if (ci ? ((t | 0x20) != l) : (t != l)) return false;
+  const uint8_t *lb = T.lbytes + off, *cm = T.lcim + off;
+  const uint32_t c = T.lchk[lit];
+  if ((ld4(p + c) | ld4(cm + c)) != ld4(lb + c)) return false;
+  uint32_t i = 0;
+  for (; i + 4 <= len; i += 4)
+    if ((ld4(p + i) | ld4(cm + i)) != ld4(lb + i)) return false;
+  if (i < len) {
+    const uint32_t m = (1u << (8 * (len - i))) - 1u;
+    if (((ld4(p + i) | ld4(cm + i)) ^ ld4(lb + i)) & m) return false;
   }
   return true;
 }
@@ -632,16 +638,6 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
   uint8_t *T = s_dyn + A.shared_bytes + wave * kWaveLds;
   uint16_t *ls = reinterpret_cast<uint16_t *>(T + kTileLds);
   uint16_t *le = ls + kLineCap;
-  uint32_t *hc = reinterpret_cast<uint32_t *>(le + kLineCap);
-  uint32_t *hs = hc + kLineCap;
-  JobSink S;
-  S.lds = reinterpret_cast<uint2 *>(hs + kLineCap * kHitSlots);
-  S.cnt = reinterpret_cast<uint32_t *>(S.lds + kWaveJobs);
-  S.jobs = A.jobs;
-  S.count = A.job_count;
-  S.cap = A.job_cap;
-  if (lane == 0) *S.cnt = 0;
-  wave_sync();
   const Lines &L = A.L;
   uint32_t n_probe = 0, n_hit = 0;
 
@@ -655,10 +651,19 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
       for (int k = 0; k < 4; ++k) q[k] = src[k];
     } else {
+      // tail tile: bytes past the batch read as 0 (clamped addresses, no branches)
       uint32_t w[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) w[k] = 0;
-      for (uint32_t k = 0; k < 64 && base + k < A.n; ++k) w[k >> 2] |= (uint32_t)A.buf[base + k] << (8 * (k & 3));
+      for (int k = 0; k < 16; ++k) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const uint64_t pos = base + 4 * k + b;
+          const uint32_t byte = A.buf[pos < A.n ? pos : A.n - 1];
+          v |= (pos < A.n ? byte : 0u) << (8 * b);
+        }
+        w[k] = v;
+      }
 #pragma unroll
       for (int k = 0; k < 4; ++k) q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
     }
@@ -677,8 +682,11 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
       if (h + 8 <= A.n) hv = *reinterpret_cast<const uint2 *>(A.buf + h);
       else if (h < A.n) {
         uint32_t a = 0, b = 0;
-        for (uint32_t k = 0; k < 8 && h + k < A.n; ++k) {
-          if (k < 4) a |= (uint32_t)A.buf[h + k] << (8 * k); else b |= (uint32_t)A.buf[h + k] << (8 * (k - 4));
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+          const uint64_t pos = h + k;
+          const uint32_t byte = pos < A.n ? (uint32_t)A.buf[pos < A.n ? pos : A.n - 1] : 0u;
+          if (k < 4) a |= byte << (8 * k); else b |= byte << (8 * (k - 4));
         }
         hv = make_uint2(a, b);
       }
@@ -732,7 +740,7 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
       const uint32_t fl = (uint32_t)__ffsll((unsigned long long)any_h) - 1;
       hfirst = kWT + fl * 8u + (uint32_t)__ffs(__shfl(hmask, fl)) - 1;
     }
-    // ---- nl[] and line start/end positions (tile-relative)
+    // ---- nl[] and the positions of lines starting in this tile (tile-relative)
     {
       uint64_t x = nlm;
       uint32_t r = pre;
@@ -747,6 +755,7 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
         ++r;
       }
     }
+    if (!B.any_prefilter || (A.debug_skip & 1)) continue;
     if (lane == 0 && head) ls[0] = 0;
     const bool last_in_halo = n_st && !last_nl && hfirst != kNone;
     const bool last_long = n_st && !last_nl && hfirst == kNone;
@@ -754,11 +763,10 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
     // the line open at the tile start is long iff it started before the previous
     // tile (that tile has no '\n') or runs past the previous tile's halo
     const bool open_long = !head && (p0 == kNone || p0 >= kHalo || tb == A.tile_base[t - 1]);
-    for (uint32_t k = lane; k < kLineCap; k += 64) hc[k] = 0;
     wave_sync();
 
     // ---- 4-gram prefilter: positions [64 lane, 64 lane + 64) and the last line's halo part
-    if (B.any_prefilter) {
+    {
       const uint32_t nxt = *reinterpret_cast<const uint32_t *>(T + lane * 64u + 64u);
       uint64_t hits = 0;
 #pragma unroll
@@ -773,9 +781,7 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
       const uint32_t hend = last_in_halo ? hfirst : kWT;
       if (lane * 8u + kWT < hend) {
         for (uint32_t k = 0; k < 8 && kWT + lane * 8u + k < hend; ++k) {
-          const uint32_t p = kWT + lane * 8u + k;
-          const uint32_t gg = (uint32_t)T[p] | (uint32_t)T[p + 1] << 8 | (uint32_t)T[p + 2] << 16 | (uint32_t)T[p + 3] << 24;
-          const uint32_t h = gram_hash(gg);
+          const uint32_t h = gram_hash(ld4(T + kWT + lane * 8u + k));
           hh |= ((s_bits[h >> 5] >> (h & 31)) & 1u) << k;
         }
       }
@@ -786,14 +792,13 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
           const uint32_t k = (uint32_t)__ffsll((unsigned long long)x) - 1;
           x &= x - 1;
           const uint32_t p = part == 0 ? lane * 64u + k : kWT + lane * 8u + k;
-          if (T[p] == '\n') continue;
-          const uint32_t g = (uint32_t)T[p] | (uint32_t)T[p + 1] << 8 | (uint32_t)T[p + 2] << 16 | (uint32_t)T[p + 3] << 24;
+          const uint32_t g = ld4(T + p);
+          if ((g & 0xFF) == '\n') continue;
           uint32_t slot = (uint32_t)mix64(g) & (B.gt2_cap - 1);
-          uint32_t key, ol;
+          uint32_t ol;
           for (;;) {
-            key = gt[2 * slot];
             ol = gt[2 * slot + 1];
-            if ((ol & 0xFFFF) == 0 || key == g) break;
+            if ((ol & 0xFFFF) == 0 || gt[2 * slot] == g) break;
             slot = (slot + 1) & (B.gt2_cap - 1);
           }
           if ((ol & 0xFFFF) == 0) continue;
@@ -808,106 +813,30 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
             lk = (int32_t)n_st - 1;
             gline = tb + tot;
           }
-          const bool is_long = lk < 0 ? open_long : (lk == (int32_t)n_st - 1 && last_long);
-          if (lk < 0 && !open_long) continue;  // decided by the previous tile
+          if (lk < 0 && !open_long) continue;  // the previous tile covered it
+          if (gline >= A.n_lines) continue;
+          // lines whose bytes are all in this window are verified here
+          const bool in_window = lk >= 0 && lk < (int32_t)kLineCap && !(lk == (int32_t)n_st - 1 && last_long);
           for (uint32_t ei = 0; ei < (ol & 0xFFFF); ++ei) {
             const uint32_t en = ge[(ol >> 16) + ei];
             const uint32_t lit = en >> 8, goff = en & 0xFF;
-            if (is_long) {
-              const int64_t q0 = (int64_t)(ts0 + p) - (int64_t)goff;
-              if (q0 < 0 || gline >= A.n_lines) continue;
-              const uint32_t c = atomicAdd(&L.cand_cnt[gline], 1u);
-              if (c < (uint32_t)kCandSlots) L.cand[gline * kCandSlots + c] = ((uint64_t)q0 << 24) | lit;
-              ++n_hit;
-            } else if (lk < (int32_t)kLineCap) {
+            const int64_t q0 = (int64_t)(ts0 + p) - (int64_t)goff;
+            if (q0 < 0) continue;
+            uint32_t flag = 0;
+            if (in_window) {
               const int32_t s0 = (int32_t)p - (int32_t)goff;
-              const uint32_t len = lit_len_of(TB, lit);
-              if (s0 < (int32_t)ls[lk] || (uint32_t)s0 + len > le[lk]) continue;
+              if (s0 < (int32_t)ls[lk] || (uint32_t)s0 + lit_len_of(TB, lit) > le[lk]) continue;
               if (!literal_at(TB, lit, T + s0)) continue;
-              const uint32_t c = atomicAdd(&hc[lk], 1u);
-              if (c < kHitSlots) hs[lk * kHitSlots + c] = ((uint32_t)s0 << 16) | lit;
-              ++n_hit;
+              flag = kCandVerified;
             }
+            const uint32_t c = atomicAdd(&L.cand_cnt[gline], 1u);
+            if (c < (uint32_t)kCandSlots) L.cand[gline * kCandSlots + c] = ((uint64_t)q0 << 24) | flag | lit;
+            ++n_hit;
           }
         }
       }
       wave_sync();
     }
-
-    // ---- one lane per line starting in this tile
-    for (uint32_t k = lane; k < n_st; k += 64) {
-      const uint64_t j = tb + k + nh;
-      if (j >= A.n_lines) break;
-      if (k >= kLineCap) { L.flags[j] = kLineSlowTs; push_list(A.slow_list, A.slow_count, j); continue; }
-      const bool is_long = k == n_st - 1 && last_long;
-      const uint32_t s = ls[k];
-      const uint32_t e = is_long ? kWT + kHalo : le[k];
-      L.counts[j] = 0;
-      // first four spaces, 4 bytes at a time (aligned LDS words)
-      uint32_t sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0, ns = 0;
-      for (uint32_t i = s & ~3u; i < e && ns < 4; i += 4) {
-        const uint32_t x = *reinterpret_cast<const uint32_t *>(T + i) ^ 0x20202020u;
-        uint32_t m = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
-        while (m && ns < 4) {
-          const uint32_t p = i + (((uint32_t)__ffs(m) - 1) >> 3);
-          m &= m - 1;
-          if (p < s || p >= e) continue;
-          if (ns == 0) sp0 = p; else if (ns == 1) sp1 = p; else if (ns == 2) sp2 = p; else sp3 = p;
-          ++ns;
-        }
-      }
-      if (ns < 4) {  // SplitN short: Error, or the header runs past the window
-        if (!is_long) L.flags[j] = kLineError;
-        else { L.flags[j] = kLineSlowTs; push_list(A.slow_list, A.slow_count, j); }
-        continue;
-      }
-      double f;
-      if (parse_float_fast(T + s, sp0 - s, &f) != 0) {
-        L.flags[j] = kLineSlowTs;
-        push_list(A.slow_list, A.slow_count, j);
-        continue;
-      }
-      const uint32_t ip_off = sp0 + 1 - s, ip_len = sp1 - sp0 - 1;
-      const uint32_t rest_off = sp1 + 1 - s, host_off = sp2 + 1 - s, host_len = sp3 - sp2 - 1;
-      const int32_t hid = host_lookup_ht(B, TB, T + s + host_off, host_len);
-      const uint32_t napp = (hid >= 0 ? B.site_off[hid + 1] - B.site_off[hid] : 0u) + B.n_global;
-      if (napp > 128) { L.flags[j] = kLineSlowTs; push_list(A.slow_list, A.slow_count, j); continue; }
-      const bool exempt = B.any_allow && check_is_allowed(B, hid, T + s + ip_off, ip_len);
-      L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
-      L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
-      L.host_id[j] = hid;
-      L.ip_hash[j] = hash_bytes(T + s + ip_off, ip_len);
-      const int64_t tsn = ns_from_seconds(f);
-      L.ts[j] = tsn;
-      uint8_t fl = 0;
-      if (go_sub(A.now_ns, tsn) > 10000000000LL) fl = kLineOld;
-      else if (exempt) fl = kLineExempt;
-      if (fl) { L.flags[j] = fl; continue; }
-      if (is_long) { L.flags[j] = kLineLong; push_list(A.long_list, A.long_count, j); continue; }
-      L.flags[j] = 0;
-      uint64_t lits = 0;
-      const uint32_t nhit = hc[k];
-      uint32_t nlit = 0;
-      const uint32_t rs = s + rest_off;
-      for (uint32_t c = 0; c < nhit && c < kHitSlots; ++c) {
-        const uint32_t v = hs[k * kHitSlots + c];
-        if ((v >> 16) >= rs) lits |= (uint64_t)(v & 0xFFFF) << (16 * nlit++);
-      }
-      decide_rules<true>(B, TB, T + rs, e - rs, hid, lits, nlit, nhit > kHitSlots, j, L, S);
-    }
-    // ---- append this tile's DFA jobs (one global atomic per wave tile)
-    wave_sync();
-    const uint32_t nj = min(*S.cnt, kWaveJobs);
-    if (nj) {
-      unsigned long long base = 0;
-      if (lane == 0) base = atomicAdd(A.job_count, (unsigned long long)nj);
-      base = __shfl(base, 0);
-      for (uint32_t i = lane; i < nj; i += 64)
-        if (base + i < A.job_cap) A.jobs[base + i] = S.lds[i];
-    }
-    wave_sync();
-    if (lane == 0) *S.cnt = 0;
-    wave_sync();
   }
   for (int o = 32; o > 0; o >>= 1) {
     n_probe += __shfl_xor(n_probe, o);
@@ -919,30 +848,136 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
   }
 }
 
-// Long lines (past the scan window): header already parsed by k_scan; decide
-// the rules from the globally recorded literal hits, bytes from HBM.
-__global__ __launch_bounds__(kBlock) void k_resolve_long(Bind B, const uint8_t *__restrict__ buf,
-                                                         const uint64_t *__restrict__ nl, const uint32_t *__restrict__ list,
-                                                         uint64_t n, Lines L) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const uint64_t j = list[t];
-  const uint64_t s = j ? nl[j - 1] + 1 : 0;
-  const uint64_t e = nl[j];
-  const uint64_t rs = s + L.rest_off[j];
-  const uint32_t cc = L.cand_cnt[j];
-  const Tabs TB = make_tabs(B.img, B.il);
-  uint64_t lits = 0;
-  uint32_t nlit = 0;
-  for (uint32_t c = 0; c < cc && c < (uint32_t)kCandSlots; ++c) {
-    const uint64_t v = L.cand[j * kCandSlots + c];
-    const uint32_t lit = (uint32_t)(v & 0xFFFFFF);
-    const uint64_t q = v >> 24;
-    if (q >= rs && q + lit_len_of(TB, lit) <= e && literal_at(TB, lit, buf + q)) lits |= (uint64_t)lit << (16 * nlit++);
+// first four spaces of the line [p, p + n): 16 B aligned loads, SWAR compare
+__device__ __forceinline__ uint32_t find_spaces(const uint8_t *p, uint32_t n, uint32_t &sp0, uint32_t &sp1,
+                                                uint32_t &sp2, uint32_t &sp3) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint4 *base = reinterpret_cast<const uint4 *>(a & ~(uintptr_t)15);
+  const uint32_t skip = (uint32_t)(a & 15);
+  uint32_t ns = 0;
+  for (uint32_t c = 0; c * 16 < n + skip && ns < 4; ++c) {
+    const uint4 v = base[c];
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t x = wv[k] ^ 0x20202020u;
+      uint32_t m = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+      while (m && ns < 4) {
+        const int32_t pos = (int32_t)(c * 16 + 4 * k + (((uint32_t)__ffs(m) - 1) >> 3)) - (int32_t)skip;
+        m &= m - 1;
+        if (pos < 0 || pos >= (int32_t)n) continue;
+        if (ns == 0) sp0 = (uint32_t)pos; else if (ns == 1) sp1 = (uint32_t)pos; else if (ns == 2) sp2 = (uint32_t)pos; else sp3 = (uint32_t)pos;
+        ++ns;
+      }
+    }
   }
-  L.flags[j] = 0;
-  JobSink S{};
-  decide_rules<false>(B, TB, buf + rs, (uint32_t)(e - rs), L.host_id[j], lits, nlit, cc > (uint32_t)kCandSlots, j, L, S);
+  return ns;
+}
+
+struct LinesArgs {
+  const uint8_t *buf;
+  const uint64_t *nl;
+  uint64_t n_lines;
+  Lines L;
+  int64_t now_ns;
+  uint32_t *slow_list;
+  unsigned long long *slow_count;
+  uint2 *jobs;
+  unsigned long long *job_count;
+  uint64_t job_cap;
+};
+
+// consumeLine up to the rule loop, one lane per line (regex_rate_limiter.go:113-214):
+// SplitN header, parseTimestamp fast path, host lookup, CheckIsAllowed, OldLine,
+// then the rule decisions from the scan pass's literal hits (DFA work to k_dfa).
+template <bool IMG_LDS>
+__global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
+  uint8_t *s_img = s_dyn;
+  if (IMG_LDS) {
+    for (uint32_t i = threadIdx.x; i < B.img_bytes / 16; i += blockDim.x)
+      reinterpret_cast<uint4 *>(s_img)[i] = reinterpret_cast<const uint4 *>(B.img)[i];
+    __syncthreads();
+  }
+  const Tabs TB = make_tabs(IMG_LDS ? s_img : B.img, B.il);
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  JobSink S;
+  S.lds = reinterpret_cast<uint2 *>(s_dyn + (IMG_LDS ? B.img_bytes : 0) + wave * (kWaveJobs * 8 + 16));
+  S.cnt = reinterpret_cast<uint32_t *>(S.lds + kWaveJobs);
+  S.jobs = A.jobs;
+  S.count = A.job_count;
+  S.cap = A.job_cap;
+  if (lane == 0) *S.cnt = 0;
+  wave_sync();
+  const Lines &L = A.L;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + wave * 64u; base < A.n_lines; base += stride) {
+    const uint64_t j = base + lane;
+    if (j < A.n_lines) {
+      const uint64_t s = j ? A.nl[j - 1] + 1 : 0;
+      const uint32_t n = (uint32_t)(A.nl[j] - s);
+      const uint8_t *p = A.buf + s;
+      uint32_t sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
+      const uint32_t ns = find_spaces(p, n, sp0, sp1, sp2, sp3);
+      double f;
+      int32_t hid = -1;
+      if (ns < 4) {
+        L.flags[j] = kLineError;
+        L.counts[j] = 0;
+      } else if (parse_float_fast(p, sp0, &f) != 0 ||
+                 (hid = host_lookup_ht(B, TB, p + sp2 + 1, sp3 - sp2 - 1),
+                  (hid >= 0 ? B.site_off[hid + 1] - B.site_off[hid] : 0u) + B.n_global > 128)) {
+        // exotic timestamp token or > 128 applicable rules: the per-line fallback
+        L.flags[j] = kLineSlowTs;
+        L.counts[j] = 0;
+        push_list(A.slow_list, A.slow_count, j);
+      } else {
+        const uint32_t ip_off = sp0 + 1, ip_len = sp1 - sp0 - 1;
+        const uint32_t rest_off = sp1 + 1, host_off = sp2 + 1, host_len = sp3 - sp2 - 1;
+        const bool exempt = B.any_allow && check_is_allowed(B, hid, p + ip_off, ip_len);
+        L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
+        L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
+        L.host_id[j] = hid;
+        L.ip_hash[j] = hash_bytes(p + ip_off, ip_len);
+        const int64_t tsn = ns_from_seconds(f);
+        L.ts[j] = tsn;
+        uint8_t fl = 0;
+        if (go_sub(A.now_ns, tsn) > 10000000000LL) fl = kLineOld;
+        else if (exempt) fl = kLineExempt;
+        L.flags[j] = fl;
+        if (fl) {
+          L.counts[j] = 0;
+        } else {
+          // literal hits of the scan pass inside rest (unverified ones checked here)
+          const uint32_t cc = B.any_prefilter ? L.cand_cnt[j] : 0u;
+          uint64_t lits = 0;
+          uint32_t nlit = 0;
+          const uint64_t rs = s + rest_off;
+          for (uint32_t c = 0; c < cc && c < (uint32_t)kCandSlots; ++c) {
+            const uint64_t v = L.cand[j * kCandSlots + c];
+            const uint32_t lit = (uint32_t)(v & 0x7FFFFF);
+            const uint64_t q = v >> 24;
+            if (q < rs) continue;
+            if (!(v & kCandVerified) && (q + lit_len_of(TB, lit) > s + n || !literal_at(TB, lit, A.buf + q))) continue;
+            lits |= (uint64_t)lit << (16 * nlit++);
+          }
+          decide_rules<true>(B, TB, p + rest_off, n - rest_off, hid, lits, nlit, cc > (uint32_t)kCandSlots, j, L, S);
+        }
+      }
+    }
+    // ---- append this wave's DFA jobs (one global atomic per 64 lines)
+    wave_sync();
+    const uint32_t nj = min(*S.cnt, kWaveJobs);
+    if (nj) {
+      unsigned long long jb = 0;
+      if (lane == 0) jb = atomicAdd(A.job_count, (unsigned long long)nj);
+      jb = __shfl(jb, 0);
+      for (uint32_t i = lane; i < nj; i += 64)
+        if (jb + i < A.job_cap) A.jobs[jb + i] = S.lds[i];
+    }
+    wave_sync();
+    if (lane == 0) *S.cnt = 0;
+    wave_sync();
+  }
 }
 
 // DFA jobs from the scan pass: one (line, rule) per lane; a match sets the
@@ -1546,9 +1581,15 @@ static bool window_variant(const uint8_t *s, const uint8_t *ci, uint32_t v, uint
 // variants) that occurs least often in a sample of the traffic being bound,
 // ties going to the compiler's static choice.  Any window of a literal is a
 // necessary condition for it, so the choice changes speed, never results.
+// Also picks each literal's check window (the rarest other window, farthest
+// from the gram on ties) that verification compares first.
 static void calibrate_grams(const std::vector<uint8_t> &lit_bytes, const std::vector<uint8_t> &lit_ci,
                             const std::vector<uint32_t> &lit_off, const std::vector<uint32_t> &lit_len,
-                            std::vector<uint32_t> &lit_gram, const uint8_t *sample, size_t n) {
+                            std::vector<uint32_t> &lit_gram, std::vector<uint8_t> &lit_chk, const uint8_t *sample,
+                            size_t n) {
+  lit_chk.assign(lit_off.size(), 0);
+  for (size_t id = 0; id < lit_off.size(); ++id)
+    lit_chk[id] = (uint8_t)(lit_gram[id] >= (lit_len[id] - 4) / 2 ? 0 : lit_len[id] - 4);
   if (n < 4 || lit_off.empty()) return;
   std::unordered_map<uint32_t, uint32_t> cnt;
   std::vector<uint64_t> seen(1u << 14, 0);  // 2^20-bit presence filter
@@ -1571,18 +1612,29 @@ static void calibrate_grams(const std::vector<uint8_t> &lit_bytes, const std::ve
     if (it != cnt.end()) ++it->second;
   }
   for (size_t id = 0; id < lit_off.size(); ++id) {
-    uint64_t best = ~0ull;
-    uint32_t best_o = lit_gram[id];
+    std::vector<uint64_t> wc;
     for (uint32_t o = 0; o + 4 <= lit_len[id]; ++o) {
       uint64_t c = 0;
       for (uint32_t v = 0; v < 16; ++v) {
         uint32_t x;
         if (window_variant(&lit_bytes[lit_off[id] + o], &lit_ci[lit_off[id] + o], v, &x)) c += cnt[x];
       }
-      c = 2 * c + (o == lit_gram[id] ? 0 : 1);
+      wc.push_back(c);
+    }
+    uint64_t best = ~0ull;
+    uint32_t best_o = lit_gram[id];
+    for (uint32_t o = 0; o < wc.size(); ++o) {
+      const uint64_t c = 2 * wc[o] + (o == lit_gram[id] ? 0 : 1);
       if (c < best) { best = c; best_o = o; }
     }
     lit_gram[id] = best_o;
+    uint64_t bc = ~0ull;
+    for (uint32_t o = 0; o < wc.size(); ++o) {
+      if (o == best_o && wc.size() > 1) continue;
+      const uint32_t dist = o > best_o ? o - best_o : best_o - o;
+      const uint64_t c = wc[o] * 256 + (255 - std::min<uint32_t>(dist, 255));
+      if (c < bc) { bc = c; lit_chk[id] = (uint8_t)o; }
+    }
   }
 }
 
@@ -1673,7 +1725,8 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     d.interval_ns = r.interval_ns;
     d.hits = r.hits;
   }
-  calibrate_grams(lit_bytes, lit_ci, lit_off, lit_len, lit_gram, sample, sample_n);
+  std::vector<uint8_t> lit_chk;
+  calibrate_grams(lit_bytes, lit_ci, lit_off, lit_len, lit_gram, lit_chk, sample, sample_n);
   // gram filter: each literal's chosen 4-byte window, every ASCII case variant
   // of its case-insensitive bytes, -> bitset bit + exact table entry
   std::map<uint32_t, std::vector<std::pair<uint32_t, uint32_t>>> gmap;
@@ -1871,10 +1924,20 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   };
   std::vector<uint64_t> hrec(hd.size());
   for (size_t i = 0; i < hd.size(); ++i) hrec[i] = ((uint64_t)hd_off[i] << 32) | hd_len[i];
-  std::vector<uint32_t> lrec(lit_off.size()), lci((lit_bytes.size() + 31) / 32 + 1, 0);
-  for (size_t i = 0; i < lit_off.size(); ++i) lrec[i] = (lit_off[i] << 8) | lit_len[i];
-  for (size_t q = 0; q < lit_ci.size(); ++q)
-    if (lit_ci[q]) lci[q >> 5] |= 1u << (q & 31);
+  // literals 4-byte aligned (+4 bytes of slack) with their case masks
+  std::vector<uint32_t> lrec(lit_off.size());
+  std::vector<uint8_t> lb_al, cm_al;
+  for (size_t i = 0; i < lit_off.size(); ++i) {
+    const uint32_t off = (uint32_t)lb_al.size();
+    lrec[i] = (off << 8) | lit_len[i];
+    for (uint32_t k = 0; k < lit_len[i]; ++k) {
+      lb_al.push_back(lit_bytes[lit_off[i] + k]);
+      cm_al.push_back(lit_ci[lit_off[i] + k] ? 0x20 : 0);
+    }
+    const size_t padded = ((lb_al.size() + 3) & ~size_t(3)) + 4;
+    lb_al.resize(padded, 0);
+    cm_al.resize(padded, 0);
+  }
   ImgLayout il;
   il.gt = put(gt2.data(), gt2.size() * 4);
   il.ge = put(gt2_ent.data(), gt2_ent.size() * 4);
@@ -1883,8 +1946,9 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   il.hid = put(hd_id.data(), hd_id.size() * 4);
   il.hbytes = put(hd_bytes.data(), hd_bytes.size());
   il.lrec = put(lrec.data(), lrec.size() * 4);
-  il.lbytes = put(lit_bytes.data(), lit_bytes.size());
-  il.lci = put(lci.data(), lci.size() * 4);
+  il.lbytes = put(lb_al.data(), lb_al.size());
+  il.lcim = put(cm_al.data(), cm_al.size());
+  il.lchk = put(lit_chk.data(), lit_chk.size());
   img.resize((img.size() + 15) & ~size_t(15), 0);
 
   BlobBuilder bb;
@@ -2229,19 +2293,17 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
   L.counts = e->l_counts.p; L.masks = e->l_masks.p;
   L.cand_cnt = e->l_ccnt.p; L.cand = e->l_cand.p;
   e->jobs.ensure(std::max<uint64_t>(e->jobs.n, n_lines + (1u << 20)));
-  uint64_t last_nl = 0;
-  unsigned long long sc4[5] = {0, 0, 0, 0, 0};
-  for (int attempt = 0;; ++attempt) {
-    HIP_OK(hipMemsetAsync(e->scalars.p, 0, 16 * sizeof(unsigned long long), st));
-    if (B.any_prefilter) HIP_OK(hipMemsetAsync(e->l_ccnt.p, 0, n_lines * 4, st));
-    mark(e, 1);
+  HIP_OK(hipMemsetAsync(e->scalars.p, 0, 16 * sizeof(unsigned long long), st));
+  if (B.any_prefilter) HIP_OK(hipMemsetAsync(e->l_ccnt.p, 0, n_lines * 4, st));
+  mark(e, 1);
 
-    // ---- the scan kernel (the hot, HBM-bound kernel)
+  // ---- the scan kernel (the hot, HBM-bound kernel): line framing + literal hits
+  uint64_t last_nl = 0;
+  {
     ScanArgs A;
     A.buf = buf; A.n = n; A.n_tiles = n_tiles; A.n_lines = n_lines; A.tile_base = e->tile_base.p; A.nl = e->nl.p;
-    A.L = L; A.now_ns = now_ns; A.slow_list = e->slow_list.p; A.slow_count = e->scalars.p;
-    A.long_list = e->long_list.p; A.long_count = e->scalars.p + 10; A.stats = e->scalars.p + 8;
-    A.jobs = e->jobs.p; A.job_count = e->scalars.p + 11; A.job_cap = e->jobs.n;
+    A.L = L; A.stats = e->scalars.p + 8;
+    A.debug_skip = getenv("BJX_DEBUG_SKIP") ? (uint32_t)atoi(getenv("BJX_DEBUG_SKIP")) : 0u;
     // block-shared LDS: gram bitset, the lookup image when it fits, then 16 wave regions
     const uint32_t fixed = kGramWords * 4 + kScanWaves * kWaveLds;
     const bool img_lds = fixed + B.img_bytes <= kScanLdsMax;
@@ -2258,30 +2320,40 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
     else hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kScanWaves * 64), lds, st, B, A);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(e->evm1, st));
-    mark(e, 2);
+  }
+  mark(e, 2);
+
+  // ---- per-line pass (header, host, exemption, rule decisions) -> DFA jobs
+  unsigned long long sc4[5] = {0, 0, 0, 0, 0};
+  for (int attempt = 0;; ++attempt) {
+    LinesArgs A;
+    A.buf = buf; A.nl = e->nl.p; A.n_lines = n_lines; A.L = L; A.now_ns = now_ns;
+    A.slow_list = e->slow_list.p; A.slow_count = e->scalars.p;
+    A.jobs = e->jobs.p; A.job_count = e->scalars.p + 11; A.job_cap = e->jobs.n;
+    const bool img_lds = B.img_bytes <= kLinesImgMax;
+    const uint32_t lds = (img_lds ? B.img_bytes : 0) + (kBlock / 64) * (kWaveJobs * 8 + 16);
+    const unsigned grid = (unsigned)std::min<uint64_t>((n_lines + kBlock - 1) / kBlock, 256 * 8);
+    if (img_lds) hipLaunchKernelGGL(k_lines<true>, dim3(grid), dim3(kBlock), lds, st, B, A);
+    else hipLaunchKernelGGL(k_lines<false>, dim3(grid), dim3(kBlock), lds, st, B, A);
+    HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(&last_nl, e->nl.p + (n_lines - 1), 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(sc4, e->scalars.p + 8, 32, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(sc4 + 4, e->scalars.p, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     if (sc4[3] <= e->jobs.n) break;
-    // more DFA jobs than the buffer holds: grow it and redo the (idempotent) scan
+    // more DFA jobs than the buffer holds: grow it and redo the (idempotent) line pass
     if (attempt > 0) throw BjxError(BJX_ERR_DEVICE, "internal: DFA job buffer overflow");
     e->jobs.ensure(sc4[3] + (1u << 20));
+    HIP_OK(hipMemsetAsync(e->scalars.p, 0, 8, st));
+    HIP_OK(hipMemsetAsync(e->scalars.p + 11, 0, 8, st));
   }
   out->consumed_bytes = last_nl + 1;
-  const unsigned long long n_slow = sc4[4], n_long = sc4[2], n_jobs = sc4[3];
+  const unsigned long long n_slow = sc4[4], n_jobs = sc4[3];
   e->last_jobs = n_jobs;
+  e->scan_stats[0] = sc4[0]; e->scan_stats[1] = sc4[1]; e->scan_stats[2] = n_slow; e->scan_stats[3] = 0;
+  e->scan_stats[4] = n_jobs;
   if (n_jobs) {
     hipLaunchKernelGGL(k_dfa, dim3(grid_for(n_jobs)), dim3(kBlock), 0, st, B, buf, e->nl.p, e->jobs.p, (uint64_t)n_jobs, L);
-    HIP_OK(hipGetLastError());
-  }
-  e->scan_stats[0] = sc4[0]; e->scan_stats[1] = sc4[1]; e->scan_stats[2] = n_slow; e->scan_stats[3] = n_long;
-  e->scan_stats[4] = n_jobs;
-
-  // ---- long lines from HBM; per-line fallback for rare lines
-  if (n_long) {
-    hipLaunchKernelGGL(k_resolve_long, dim3(grid_for(n_long)), dim3(kBlock), 0, st, B, buf, e->nl.p, e->long_list.p,
-                       (uint64_t)n_long, L);
     HIP_OK(hipGetLastError());
   }
   if (n_slow) {

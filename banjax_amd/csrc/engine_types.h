@@ -35,7 +35,8 @@ __host__ __device__ inline uint32_t gram_hash(uint32_t g) {
   const uint32_t x = g ^ (g >> 15);
   return ((x & 0xFFFFFFu) * 0x2C1B3Bu >> 8) & ((1u << kGramLog2) - 1);
 }
-constexpr int kCandSlots = 4;  // literal hits kept per long line (more = overflow: every rule by DFA)
+constexpr int kCandSlots = 4;  // literal hits kept per line (more = overflow: every literal rule by DFA)
+constexpr uint64_t kCandVerified = 1u << 23;  // hit bytes already checked by the scan pass
 
 struct Subnet {
   uint8_t net[16];
@@ -45,7 +46,7 @@ struct Subnet {
 };
 
 struct ImgLayout {
-  uint32_t gt, ge, ht, hrec, hid, hbytes, lrec, lbytes, lci;
+  uint32_t gt, ge, ht, hrec, hid, hbytes, lrec, lbytes, lcim, lchk;
 };
 
 // Everything the per-line kernels need about the current (ruleset, decision
@@ -97,7 +98,8 @@ struct Bind {
   //               entries (lit << 8 | window offset)
   //   host table  ht_cap slots of (hash tag, hd index); host records
   //               (bytes offset << 32 | len) and ids; host bytes
-  //   literals    (bytes offset << 8 | len); bytes; ASCII-ci bits
+  //   literals    (bytes offset << 8 | len); bytes and case masks (0x20 where
+  //               ASCII-case-insensitive), 4-byte aligned; check-window offsets
   const uint8_t *img;
   uint32_t img_bytes;
   uint32_t gt2_cap, gt2_nent;
@@ -134,8 +136,8 @@ struct Lines {
   uint8_t *flags;
   uint64_t *counts;    // (n_results << 32) | n_events per line, then scanned in place
   uint64_t *masks;     // mask_words per line
-  uint32_t *cand_cnt;  // long lines: literal hits recorded by the scan pass
-  uint64_t *cand;      // kCandSlots per line: (literal start << 24) | literal id
+  uint32_t *cand_cnt;  // literal hits recorded by the scan pass
+  uint64_t *cand;      // kCandSlots per line: (literal start << 24) | verified | literal id
 };
 
 // Persistent rate-limit state (RegexRateLimitStates, rate_limit.go:17-21),
