@@ -1000,183 +1000,272 @@ __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restric
 }
 
 // RuleResults (reference order) and rate-limit events from the per-line masks.
+// Events carry their line, rule and result index; bounds[0] += lines with
+// events, bounds[1] += their IP bytes (capacity of the IP table / arena),
+// reduced per block (grid-stride; one atomic pair per block).
 __global__ __launch_bounds__(kBlock) void k_emit(Bind B, uint64_t n_lines, Lines L, const uint64_t *__restrict__ offs,
                                                  uint64_t *__restrict__ res_seq, uint32_t *__restrict__ res_rule,
-                                                 uint32_t *__restrict__ ev_key, uint32_t *__restrict__ ev_res) {
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n_lines) return;
-  if (L.counts[j] == 0) return;
-  uint64_t ro = offs[j] >> 32, eo = offs[j] & 0xFFFFFFFFull;
-  const int32_t hid = L.host_id[j];
-  uint32_t s_begin = 0, s_end = 0;
-  if (hid >= 0) { s_begin = B.site_off[hid]; s_end = B.site_off[hid + 1]; }
-  const uint32_t nsite = s_end - s_begin;
-  const uint32_t napp = nsite + B.n_global;
-  const uint32_t key = (uint32_t)L.ip_hash[j];
-  const uint64_t *mask = L.masks + j * B.mask_words;
-  for (uint32_t w = 0; w * 64 < napp; ++w) {
-    uint64_t m = mask[w];
-    while (m) {
-      const uint32_t b = (uint32_t)__ffsll((unsigned long long)m) - 1;
-      m &= m - 1;
-      const uint32_t pos = w * 64 + b;
-      const uint32_t r = pos < nsite ? B.site_rules[s_begin + pos] : B.global_rules[pos - nsite];
-      const bool skip = is_skip(B, r, hid);
-      res_seq[ro] = (j << 16) | pos;
-      res_rule[ro] = r | (skip ? 0x80000000u : 0u);
-      if (!skip) { ev_key[eo] = key; ev_res[eo] = (uint32_t)ro; ++eo; }
-      ++ro;
+                                                 uint32_t *__restrict__ ev_el, uint32_t *__restrict__ ev_rule,
+                                                 uint32_t *__restrict__ ev_res, unsigned long long *bounds) {
+  __shared__ unsigned long long s_acc[2][kBlock / 64];
+  unsigned long long has_ev = 0, ipb = 0;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n_lines; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t cnt = L.counts[j];
+    if (cnt == 0) continue;
+    uint64_t ro = offs[j] >> 32, eo = offs[j] & 0xFFFFFFFFull;
+    const int32_t hid = L.host_id[j];
+    uint32_t s_begin = 0, s_end = 0;
+    if (hid >= 0) { s_begin = B.site_off[hid]; s_end = B.site_off[hid + 1]; }
+    const uint32_t nsite = s_end - s_begin;
+    const uint32_t napp = nsite + B.n_global;
+    const uint64_t *mask = L.masks + j * B.mask_words;
+    for (uint32_t w = 0; w * 64 < napp; ++w) {
+      uint64_t m = mask[w];
+      while (m) {
+        const uint32_t b = (uint32_t)__ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+        const uint32_t pos = w * 64 + b;
+        const uint32_t r = pos < nsite ? B.site_rules[s_begin + pos] : B.global_rules[pos - nsite];
+        const bool skip = is_skip(B, r, hid);
+        res_seq[ro] = (j << 16) | pos;
+        res_rule[ro] = r | (skip ? 0x80000000u : 0u);
+        if (!skip) { ev_el[eo] = (uint32_t)j; ev_rule[eo] = r; ev_res[eo] = (uint32_t)ro; ++eo; }
+        ++ro;
+      }
     }
+    if (cnt & 0xFFFFFFFFull) { ++has_ev; ipb += L.ip_len[j]; }
   }
-}
-
-// segment heads of the IP-hash-sorted events + bounds on new IPs / arena bytes
-__global__ __launch_bounds__(kBlock) void k_heads(uint64_t n_ev, const uint32_t *__restrict__ key,
-                                                  const uint32_t *__restrict__ ev_res, const uint64_t *__restrict__ res_seq,
-                                                  Lines L, uint8_t *__restrict__ head, unsigned long long *bounds) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_ev) return;
-  head[t] = (t == 0 || key[t] != key[t - 1]) ? 1 : 0;
-  const uint64_t line = res_seq[ev_res[t]] >> 16;
-  const uint64_t h = L.ip_hash[line];
-  const uint64_t hp = t ? L.ip_hash[res_seq[ev_res[t - 1]] >> 16] : ~h;
-  if (h != hp) {
-    atomicAdd(&bounds[0], 1ull);
-    atomicAdd(&bounds[1], (unsigned long long)L.ip_len[line]);
+  for (int o = 32; o > 0; o >>= 1) {
+    has_ev += __shfl_xor(has_ev, o);
+    ipb += __shfl_xor(ipb, o);
+  }
+  if ((threadIdx.x & 63) == 0) { s_acc[0][threadIdx.x >> 6] = has_ev; s_acc[1][threadIdx.x >> 6] = ipb; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long a0 = 0, a1 = 0;
+    for (int w = 0; w < kBlock / 64; ++w) { a0 += s_acc[0][w]; a1 += s_acc[1][w]; }
+    if (a0) { atomicAdd(&bounds[0], a0); atomicAdd(&bounds[1], a1); }
   }
 }
 
 // --------------------------------------------------------------- state
+//
+// RegexRateLimitStates.Apply (rate_limit.go:37-78) for a batch of events, in
+// four data-parallel steps (DESIGN.md "Rate limiting"):
+//   k_ip_claim    one lane per event line: find the IP's slot (full byte
+//                 compare against IPs of earlier batches) or claim a new one
+//   k_ip_commit   one lane per event line: the first line of a new IP writes
+//                 its bytes; other lines check theirs against it (a 64-bit
+//                 hash collision inside the batch -> k_ip_collide, serial)
+//   k_st_claim    one lane per event: (ip id, rule name) -> state slot, seenIp
+//   radix sort by state slot (stable: reference order inside a slot)
+//   k_apply       one lane per state slot run: the fixed-window automaton
 
 __device__ __forceinline__ uint64_t line_start(const uint64_t *nl, uint64_t line) { return line ? nl[line - 1] + 1 : 0; }
 
-// find-or-insert an IP string.  All events of one 64-bit hash are owned by one
-// thread (same segment), so a slot holding this hash was published by an
-// earlier kernel or by this thread; other threads only race on claiming empty
-// slots (CAS), never on reading payloads.
-__device__ uint32_t ip_find_insert(const State &S, uint64_t h, const uint8_t *ip, uint32_t len, bool *existed) {
-  uint64_t i = h & S.ip_mask;
+__device__ __forceinline__ const uint8_t *ev_ip(const EvSrc &E, uint64_t i) {
+  return E.bytes + (E.nl ? line_start(E.nl, i) + E.ip_off[i] : E.ip_pos[i]);
+}
+__device__ __forceinline__ bool ev_has(const EvSrc &E, uint64_t i) {
+  return !E.counts || (E.counts[i] & 0xFFFFFFFFull) != 0;
+}
+
+constexpr uint32_t kNewIp = 0xFFFFFFFFu;   // el_id: IP created in this batch, id not known to this line
+constexpr uint32_t kFirstIp = 0x80000000u; // el_id: this line is the first event line of a new IP
+
+__global__ __launch_bounds__(kBlock) void k_ip_claim(EvSrc E, State S, uint32_t epoch, uint32_t *__restrict__ el_slot,
+                                                     uint32_t *__restrict__ el_id) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E.n || !ev_has(E, i)) return;
+  const uint64_t h = E.ip_hash[i];
+  const uint32_t len = E.ip_len[i];
+  const uint8_t *ip = ev_ip(E, i);
+  uint64_t s = h & S.ip_mask;
   for (;;) {
-    uint64_t cur = S.ip_slot_hash[i];
+    uint64_t cur = S.ip[s].hash;
     if (cur == 0) {
-      unsigned long long prev = atomicCAS((unsigned long long *)&S.ip_slot_hash[i], 0ull, (unsigned long long)h);
-      if (prev == 0) {
-        const uint32_t id = (uint32_t)atomicAdd((unsigned long long *)&S.counters[0], 1ull);
-        const uint64_t off = atomicAdd((unsigned long long *)&S.counters[1], (unsigned long long)len);
+      cur = atomicCAS((unsigned long long *)&S.ip[s].hash, 0ull, (unsigned long long)h);
+      if (cur == 0) cur = h;
+    }
+    if (cur == h) {
+      uint32_t b = S.ip[s].born;
+      if (b == 0 || b == epoch) b = atomicCAS(&S.ip[s].born, 0u, epoch);
+      if (b == 0 || b == epoch) {  // created in this batch: identity checked by k_ip_commit
+        atomicMin(&S.ip_first[s], (uint32_t)i);
+        el_slot[i] = (uint32_t)s;
+        el_id[i] = kNewIp;
+        return;
+      }
+      const uint32_t id = S.ip[s].id;  // created by an earlier batch: its bytes are in the arena
+      if (S.ip_len[id] == len && bytes_eq(S.arena + S.ip_off[id], ip, len)) {
+        el_slot[i] = (uint32_t)s;
+        el_id[i] = id;
+        return;
+      }
+    }
+    s = (s + 1) & S.ip_mask;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_ip_commit(EvSrc E, State S, uint32_t epoch, const uint32_t *__restrict__ el_slot,
+                                                      uint32_t *__restrict__ el_id, uint32_t *__restrict__ coll) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E.n || !ev_has(E, i)) return;
+  const uint32_t s = el_slot[i];
+  if (S.ip[s].born != epoch) return;
+  const uint32_t f = S.ip_first[s];
+  const uint32_t len = E.ip_len[i];
+  const uint8_t *ip = ev_ip(E, i);
+  if (f == (uint32_t)i) {
+    const uint32_t id = (uint32_t)atomicAdd((unsigned long long *)&S.counters[0], 1ull);
+    const uint64_t off = atomicAdd((unsigned long long *)&S.counters[1], (unsigned long long)len);
+    for (uint32_t k = 0; k < len; ++k) S.arena[off + k] = ip[k];
+    S.ip_off[id] = off;
+    S.ip_len[id] = len;
+    S.ip[s].id = id;
+    el_id[i] = id | kFirstIp;
+  } else if (E.ip_len[f] != len || !bytes_eq(ev_ip(E, f), ip, len)) {
+    const uint64_t k = atomicAdd((unsigned long long *)&S.counters[3], 1ull);
+    coll[k] = (uint32_t)i;
+  }
+}
+
+// Lines whose IP differs from the first line of its slot (equal 64-bit hash):
+// one thread, in line order, with full byte compares; each distinct string
+// gets its own slot.  coll[] is sorted ascending.
+__global__ void k_ip_collide(EvSrc E, State S, uint32_t epoch, uint32_t *__restrict__ el_slot,
+                             uint32_t *__restrict__ el_id, const uint32_t *__restrict__ coll, uint64_t n_coll) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  for (uint64_t c = 0; c < n_coll; ++c) {
+    const uint32_t i = coll[c];
+    const uint64_t h = E.ip_hash[i];
+    const uint32_t len = E.ip_len[i];
+    const uint8_t *ip = ev_ip(E, i);
+    uint64_t s = h & S.ip_mask;
+    for (;;) {
+      const uint64_t cur = S.ip[s].hash;
+      if (cur == 0) {
+        const uint32_t id = (uint32_t)S.counters[0]++;
+        const uint64_t off = S.counters[1];
+        S.counters[1] += len;
         for (uint32_t k = 0; k < len; ++k) S.arena[off + k] = ip[k];
         S.ip_off[id] = off;
         S.ip_len[id] = len;
-        S.ip_slot_id[i] = id;
-        *existed = false;
-        return id;
+        S.ip[s].hash = h;
+        S.ip[s].id = id;
+        S.ip[s].born = epoch;
+        S.ip_first[s] = i;
+        el_slot[i] = (uint32_t)s;
+        el_id[i] = id | kFirstIp;
+        break;
       }
-      cur = prev;
-    }
-    if (cur == h) {
-      const uint32_t id = S.ip_slot_id[i];
-      if (S.ip_len[id] == len && bytes_eq(S.arena + S.ip_off[id], ip, len)) { *existed = true; return id; }
-    }
-    i = (i + 1) & S.ip_mask;
-  }
-}
-
-__device__ uint64_t st_find_insert(const State &S, uint64_t key, bool *fresh) {
-  uint64_t i = mix64(key) & S.st_mask;
-  for (;;) {
-    uint64_t cur = S.st_key[i];
-    if (cur == 0) {
-      unsigned long long prev = atomicCAS((unsigned long long *)&S.st_key[i], 0ull, (unsigned long long)key);
-      if (prev == 0) {
-        atomicAdd((unsigned long long *)&S.counters[2], 1ull);
-        *fresh = true;
-        return i;
-      }
-      cur = prev;
-    }
-    if (cur == key) { *fresh = false; return i; }
-    i = (i + 1) & S.st_mask;
-  }
-}
-
-// RegexRateLimitStates.Apply (rate_limit.go:37-78) for every event of one IP
-// group, in (line, rule-position) order.  rl_out bit0 seenIp, bits1-2
-// MatchType, bit3 Exceeded, bit7 valid.
-__global__ __launch_bounds__(kBlock) void k_ratelimit(
-    uint64_t n_seg, uint64_t n_ev, const uint32_t *__restrict__ heads, const uint32_t *__restrict__ ev_res,
-    const uint64_t *__restrict__ res_seq, const uint32_t *__restrict__ res_rule, const uint64_t *__restrict__ nl,
-    const uint8_t *__restrict__ buf, Lines L, const DevRule *__restrict__ rules, State S, uint8_t *__restrict__ rl_out,
-    uint8_t *__restrict__ processed) {
-  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_seg) return;
-  const uint64_t b = heads[k], e = (k + 1 < n_seg) ? heads[k + 1] : n_ev;
-  uint64_t first = b;
-  for (;;) {
-    const uint32_t r0 = ev_res[first];
-    const uint64_t line0 = res_seq[r0] >> 16;
-    const uint64_t h0 = L.ip_hash[line0];
-    const uint8_t *ip0 = buf + line_start(nl, line0) + L.ip_off[line0];
-    const uint32_t len0 = L.ip_len[line0];
-    bool existed;
-    const uint32_t ip_id = ip_find_insert(S, h0, ip0, len0, &existed);
-    bool seen = existed;
-    bool other = false;
-    uint64_t next_first = e;
-    for (uint64_t t = first; t < e; ++t) {
-      if (processed[t]) continue;
-      const uint32_t r = ev_res[t];
-      const uint64_t line = res_seq[r] >> 16;
-      if (t != first) {
-        const bool same = L.ip_hash[line] == h0 && L.ip_len[line] == len0 &&
-                          bytes_eq(buf + line_start(nl, line) + L.ip_off[line], ip0, len0);
-        if (!same) {
-          if (!other) { other = true; next_first = t; }
-          continue;
+      if (cur == h) {
+        const uint32_t id = S.ip[s].id;
+        if (S.ip_len[id] == len && bytes_eq(S.arena + S.ip_off[id], ip, len)) {
+          el_slot[i] = (uint32_t)s;
+          el_id[i] = id;
+          break;
         }
       }
-      processed[t] = 1;
-      const DevRule R = rules[res_rule[r] & 0x7FFFFFFFu];
-      const uint64_t key = ((uint64_t)(ip_id + 1) << 24) | R.name_id;
-      bool fresh;
-      const uint64_t slot = st_find_insert(S, key, &fresh);
-      const int64_t ts = L.ts[line];
-      int64_t hits, start;
-      uint8_t mt;
-      if (fresh) { hits = 1; start = ts; mt = BJX_FIRST_TIME; }
-      else {
-        hits = S.st_hits[slot];
-        start = S.st_start[slot];
-        if (go_sub(ts, start) > R.interval_ns) { mt = BJX_OUTSIDE_INTERVAL; hits = 1; start = ts; }
-        else { mt = BJX_INSIDE_INTERVAL; hits++; }
-      }
-      const bool ex = hits > R.hits;
-      if (ex) hits = 0;
-      S.st_hits[slot] = hits;
-      S.st_start[slot] = start;
-      rl_out[r] = (uint8_t)(0x80 | (seen ? 1 : 0) | (mt << 1) | (ex ? 8 : 0));
-      seen = true;
+      s = (s + 1) & S.ip_mask;
     }
-    if (!other) break;
-    first = next_first;
   }
 }
 
-__global__ void k_flag_trips(uint64_t n, const uint8_t *__restrict__ rl_out, uint8_t *__restrict__ f) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) f[i] = (rl_out[i] & 8) ? 1 : 0;
+// event k -> state slot and its sort record.  seenIp is false only for the
+// first event of an IP created in this batch.
+__global__ __launch_bounds__(kBlock) void k_st_claim(EvSrc E, uint64_t n_ev, const uint32_t *__restrict__ ev_el,
+                                                     const uint32_t *__restrict__ ev_rule, const uint32_t *__restrict__ el_slot,
+                                                     const uint32_t *__restrict__ el_id, const DevRule *__restrict__ rules,
+                                                     State S, uint32_t *__restrict__ ev_st, EvRec *__restrict__ ev_rec) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_ev) return;
+  const uint32_t i = ev_el[k];
+  const uint32_t r = ev_rule[k];
+  uint32_t id = el_id[i];
+  const bool first = id != kNewIp && (id & kFirstIp) && (k == 0 || ev_el[k - 1] != i);
+  id = id == kNewIp ? S.ip[el_slot[i]].id : (id & ~kFirstIp);
+  const uint64_t key = ((uint64_t)(id + 1) << 24) | rules[r].name_id;
+  uint64_t q = mix64(key) & S.st_mask;
+  bool claimed = false;
+  for (;;) {
+    uint64_t cur = S.st[q].key;
+    if (cur == 0) {
+      cur = atomicCAS((unsigned long long *)&S.st[q].key, 0ull, (unsigned long long)key);
+      if (cur == 0) { claimed = true; break; }
+    }
+    if (cur == key) break;
+    q = (q + 1) & S.st_mask;
+  }
+  ev_st[k] = (uint32_t)q;
+  EvRec rec;
+  rec.ts = E.ts[i];
+  rec.rule = r | (first ? 0x80000000u : 0u);
+  rec.ev = (uint32_t)k;
+  ev_rec[k] = rec;
+  // table load (counters[2]): one atomic per wave
+  const uint64_t won = __ballot(claimed);
+  if (won && (threadIdx.x & 63) == (uint32_t)(__ffsll((unsigned long long)won) - 1))
+    atomicAdd((unsigned long long *)&S.counters[2], (unsigned long long)__popcll(won));
 }
 
-__global__ void k_build_trips(uint64_t n_trips, const uint32_t *__restrict__ idx, const uint64_t *__restrict__ res_seq,
-                              const uint32_t *__restrict__ res_rule, const uint64_t *__restrict__ nl, Lines L,
+// run heads of the slot-sorted events
+__global__ __launch_bounds__(kBlock) void k_run_heads(uint64_t n_ev, const uint32_t *__restrict__ key, uint8_t *__restrict__ f) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n_ev) f[t] = (t == 0 || key[t] != key[t - 1]) ? 1 : 0;
+}
+
+// The fixed-window automaton of one (ip, rule name) state over its events in
+// reference order (records sorted by slot, stable).  One lane per run,
+// grid-stride over the run heads.  ev_out[k]: bit0 seenIp, bits1-2
+// MatchType, bit3 Exceeded, bit7 valid.
+__global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const unsigned long long *__restrict__ n_runs_p,
+                                                  const uint32_t *__restrict__ heads, const uint32_t *__restrict__ key,
+                                                  const EvRec *__restrict__ rec, const DevRule *__restrict__ rules,
+                                                  StSlot *__restrict__ st, uint8_t *__restrict__ ev_out) {
+  const uint64_t n_runs = *n_runs_p;
+  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n_runs; h += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = heads[h], e = h + 1 < n_runs ? heads[h + 1] : n_ev;
+    const uint32_t q = key[b];
+    const StSlot cur = st[q];
+    bool valid = cur.valid != 0;
+    int64_t hits = cur.hits, start = cur.start;
+    for (uint64_t u = b; u < e; ++u) {
+      const EvRec v = rec[u];
+      const uint32_t r = v.rule & 0x7FFFFFFFu;
+      const bool seen = (v.rule >> 31) == 0;
+      const int64_t interval = rules[r].interval_ns, limit = rules[r].hits;
+      uint8_t mt;
+      if (!valid) { hits = 1; start = v.ts; mt = BJX_FIRST_TIME; valid = true; }
+      else if (go_sub(v.ts, start) > interval) { mt = BJX_OUTSIDE_INTERVAL; hits = 1; start = v.ts; }
+      else { mt = BJX_INSIDE_INTERVAL; ++hits; }
+      const bool ex = hits > limit;
+      if (ex) hits = 0;
+      ev_out[v.ev] = (uint8_t)(0x80 | (seen ? 1 : 0) | (mt << 1) | (ex ? 8 : 0));
+    }
+    st[q].hits = hits;
+    st[q].start = start;
+    st[q].valid = 1;
+  }
+}
+
+__global__ void k_flag_trips(uint64_t n, const uint8_t *__restrict__ ev_out, uint8_t *__restrict__ f) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) f[i] = (ev_out[i] & 8) ? 1 : 0;
+}
+
+__global__ void k_build_trips(uint64_t n_trips, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ ev_el,
+                              const uint32_t *__restrict__ ev_rule, const uint64_t *__restrict__ nl, Lines L,
                               const DevRule *__restrict__ rules, bjx_trip *__restrict__ out) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_trips) return;
-  const uint32_t r = idx[t];
-  const uint64_t line = res_seq[r] >> 16;
+  const uint32_t k = idx[t];
+  const uint64_t line = ev_el[k];
   bjx_trip tr;
   tr.line_idx = line;
   tr.line_offset = line_start(nl, line);
   tr.line_len = (uint32_t)(nl[line] - tr.line_offset);
-  tr.rule_idx = res_rule[r] & 0x7FFFFFFFu;
+  tr.rule_idx = ev_rule[k];
   tr.ts_ns = L.ts[line];
   tr.ip_off = L.ip_off[line];
   tr.ip_len = L.ip_len[line];
@@ -1185,6 +1274,12 @@ __global__ void k_build_trips(uint64_t n_trips, const uint32_t *__restrict__ idx
   tr.rest_off = L.rest_off[line];
   tr.decision = rules[tr.rule_idx].decision;
   out[t] = tr;
+}
+
+__global__ void k_scatter_rl(uint64_t n_ev, const uint32_t *__restrict__ ev_res, const uint8_t *__restrict__ ev_out,
+                             uint8_t *__restrict__ rl_out) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n_ev) rl_out[ev_res[k]] = ev_out[k];
 }
 
 __global__ void k_build_results(uint64_t n, const uint64_t *__restrict__ res_seq, const uint32_t *__restrict__ res_rule,
@@ -1210,26 +1305,23 @@ __global__ void k_final_flags(uint64_t n, uint8_t *__restrict__ f) {
 }
 
 // rehash (table growth)
-__global__ void k_rehash_ip(uint64_t old_cap, const uint64_t *__restrict__ oh, const uint32_t *__restrict__ oid,
-                            uint64_t *__restrict__ nh, uint32_t *__restrict__ nid, uint64_t nmask) {
+__global__ void k_rehash_ip(uint64_t old_cap, const IpSlot *__restrict__ o, IpSlot *__restrict__ nt, uint64_t nmask) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= old_cap || oh[i] == 0) return;
-  uint64_t j = oh[i] & nmask;
+  if (i >= old_cap || o[i].hash == 0) return;
+  uint64_t j = o[i].hash & nmask;
   for (;;) {
-    unsigned long long prev = atomicCAS((unsigned long long *)&nh[j], 0ull, (unsigned long long)oh[i]);
-    if (prev == 0) { nid[j] = oid[i]; return; }
+    const unsigned long long prev = atomicCAS((unsigned long long *)&nt[j].hash, 0ull, (unsigned long long)o[i].hash);
+    if (prev == 0) { nt[j].id = o[i].id; nt[j].born = o[i].born; return; }
     j = (j + 1) & nmask;
   }
 }
-__global__ void k_rehash_st(uint64_t old_cap, const uint64_t *__restrict__ ok, const int64_t *__restrict__ ohit,
-                            const int64_t *__restrict__ ost, uint64_t *__restrict__ nk, int64_t *__restrict__ nhit,
-                            int64_t *__restrict__ nst, uint64_t nmask) {
+__global__ void k_rehash_st(uint64_t old_cap, const StSlot *__restrict__ o, StSlot *__restrict__ nt, uint64_t nmask) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= old_cap || ok[i] == 0) return;
-  uint64_t j = mix64(ok[i]) & nmask;
+  if (i >= old_cap || o[i].key == 0) return;
+  uint64_t j = mix64(o[i].key) & nmask;
   for (;;) {
-    unsigned long long prev = atomicCAS((unsigned long long *)&nk[j], 0ull, (unsigned long long)ok[i]);
-    if (prev == 0) { nhit[j] = ohit[i]; nst[j] = ost[i]; return; }
+    const unsigned long long prev = atomicCAS((unsigned long long *)&nt[j].key, 0ull, (unsigned long long)o[i].key);
+    if (prev == 0) { nt[j].hits = o[i].hits; nt[j].start = o[i].start; nt[j].valid = o[i].valid; return; }
     j = (j + 1) & nmask;
   }
 }
@@ -1239,17 +1331,21 @@ __global__ void k_state_get(State S, uint64_t h, const uint8_t *ip, uint32_t len
   out[0] = 0;
   uint64_t i = h & S.ip_mask;
   for (;;) {
-    const uint64_t cur = S.ip_slot_hash[i];
+    const uint64_t cur = S.ip[i].hash;
     if (cur == 0) return;
     if (cur == h) {
-      const uint32_t id = S.ip_slot_id[i];
+      const uint32_t id = S.ip[i].id;
       if (S.ip_len[id] == len && bytes_eq(S.arena + S.ip_off[id], ip, len)) {
         const uint64_t key = ((uint64_t)(id + 1) << 24) | name_id;
         uint64_t j = mix64(key) & S.st_mask;
         for (;;) {
-          const uint64_t k = S.st_key[j];
+          const uint64_t k = S.st[j].key;
           if (k == 0) { out[0] = 1; return; }  // ip known, rule state absent
-          if (k == key) { out[0] = 2; out[1] = S.st_hits[j]; out[2] = S.st_start[j]; return; }
+          if (k == key) {
+            if (!S.st[j].valid) { out[0] = 1; return; }
+            out[0] = 2; out[1] = S.st[j].hits; out[2] = S.st[j].start;
+            return;
+          }
           j = (j + 1) & S.st_mask;
         }
       }
@@ -1444,7 +1540,8 @@ struct bjx_engine {
 
   // persistent state
   State S{};
-  uint64_t ip_cap = 0, st_cap = 0, max_ips = 0;
+  uint64_t ip_cap = 0, st_cap = 0;
+  uint32_t epoch = 0;  // batch counter (IpSlot.born)
   uint64_t host_counters[3] = {0, 0, 0};
 
   // batch workspace
@@ -1466,8 +1563,11 @@ struct bjx_engine {
   DevBuf<uint8_t> l_flags;
   DevBuf<unsigned long long> scalars;  // [0] slow count, [1..2] bounds, [3] selected
   DevBuf<uint64_t> res_seq;
-  DevBuf<uint32_t> res_rule, ev_key, ev_res, ev_key2, ev_res2, heads, trip_idx;
-  DevBuf<uint8_t> head_flag, rl_out, processed, trip_flag;
+  DevBuf<uint32_t> res_rule, ev_el, ev_rule, ev_res, ev_st, ev_st2, ev_idx, ev_idx2, el_slot, coll, trip_idx;
+  DevBuf<EvRec> ev_rec, ev_rec2;
+  DevBuf<uint32_t> el_id, run_heads;
+  DevBuf<uint8_t> run_flag;
+  DevBuf<uint8_t> rl_out, ev_out, trip_flag;
   DevBuf<bjx_trip> d_trips;
   DevBuf<bjx_rule_result> d_results;
   DevBuf<uint8_t> cub_tmp;
@@ -2033,30 +2133,28 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
 
 void alloc_state(bjx_engine *e, uint64_t ip_cap, uint64_t st_cap, uint64_t arena_cap) {
   State &S = e->S;
-  HIP_OK(hipMalloc(&S.ip_slot_hash, ip_cap * 8));
-  HIP_OK(hipMalloc(&S.ip_slot_id, ip_cap * 4));
+  HIP_OK(hipMalloc(&S.ip, ip_cap * sizeof(IpSlot)));
+  HIP_OK(hipMalloc(&S.ip_first, ip_cap * 4));
   HIP_OK(hipMalloc(&S.ip_off, ip_cap * 8));
   HIP_OK(hipMalloc(&S.ip_len, ip_cap * 4));
   HIP_OK(hipMalloc(&S.arena, arena_cap));
-  HIP_OK(hipMalloc(&S.st_key, st_cap * 8));
-  HIP_OK(hipMalloc(&S.st_hits, st_cap * 8));
-  HIP_OK(hipMalloc(&S.st_start, st_cap * 8));
+  HIP_OK(hipMalloc(&S.st, st_cap * sizeof(StSlot)));
   HIP_OK(hipMalloc(&S.counters, 64));
-  HIP_OK(hipMemset(S.ip_slot_hash, 0, ip_cap * 8));
-  HIP_OK(hipMemset(S.st_key, 0, st_cap * 8));
+  HIP_OK(hipMemset(S.ip, 0, ip_cap * sizeof(IpSlot)));
+  HIP_OK(hipMemset(S.ip_first, 0xFF, ip_cap * 4));
+  HIP_OK(hipMemset(S.st, 0, st_cap * sizeof(StSlot)));
   HIP_OK(hipMemset(S.counters, 0, 64));
   S.ip_mask = ip_cap - 1;
   S.st_mask = st_cap - 1;
   S.arena_cap = arena_cap;
   e->ip_cap = ip_cap;
   e->st_cap = st_cap;
-  e->max_ips = ip_cap - ip_cap / 4;
 }
 
 void free_state(bjx_engine *e) {
   State &S = e->S;
-  for (void *p : {(void *)S.ip_slot_hash, (void *)S.ip_slot_id, (void *)S.ip_off, (void *)S.ip_len, (void *)S.arena,
-                  (void *)S.st_key, (void *)S.st_hits, (void *)S.st_start, (void *)S.counters})
+  for (void *p : {(void *)S.ip, (void *)S.ip_first, (void *)S.ip_off, (void *)S.ip_len, (void *)S.arena, (void *)S.st,
+                  (void *)S.counters})
     if (p) (void)hipFree(p);
   S = State{};
 }
@@ -2067,33 +2165,33 @@ void read_counters(bjx_engine *e) {
 }
 
 // grow tables so that `new_ips` more IPs, `new_bytes` more arena bytes and
-// `new_states` more states fit under a 3/4 load factor
+// `new_states` more states fit under a 3/4 load factor (every probe loop
+// then terminates: a table is never full)
 void ensure_capacity(bjx_engine *e, uint64_t new_ips, uint64_t new_bytes, uint64_t new_states) {
   read_counters(e);
   State &S = e->S;
   const uint64_t n_ips = e->host_counters[0], used = e->host_counters[1], n_st = e->host_counters[2];
   if ((n_ips + new_ips) * 4 > e->ip_cap * 3) {
-    uint64_t cap = next_pow2((n_ips + new_ips) * 2 + 1024);
-    uint64_t *nh; uint32_t *nid; uint64_t *noff; uint32_t *nlen;
-    HIP_OK(hipMalloc(&nh, cap * 8));
-    HIP_OK(hipMalloc(&nid, cap * 4));
+    const uint64_t cap = next_pow2((n_ips + new_ips) * 2 + 1024);
+    IpSlot *nt; uint32_t *nf; uint64_t *noff; uint32_t *nlen;
+    HIP_OK(hipMalloc(&nt, cap * sizeof(IpSlot)));
+    HIP_OK(hipMalloc(&nf, cap * 4));
     HIP_OK(hipMalloc(&noff, cap * 8));
     HIP_OK(hipMalloc(&nlen, cap * 4));
-    HIP_OK(hipMemsetAsync(nh, 0, cap * 8, e->stream));
+    HIP_OK(hipMemsetAsync(nt, 0, cap * sizeof(IpSlot), e->stream));
+    HIP_OK(hipMemsetAsync(nf, 0xFF, cap * 4, e->stream));
     HIP_OK(hipMemcpyAsync(noff, S.ip_off, n_ips * 8, hipMemcpyDeviceToDevice, e->stream));
     HIP_OK(hipMemcpyAsync(nlen, S.ip_len, n_ips * 4, hipMemcpyDeviceToDevice, e->stream));
-    hipLaunchKernelGGL(k_rehash_ip, dim3(grid_for(e->ip_cap)), dim3(kBlock), 0, e->stream, e->ip_cap, S.ip_slot_hash,
-                       S.ip_slot_id, nh, nid, cap - 1);
+    hipLaunchKernelGGL(k_rehash_ip, dim3(grid_for(e->ip_cap)), dim3(kBlock), 0, e->stream, e->ip_cap, S.ip, nt, cap - 1);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(e->stream));
-    (void)hipFree(S.ip_slot_hash); (void)hipFree(S.ip_slot_id); (void)hipFree(S.ip_off); (void)hipFree(S.ip_len);
-    S.ip_slot_hash = nh; S.ip_slot_id = nid; S.ip_off = noff; S.ip_len = nlen;
+    (void)hipFree(S.ip); (void)hipFree(S.ip_first); (void)hipFree(S.ip_off); (void)hipFree(S.ip_len);
+    S.ip = nt; S.ip_first = nf; S.ip_off = noff; S.ip_len = nlen;
     S.ip_mask = cap - 1;
     e->ip_cap = cap;
-    e->max_ips = cap - cap / 4;
   }
   if (used + new_bytes > S.arena_cap) {
-    uint64_t cap = std::max<uint64_t>(S.arena_cap * 2, used + new_bytes + (1 << 20));
+    const uint64_t cap = std::max<uint64_t>(S.arena_cap * 2, used + new_bytes + (1 << 20));
     uint8_t *na;
     HIP_OK(hipMalloc(&na, cap));
     HIP_OK(hipMemcpyAsync(na, S.arena, used, hipMemcpyDeviceToDevice, e->stream));
@@ -2103,18 +2201,15 @@ void ensure_capacity(bjx_engine *e, uint64_t new_ips, uint64_t new_bytes, uint64
     S.arena_cap = cap;
   }
   if ((n_st + new_states) * 4 > e->st_cap * 3) {
-    uint64_t cap = next_pow2((n_st + new_states) * 2 + 1024);
-    uint64_t *nk; int64_t *nh, *ns;
-    HIP_OK(hipMalloc(&nk, cap * 8));
-    HIP_OK(hipMalloc(&nh, cap * 8));
-    HIP_OK(hipMalloc(&ns, cap * 8));
-    HIP_OK(hipMemsetAsync(nk, 0, cap * 8, e->stream));
-    hipLaunchKernelGGL(k_rehash_st, dim3(grid_for(e->st_cap)), dim3(kBlock), 0, e->stream, e->st_cap, S.st_key,
-                       S.st_hits, S.st_start, nk, nh, ns, cap - 1);
+    const uint64_t cap = next_pow2((n_st + new_states) * 2 + 1024);
+    StSlot *nt;
+    HIP_OK(hipMalloc(&nt, cap * sizeof(StSlot)));
+    HIP_OK(hipMemsetAsync(nt, 0, cap * sizeof(StSlot), e->stream));
+    hipLaunchKernelGGL(k_rehash_st, dim3(grid_for(e->st_cap)), dim3(kBlock), 0, e->stream, e->st_cap, S.st, nt, cap - 1);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(e->stream));
-    (void)hipFree(S.st_key); (void)hipFree(S.st_hits); (void)hipFree(S.st_start);
-    S.st_key = nk; S.st_hits = nh; S.st_start = ns;
+    (void)hipFree(S.st);
+    S.st = nt;
     S.st_mask = cap - 1;
     e->st_cap = cap;
   }
@@ -2170,14 +2265,16 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   (void)hipStreamSynchronize(e->stream);
   free_state(e);
   e->trips.release(); e->results.release(); e->line_flags.release();
-  for (auto *b : {&e->staging, &e->l_flags, &e->head_flag, &e->rl_out, &e->processed, &e->trip_flag, &e->bind_blob,
+  for (auto *b : {&e->staging, &e->l_flags, &e->ev_out, &e->rl_out, &e->trip_flag, &e->bind_blob,
                   &e->cub_tmp, &e->q_ip})
     b->release();
   e->tile_counts.release(); e->tile_base.release(); e->nl.release(); e->l_ts.release(); e->l_iph.release();
   e->l_counts.release(); e->l_offs.release(); e->l_masks.release(); e->l_ipoff.release(); e->l_iplen.release();
   e->l_hoff.release(); e->l_hlen.release(); e->l_roff.release(); e->slow_list.release(); e->l_hid.release();
-  e->scalars.release(); e->res_seq.release(); e->res_rule.release(); e->ev_key.release(); e->ev_res.release();
-  e->ev_key2.release(); e->ev_res2.release(); e->heads.release(); e->trip_idx.release(); e->d_trips.release();
+  e->scalars.release(); e->res_seq.release(); e->res_rule.release(); e->ev_el.release(); e->ev_rule.release();
+  e->ev_res.release(); e->ev_st.release(); e->ev_st2.release(); e->ev_idx.release(); e->ev_idx2.release();
+  e->el_slot.release(); e->coll.release(); e->ev_rec.release(); e->ev_rec2.release(); e->el_id.release();
+  e->run_heads.release(); e->run_flag.release(); e->trip_idx.release(); e->d_trips.release();
   e->d_results.release(); e->q_out.release();
   e->long_list.release(); e->jobs.release(); e->l_cand.release(); e->l_ccnt.release();
   (void)hipEventDestroy(e->ev0); (void)hipEventDestroy(e->ev1); (void)hipEventDestroy(e->evm0); (void)hipEventDestroy(e->evm1);
@@ -2220,6 +2317,69 @@ static void mark(bjx_engine *e, int k) {
     HIP_OK(hipStreamSynchronize(e->stream));
     fprintf(stderr, "[bjx] phase %d done\n", k);
   }
+}
+
+// RegexRateLimitStates.Apply for n_ev events (reference order) whose lines are
+// E; writes e->ev_out[k].  n_el / el_bytes bound the new IPs / arena bytes.
+// Phases 5 (IP + state slots), 6 (sort), 7 (automaton).
+static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t n_el, uint64_t el_bytes, uint64_t n_ev,
+                             const uint32_t *ev_el, const uint32_t *ev_rule) {
+  hipStream_t st = e->stream;
+  if (E.n >= 0x7FFFFFFFull || n_ev >= 0xFFFFFFFFull) throw BjxError(BJX_ERR_ARG, "batch too large (2^31 lines / 2^32 events)");
+  ensure_capacity(e, n_el, el_bytes, n_ev);
+  if (e->host_counters[0] + n_el >= 0x7FFFFFFFull) throw BjxError(BJX_ERR_CAPACITY, "more than 2^31 distinct IPs");
+  if (++e->epoch == 0) ++e->epoch;  // 0 marks a slot being claimed
+  const uint32_t epoch = e->epoch;
+  e->el_slot.ensure(E.n); e->el_id.ensure(E.n); e->coll.ensure(E.n);
+  e->ev_st.ensure(n_ev); e->ev_st2.ensure(n_ev); e->ev_rec.ensure(n_ev); e->ev_rec2.ensure(n_ev);
+  e->ev_out.ensure(n_ev); e->run_flag.ensure(n_ev); e->run_heads.ensure(n_ev);
+  HIP_OK(hipMemsetAsync(e->S.counters + 3, 0, 8, st));
+  mark(e, 5);
+  hipLaunchKernelGGL(k_ip_claim, dim3(grid_for(E.n)), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p);
+  HIP_OK(hipGetLastError());
+  hipLaunchKernelGGL(k_ip_commit, dim3(grid_for(E.n)), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p,
+                     e->coll.p);
+  HIP_OK(hipGetLastError());
+  uint64_t n_coll = 0;
+  HIP_OK(hipMemcpyAsync(&n_coll, e->S.counters + 3, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  if (n_coll) {  // distinct IPs with one 64-bit hash in this batch: resolve exactly, in line order
+    if (n_coll > 1) {
+      uint32_t *ki = e->coll.p, *ko = e->ev_st2.p;
+      cub_call(e, [&](void *tmp, size_t &bytes) {
+        return hipcub::DeviceRadixSort::SortKeys(tmp, bytes, ki, ko, (int)n_coll, 0, 32, st);
+      });
+      HIP_OK(hipMemcpyAsync(e->coll.p, e->ev_st2.p, n_coll * 4, hipMemcpyDeviceToDevice, st));
+    }
+    hipLaunchKernelGGL(k_ip_collide, dim3(1), dim3(64), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p, e->coll.p, n_coll);
+    HIP_OK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_st_claim, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, E, n_ev, ev_el, ev_rule, e->el_slot.p,
+                     e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_rec.p);
+  HIP_OK(hipGetLastError());
+  mark(e, 6);
+  {
+    uint32_t *ki = e->ev_st.p, *ko = e->ev_st2.p;
+    EvRec *vi = e->ev_rec.p, *vo = e->ev_rec2.p;
+    const int bits = std::max(1, bit_width(e->st_cap - 1));
+    cub_call(e, [&](void *tmp, size_t &bytes) {
+      return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)n_ev, 0, bits, st);
+    });
+  }
+  hipLaunchKernelGGL(k_run_heads, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_st2.p, e->run_flag.p);
+  HIP_OK(hipGetLastError());
+  {
+    hipcub::CountingInputIterator<uint32_t> it(0);
+    uint8_t *fl = e->run_flag.p;
+    uint32_t *o = e->run_heads.p;
+    unsigned long long *ns = e->scalars.p + 5;
+    cub_call(e, [&](void *tmp, size_t &bytes) {
+      return hipcub::DeviceSelect::Flagged(tmp, bytes, it, fl, o, ns, (int)n_ev, st);
+    });
+  }
+  hipLaunchKernelGGL(k_apply, dim3(2048), dim3(kBlock), 0, st, n_ev, e->scalars.p + 5, e->run_heads.p, e->ev_st2.p,
+                     e->ev_rec2.p, B.rules, e->S.st, e->ev_out.p);
+  HIP_OK(hipGetLastError());
 }
 
 static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns, uint32_t flags,
@@ -2379,61 +2539,37 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
   out->n_results = n_res;
   out->n_events = n_ev;
   e->res_seq.ensure(n_res + 1); e->res_rule.ensure(n_res + 1); e->rl_out.ensure(n_res + 1);
-  e->ev_key.ensure(n_ev + 1); e->ev_res.ensure(n_ev + 1); e->ev_key2.ensure(n_ev + 1); e->ev_res2.ensure(n_ev + 1);
+  e->ev_el.ensure(n_ev + 1); e->ev_rule.ensure(n_ev + 1); e->ev_res.ensure(n_ev + 1);
+  HIP_OK(hipMemsetAsync(e->scalars.p + 1, 0, 2 * 8, st));
   if (n_res) {
-    hipLaunchKernelGGL(k_emit, dim3(grid_for(n_lines)), dim3(kBlock), 0, st, B, n_lines, L, e->l_offs.p, e->res_seq.p,
-                       e->res_rule.p, e->ev_key.p, e->ev_res.p);
+    hipLaunchKernelGGL(k_emit, dim3((unsigned)std::min<uint64_t>(grid_for(n_lines), 4096)), dim3(kBlock), 0, st, B, n_lines, L, e->l_offs.p, e->res_seq.p,
+                       e->res_rule.p, e->ev_el.p, e->ev_rule.p, e->ev_res.p, e->scalars.p + 1);
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemsetAsync(e->rl_out.p, 0, n_res, st));
   }
   mark(e, 4);
 
-  // ---- rate limiting: group events per IP (stable), one thread per IP
+  // ---- rate limiting (RegexRateLimitStates.Apply for every event)
   uint64_t n_trips = 0;
   if (n_ev) {
-    {
-      uint32_t *ki = e->ev_key.p, *ko = e->ev_key2.p, *vi = e->ev_res.p, *vo = e->ev_res2.p;
-      cub_call(e, [&](void *tmp, size_t &bytes) {
-        return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)n_ev, 0, 32, st);
-      });
-    }
-    mark(e, 5);
-    e->head_flag.ensure(n_ev); e->heads.ensure(n_ev + 1); e->processed.ensure(n_ev);
-    HIP_OK(hipMemsetAsync(e->scalars.p + 1, 0, 3 * 8, st));
-    hipLaunchKernelGGL(k_heads, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_key2.p, e->ev_res2.p, e->res_seq.p,
-                       L, e->head_flag.p, e->scalars.p + 1);
-    HIP_OK(hipGetLastError());
-    {
-      hipcub::CountingInputIterator<uint32_t> it(0);
-      uint8_t *fl = e->head_flag.p;
-      uint32_t *o = e->heads.p;
-      unsigned long long *ns = e->scalars.p + 3;
-      cub_call(e, [&](void *tmp, size_t &bytes) {
-        return hipcub::DeviceSelect::Flagged(tmp, bytes, it, fl, o, ns, (int)n_ev, st);
-      });
-    }
-    unsigned long long sc[3] = {0, 0, 0};
-    HIP_OK(hipMemcpyAsync(sc, e->scalars.p + 1, 24, hipMemcpyDeviceToHost, st));
+    unsigned long long bnd[2] = {0, 0};
+    HIP_OK(hipMemcpyAsync(bnd, e->scalars.p + 1, 16, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    const uint64_t n_seg = sc[2];
-    if (n_seg == 0) throw BjxError(BJX_ERR_DEVICE, "internal: no event segments");
-    ensure_capacity(e, sc[0] + 1024, sc[1] + 4096, n_ev);
-    HIP_OK(hipMemsetAsync(e->processed.p, 0, n_ev, st));
-    mark(e, 6);
-    hipLaunchKernelGGL(k_ratelimit, dim3(grid_for(n_seg)), dim3(kBlock), 0, st, n_seg, n_ev, e->heads.p, e->ev_res2.p,
-                       e->res_seq.p, e->res_rule.p, e->nl.p, buf, L, B.rules, e->S, e->rl_out.p, e->processed.p);
-    HIP_OK(hipGetLastError());
+    EvSrc E;
+    E.bytes = buf; E.nl = e->nl.p; E.ip_off = L.ip_off; E.ip_pos = nullptr; E.ip_len = L.ip_len;
+    E.ip_hash = L.ip_hash; E.ts = L.ts; E.counts = L.counts; E.n = n_lines;
+    rate_limit_stage(e, B, E, bnd[0], bnd[1], n_ev, e->ev_el.p, e->ev_rule.p);
     mark(e, 7);
-    // trips in reference order
-    e->trip_flag.ensure(n_res); e->trip_idx.ensure(n_res + 1);
-    hipLaunchKernelGGL(k_flag_trips, dim3(grid_for(n_res)), dim3(kBlock), 0, st, n_res, e->rl_out.p, e->trip_flag.p);
+    // trips in reference order (events are in reference order)
+    e->trip_flag.ensure(n_ev); e->trip_idx.ensure(n_ev + 1);
+    hipLaunchKernelGGL(k_flag_trips, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_out.p, e->trip_flag.p);
     {
       hipcub::CountingInputIterator<uint32_t> it(0);
       uint8_t *fl = e->trip_flag.p;
       uint32_t *o = e->trip_idx.p;
       unsigned long long *ns = e->scalars.p + 4;
       cub_call(e, [&](void *tmp, size_t &bytes) {
-        return hipcub::DeviceSelect::Flagged(tmp, bytes, it, fl, o, ns, (int)n_res, st);
+        return hipcub::DeviceSelect::Flagged(tmp, bytes, it, fl, o, ns, (int)n_ev, st);
       });
     }
     unsigned long long nt = 0;
@@ -2442,11 +2578,15 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
     n_trips = nt;
     if (n_trips) {
       e->d_trips.ensure(n_trips);
-      hipLaunchKernelGGL(k_build_trips, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_idx.p, e->res_seq.p,
-                         e->res_rule.p, e->nl.p, L, B.rules, e->d_trips.p);
+      hipLaunchKernelGGL(k_build_trips, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_idx.p, e->ev_el.p,
+                         e->ev_rule.p, e->nl.p, L, B.rules, e->d_trips.p);
       HIP_OK(hipGetLastError());
       e->trips.resize(n_trips);
       HIP_OK(hipMemcpyAsync(e->trips.data(), e->d_trips.p, n_trips * sizeof(bjx_trip), hipMemcpyDeviceToHost, st));
+    }
+    if (flags & BJX_COPY_RESULTS) {
+      hipLaunchKernelGGL(k_scatter_rl, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_res.p, e->ev_out.p, e->rl_out.p);
+      HIP_OK(hipGetLastError());
     }
   }
   HIP_OK(hipEventRecord(e->ev1, st));
@@ -2546,8 +2686,9 @@ extern "C" int bjx_state_clear(bjx_engine *e) {
   std::lock_guard<std::mutex> g(e->mu);
   try {
     HIP_OK(hipSetDevice(e->device));
-    HIP_OK(hipMemsetAsync(e->S.ip_slot_hash, 0, e->ip_cap * 8, e->stream));
-    HIP_OK(hipMemsetAsync(e->S.st_key, 0, e->st_cap * 8, e->stream));
+    HIP_OK(hipMemsetAsync(e->S.ip, 0, e->ip_cap * sizeof(IpSlot), e->stream));
+    HIP_OK(hipMemsetAsync(e->S.ip_first, 0xFF, e->ip_cap * 4, e->stream));
+    HIP_OK(hipMemsetAsync(e->S.st, 0, e->st_cap * sizeof(StSlot), e->stream));
     HIP_OK(hipMemsetAsync(e->S.counters, 0, 64, e->stream));
     HIP_OK(hipStreamSynchronize(e->stream));
     return BJX_OK;
@@ -2564,19 +2705,17 @@ extern "C" size_t bjx_state_dump(bjx_engine *e, char *out, size_t cap) {
     HIP_OK(hipSetDevice(e->device));
     read_counters(e);
     const uint64_t n_ips = e->host_counters[0], used = e->host_counters[1];
-    std::vector<uint64_t> off(n_ips), keys(e->st_cap);
+    std::vector<uint64_t> off(n_ips);
     std::vector<uint32_t> len(n_ips);
-    std::vector<int64_t> hits(e->st_cap), start(e->st_cap);
+    std::vector<StSlot> st(e->st_cap);
     std::vector<uint8_t> arena(used);
     HIP_OK(hipMemcpy(off.data(), e->S.ip_off, n_ips * 8, hipMemcpyDeviceToHost));
     HIP_OK(hipMemcpy(len.data(), e->S.ip_len, n_ips * 4, hipMemcpyDeviceToHost));
     HIP_OK(hipMemcpy(arena.data(), e->S.arena, used, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(keys.data(), e->S.st_key, e->st_cap * 8, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(hits.data(), e->S.st_hits, e->st_cap * 8, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(start.data(), e->S.st_start, e->st_cap * 8, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(st.data(), e->S.st, e->st_cap * sizeof(StSlot), hipMemcpyDeviceToHost));
     std::vector<std::vector<std::pair<uint32_t, uint64_t>>> per_ip(n_ips);
     for (uint64_t i = 0; i < e->st_cap; ++i)
-      if (keys[i]) per_ip[(keys[i] >> 24) - 1].push_back({(uint32_t)(keys[i] & 0xFFFFFF), i});
+      if (st[i].key && st[i].valid) per_ip[(st[i].key >> 24) - 1].push_back({(uint32_t)(st[i].key & 0xFFFFFF), i});
     std::string s;
     char buf[96];
     for (uint64_t id = 0; id < n_ips; ++id) {
@@ -2588,7 +2727,7 @@ extern "C" size_t bjx_state_dump(bjx_engine *e, char *out, size_t cap) {
                 });
       for (auto &p : per_ip[id]) {
         s += "\t" + e->names[p.first] + ":\n";
-        snprintf(buf, sizeof buf, "\t\t{%lld %lld}\n", (long long)hits[p.second], (long long)start[p.second]);
+        snprintf(buf, sizeof buf, "\t\t{%lld %lld}\n", (long long)st[p.second].hits, (long long)st[p.second].start);
         s += buf;
       }
       s += "\n";

@@ -142,19 +142,60 @@ struct Lines {
 
 // Persistent rate-limit state (RegexRateLimitStates, rate_limit.go:17-21),
 // keyed by IP string and rule name, never evicted (as in the reference).
+//   IP table: open addressing on the 64-bit hash of the IP bytes, one 16 B
+//   slot per probe; the IP bytes live in the arena (id -> offset, length) and
+//   every lookup of an IP created in an earlier batch compares them in full.
+//   born = batch epoch that created the slot; first = smallest event-line
+//   index of the batch that created it (seenIp of its first event).
+struct IpSlot {
+  uint64_t hash;  // 0 = empty
+  uint32_t id;    // dense IP id (arena index)
+  uint32_t born;  // epoch of creation (0 only while being claimed)
+};
+//   State table: open addressing on key = ((ip_id + 1) << 24) | name_id,
+//   one 32 B slot per probe (NumHitsAndIntervalStart, rate_limit.go:165-168).
+struct StSlot {
+  uint64_t key;    // 0 = empty
+  int64_t hits;    // NumHits (Go int)
+  int64_t start;   // IntervalStartTime, ns
+  uint64_t valid;  // 0 = claimed this batch, no state yet (Apply's FirstTime branch)
+};
 struct State {
-  uint64_t *ip_slot_hash;  // 0 = empty
-  uint32_t *ip_slot_id;
-  uint64_t *ip_off;        // id -> arena offset
+  IpSlot *ip;
+  uint32_t *ip_first;  // per IP slot (meaningful while born == current epoch)
+  uint64_t *ip_off;    // id -> arena offset
   uint32_t *ip_len;
   uint8_t *arena;
-  uint64_t *st_key;        // 0 = empty; key = ((ip_id + 1) << 24) | name_id
-  int64_t *st_hits;
-  int64_t *st_start;
-  uint64_t *counters;      // [0] ips, [1] arena bytes, [2] states
+  StSlot *st;
+  uint64_t *counters;  // [0] ips, [1] arena bytes, [2] states, [3] hash-collision lines (per batch)
   uint64_t ip_mask;
   uint64_t st_mask;
   uint64_t arena_cap;
+};
+
+// One rate-limit event as the sort carries it (16 B): line timestamp, rule
+// index | (first event of a new IP) << 31, event index (reference order).
+struct EvRec {
+  int64_t ts;
+  uint32_t rule;
+  uint32_t ev;
+};
+
+// Rate-limit input: the lines ("event lines") whose matched rules reach
+// RegexRateLimitStates.Apply, and the events themselves in reference order.
+// A local batch uses the line arrays directly (nl != nullptr: the IP is at
+// line start + ip_off); records exchanged between GPUs carry explicit IP
+// offsets into their own byte pool (nl == nullptr).
+struct EvSrc {
+  const uint8_t *bytes;
+  const uint64_t *nl;
+  const uint32_t *ip_off;
+  const uint64_t *ip_pos;
+  const uint32_t *ip_len;
+  const uint64_t *ip_hash;
+  const int64_t *ts;
+  const uint64_t *counts;  // local batch: low 32 bits = events of line i; nullptr: every record has events
+  uint64_t n;
 };
 
 enum LineFlagBits : uint8_t {

@@ -98,7 +98,7 @@ class Engine:
         self._check(rc, "process_batch")
         return BatchOutput(res, copy_results)
 
-    PHASES = ("count", "scan", "resolve", "emit", "event_sort", "segment", "rate_limit", "trips")
+    PHASES = ("count", "scan", "resolve", "emit", "capacity", "ip_state_claim", "sort_apply", "trips")
 
     def scan_stats(self):
         out = (C.c_uint64 * 5)()
