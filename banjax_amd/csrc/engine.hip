@@ -1249,6 +1249,11 @@ __global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const unsigned 
   }
 }
 
+__global__ void k_dbg_mask_hash(uint64_t n, uint64_t *__restrict__ h, uint64_t mask) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) h[i] = (h[i] & mask) | 1;
+}
+
 __global__ void k_flag_trips(uint64_t n, const uint8_t *__restrict__ ev_out, uint8_t *__restrict__ f) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) f[i] = (ev_out[i] & 8) ? 1 : 0;
@@ -1542,6 +1547,7 @@ struct bjx_engine {
   State S{};
   uint64_t ip_cap = 0, st_cap = 0;
   uint32_t epoch = 0;  // batch counter (IpSlot.born)
+  uint64_t dbg_hash_mask = 0;  // bjx_debug_set_ip_hash_mask
   uint64_t host_counters[3] = {0, 0, 0};
 
   // batch workspace
@@ -2522,6 +2528,8 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
     HIP_OK(hipGetLastError());
   }
   e->last_slow = n_slow;
+  if (e->dbg_hash_mask)
+    hipLaunchKernelGGL(k_dbg_mask_hash, dim3(grid_for(n_lines)), dim3(kBlock), 0, st, n_lines, L.ip_hash, e->dbg_hash_mask);
   mark(e, 3);
 
   // ---- RuleResults + events in reference order
@@ -2652,7 +2660,8 @@ extern "C" int bjx_state_get(bjx_engine *e, const char *ip, size_t ip_len, const
     e->q_ip.ensure(ip_len + 1);
     e->q_out.ensure(4);
     if (ip_len) HIP_OK(hipMemcpyAsync(e->q_ip.p, ip, ip_len, hipMemcpyHostToDevice, e->stream));
-    const uint64_t h = hash_bytes(reinterpret_cast<const uint8_t *>(ip), (uint32_t)ip_len);
+    uint64_t h = hash_bytes(reinterpret_cast<const uint8_t *>(ip), (uint32_t)ip_len);
+    if (e->dbg_hash_mask) h = (h & e->dbg_hash_mask) | 1;
     hipLaunchKernelGGL(k_state_get, dim3(1), dim3(1), 0, e->stream, e->S, h, e->q_ip.p, (uint32_t)ip_len, it->second, e->q_out.p);
     HIP_OK(hipGetLastError());
     int64_t o[3];
@@ -2746,6 +2755,12 @@ extern "C" size_t bjx_state_dump(bjx_engine *e, char *out, size_t cap) {
 extern "C" int bjx_debug_rule_match_host(const bjx_ruleset *rs, size_t i, const uint8_t *text, size_t n) {
   if (!rs || i >= rs->rules.size() || (n && !text)) return BJX_ERR_ARG;
   return dfa_match_host(rs->rules[i].rx, text, n) ? 1 : 0;
+}
+extern "C" int bjx_debug_set_ip_hash_mask(bjx_engine *e, uint64_t mask) {
+  if (!e) return BJX_ERR_ARG;
+  std::lock_guard<std::mutex> g(e->mu);
+  e->dbg_hash_mask = mask;
+  return BJX_OK;
 }
 extern "C" size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap) {
   if (!e) return 0;

@@ -121,6 +121,10 @@ class Engine:
     def state_len(self) -> int:
         return self._check(_lib.lib().bjx_state_len(self._h), "state_len")
 
+    def debug_set_ip_hash_mask(self, mask: int):
+        """Test hook: IP hashes become (hash & mask) | 1 (0 = off)."""
+        self._check(_lib.lib().bjx_debug_set_ip_hash_mask(self._h, mask), "debug_set_ip_hash_mask")
+
     def state_clear(self):
         self._check(_lib.lib().bjx_state_clear(self._h), "state_clear")
 

@@ -18,12 +18,16 @@ extern "C" {
 int bjx_debug_rule_match_host(const bjx_ruleset *rs, size_t rule_idx, const uint8_t *text, size_t n);
 /* required literal the prefilter uses for a rule (bytes written, full length returned) */
 size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t rule_idx, char *out, size_t cap);
-/* device ms of the last batch's phases: framing, match, slow timestamps, emit,
-   event sort, segmenting, rate limit, trips (returns the phase count) */
+/* device ms of the last batch's phases: framing count, scan, per-line resolve,
+   emit, capacity check, IP/state slot claim, sort + automaton, trips
+   (returns the phase count) */
 size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap);
 /* last batch: gram bitset hits, recorded literal hits, lines sent to the per-line
    fallback, lines decided by the long-line pass, DFA jobs */
 size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap);
+/* Test hook: IP hashes become (hash & mask) | 1 (0 = off), so distinct IPs
+   share 64-bit hashes and the exact collision path of the IP table runs. */
+int bjx_debug_set_ip_hash_mask(bjx_engine *e, uint64_t mask);
 #ifdef __cplusplus
 }
 #endif

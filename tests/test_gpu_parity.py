@@ -395,3 +395,25 @@ def test_tile_geometry(engine, seed):
     # same bytes shifted by a few bytes: every literal lands on other tile offsets
     pair.feed(b"\n" * (seed * 7) + data, t * S)
     pair.compare_state(["10.0.0.1", "10.0.1.2", "9.9.9.1"])
+
+
+@pytest.mark.parametrize("mask", [0xFF, 0xFFF])
+def test_ip_hash_collisions(engine, mask):
+    """Distinct IPs forced onto a few 64-bit hash values (test hook): the IP
+    table's exact byte compares and the serial collision resolver
+    (k_ip_collide) must keep every IP's state separate, across batches."""
+    w = W.scaled(W.CFG5, 30_000, n_ips=6_000)
+    engine.debug_set_ip_hash_mask(mask)
+    try:
+        pair = Pair(w.rules_yaml, engine)
+        ips = set()
+        for b in range(3):
+            data = w.host_lines(b * 10_000, 10_000)
+            for ln in data.split(b"\n")[:300]:
+                parts = ln.split(b" ")
+                if len(parts) > 2:
+                    ips.add(parts[1].decode())
+            pair.feed(data, w.now_ns(b * 10_000, 10_000))
+        pair.compare_state(sorted(ips)[:60])
+    finally:
+        engine.debug_set_ip_hash_mask(0)
