@@ -58,12 +58,19 @@ class BatchResult(C.Structure):
                 ("match_kernel_ms", C.c_double)]
 
 
+class EventLine(C.Structure):
+    """bjx_event_line: one rate-limit record exchanged between GPUs (32 B)."""
+    _fields_ = [("ts_ns", C.c_int64), ("ip_hash", C.c_uint64), ("ip_off", C.c_uint32), ("ip_len", C.c_uint32),
+                ("n_events", C.c_uint32), ("_pad", C.c_uint32)]
+
+
 # every symbol include/banjax_gpu.h declares
 EXPORTS = [
     "bjx_abi_version", "bjx_ruleset_compile", "bjx_ruleset_release", "bjx_ruleset_num_rules",
     "bjx_ruleset_rule_info", "bjx_engine_create", "bjx_engine_destroy", "bjx_engine_set_decision_lists",
     "bjx_process_batch", "bjx_state_get", "bjx_state_len", "bjx_state_clear", "bjx_state_dump",
-    "bjx_engine_last_error",
+    "bjx_engine_last_error", "bjx_match_batch", "bjx_events_partition", "bjx_events_pack", "bjx_apply_events",
+    "bjx_finish_batch",
 ]
 
 _lib = None
@@ -107,6 +114,16 @@ def lib():
     L.bjx_engine_set_decision_lists.argtypes = [vp, C.POINTER(DecisionEntry), sz]
     L.bjx_process_batch.restype = C.c_int
     L.bjx_process_batch.argtypes = [vp, vp, vp, sz, C.c_int64, C.c_uint32, C.POINTER(BatchResult)]
+    L.bjx_match_batch.restype = C.c_int
+    L.bjx_match_batch.argtypes = [vp, vp, vp, sz, C.c_int64, C.c_uint32, C.POINTER(BatchResult)]
+    L.bjx_events_partition.restype = C.c_int
+    L.bjx_events_partition.argtypes = [vp, C.c_uint32, C.POINTER(C.c_uint64)]
+    L.bjx_events_pack.restype = C.c_int
+    L.bjx_events_pack.argtypes = [vp, vp, vp, vp]
+    L.bjx_apply_events.restype = C.c_int
+    L.bjx_apply_events.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, C.POINTER(C.c_uint64), vp]
+    L.bjx_finish_batch.restype = C.c_int
+    L.bjx_finish_batch.argtypes = [vp, vp, C.c_uint32, C.POINTER(BatchResult)]
     L.bjx_state_get.restype = C.c_int
     L.bjx_state_get.argtypes = [vp, C.c_char_p, sz, C.c_char_p, sz, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.bjx_state_len.restype = C.c_int64

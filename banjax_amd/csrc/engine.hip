@@ -1331,6 +1331,115 @@ __global__ void k_rehash_st(uint64_t old_cap, const StSlot *__restrict__ o, StSl
   }
 }
 
+// --------------------------------------------------------------- multi-GPU exchange
+// owner of each event line: (ip_hash >> 32) % n_parts; lines without events sort last
+__global__ void k_part_keys(uint64_t n_lines, const uint64_t *__restrict__ counts, const uint64_t *__restrict__ ip_hash,
+                            uint32_t n_parts, uint32_t *__restrict__ key, uint32_t *__restrict__ val) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_lines) return;
+  key[j] = (counts[j] & 0xFFFFFFFFull) ? (uint32_t)((ip_hash[j] >> 32) % n_parts) : n_parts;
+  val[j] = (uint32_t)j;
+}
+
+// scan inputs per packed line (index n_el: 0, so the exclusive scans end in totals)
+__global__ void k_pack_prep(uint64_t n_el, const uint32_t *__restrict__ line, const uint64_t *__restrict__ counts,
+                            const uint32_t *__restrict__ ip_len, uint64_t *__restrict__ nev, uint64_t *__restrict__ ipl) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p > n_el) return;
+  if (p == n_el) { nev[p] = 0; ipl[p] = 0; return; }
+  const uint32_t j = line[p];
+  nev[p] = counts[j] & 0xFFFFFFFFull;
+  ipl[p] = ip_len[j];
+}
+
+// first packed index of each owner (keys sorted); start[] preset to n_el
+__global__ void k_part_bounds(uint64_t n_el, const uint32_t *__restrict__ key, uint64_t *__restrict__ start) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n_el && (p == 0 || key[p] != key[p - 1])) start[key[p]] = p;
+}
+
+// per owner: (lines, events, bytes) and the owner's first byte; one thread
+__global__ void k_part_counts(uint32_t n_parts, uint64_t n_el, uint64_t *__restrict__ start,
+                              const uint64_t *__restrict__ ev_off, const uint64_t *__restrict__ by_off,
+                              uint64_t *__restrict__ counts, uint64_t *__restrict__ byte_base) {
+  if (blockIdx.x || threadIdx.x) return;
+  uint64_t nxt = n_el;
+  for (int k = (int)n_parts - 1; k >= 0; --k) {  // owners without lines start where the next one does
+    if (start[k] > nxt) start[k] = nxt;
+    nxt = start[k];
+  }
+  for (uint32_t k = 0; k < n_parts; ++k) {
+    const uint64_t b = start[k], e = k + 1 < n_parts ? start[k + 1] : n_el;
+    counts[3 * k + 0] = e - b;
+    counts[3 * k + 1] = ev_off[e] - ev_off[b];
+    counts[3 * k + 2] = by_off[e] - by_off[b];
+    byte_base[k] = by_off[b];
+  }
+}
+
+__global__ void k_pack(uint64_t n_el, const uint32_t *__restrict__ key, const uint32_t *__restrict__ line,
+                       const uint64_t *__restrict__ ev_off, const uint64_t *__restrict__ by_off,
+                       const uint64_t *__restrict__ part_byte_base, const uint8_t *__restrict__ buf,
+                       const uint64_t *__restrict__ nl, Lines L, const uint64_t *__restrict__ offs,
+                       const uint32_t *__restrict__ ev_rule, bjx_event_line *__restrict__ d_lines,
+                       uint32_t *__restrict__ d_events, uint8_t *__restrict__ d_bytes, uint32_t *__restrict__ pack_src) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_el) return;
+  const uint32_t j = line[p];
+  const uint32_t ne = (uint32_t)(L.counts[j] & 0xFFFFFFFFull);
+  const uint32_t len = L.ip_len[j];
+  bjx_event_line r;
+  r.ts_ns = L.ts[j];
+  r.ip_hash = L.ip_hash[j];
+  r.ip_off = (uint32_t)(by_off[p] - part_byte_base[key[p]]);
+  r.ip_len = len;
+  r.n_events = ne;
+  r._pad = 0;
+  d_lines[p] = r;
+  const uint64_t eo = offs[j] & 0xFFFFFFFFull, pe = ev_off[p];
+  for (uint32_t t = 0; t < ne; ++t) {
+    d_events[pe + t] = ev_rule[eo + t];
+    pack_src[pe + t] = (uint32_t)(eo + t);
+  }
+  const uint8_t *ip = buf + line_start(nl, j) + L.ip_off[j];
+  uint8_t *dst = d_bytes + by_off[p];
+  for (uint32_t k = 0; k < len; ++k) dst[k] = ip[k];
+}
+
+// received records of one source -> SoA rate-limit input (absolute IP offsets)
+__global__ void k_unpack_lines(uint64_t n, uint64_t first, uint64_t byte_base, const bjx_event_line *__restrict__ rec,
+                               int64_t *__restrict__ ts, uint64_t *__restrict__ hash, uint64_t *__restrict__ pos,
+                               uint32_t *__restrict__ len, uint64_t *__restrict__ nev) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bjx_event_line r = rec[first + i];
+  ts[first + i] = r.ts_ns;
+  hash[first + i] = r.ip_hash;
+  pos[first + i] = byte_base + r.ip_off;
+  len[first + i] = r.ip_len;
+  nev[first + i] = r.n_events;
+}
+
+// event -> its line (events of line i are [off[i], off[i] + nev[i])); flags bad rule ids
+__global__ void k_expand_events(uint64_t n, const uint64_t *__restrict__ off, const uint64_t *__restrict__ nev,
+                                uint64_t n_ev, const uint32_t *__restrict__ ev_rule, uint32_t n_rules,
+                                uint32_t *__restrict__ ev_el, unsigned long long *__restrict__ bad) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t b = off[i], e = b + nev[i];
+  if (e > n_ev) { atomicAdd(bad, 1ull); return; }
+  for (uint64_t k = b; k < e; ++k) {
+    if (ev_rule[k] >= n_rules) atomicAdd(bad, 1ull);
+    ev_el[k] = (uint32_t)i;
+  }
+}
+
+__global__ void k_scatter_outcomes(uint64_t n, const uint32_t *__restrict__ src, const uint8_t *__restrict__ in,
+                                   uint8_t *__restrict__ out) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) out[src[k]] = in[k];
+}
+
 // state query (RegexRateLimitStates.Get for one (ip, name))
 __global__ void k_state_get(State S, uint64_t h, const uint8_t *ip, uint32_t len, uint32_t name_id, int64_t *out) {
   out[0] = 0;
@@ -1517,6 +1626,15 @@ extern "C" int bjx_ruleset_rule_info(const bjx_ruleset *rs, size_t i, uint32_t *
 
 // ------------------------------------------------------------ engine
 
+struct BatchCtx {
+  const uint8_t *buf = nullptr;
+  uint64_t n_lines = 0, n_res = 0, n_ev = 0;
+  uint64_t n_el = 0, el_bytes = 0;  // lines with events, their IP bytes
+  uint64_t consumed = 0;
+  Lines L{};
+  bool live = false;
+};
+
 struct bjx_engine {
   int device = 0;
   std::mutex mu;
@@ -1579,6 +1697,16 @@ struct bjx_engine {
   DevBuf<uint8_t> cub_tmp;
   DevBuf<int64_t> q_out;
   DevBuf<uint8_t> q_ip;
+
+  // the batch between its match phase and its finish (bjx_match_batch / bjx_finish_batch)
+  BatchCtx bc;
+  // multi-GPU exchange workspace
+  DevBuf<uint32_t> pk_key, pk_key2, pk_line, pk_line2, pack_src, rx_len, rx_ev_el;
+  DevBuf<uint64_t> pk_nev, pk_ipl, pk_evoff, pk_byoff, pk_start, pk_counts, pk_bbase, rx_hash, rx_pos, rx_nev, rx_evoff;
+  DevBuf<int64_t> rx_ts;
+  uint32_t pk_parts = 0;
+  uint64_t pk_n_ev = 0;
+  bool partitioned = false;
 
   // host copies of the last batch
   HostBuf<bjx_trip> trips;
@@ -2280,7 +2408,12 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   e->scalars.release(); e->res_seq.release(); e->res_rule.release(); e->ev_el.release(); e->ev_rule.release();
   e->ev_res.release(); e->ev_st.release(); e->ev_st2.release(); e->ev_idx.release(); e->ev_idx2.release();
   e->el_slot.release(); e->coll.release(); e->ev_rec.release(); e->ev_rec2.release(); e->el_id.release();
-  e->run_heads.release(); e->run_flag.release(); e->trip_idx.release(); e->d_trips.release();
+  e->run_heads.release(); e->run_flag.release();
+  for (auto *b : {&e->pk_key, &e->pk_key2, &e->pk_line, &e->pk_line2, &e->pack_src, &e->rx_len, &e->rx_ev_el}) b->release();
+  for (auto *b : {&e->pk_nev, &e->pk_ipl, &e->pk_evoff, &e->pk_byoff, &e->pk_start, &e->pk_counts, &e->pk_bbase,
+                  &e->rx_hash, &e->rx_pos, &e->rx_nev, &e->rx_evoff})
+    b->release();
+  e->rx_ts.release(); e->trip_idx.release(); e->d_trips.release();
   e->d_results.release(); e->q_out.release();
   e->long_list.release(); e->jobs.release(); e->l_cand.release(); e->l_ccnt.release();
   (void)hipEventDestroy(e->ev0); (void)hipEventDestroy(e->ev1); (void)hipEventDestroy(e->evm0); (void)hipEventDestroy(e->evm1);
@@ -2388,8 +2521,12 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
   HIP_OK(hipGetLastError());
 }
 
-static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns, uint32_t flags,
-                      bjx_batch_result *out) {
+// consumeLine up to Apply for every line: framing, header, exemption, rule
+// matching, RuleResults and events in reference order (phases 0-4).  Leaves
+// the batch context in e->bc; false if the batch has no complete line.
+static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns, uint32_t flags,
+                        bjx_batch_result *out) {
+  e->bc = BatchCtx{};
   HIP_OK(hipSetDevice(e->device));
   if (e->bound_uid != rs->uid || e->bound_dec_version != e->decisions_version) {
     // (re)binding: calibrate the gram filter on the head of this batch
@@ -2409,7 +2546,7 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
   e->trips.clear();
   e->results.clear();
   e->line_flags.clear();
-  if (n == 0) return;
+  if (n == 0) return false;
 
   const uint8_t *buf = bytes;
   if (!(flags & BJX_INPUT_DEVICE) || (reinterpret_cast<uintptr_t>(bytes) & 15)) {
@@ -2442,7 +2579,7 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
   HIP_OK(hipStreamSynchronize(st));
   const uint64_t n_lines = last_base + last_cnt;
   out->n_lines = n_lines;
-  if (n_lines == 0) return;
+  if (n_lines == 0) return false;
 
   // ---- per-line arrays
   e->nl.ensure(n_lines);
@@ -2556,17 +2693,37 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
     HIP_OK(hipMemsetAsync(e->rl_out.p, 0, n_res, st));
   }
   mark(e, 4);
-
-  // ---- rate limiting (RegexRateLimitStates.Apply for every event)
-  uint64_t n_trips = 0;
+  unsigned long long bnd[2] = {0, 0};
   if (n_ev) {
-    unsigned long long bnd[2] = {0, 0};
     HIP_OK(hipMemcpyAsync(bnd, e->scalars.p + 1, 16, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    EvSrc E;
-    E.bytes = buf; E.nl = e->nl.p; E.ip_off = L.ip_off; E.ip_pos = nullptr; E.ip_len = L.ip_len;
-    E.ip_hash = L.ip_hash; E.ts = L.ts; E.counts = L.counts; E.n = n_lines;
-    rate_limit_stage(e, B, E, bnd[0], bnd[1], n_ev, e->ev_el.p, e->ev_rule.p);
+  }
+  BatchCtx &c = e->bc;
+  c.buf = buf; c.n_lines = n_lines; c.n_res = n_res; c.n_ev = n_ev; c.L = L; c.n_el = bnd[0]; c.el_bytes = bnd[1];
+  c.consumed = out->consumed_bytes;
+  c.live = true;
+  return true;
+}
+
+// the local batch's events as rate-limit input
+static EvSrc local_evsrc(bjx_engine *e) {
+  const BatchCtx &c = e->bc;
+  EvSrc E;
+  E.bytes = c.buf; E.nl = e->nl.p; E.ip_off = c.L.ip_off; E.ip_pos = nullptr; E.ip_len = c.L.ip_len;
+  E.ip_hash = c.L.ip_hash; E.ts = c.L.ts; E.counts = c.L.counts; E.n = c.n_lines;
+  return E;
+}
+
+// Trips (reference order) and the optional per-line / RuleResult copies, once
+// e->ev_out holds every local event's Apply outcome (phases 7-8).
+static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out) {
+  const Bind &B = e->bind;
+  hipStream_t st = e->stream;
+  const BatchCtx &c = e->bc;
+  const uint64_t n_lines = c.n_lines, n_res = c.n_res, n_ev = c.n_ev;
+  const Lines &L = c.L;
+  uint64_t n_trips = 0;
+  if (n_ev) {
     mark(e, 7);
     // trips in reference order (events are in reference order)
     e->trip_flag.ensure(n_ev); e->trip_idx.ensure(n_ev + 1);
@@ -2633,6 +2790,14 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
   out->line_flags = e->line_flags.empty() ? nullptr : e->line_flags.data();
 }
 
+static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns, uint32_t flags,
+                      bjx_batch_result *out) {
+  if (!match_phase(e, rs, bytes, n, now_ns, flags, out)) return;
+  if (e->bc.n_ev)
+    rate_limit_stage(e, e->bind, local_evsrc(e), e->bc.n_el, e->bc.el_bytes, e->bc.n_ev, e->ev_el.p, e->ev_rule.p);
+  finish_phase(e, flags, out);
+}
+
 extern "C" int bjx_process_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns,
                                  uint32_t flags, bjx_batch_result *out) {
   if (!e || !rs || !out || (n && !bytes)) return BJX_ERR_ARG;
@@ -2647,6 +2812,175 @@ extern "C" int bjx_process_batch(bjx_engine *e, const bjx_ruleset *rs, const uin
     e->last_error = "host out of memory";
     return BJX_ERR_NOMEM;
   }
+}
+
+// ------------------------------------------------------------ multi-GPU batch
+
+template <typename F>
+static int guarded(bjx_engine *e, F f) {
+  if (!e) return BJX_ERR_ARG;
+  std::lock_guard<std::mutex> g(e->mu);
+  try {
+    HIP_OK(hipSetDevice(e->device));
+    return f();
+  } catch (const BjxError &x) {
+    e->last_error = x.what();
+    return x.code;
+  } catch (const std::bad_alloc &) {
+    e->last_error = "host out of memory";
+    return BJX_ERR_NOMEM;
+  }
+}
+
+extern "C" int bjx_match_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns,
+                               uint32_t flags, bjx_batch_result *out) {
+  if (!rs || !out || (n && !bytes)) return BJX_ERR_ARG;
+  return guarded(e, [&]() -> int {
+    e->partitioned = false;
+    match_phase(e, rs, bytes, n, now_ns, flags, out);
+    return BJX_OK;
+  });
+}
+
+extern "C" int bjx_events_partition(bjx_engine *e, uint32_t n_parts, uint64_t *counts) {
+  if (!counts || n_parts == 0 || n_parts > 4096) return BJX_ERR_ARG;
+  return guarded(e, [&]() -> int {
+    const BatchCtx &c = e->bc;
+    memset(counts, 0, sizeof(uint64_t) * 3 * n_parts);
+    e->pk_parts = n_parts;
+    e->pk_n_ev = 0;
+    e->partitioned = true;
+    if (!c.live || c.n_ev == 0) return BJX_OK;
+    hipStream_t st = e->stream;
+    const uint64_t nl = c.n_lines, n_el = c.n_el;
+    e->pk_key.ensure(nl); e->pk_key2.ensure(nl); e->pk_line.ensure(nl); e->pk_line2.ensure(nl);
+    e->pk_nev.ensure(n_el + 1); e->pk_ipl.ensure(n_el + 1); e->pk_evoff.ensure(n_el + 1); e->pk_byoff.ensure(n_el + 1);
+    e->pk_start.ensure(n_parts + 1); e->pk_counts.ensure(3 * n_parts); e->pk_bbase.ensure(n_parts);
+    hipLaunchKernelGGL(k_part_keys, dim3(grid_for(nl)), dim3(kBlock), 0, st, nl, c.L.counts, c.L.ip_hash, n_parts,
+                       e->pk_key.p, e->pk_line.p);
+    HIP_OK(hipGetLastError());
+    {
+      uint32_t *ki = e->pk_key.p, *ko = e->pk_key2.p, *vi = e->pk_line.p, *vo = e->pk_line2.p;
+      const int bits = std::max(1, bit_width(n_parts));
+      cub_call(e, [&](void *tmp, size_t &bytes) {
+        return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)nl, 0, bits, st);
+      });
+    }
+    hipLaunchKernelGGL(k_pack_prep, dim3(grid_for(n_el + 1)), dim3(kBlock), 0, st, n_el, e->pk_line2.p, c.L.counts,
+                       c.L.ip_len, e->pk_nev.p, e->pk_ipl.p);
+    HIP_OK(hipGetLastError());
+    for (int k = 0; k < 2; ++k) {
+      uint64_t *in = k ? e->pk_ipl.p : e->pk_nev.p, *o = k ? e->pk_byoff.p : e->pk_evoff.p;
+      cub_call(e, [&](void *tmp, size_t &bytes) {
+        return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)(n_el + 1), st);
+      });
+    }
+    HIP_OK(hipMemsetAsync(e->pk_start.p, 0xFF, (n_parts + 1) * 8, st));
+    hipLaunchKernelGGL(k_part_bounds, dim3(grid_for(n_el)), dim3(kBlock), 0, st, n_el, e->pk_key2.p, e->pk_start.p);
+    hipLaunchKernelGGL(k_part_counts, dim3(1), dim3(64), 0, st, n_parts, n_el, e->pk_start.p, e->pk_evoff.p,
+                       e->pk_byoff.p, e->pk_counts.p, e->pk_bbase.p);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(counts, e->pk_counts.p, 3 * n_parts * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    uint64_t tl = 0, te = 0;
+    for (uint32_t k = 0; k < n_parts; ++k) { tl += counts[3 * k]; te += counts[3 * k + 1]; }
+    if (tl != n_el || te != c.n_ev) throw BjxError(BJX_ERR_DEVICE, "internal: partition counts disagree with the batch");
+    e->pk_n_ev = te;
+    return BJX_OK;
+  });
+}
+
+extern "C" int bjx_events_pack(bjx_engine *e, bjx_event_line *d_lines, uint32_t *d_events, uint8_t *d_bytes) {
+  return guarded(e, [&]() -> int {
+    const BatchCtx &c = e->bc;
+    if (!e->partitioned) throw BjxError(BJX_ERR_ARG, "bjx_events_pack before bjx_events_partition");
+    if (!c.live || c.n_ev == 0) return BJX_OK;
+    if (!d_lines || !d_events || (c.el_bytes && !d_bytes)) return BJX_ERR_ARG;
+    hipStream_t st = e->stream;
+    e->pack_src.ensure(c.n_ev);
+    hipLaunchKernelGGL(k_pack, dim3(grid_for(c.n_el)), dim3(kBlock), 0, st, c.n_el, e->pk_key2.p, e->pk_line2.p,
+                       e->pk_evoff.p, e->pk_byoff.p, e->pk_bbase.p, c.buf, e->nl.p, c.L, e->l_offs.p, e->ev_rule.p, d_lines,
+                       d_events, d_bytes, e->pack_src.p);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(st));
+    return BJX_OK;
+  });
+}
+
+extern "C" int bjx_apply_events(bjx_engine *e, const bjx_ruleset *rs, const bjx_event_line *d_lines, const uint32_t *d_events,
+                                const uint8_t *d_bytes, uint32_t n_src, const uint64_t *src_counts, uint8_t *d_out) {
+  if (!rs || (n_src && !src_counts)) return BJX_ERR_ARG;
+  return guarded(e, [&]() -> int {
+    uint64_t n_lines = 0, n_ev = 0, n_bytes = 0;
+    for (uint32_t k = 0; k < n_src; ++k) {
+      n_lines += src_counts[3 * k];
+      n_ev += src_counts[3 * k + 1];
+      n_bytes += src_counts[3 * k + 2];
+    }
+    if (n_ev == 0) return BJX_OK;
+    if (!d_lines || !d_events || !d_out || (n_bytes && !d_bytes)) return BJX_ERR_ARG;
+    if (e->bound_uid != rs->uid || e->bound_dec_version != e->decisions_version) bind_ruleset(e, rs, nullptr, 0);
+    const Bind &B = e->bind;
+    hipStream_t st = e->stream;
+    e->rx_ts.ensure(n_lines); e->rx_hash.ensure(n_lines); e->rx_pos.ensure(n_lines); e->rx_len.ensure(n_lines);
+    e->rx_nev.ensure(n_lines + 1); e->rx_evoff.ensure(n_lines + 1); e->rx_ev_el.ensure(n_ev);
+    uint64_t first = 0, bbase = 0;
+    for (uint32_t k = 0; k < n_src; ++k) {
+      const uint64_t nk = src_counts[3 * k];
+      if (nk)
+        hipLaunchKernelGGL(k_unpack_lines, dim3(grid_for(nk)), dim3(kBlock), 0, st, nk, first, bbase, d_lines, e->rx_ts.p,
+                           e->rx_hash.p, e->rx_pos.p, e->rx_len.p, e->rx_nev.p);
+      first += nk;
+      bbase += src_counts[3 * k + 2];
+    }
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemsetAsync(e->rx_nev.p + n_lines, 0, 8, st));
+    {
+      uint64_t *in = e->rx_nev.p, *o = e->rx_evoff.p;
+      cub_call(e, [&](void *tmp, size_t &bytes) {
+        return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)(n_lines + 1), st);
+      });
+    }
+    HIP_OK(hipMemsetAsync(e->scalars.p + 6, 0, 8, st));
+    hipLaunchKernelGGL(k_expand_events, dim3(grid_for(n_lines)), dim3(kBlock), 0, st, n_lines, e->rx_evoff.p, e->rx_nev.p,
+                       n_ev, d_events, B.n_rules, e->rx_ev_el.p, e->scalars.p + 6);
+    HIP_OK(hipGetLastError());
+    uint64_t chk[2] = {0, 0};
+    HIP_OK(hipMemcpyAsync(&chk[0], e->rx_evoff.p + n_lines, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(&chk[1], e->scalars.p + 6, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (chk[0] != n_ev || chk[1]) throw BjxError(BJX_ERR_ARG, "received event records are inconsistent");
+    EvSrc E;
+    E.bytes = d_bytes; E.nl = nullptr; E.ip_off = nullptr; E.ip_pos = e->rx_pos.p; E.ip_len = e->rx_len.p;
+    E.ip_hash = e->rx_hash.p; E.ts = e->rx_ts.p; E.counts = nullptr; E.n = n_lines;
+    rate_limit_stage(e, B, E, n_lines, n_bytes, n_ev, e->rx_ev_el.p, d_events);
+    HIP_OK(hipMemcpyAsync(d_out, e->ev_out.p, n_ev, hipMemcpyDeviceToDevice, st));
+    HIP_OK(hipStreamSynchronize(st));
+    return BJX_OK;
+  });
+}
+
+extern "C" int bjx_finish_batch(bjx_engine *e, const uint8_t *d_outcomes, uint32_t flags, bjx_batch_result *out) {
+  if (!out) return BJX_ERR_ARG;
+  return guarded(e, [&]() -> int {
+    const BatchCtx &c = e->bc;
+    memset(out, 0, sizeof *out);
+    if (!c.live) return BJX_OK;
+    if (c.n_ev) {
+      if (!e->partitioned || e->pk_n_ev != c.n_ev || !d_outcomes) throw BjxError(BJX_ERR_ARG, "bjx_finish_batch without a packed batch");
+      e->ev_out.ensure(c.n_ev);
+      hipLaunchKernelGGL(k_scatter_outcomes, dim3(grid_for(c.n_ev)), dim3(kBlock), 0, e->stream, c.n_ev, e->pack_src.p,
+                         d_outcomes, e->ev_out.p);
+      HIP_OK(hipGetLastError());
+    }
+    out->n_lines = c.n_lines;
+    out->consumed_bytes = c.consumed;
+    out->n_results = c.n_res;
+    out->n_events = c.n_ev;
+    finish_phase(e, flags, out);
+    e->partitioned = false;
+    return BJX_OK;
+  });
 }
 
 extern "C" int bjx_state_get(bjx_engine *e, const char *ip, size_t ip_len, const char *name, size_t name_len,

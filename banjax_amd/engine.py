@@ -98,6 +98,41 @@ class Engine:
         self._check(rc, "process_batch")
         return BatchOutput(res, copy_results)
 
+    # ---- multi-GPU batch (include/banjax_gpu.h); buffers are device pointers
+    def match(self, rs: Ruleset, now_ns: int, device_ptr: int, nbytes: int, copy_results: bool = False):
+        """consumeLine up to Apply (bjx_match_batch) over a device buffer."""
+        res = _lib.BatchResult()
+        flags = (_lib.COPY_RESULTS if copy_results else 0) | _lib.INPUT_DEVICE
+        self._check(_lib.lib().bjx_match_batch(self._h, rs.handle, C.c_void_p(device_ptr), nbytes, now_ns, flags,
+                                               C.byref(res)), "match_batch")
+        return res
+
+    def events_partition(self, n_parts: int) -> List[Tuple[int, int, int]]:
+        """Per owner: (event lines, events, IP bytes) this engine sends."""
+        arr = (C.c_uint64 * (3 * n_parts))()
+        self._check(_lib.lib().bjx_events_partition(self._h, n_parts, arr), "events_partition")
+        return [(arr[3 * k], arr[3 * k + 1], arr[3 * k + 2]) for k in range(n_parts)]
+
+    def events_pack(self, lines_ptr: int, events_ptr: int, bytes_ptr: int):
+        self._check(_lib.lib().bjx_events_pack(self._h, C.c_void_p(lines_ptr), C.c_void_p(events_ptr),
+                                               C.c_void_p(bytes_ptr)), "events_pack")
+
+    def apply_events(self, rs: Ruleset, lines_ptr: int, events_ptr: int, bytes_ptr: int,
+                     src_counts: List[Tuple[int, int, int]], out_ptr: int):
+        arr = (C.c_uint64 * max(1, 3 * len(src_counts)))()
+        for k, (a, b, c) in enumerate(src_counts):
+            arr[3 * k], arr[3 * k + 1], arr[3 * k + 2] = a, b, c
+        self._check(_lib.lib().bjx_apply_events(self._h, rs.handle, C.c_void_p(lines_ptr), C.c_void_p(events_ptr),
+                                                C.c_void_p(bytes_ptr), len(src_counts), arr, C.c_void_p(out_ptr)),
+                    "apply_events")
+
+    def finish(self, outcomes_ptr: int, copy_results: bool = False) -> BatchOutput:
+        res = _lib.BatchResult()
+        flags = _lib.COPY_RESULTS if copy_results else 0
+        self._check(_lib.lib().bjx_finish_batch(self._h, C.c_void_p(outcomes_ptr), flags, C.byref(res)),
+                    "finish_batch")
+        return BatchOutput(res, copy_results)
+
     PHASES = ("count", "scan", "resolve", "emit", "capacity", "ip_state_claim", "sort_apply", "trips")
 
     def scan_stats(self):

@@ -41,6 +41,50 @@ def cpu_baseline(w, sample_lines):
                       "goroutine, regex_rate_limiter.go:54-77), %.1f s" % (sample_lines, w.name, len(data) / 1e6, dt)}
 
 
+def pmc_traffic(nbytes):
+    """HBM bytes per k_scan launch from the committed rocprofv3 PMC passes over
+    this same command (profiles/<round>/cfg3_bench_pmc_{fetch,write}.csv):
+    FETCH_SIZE x 2 (gfx950 reports half of a wide streaming read,
+    MI355X_MICROARCH.md "HBM") + WRITE_SIZE, both in KB."""
+    import csv
+    import glob
+    best = None
+    for d in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*"))):
+        f, wr = os.path.join(d, "cfg3_bench_pmc_fetch.csv"), os.path.join(d, "cfg3_bench_pmc_write.csv")
+        if os.path.exists(f) and os.path.exists(wr):
+            best = (d, f, wr)
+    if best is None:
+        return None, None
+
+    def mean(path, counter):
+        v = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+             if "k_scan" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+        return sum(v) / len(v) if v else None
+    fe, wb = mean(best[1], "FETCH_SIZE"), mean(best[2], "WRITE_SIZE")
+    if fe is None or wb is None:
+        return None, None
+    return round((2 * fe + wb) * 1024 / 1e9, 3), os.path.relpath(best[0], ROOT)
+
+
+def roofline(achieved, match_ms, nbytes, args):
+    default = args.config == "cfg3" and not args.lines
+    traffic, src = pmc_traffic(nbytes) if default else (None, None)
+    r = {
+        "bound": "hbm",
+        "kernel": "k_scan (HBM-streaming match pass: framing + literal prefilter over every byte)",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": traffic,
+        "algorithmic_GB_per_launch": round(nbytes / 1e9, 3),
+        "kernel_ms": round(match_ms, 3),
+    }
+    if src:
+        r["traffic_source"] = src + " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, same command, GB per launch)"
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -48,7 +92,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--lines", type=int, default=0, help="lines per GPU (default: workload size)")
-    ap.add_argument("--cpu-sample", type=int, default=300_000)
+    ap.add_argument("--cpu-sample", type=int, default=600_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -78,8 +122,15 @@ def main():
     eng.set_decision_lists(cfg.decision_entries)
     now = w.now_ns(first, n_lines)
 
+    ex = None
+    if world > 1:
+        from banjax_amd.distributed import TorchExchange, sharded_batch
+        ex = TorchExchange(torch.device("cuda", local))
+
     def step():
-        return eng.process(rs, None, now, device_ptr=data.data_ptr(), nbytes=nbytes)
+        if ex is None:
+            return eng.process(rs, None, now, device_ptr=data.data_ptr(), nbytes=nbytes)
+        return sharded_batch(eng, rs, now, data.data_ptr(), nbytes, ex)
 
     for _ in range(args.warmup):
         step()
@@ -124,25 +175,18 @@ def main():
                 "lines_per_gpu": n_lines,
                 "bytes_per_gpu": nbytes,
                 "distinct_ips": w.n_ips,
-                "rule_results_per_step": o.n_results,
-                "rate_limit_events_per_step": o.n_events,
-                "trips_per_step": o.n_trips,
-                "device_ms_per_step": round(dev_ms, 3),
-                "phase_ms_last_step": phases,
-                "parallelism": "dp%d: chunk-sharded lines" % world,
+                "rule_results_per_step_rank0": o.n_results,
+                "rate_limit_events_per_step_rank0": o.n_events,
+                "trips_per_step_rank0": o.n_trips,
+                "device_ms_per_step_rank0": round(dev_ms, 3),
+                "pipeline_GBps_rank0": round(nbytes / (ms_per_step / 1000.0) / 1e9, 1),
+                "phase_ms_last_step_rank0": phases,
+                "parallelism": ("dp%d: chunk-sharded match, IP-hash-sharded rate-limit state, RCCL all-to-all of "
+                                "event records" % world) if world > 1 else "dp1",
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "k_parse_match<false> (framing excluded)",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
-                "match_kernel_ms": round(match_ms, 3),
-            },
+            "roofline": roofline(achieved, match_ms, nbytes, args),
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(w, args.cpu_sample)
         print(json.dumps(line), flush=True)
     if dist:

@@ -168,6 +168,41 @@ typedef struct bjx_batch_result {
 int bjx_process_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns,
                       uint32_t flags, bjx_batch_result *out);
 
+/* ---- Multi-GPU batch.  One engine per GPU; each matches its
+   own contiguous chunk of the log, and RegexRateLimitStates shards by IP:
+   event lines go to owner (ip_hash >> 32) % n_parts.  Sequence per engine:
+     bjx_match_batch                     consumeLine up to Apply (no state touched)
+     bjx_events_partition                per-owner sizes of the outgoing records
+     bjx_events_pack                     records into caller device buffers, owner-major
+     -- caller: all-to-all of the three buffers (RCCL) --
+     bjx_apply_events                    Apply for the received records, in source order
+     -- caller: all-to-all of the outcome bytes back --
+     bjx_finish_batch                    trips / RuleResults of the local lines
+   Source order must be stream order (rank r holds the r-th chunk), which makes
+   the owner's event order the reference's.  All buffers are device pointers
+   allocated by the caller; the engine never retains them. */
+typedef struct bjx_event_line {
+  int64_t ts_ns;     /* parsed line timestamp */
+  uint64_t ip_hash;  /* engine hash of the IP bytes */
+  uint32_t ip_off;   /* offset of the IP bytes in this owner's part of the byte buffer */
+  uint32_t ip_len;
+  uint32_t n_events; /* events of the line; their rule indices follow in the event buffer */
+  uint32_t _pad;
+} bjx_event_line;
+
+int bjx_match_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns, uint32_t flags,
+                    bjx_batch_result *out);
+/* counts[3*p + 0/1/2] = event lines / events / IP bytes going to owner p (host array) */
+int bjx_events_partition(bjx_engine *e, uint32_t n_parts, uint64_t *counts);
+int bjx_events_pack(bjx_engine *e, bjx_event_line *d_lines, uint32_t *d_events, uint8_t *d_bytes);
+/* received records of n_src sources, concatenated in source order; src_counts as
+   bjx_events_partition's counts, one triple per source.  d_out: one outcome
+   byte per received event (bit0 seenIp, bits1-2 MatchType, bit3 Exceeded). */
+int bjx_apply_events(bjx_engine *e, const bjx_ruleset *rs, const bjx_event_line *d_lines, const uint32_t *d_events,
+                     const uint8_t *d_bytes, uint32_t n_src, const uint64_t *src_counts, uint8_t *d_out);
+/* d_outcomes: one byte per packed event, in bjx_events_pack order */
+int bjx_finish_batch(bjx_engine *e, const uint8_t *d_outcomes, uint32_t flags, bjx_batch_result *out);
+
 /* RegexRateLimitStates.Get(ip)[name]: 1 found (num_hits, start_ns set), 0 not found, <0 error. */
 int bjx_state_get(bjx_engine *e, const char *ip, size_t ip_len, const char *name, size_t name_len,
                   int64_t *num_hits, int64_t *interval_start_ns);

@@ -12,7 +12,7 @@ import pytest
 import workloads as W
 from banjax_amd import Config, Engine, MockBanner, RegexRateLimiter, consume_line
 from oracle import oracle as O
-from tests.parity import Pair
+from tests.parity import Pair, oracle_config
 
 pytestmark = pytest.mark.gpu
 S = 1_000_000_000
@@ -417,3 +417,70 @@ def test_ip_hash_collisions(engine, mask):
         pair.compare_state(sorted(ips)[:60])
     finally:
         engine.debug_set_ip_hash_mask(0)
+
+
+@pytest.mark.parametrize("wl,world", [(("cfg5", 3000), 2), (("cfg3", 2000), 3)])
+def test_sharded_engines_match_single_process(wl, world):
+    """The multi-GPU path on one GPU: `world` engines as threads (ThreadMesh),
+    each matching its chunk, rate limits sharded by IP hash with the real
+    bjx_events_pack / bjx_apply_events / bjx_finish_batch.  Bit-exact against
+    one oracle over the stream, and each IP's state lives on exactly one engine."""
+    import threading
+
+    import torch
+
+    from banjax_amd import Ruleset
+    from banjax_amd.distributed import ThreadMesh, sharded_batch
+    n_chunks, per = 2 * world, 8000
+    w = W.scaled(W.ALL[wl[0]], per * n_chunks, n_ips=wl[1])
+    cfg = Config.from_yaml(w.rules_yaml)
+    chunks = [w.host_lines(k * per, per) for k in range(n_chunks)]
+    dev = torch.device("cuda", 0)
+    engines = [Engine(0) for _ in range(world)]
+    mesh = ThreadMesh(world)
+    got, errs = {}, []
+
+    def run(r):
+        try:
+            rs = Ruleset(cfg)
+            engines[r].set_decision_lists(cfg.decision_entries)
+            ex = mesh.rank(r, dev)
+            for step in range(n_chunks // world):
+                k = step * world + r
+                t = torch.frombuffer(bytearray(chunks[k]), dtype=torch.uint8).to(dev)
+                out = sharded_batch(engines[r], rs, w.now_ns(0, per), t.data_ptr(), len(chunks[k]), ex,
+                                    copy_results=True)
+                got[k] = ([[x.line_idx, x.rule_idx, x.rule_pos, x.skip_host, x.seen_ip, x.match_type, x.exceeded]
+                           for x in out.results], [(x.line_idx, x.rule_idx) for x in out.trips], bytes(out.line_flags))
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            mesh.barrier.abort()
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    oc = oracle_config(cfg)
+    st = O.State()
+    n_trips = 0
+    for k, data in enumerate(chunks):
+        oflags, ores, _ = st.consume(oc, data, w.now_ns(0, per), cap=(data.count(b"\n") + 1) * (len(cfg.all_rules()) + 1))
+        exp = [[r.line_idx, r.rule_id, r.rule_pos, r.skip_host, r.seen_ip, r.match_type, r.exceeded] for r in ores]
+        results, trips, flags = got[k]
+        assert list(flags) == oflags
+        assert results == exp, "chunk %d" % k
+        assert trips == [(r[0], r[1]) for r in exp if r[6]]
+        n_trips += len(trips)
+    assert n_trips > 0
+    assert sum(e.state_len() for e in engines) == len(st)
+    names = sorted(set(r.rule for r in cfg.all_rules()))
+    for ln in chunks[0].split(b"\n")[:40]:
+        ip = ln.split(b" ")[1]
+        for nm in names:
+            have = [e.state_get(ip, nm) for e in engines]
+            exp = st.get(ip, nm)
+            assert [h for h in have if h is not None] == ([exp] if exp is not None else [])
+    for e in engines:
+        e.close()
