@@ -170,7 +170,7 @@ __device__ __forceinline__ uint64_t be64(const uint8_t *a) {
 
 // IPFilter.Allowed restricted to one scope (decision.go:185-216 with
 // github.com/jeremy5189/ipfilter-no-iploc/v2: exact canonical IPs, then subnets).
-__device__ bool scope_allows_addr(const Bind &B, int sc, const uint8_t a[16]) {
+__device__ __forceinline__ bool scope_allows_addr(const Bind &B, int sc, const uint8_t a[16]) {
   const uint64_t hi = be64(a), lo = be64(a + 8);
   uint32_t b = B.sc_addr_off[sc], e = B.sc_addr_off[sc + 1];
   while (b < e) {
@@ -193,7 +193,7 @@ __device__ bool scope_allows_addr(const Bind &B, int sc, const uint8_t a[16]) {
   return false;
 }
 // exact-map Allow entries that net.ParseIP refuses (compared byte for byte)
-__device__ bool scope_allows_str(const Bind &B, int sc, uint64_t h, const uint8_t *s, uint32_t n) {
+__device__ __forceinline__ bool scope_allows_str(const Bind &B, int sc, uint64_t h, const uint8_t *s, uint32_t n) {
   uint32_t b = B.sc_str_off[sc], e = B.sc_str_off[sc + 1];
   while (b < e) {
     uint32_t m = (b + e) >> 1;
@@ -204,7 +204,7 @@ __device__ bool scope_allows_str(const Bind &B, int sc, uint64_t h, const uint8_
   return false;
 }
 // StaticDecisionLists.CheckIsAllowed(site, clientIp)
-__device__ bool check_is_allowed(const Bind &B, int32_t host_id, const uint8_t *ip, uint32_t n) {
+__device__ __forceinline__ bool check_is_allowed(const Bind &B, int32_t host_id, const uint8_t *ip, uint32_t n) {
   const int32_t site_sc = host_id >= 0 ? B.host_scope[host_id] : -1;
   uint8_t a[16];
   bool is4;
@@ -380,10 +380,12 @@ constexpr uint32_t kHitSlots = 4;     // verified literal hits kept per line
 constexpr int kScanWaves = 16;        // waves per block (one block per CU)
 constexpr uint32_t kTileLds = kWT + kHalo + 16;
 constexpr uint32_t kWaveJobs = 64;   // DFA jobs staged per wave before one global append
-constexpr uint32_t kWaveLds = kTileLds + kLineCap * (2 + 2);
+constexpr uint32_t kCandList = 128;   // candidate positions verified per round (one per lane)
+constexpr uint32_t kWaveLds = kTileLds + kLineCap * (2 + 2) + kCandList * 4 + kLineCap * 4;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kScanLdsMax = 160 * 1024;  // gfx950 LDS per CU (one scan block per CU)
-constexpr uint32_t kLinesImgMax = 32 * 1024;  // k_lines copies the lookup image to LDS up to this size
+constexpr uint32_t kLinesImgMax = 16 * 1024;  // k_lines copies the lookup image to LDS up to this size
+constexpr uint32_t kSpanBytes = 12 * 1024;    // k_lines: bytes of 64 lines staged per wave
 
 struct ScanArgs {
   const uint8_t *buf;
@@ -452,7 +454,7 @@ __device__ __forceinline__ Tabs make_tabs(const uint8_t *base, const ImgLayout &
 }
 
 // host id from the open-addressing host table
-__device__ int32_t host_lookup_ht(const Bind &B, const Tabs &T, const uint8_t *h, uint32_t n) {
+__device__ __forceinline__ int32_t host_lookup_ht(const Bind &B, const Tabs &T, const uint8_t *h, uint32_t n) {
   if (B.n_hd == 0) return -1;
   const uint64_t hh = hash_bytes(h, n);
   const uint32_t tag = (uint32_t)(hh >> 32) | 1u;
@@ -503,7 +505,7 @@ __device__ __forceinline__ bool has_pos(uint64_t m0, uint64_t m1, uint32_t pos) 
 struct JobSink {
   uint2 *lds;
   uint32_t *cnt;
-  uint2 *jobs;
+  uint32_t *jline, *jkey;  // job = (line, rule | position << 24)
   unsigned long long *count;
   uint64_t cap;
 };
@@ -512,7 +514,7 @@ __device__ __forceinline__ void emit_job(const JobSink &S, uint64_t j, uint32_t 
   const uint32_t c = atomicAdd(S.cnt, 1u);
   if (c < kWaveJobs) { S.lds[c] = v; return; }
   const unsigned long long g = atomicAdd(S.count, 1ull);
-  if (g < S.cap) S.jobs[g] = v;
+  if (g < S.cap) { S.jline[g] = v.x; S.jkey[g] = v.y; }
 }
 
 // One rule whose decision needs its automaton: an anchored prefix may decide
@@ -543,7 +545,7 @@ __device__ __forceinline__ void dfa_rule(const Bind &B, const Tabs &T, uint32_t 
 // of the rules decided here; rules left to k_dfa add theirs atomically.
 // lits: up to 4 literal ids packed 16 bits each.
 template <bool EMIT>
-__device__ void decide_rules(const Bind &B, const Tabs &T, const uint8_t *rest, uint32_t rest_len, int32_t hid,
+__device__ __forceinline__ void decide_rules(const Bind &B, const Tabs &T, const uint8_t *rest, uint32_t rest_len, int32_t hid,
                              uint64_t lits, uint32_t nlit, bool ovf, uint64_t j, const Lines &L, const JobSink &S) {
   const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
   uint32_t s_begin = 0, s_end = 0;
@@ -786,12 +788,48 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
         }
       }
       n_probe += __popcll(hits) + __popc(hh);
-      for (int part = 0; part < 2; ++part) {
-        uint64_t x = part == 0 ? hits : (uint64_t)hh;
-        while (x) {
-          const uint32_t k = (uint32_t)__ffsll((unsigned long long)x) - 1;
-          x &= x - 1;
-          const uint32_t p = part == 0 ? lane * 64u + k : kWT + lane * 8u + k;
+      // ---- candidates, lane-compacted: every lane appends its surviving
+      // positions (with the started-line index they belong to) to a wave list,
+      // then the list is verified one candidate per lane
+      uint32_t *clist = reinterpret_cast<uint32_t *>(le + kLineCap);
+      uint32_t *lcnt = clist + kCandList;
+      for (uint32_t i = lane; i < kLineCap; i += 64) lcnt[i] = 0;
+      uint64_t rem = hits;
+      uint32_t remh = hh;
+      for (;;) {
+        const uint32_t cnt = __popcll(rem) + __popc(remh);
+        uint32_t off = cnt;  // inclusive scan
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t v = __shfl_up(off, o);
+          if (lane >= (uint32_t)o) off += v;
+        }
+        const uint32_t total = __shfl(off, 63);
+        if (total == 0) break;
+        off -= cnt;
+        // append while the list has room (the rest waits for the next round)
+        while ((rem | remh) && off < kCandList) {
+          uint32_t pos;
+          int32_t lk;
+          if (rem) {
+            const uint32_t k = (uint32_t)__ffsll((unsigned long long)rem) - 1;
+            rem &= rem - 1;
+            pos = lane * 64u + k;
+            lk = (int32_t)(pre + (uint32_t)__popcll(nlm & ((1ull << k) - 1ull))) - (int32_t)nh;
+          } else {
+            const uint32_t k = (uint32_t)__ffs(remh) - 1;
+            remh &= remh - 1;
+            pos = kWT + lane * 8u + k;
+            lk = (int32_t)n_st - 1;
+          }
+          clist[off++] = pos | ((uint32_t)(lk + 1) << 16);
+        }
+        wave_sync();
+        const uint32_t nc = total < kCandList ? total : kCandList;
+        for (uint32_t c = lane; c < nc; c += 64) {
+          const uint32_t e = clist[c];
+          const uint32_t p = e & 0xFFFF;
+          const int32_t lk = (int32_t)(e >> 16) - 1;
           const uint32_t g = ld4(T + p);
           if ((g & 0xFF) == '\n') continue;
           uint32_t slot = (uint32_t)mix64(g) & (B.gt2_cap - 1);
@@ -802,39 +840,36 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
             slot = (slot + 1) & (B.gt2_cap - 1);
           }
           if ((ol & 0xFFFF) == 0) continue;
-          // owning line: started-line index lk, or the open line (lk < 0)
-          int32_t lk;
-          uint64_t gline;
-          if (part == 0) {
-            const uint32_t before = pre + (uint32_t)__popcll(nlm & ((1ull << k) - 1ull));
-            gline = tb + before;
-            lk = (int32_t)before - (int32_t)nh;
-          } else {
-            lk = (int32_t)n_st - 1;
-            gline = tb + tot;
-          }
           if (lk < 0 && !open_long) continue;  // the previous tile covered it
+          const uint64_t gline = tb + nh + (uint64_t)(int64_t)lk;
           if (gline >= A.n_lines) continue;
-          // lines whose bytes are all in this window are verified here
+          // lines whose bytes are all in this window are verified here and
+          // counted in LDS (no other tile sees them)
           const bool in_window = lk >= 0 && lk < (int32_t)kLineCap && !(lk == (int32_t)n_st - 1 && last_long);
           for (uint32_t ei = 0; ei < (ol & 0xFFFF); ++ei) {
             const uint32_t en = ge[(ol >> 16) + ei];
             const uint32_t lit = en >> 8, goff = en & 0xFF;
             const int64_t q0 = (int64_t)(ts0 + p) - (int64_t)goff;
             if (q0 < 0) continue;
-            uint32_t flag = 0;
             if (in_window) {
               const int32_t s0 = (int32_t)p - (int32_t)goff;
               if (s0 < (int32_t)ls[lk] || (uint32_t)s0 + lit_len_of(TB, lit) > le[lk]) continue;
               if (!literal_at(TB, lit, T + s0)) continue;
-              flag = kCandVerified;
+              const uint32_t cc = atomicAdd(&lcnt[lk], 1u);
+              if (cc < (uint32_t)kCandSlots) L.cand[gline * kCandSlots + cc] = ((uint64_t)q0 << 24) | kCandVerified | lit;
+            } else {
+              const uint32_t cc = atomicAdd(&L.cand_cnt[gline], 1u);
+              if (cc < (uint32_t)kCandSlots) L.cand[gline * kCandSlots + cc] = ((uint64_t)q0 << 24) | lit;
             }
-            const uint32_t c = atomicAdd(&L.cand_cnt[gline], 1u);
-            if (c < (uint32_t)kCandSlots) L.cand[gline * kCandSlots + c] = ((uint64_t)q0 << 24) | flag | lit;
             ++n_hit;
           }
         }
+        wave_sync();
       }
+      // hit counts of the lines decided in this window
+      const uint32_t n_win = min(n_st, kLineCap) - ((last_long && n_st <= kLineCap) ? 1u : 0u);
+      for (uint32_t i = lane; i < n_win; i += 64)
+        if (tb + nh + i < A.n_lines) L.cand_cnt[tb + nh + i] = lcnt[i];
       wave_sync();
     }
   }
@@ -857,18 +892,26 @@ __device__ __forceinline__ uint32_t find_spaces(const uint8_t *p, uint32_t n, ui
   uint32_t ns = 0;
   for (uint32_t c = 0; c * 16 < n + skip && ns < 4; ++c) {
     const uint4 v = base[c];
+    // 16-bit mask of the spaces of this chunk inside [p, p + n)
+    uint32_t m16 = 0;
     const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint32_t x = wv[k] ^ 0x20202020u;
-      uint32_t m = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
-      while (m && ns < 4) {
-        const int32_t pos = (int32_t)(c * 16 + 4 * k + (((uint32_t)__ffs(m) - 1) >> 3)) - (int32_t)skip;
-        m &= m - 1;
-        if (pos < 0 || pos >= (int32_t)n) continue;
-        if (ns == 0) sp0 = (uint32_t)pos; else if (ns == 1) sp1 = (uint32_t)pos; else if (ns == 2) sp2 = (uint32_t)pos; else sp3 = (uint32_t)pos;
-        ++ns;
-      }
+      const uint32_t hb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+      m16 |= (((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u)) << (4 * k);
+    }
+    const int32_t lo = (int32_t)skip - (int32_t)(c * 16), hi = lo + (int32_t)n;  // valid chunk bytes [lo, hi)
+    if (lo > 0) m16 &= ~((1u << lo) - 1u);
+    if (hi < 16) m16 &= hi > 0 ? (1u << hi) - 1u : 0u;
+    while (m16 && ns < 4) {  // selects, not an indexed store: no scratch
+      const uint32_t pos = c * 16 + (uint32_t)__ffs(m16) - 1 - skip;
+      m16 &= m16 - 1;
+      sp0 = ns == 0 ? pos : sp0;
+      sp1 = ns == 1 ? pos : sp1;
+      sp2 = ns == 2 ? pos : sp2;
+      sp3 = ns == 3 ? pos : sp3;
+      ++ns;
     }
   }
   return ns;
@@ -876,16 +919,75 @@ __device__ __forceinline__ uint32_t find_spaces(const uint8_t *p, uint32_t n, ui
 
 struct LinesArgs {
   const uint8_t *buf;
+  uint64_t n;  // batch bytes
   const uint64_t *nl;
   uint64_t n_lines;
   Lines L;
   int64_t now_ns;
   uint32_t *slow_list;
   unsigned long long *slow_count;
-  uint2 *jobs;
+  uint32_t *jline, *jkey;
   unsigned long long *job_count;
   uint64_t job_cap;
 };
+
+// consumeLine up to the rule loop for line j (bytes at base + (s - origin)):
+// SplitN header, parseTimestamp fast path, host lookup, CheckIsAllowed,
+// OldLine, then the rule decisions from the scan pass's literal hits.
+__device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const LinesArgs &A, const uint8_t *base,
+                                          uint64_t origin, uint64_t s, uint32_t n, uint64_t j, const JobSink &S) {
+  const Lines &L = A.L;
+  const uint8_t *p = base + (s - origin);
+  uint32_t sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
+  const uint32_t ns = find_spaces(p, n, sp0, sp1, sp2, sp3);
+  double f;
+  int32_t hid = -1;
+  if (ns < 4) {
+    L.flags[j] = kLineError;
+    L.counts[j] = 0;
+  } else if (parse_float_fast(p, sp0, &f) != 0 ||
+             (hid = host_lookup_ht(B, TB, p + sp2 + 1, sp3 - sp2 - 1),
+              (hid >= 0 ? B.site_off[hid + 1] - B.site_off[hid] : 0u) + B.n_global > 128)) {
+    // exotic timestamp token or > 128 applicable rules: the per-line fallback
+    L.flags[j] = kLineSlowTs;
+    L.counts[j] = 0;
+    push_list(A.slow_list, A.slow_count, j);
+  } else {
+    const uint32_t ip_off = sp0 + 1, ip_len = sp1 - sp0 - 1;
+    const uint32_t rest_off = sp1 + 1, host_off = sp2 + 1, host_len = sp3 - sp2 - 1;
+    const bool exempt = B.any_allow && check_is_allowed(B, hid, p + ip_off, ip_len);
+    L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
+    L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
+    L.host_id[j] = hid;
+    L.ip_hash[j] = hash_bytes(p + ip_off, ip_len);
+    const int64_t tsn = ns_from_seconds(f);
+    L.ts[j] = tsn;
+    uint8_t fl = 0;
+    if (go_sub(A.now_ns, tsn) > 10000000000LL) fl = kLineOld;
+    else if (exempt) fl = kLineExempt;
+    L.flags[j] = fl;
+    if (fl) {
+      L.counts[j] = 0;
+    } else {
+      // literal hits of the scan pass inside rest (unverified ones checked here)
+      const uint32_t cc = B.any_prefilter ? L.cand_cnt[j] : 0u;
+      uint64_t lits = 0;
+      uint32_t nlit = 0;
+      const uint64_t rs = s + rest_off;
+      for (uint32_t c = 0; c < cc && c < (uint32_t)kCandSlots; ++c) {
+        const uint64_t v = L.cand[j * kCandSlots + c];
+        const uint32_t lit = (uint32_t)(v & 0x7FFFFF);
+        const uint64_t q = v >> 24;
+        if (q < rs) continue;
+        if (!(v & kCandVerified) &&
+            (q + lit_len_of(TB, lit) > s + n || !literal_at(TB, lit, base + (q - origin))))
+          continue;
+        lits |= (uint64_t)lit << (16 * nlit++);
+      }
+      decide_rules<true>(B, TB, p + rest_off, n - rest_off, hid, lits, nlit, cc > (uint32_t)kCandSlots, j, L, S);
+    }
+  }
+}
 
 // consumeLine up to the rule loop, one lane per line (regex_rate_limiter.go:113-214):
 // SplitN header, parseTimestamp fast path, host lookup, CheckIsAllowed, OldLine,
@@ -901,68 +1003,57 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
   const Tabs TB = make_tabs(IMG_LDS ? s_img : B.img, B.il);
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   JobSink S;
-  S.lds = reinterpret_cast<uint2 *>(s_dyn + (IMG_LDS ? B.img_bytes : 0) + wave * (kWaveJobs * 8 + 16));
+  S.lds = reinterpret_cast<uint2 *>(s_dyn + ((IMG_LDS ? B.img_bytes : 0) + 15u & ~15u) + wave * (kWaveJobs * 8 + 16));
   S.cnt = reinterpret_cast<uint32_t *>(S.lds + kWaveJobs);
-  S.jobs = A.jobs;
+  S.jline = A.jline;
+  S.jkey = A.jkey;
   S.count = A.job_count;
   S.cap = A.job_cap;
   if (lane == 0) *S.cnt = 0;
   wave_sync();
   const Lines &L = A.L;
+  // this wave's 64 lines, staged whole in LDS with coalesced 16 B loads when
+  // they span at most kSpanBytes (otherwise read from HBM per lane)
+  uint8_t *span = s_dyn + ((IMG_LDS ? B.img_bytes : 0) + 15u & ~15u) + (kBlock / 64) * (kWaveJobs * 8 + 16) +
+                  wave * (kSpanBytes + 32);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + wave * 64u; base < A.n_lines; base += stride) {
     const uint64_t j = base + lane;
+    const uint64_t jl = min(base + 63, A.n_lines - 1);
+    const uint64_t s0 = base ? A.nl[base - 1] + 1 : 0;
+    const uint64_t s1 = A.nl[jl];
+    const uint64_t b16 = s0 & ~15ull;
+    const bool staged = s1 + 16 - b16 <= kSpanBytes;  // 16 B of slack for word-wise over-reads
+    if (staged) {
+      const uint32_t n16 = (uint32_t)((s1 + 16 - b16 + 15) >> 4);
+      for (uint32_t i = lane; i < n16; i += 64) {
+        const uint64_t a = b16 + 16ull * i;
+        uint4 v;
+        if (a + 16 <= A.n) {
+          v = *reinterpret_cast<const uint4 *>(A.buf + a);
+        } else {
+          uint32_t w[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            uint32_t x = 0;
+            for (int b = 0; b < 4; ++b) {
+              const uint64_t q = a + 4 * k + b;
+              if (q < A.n) x |= (uint32_t)A.buf[q] << (8 * b);
+            }
+            w[k] = x;
+          }
+          v = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        reinterpret_cast<uint4 *>(span)[i] = v;
+      }
+      wave_sync();
+    }
     if (j < A.n_lines) {
       const uint64_t s = j ? A.nl[j - 1] + 1 : 0;
       const uint32_t n = (uint32_t)(A.nl[j] - s);
-      const uint8_t *p = A.buf + s;
-      uint32_t sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
-      const uint32_t ns = find_spaces(p, n, sp0, sp1, sp2, sp3);
-      double f;
-      int32_t hid = -1;
-      if (ns < 4) {
-        L.flags[j] = kLineError;
-        L.counts[j] = 0;
-      } else if (parse_float_fast(p, sp0, &f) != 0 ||
-                 (hid = host_lookup_ht(B, TB, p + sp2 + 1, sp3 - sp2 - 1),
-                  (hid >= 0 ? B.site_off[hid + 1] - B.site_off[hid] : 0u) + B.n_global > 128)) {
-        // exotic timestamp token or > 128 applicable rules: the per-line fallback
-        L.flags[j] = kLineSlowTs;
-        L.counts[j] = 0;
-        push_list(A.slow_list, A.slow_count, j);
-      } else {
-        const uint32_t ip_off = sp0 + 1, ip_len = sp1 - sp0 - 1;
-        const uint32_t rest_off = sp1 + 1, host_off = sp2 + 1, host_len = sp3 - sp2 - 1;
-        const bool exempt = B.any_allow && check_is_allowed(B, hid, p + ip_off, ip_len);
-        L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
-        L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
-        L.host_id[j] = hid;
-        L.ip_hash[j] = hash_bytes(p + ip_off, ip_len);
-        const int64_t tsn = ns_from_seconds(f);
-        L.ts[j] = tsn;
-        uint8_t fl = 0;
-        if (go_sub(A.now_ns, tsn) > 10000000000LL) fl = kLineOld;
-        else if (exempt) fl = kLineExempt;
-        L.flags[j] = fl;
-        if (fl) {
-          L.counts[j] = 0;
-        } else {
-          // literal hits of the scan pass inside rest (unverified ones checked here)
-          const uint32_t cc = B.any_prefilter ? L.cand_cnt[j] : 0u;
-          uint64_t lits = 0;
-          uint32_t nlit = 0;
-          const uint64_t rs = s + rest_off;
-          for (uint32_t c = 0; c < cc && c < (uint32_t)kCandSlots; ++c) {
-            const uint64_t v = L.cand[j * kCandSlots + c];
-            const uint32_t lit = (uint32_t)(v & 0x7FFFFF);
-            const uint64_t q = v >> 24;
-            if (q < rs) continue;
-            if (!(v & kCandVerified) && (q + lit_len_of(TB, lit) > s + n || !literal_at(TB, lit, A.buf + q))) continue;
-            lits |= (uint64_t)lit << (16 * nlit++);
-          }
-          decide_rules<true>(B, TB, p + rest_off, n - rest_off, hid, lits, nlit, cc > (uint32_t)kCandSlots, j, L, S);
-        }
-      }
+      // two inlined copies: LDS addressing for staged waves, global otherwise
+      if (staged) line_body(B, TB, A, span, b16, s, n, j, S);
+      else line_body(B, TB, A, A.buf, 0, s, n, j, S);
     }
     // ---- append this wave's DFA jobs (one global atomic per 64 lines)
     wave_sync();
@@ -972,7 +1063,7 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
       if (lane == 0) jb = atomicAdd(A.job_count, (unsigned long long)nj);
       jb = __shfl(jb, 0);
       for (uint32_t i = lane; i < nj; i += 64)
-        if (jb + i < A.job_cap) A.jobs[jb + i] = S.lds[i];
+        if (jb + i < A.job_cap) { A.jline[jb + i] = S.lds[i].x; A.jkey[jb + i] = S.lds[i].y; }
     }
     wave_sync();
     if (lane == 0) *S.cnt = 0;
@@ -980,18 +1071,100 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
   }
 }
 
-// DFA jobs from the scan pass: one (line, rule) per lane; a match sets the
-// rule's bit and adds to the line's result / event counts.
-__global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restrict__ buf, const uint64_t *__restrict__ nl,
-                                                const uint2 *__restrict__ jobs, uint64_t n, Lines L) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// DFA jobs of the line pass, sorted by rule: one (line, rule) per lane.  A
+// block whose jobs share one rule (the common case) stages that rule's
+// transition rows and ASCII class map in LDS; every lane reads its text 16 B
+// at a time and steps the DFA over the ASCII bytes from registers (a non-ASCII
+// byte hands the rest of the text to the rune-decoding loop).  A match sets
+// the rule's bit and adds to the line's result / event counts.
+constexpr uint32_t kDfaLdsEntries = 8192;  // u16 transitions staged per block (16 KB)
+
+__device__ __forceinline__ bool dfa_text(const Bind &B, const DevRule &R, const uint16_t *tr, const uint8_t *ac,
+                                         const uint8_t *__restrict__ buf, uint64_t n_buf, uint64_t t0, uint32_t len) {
+  const uint32_t ncls = R.ncls;
+  uint32_t st = R.start;
+  uint64_t a = t0 & ~15ull;
+  const uint64_t end = t0 + len;
+  uint32_t skip = (uint32_t)(t0 - a);
+  while (a < end) {
+    uint4 v;
+    if (a + 16 <= n_buf) {
+      v = *reinterpret_cast<const uint4 *>(buf + a);
+    } else {
+      uint32_t w[4];
+      for (int k = 0; k < 4; ++k) {
+        uint32_t x = 0;
+        for (int b = 0; b < 4; ++b) x |= (a + 4 * k + b < n_buf ? (uint32_t)buf[a + 4 * k + b] : 0u) << (8 * b);
+        w[k] = x;
+      }
+      v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t lim = end - a < 16 ? (uint32_t)(end - a) : 16u;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) {
+      if (k < skip || k >= lim) continue;
+      const uint32_t b = (wv[k >> 2] >> (8 * (k & 3))) & 0xFF;
+      if (b >= 0x80) {
+        // non-ASCII: decode runes from here on (Go's regexp steps by rune)
+        const DevRule *Rp = &R;
+        uint64_t i = a + k;
+        while (i < end) {
+          int w;
+          const int32_t rune = decode_rune_hd(buf + i, (uint32_t)(end - i), &w);
+          uint32_t c;
+          if (rune < 0x80) c = ac[rune];
+          else {
+            const uint32_t *na = B.nonascii + 2 * Rp->na_off;
+            uint32_t lo = 0, hi = Rp->n_na;
+            while (hi - lo > 1) {
+              const uint32_t m = (lo + hi) >> 1;
+              if (na[2 * m] <= (uint32_t)rune) lo = m; else hi = m;
+            }
+            c = na[2 * lo + 1];
+          }
+          i += (uint32_t)w;
+          st = tr[st * ncls + c];
+          if (st <= 1) break;
+        }
+        return B.accept_end[R.ae_off + st] != 0;
+      }
+      st = tr[st * ncls + ac[b]];
+      if (st <= 1) return st == kAccept;
+    }
+    skip = 0;
+    a += 16;
+  }
+  return B.accept_end[R.ae_off + st] != 0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restrict__ buf, uint64_t n_buf,
+                                                const uint64_t *__restrict__ nl, const uint32_t *__restrict__ jkey,
+                                                const uint32_t *__restrict__ jline, uint64_t n, Lines L) {
+  __shared__ uint16_t s_tr[kDfaLdsEntries];
+  __shared__ uint8_t s_ac[128];
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x;
+  const uint64_t t = t0 + threadIdx.x;
+  const uint64_t tl = t0 + blockDim.x - 1 < n ? t0 + blockDim.x - 1 : n - 1;
+  const uint32_t r0 = jkey[t0] & 0xFFFFFF;
+  const DevRule R0 = B.rules[r0];
+  const bool staged = (jkey[tl] & 0xFFFFFF) == r0 && (uint32_t)R0.ncls * R0.n_states <= kDfaLdsEntries;
+  if (staged) {
+    const uint16_t *g = B.trans + R0.trans_off;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)R0.ncls * R0.n_states; i += blockDim.x) s_tr[i] = g[i];
+    if (threadIdx.x < 128) s_ac[threadIdx.x] = B.ascii_cls[(size_t)r0 * 128 + threadIdx.x];
+  }
+  __syncthreads();
   if (t >= n) return;
-  const uint2 v = jobs[t];
-  const uint64_t j = v.x;
-  const uint32_t r = v.y & 0xFFFFFF, pos = v.y >> 24;
+  const uint32_t key = jkey[t];
+  const uint32_t r = key & 0xFFFFFF, pos = key >> 24;
+  const uint64_t j = jline[t];
+  const DevRule R = staged ? R0 : B.rules[r];
+  const uint16_t *tr = staged ? s_tr : B.trans + R.trans_off;
+  const uint8_t *ac = staged ? s_ac : B.ascii_cls + (size_t)r * 128;
   const uint64_t s = j ? nl[j - 1] + 1 : 0;
   const uint64_t rs = s + L.rest_off[j];
-  if (!rule_match(B, r, buf + rs, (uint32_t)(nl[j] - rs))) return;
+  if (!dfa_text(B, R, tr, ac, buf, n_buf, rs, (uint32_t)(nl[j] - rs))) return;
   const int32_t hid = L.host_id[j];
   const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
   const bool skip = (B.sc_skip[2 * sc + (pos >> 6)] >> (pos & 63)) & 1;
@@ -1678,9 +1851,10 @@ struct bjx_engine {
   DevBuf<int32_t> l_hid;
   DevBuf<uint64_t> l_cand;
   DevBuf<uint32_t> long_list;
-  DevBuf<uint2> jobs;
+  DevBuf<uint32_t> jline, jkey, jline2, jkey2;
   uint64_t last_jobs = 0;
   uint32_t scan_lds[2] = {0, 0};
+  bool lines_attr = false;
   DevBuf<uint32_t> l_ccnt;
   unsigned long long scan_stats[5] = {0, 0, 0, 0, 0};
   uint64_t last_slow = 0;
@@ -1921,6 +2095,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     for (auto &p : r.rx.nonascii) { nonascii.push_back(p.first); nonascii.push_back(p.second); }
     d.n_na = (uint16_t)r.rx.nonascii.size();
     d.ncls = (uint16_t)r.rx.ncls;
+    d.n_states = r.rx.nstates;
     d.start = r.rx.start;
     d.flags = (uint16_t)r.rx.flags;
     memcpy(&ascii[i * 128], r.rx.ascii_cls, 128);
@@ -2415,7 +2590,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
     b->release();
   e->rx_ts.release(); e->trip_idx.release(); e->d_trips.release();
   e->d_results.release(); e->q_out.release();
-  e->long_list.release(); e->jobs.release(); e->l_cand.release(); e->l_ccnt.release();
+  e->long_list.release(); e->jline.release(); e->jkey.release(); e->jline2.release(); e->jkey2.release(); e->l_cand.release(); e->l_ccnt.release();
   (void)hipEventDestroy(e->ev0); (void)hipEventDestroy(e->ev1); (void)hipEventDestroy(e->evm0); (void)hipEventDestroy(e->evm1);
   for (auto &x : e->ph) (void)hipEventDestroy(x);
   (void)hipStreamDestroy(e->stream);
@@ -2595,7 +2770,8 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   L.host_len = e->l_hlen.p; L.rest_off = e->l_roff.p; L.host_id = e->l_hid.p; L.flags = e->l_flags.p;
   L.counts = e->l_counts.p; L.masks = e->l_masks.p;
   L.cand_cnt = e->l_ccnt.p; L.cand = e->l_cand.p;
-  e->jobs.ensure(std::max<uint64_t>(e->jobs.n, n_lines + (1u << 20)));
+  e->jline.ensure(std::max<uint64_t>(e->jline.n, n_lines + (1u << 20)));
+  e->jkey.ensure(e->jline.n);
   HIP_OK(hipMemsetAsync(e->scalars.p, 0, 16 * sizeof(unsigned long long), st));
   if (B.any_prefilter) HIP_OK(hipMemsetAsync(e->l_ccnt.p, 0, n_lines * 4, st));
   mark(e, 1);
@@ -2630,11 +2806,18 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   unsigned long long sc4[5] = {0, 0, 0, 0, 0};
   for (int attempt = 0;; ++attempt) {
     LinesArgs A;
-    A.buf = buf; A.nl = e->nl.p; A.n_lines = n_lines; A.L = L; A.now_ns = now_ns;
+    A.buf = buf; A.n = n; A.nl = e->nl.p; A.n_lines = n_lines; A.L = L; A.now_ns = now_ns;
     A.slow_list = e->slow_list.p; A.slow_count = e->scalars.p;
-    A.jobs = e->jobs.p; A.job_count = e->scalars.p + 11; A.job_cap = e->jobs.n;
+    A.jline = e->jline.p; A.jkey = e->jkey.p; A.job_count = e->scalars.p + 11; A.job_cap = std::min(e->jline.n, e->jkey.n);
     const bool img_lds = B.img_bytes <= kLinesImgMax;
-    const uint32_t lds = (img_lds ? B.img_bytes : 0) + (kBlock / 64) * (kWaveJobs * 8 + 16);
+    const uint32_t lds = ((img_lds ? B.img_bytes : 0) + 15u & ~15u) + (kBlock / 64) * (kWaveJobs * 8 + 16 + kSpanBytes + 32);
+    if (!e->lines_attr) {
+      HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_lines<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)kScanLdsMax));
+      HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_lines<false>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)kScanLdsMax));
+      e->lines_attr = true;
+    }
     const unsigned grid = (unsigned)std::min<uint64_t>((n_lines + kBlock - 1) / kBlock, 256 * 8);
     if (img_lds) hipLaunchKernelGGL(k_lines<true>, dim3(grid), dim3(kBlock), lds, st, B, A);
     else hipLaunchKernelGGL(k_lines<false>, dim3(grid), dim3(kBlock), lds, st, B, A);
@@ -2643,20 +2826,31 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     HIP_OK(hipMemcpyAsync(sc4, e->scalars.p + 8, 32, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(sc4 + 4, e->scalars.p, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    if (sc4[3] <= e->jobs.n) break;
+    if (sc4[3] <= std::min(e->jline.n, e->jkey.n)) break;
     // more DFA jobs than the buffer holds: grow it and redo the (idempotent) line pass
     if (attempt > 0) throw BjxError(BJX_ERR_DEVICE, "internal: DFA job buffer overflow");
-    e->jobs.ensure(sc4[3] + (1u << 20));
+    e->jline.ensure(sc4[3] + (1u << 20));
+    e->jkey.ensure(sc4[3] + (1u << 20));
     HIP_OK(hipMemsetAsync(e->scalars.p, 0, 8, st));
     HIP_OK(hipMemsetAsync(e->scalars.p + 11, 0, 8, st));
   }
   out->consumed_bytes = last_nl + 1;
   const unsigned long long n_slow = sc4[4], n_jobs = sc4[3];
   e->last_jobs = n_jobs;
-  e->scan_stats[0] = sc4[0]; e->scan_stats[1] = sc4[1]; e->scan_stats[2] = n_slow; e->scan_stats[3] = 0;
+  e->scan_stats[0] = sc4[0]; e->scan_stats[1] = sc4[1]; e->scan_stats[2] = n_slow; e->scan_stats[3] = B.img_bytes;
   e->scan_stats[4] = n_jobs;
   if (n_jobs) {
-    hipLaunchKernelGGL(k_dfa, dim3(grid_for(n_jobs)), dim3(kBlock), 0, st, B, buf, e->nl.p, e->jobs.p, (uint64_t)n_jobs, L);
+    // group the jobs by rule (stable: line order inside a rule), then one lane per job
+    e->jline2.ensure(n_jobs); e->jkey2.ensure(n_jobs);
+    {
+      uint32_t *ki = e->jkey.p, *ko = e->jkey2.p, *vi = e->jline.p, *vo = e->jline2.p;
+      const int bits = std::max(1, bit_width(B.n_rules ? B.n_rules - 1 : 0));
+      cub_call(e, [&](void *tmp, size_t &bytes) {
+        return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)n_jobs, 0, bits, st);
+      });
+    }
+    hipLaunchKernelGGL(k_dfa, dim3(grid_for(n_jobs)), dim3(kBlock), 0, st, B, buf, (uint64_t)n, e->nl.p, e->jkey2.p,
+                       e->jline2.p, (uint64_t)n_jobs, L);
     HIP_OK(hipGetLastError());
   }
   if (n_slow) {

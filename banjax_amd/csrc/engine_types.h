@@ -23,6 +23,7 @@ struct DevRule {
   uint16_t anc_len;
   uint8_t anc_equiv;     // match <=> rest starts with one of them
   uint8_t _pad;
+  uint32_t n_states;     // DFA states (rows of trans)
   int64_t interval_ns;
   int64_t hits;
 };

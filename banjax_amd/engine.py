@@ -138,7 +138,7 @@ class Engine:
     def scan_stats(self):
         out = (C.c_uint64 * 5)()
         _lib.lib().bjx_debug_scan_stats(self._h, out, 5)
-        return {"gram_bitset_hits": out[0], "literal_hits": out[1], "fallback_lines": out[2], "long_lines": out[3],
+        return {"gram_bitset_hits": out[0], "literal_hits": out[1], "fallback_lines": out[2], "lookup_image_bytes": out[3],
                 "dfa_jobs": out[4]}
 
     def phase_ms(self):

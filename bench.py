@@ -58,7 +58,7 @@ def pmc_traffic(nbytes):
 
     def mean(path, counter):
         v = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-             if "k_scan" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+             if "::k_scan<" in r["Kernel_Name"] and r["Counter_Name"] == counter]
         return sum(v) / len(v) if v else None
     fe, wb = mean(best[1], "FETCH_SIZE"), mean(best[2], "WRITE_SIZE")
     if fe is None or wb is None:
