@@ -546,19 +546,20 @@ __device__ __forceinline__ void dfa_rule(const Bind &B, const Tabs &T, uint32_t 
 // lits: up to 4 literal ids packed 16 bits each.
 template <bool EMIT>
 __device__ __forceinline__ void decide_rules(const Bind &B, const Tabs &T, const uint8_t *rest, uint32_t rest_len, int32_t hid,
-                             uint64_t lits, uint32_t nlit, bool ovf, uint64_t j, const Lines &L, const JobSink &S) {
+                             uint64_t lits, uint32_t nlit, bool ovf, uint64_t j, const Lines &L, const JobSink &S,
+                             uint32_t dbg = 0) {
   const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
   uint32_t s_begin = 0, s_end = 0;
   if (hid >= 0) { s_begin = B.site_off[hid]; s_end = B.site_off[hid + 1]; }
   const uint32_t nsite = s_end - s_begin;
   uint64_t m0 = B.sc_always[2 * sc], m1 = B.sc_always[2 * sc + 1];
   // anchored / no-literal rules: every line
-  if (hid >= 0)
+  if (hid >= 0 && !(dbg & 1))
     for (uint32_t i = B.dfa_site_off[hid]; i < B.dfa_site_off[hid + 1]; ++i) {
       const uint2 e = B.dfa_site[i];
       dfa_rule<EMIT>(B, T, e.x, e.y, true, rest, rest_len, m0, m1, j, S);
     }
-  for (uint32_t i = 0; i < B.n_dfa_glob; ++i) {
+  for (uint32_t i = 0; i < (dbg & 1 ? 0u : B.n_dfa_glob); ++i) {
     const uint2 e = B.dfa_glob[i];
     dfa_rule<EMIT>(B, T, e.x, nsite + e.y, true, rest, rest_len, m0, m1, j, S);
   }
@@ -918,6 +919,7 @@ __device__ __forceinline__ uint32_t find_spaces(const uint8_t *p, uint32_t n, ui
 }
 
 struct LinesArgs {
+  uint32_t dbg;  // timing experiments only (BJX_DEBUG_LINES): 1 no anchored checks, 2 no literal hits, 4 unstaged, 8 no host lookup
   const uint8_t *buf;
   uint64_t n;  // batch bytes
   const uint64_t *nl;
@@ -946,7 +948,7 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
     L.flags[j] = kLineError;
     L.counts[j] = 0;
   } else if (parse_float_fast(p, sp0, &f) != 0 ||
-             (hid = host_lookup_ht(B, TB, p + sp2 + 1, sp3 - sp2 - 1),
+             (hid = (A.dbg & 8) ? -1 : host_lookup_ht(B, TB, p + sp2 + 1, sp3 - sp2 - 1),
               (hid >= 0 ? B.site_off[hid + 1] - B.site_off[hid] : 0u) + B.n_global > 128)) {
     // exotic timestamp token or > 128 applicable rules: the per-line fallback
     L.flags[j] = kLineSlowTs;
@@ -984,7 +986,8 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
           continue;
         lits |= (uint64_t)lit << (16 * nlit++);
       }
-      decide_rules<true>(B, TB, p + rest_off, n - rest_off, hid, lits, nlit, cc > (uint32_t)kCandSlots, j, L, S);
+      decide_rules<true>(B, TB, p + rest_off, n - rest_off, hid, lits, (A.dbg & 2) ? 0u : nlit, cc > (uint32_t)kCandSlots, j, L, S,
+                         A.dbg);
     }
   }
 }
@@ -1023,7 +1026,7 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
     const uint64_t s0 = base ? A.nl[base - 1] + 1 : 0;
     const uint64_t s1 = A.nl[jl];
     const uint64_t b16 = s0 & ~15ull;
-    const bool staged = s1 + 16 - b16 <= kSpanBytes;  // 16 B of slack for word-wise over-reads
+    const bool staged = s1 + 16 - b16 <= kSpanBytes && !(A.dbg & 4);  // 16 B of slack for word-wise over-reads
     if (staged) {
       const uint32_t n16 = (uint32_t)((s1 + 16 - b16 + 15) >> 4);
       for (uint32_t i = lane; i < n16; i += 64) {
@@ -1283,9 +1286,8 @@ __global__ __launch_bounds__(kBlock) void k_ip_claim(EvSrc E, State S, uint32_t 
 __global__ __launch_bounds__(kBlock) void k_ip_commit(EvSrc E, State S, uint32_t epoch, const uint32_t *__restrict__ el_slot,
                                                       uint32_t *__restrict__ el_id, uint32_t *__restrict__ coll) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= E.n || !ev_has(E, i)) return;
+  if (i >= E.n || !ev_has(E, i) || el_id[i] != kNewIp) return;  // IPs of earlier batches: settled by k_ip_claim
   const uint32_t s = el_slot[i];
-  if (S.ip[s].born != epoch) return;
   const uint32_t f = S.ip_first[s];
   const uint32_t len = E.ip_len[i];
   const uint8_t *ip = ev_ip(E, i);
@@ -1390,12 +1392,13 @@ __global__ __launch_bounds__(kBlock) void k_run_heads(uint64_t n_ev, const uint3
 
 // The fixed-window automaton of one (ip, rule name) state over its events in
 // reference order (records sorted by slot, stable).  One lane per run,
-// grid-stride over the run heads.  ev_out[k]: bit0 seenIp, bits1-2
-// MatchType, bit3 Exceeded, bit7 valid.
+// grid-stride over the run heads.  out_sorted[u] = outcome of record u in
+// sorted order (sequential stores): bit0 seenIp, bits1-2 MatchType, bit3
+// Exceeded, bit7 valid.
 __global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const unsigned long long *__restrict__ n_runs_p,
                                                   const uint32_t *__restrict__ heads, const uint32_t *__restrict__ key,
                                                   const EvRec *__restrict__ rec, const DevRule *__restrict__ rules,
-                                                  StSlot *__restrict__ st, uint8_t *__restrict__ ev_out) {
+                                                  StSlot *__restrict__ st, uint8_t *__restrict__ out_sorted) {
   const uint64_t n_runs = *n_runs_p;
   for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n_runs; h += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t b = heads[h], e = h + 1 < n_runs ? heads[h + 1] : n_ev;
@@ -1414,7 +1417,7 @@ __global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const unsigned 
       else { mt = BJX_INSIDE_INTERVAL; ++hits; }
       const bool ex = hits > limit;
       if (ex) hits = 0;
-      ev_out[v.ev] = (uint8_t)(0x80 | (seen ? 1 : 0) | (mt << 1) | (ex ? 8 : 0));
+      out_sorted[u] = (uint8_t)(0x80 | (seen ? 1 : 0) | (mt << 1) | (ex ? 8 : 0));
     }
     st[q].hits = hits;
     st[q].start = start;
@@ -1426,6 +1429,23 @@ __global__ void k_dbg_mask_hash(uint64_t n, uint64_t *__restrict__ h, uint64_t m
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) h[i] = (h[i] & mask) | 1;
 }
+
+// sorted outcomes -> event order
+__global__ void k_unsort(uint64_t n, const EvRec *__restrict__ rec, const uint8_t *__restrict__ in, uint8_t *__restrict__ out) {
+  const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u < n) out[rec[u].ev] = in[u];
+}
+
+// event index of each trip found in sorted order
+__global__ void k_trip_events(uint64_t n, const uint32_t *__restrict__ pos, const EvRec *__restrict__ rec,
+                              uint32_t *__restrict__ ev) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) ev[t] = rec[pos[t]].ev;
+}
+
+struct TripBit {
+  __host__ __device__ __forceinline__ bool operator()(uint8_t v) const { return (v & 8) != 0; }
+};
 
 __global__ void k_flag_trips(uint64_t n, const uint8_t *__restrict__ ev_out, uint8_t *__restrict__ f) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1865,7 +1885,8 @@ struct bjx_engine {
   DevBuf<EvRec> ev_rec, ev_rec2;
   DevBuf<uint32_t> el_id, run_heads;
   DevBuf<uint8_t> run_flag;
-  DevBuf<uint8_t> rl_out, ev_out, trip_flag;
+  DevBuf<uint8_t> rl_out, ev_out, ev_out_s, trip_flag;
+  DevBuf<uint32_t> trip_ev, trip_ev2;
   DevBuf<bjx_trip> d_trips;
   DevBuf<bjx_rule_result> d_results;
   DevBuf<uint8_t> cub_tmp;
@@ -2574,6 +2595,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   (void)hipStreamSynchronize(e->stream);
   free_state(e);
   e->trips.release(); e->results.release(); e->line_flags.release();
+  e->ev_out_s.release(); e->trip_ev.release(); e->trip_ev2.release();
   for (auto *b : {&e->staging, &e->l_flags, &e->ev_out, &e->rl_out, &e->trip_flag, &e->bind_blob,
                   &e->cub_tmp, &e->q_ip})
     b->release();
@@ -2646,7 +2668,7 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
   const uint32_t epoch = e->epoch;
   e->el_slot.ensure(E.n); e->el_id.ensure(E.n); e->coll.ensure(E.n);
   e->ev_st.ensure(n_ev); e->ev_st2.ensure(n_ev); e->ev_rec.ensure(n_ev); e->ev_rec2.ensure(n_ev);
-  e->ev_out.ensure(n_ev); e->run_flag.ensure(n_ev); e->run_heads.ensure(n_ev);
+  e->ev_out.ensure(n_ev); e->ev_out_s.ensure(n_ev); e->run_flag.ensure(n_ev); e->run_heads.ensure(n_ev);
   HIP_OK(hipMemsetAsync(e->S.counters + 3, 0, 8, st));
   mark(e, 5);
   hipLaunchKernelGGL(k_ip_claim, dim3(grid_for(E.n)), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p);
@@ -2692,7 +2714,7 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
     });
   }
   hipLaunchKernelGGL(k_apply, dim3(2048), dim3(kBlock), 0, st, n_ev, e->scalars.p + 5, e->run_heads.p, e->ev_st2.p,
-                     e->ev_rec2.p, B.rules, e->S.st, e->ev_out.p);
+                     e->ev_rec2.p, B.rules, e->S.st, e->ev_out_s.p);
   HIP_OK(hipGetLastError());
 }
 
@@ -2807,6 +2829,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   for (int attempt = 0;; ++attempt) {
     LinesArgs A;
     A.buf = buf; A.n = n; A.nl = e->nl.p; A.n_lines = n_lines; A.L = L; A.now_ns = now_ns;
+    A.dbg = getenv("BJX_DEBUG_LINES") ? (uint32_t)atoi(getenv("BJX_DEBUG_LINES")) : 0u;
     A.slow_list = e->slow_list.p; A.slow_count = e->scalars.p;
     A.jline = e->jline.p; A.jkey = e->jkey.p; A.job_count = e->scalars.p + 11; A.job_cap = std::min(e->jline.n, e->jkey.n);
     const bool img_lds = B.img_bytes <= kLinesImgMax;
@@ -2910,7 +2933,7 @@ static EvSrc local_evsrc(bjx_engine *e) {
 
 // Trips (reference order) and the optional per-line / RuleResult copies, once
 // e->ev_out holds every local event's Apply outcome (phases 7-8).
-static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out) {
+static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, bool sorted) {
   const Bind &B = e->bind;
   hipStream_t st = e->stream;
   const BatchCtx &c = e->bc;
@@ -2919,31 +2942,44 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out) {
   uint64_t n_trips = 0;
   if (n_ev) {
     mark(e, 7);
-    // trips in reference order (events are in reference order)
-    e->trip_flag.ensure(n_ev); e->trip_idx.ensure(n_ev + 1);
-    hipLaunchKernelGGL(k_flag_trips, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_out.p, e->trip_flag.p);
-    {
-      hipcub::CountingInputIterator<uint32_t> it(0);
-      uint8_t *fl = e->trip_flag.p;
-      uint32_t *o = e->trip_idx.p;
-      unsigned long long *ns = e->scalars.p + 4;
-      cub_call(e, [&](void *tmp, size_t &bytes) {
-        return hipcub::DeviceSelect::Flagged(tmp, bytes, it, fl, o, ns, (int)n_ev, st);
-      });
-    }
+    // trips: Exceeded outcomes.  sorted: outcomes in state-slot order (this
+    // engine's rate-limit stage), selected there and put back in reference
+    // order; otherwise outcomes already in event (= reference) order
+    e->trip_idx.ensure(n_ev + 1);
+    hipcub::CountingInputIterator<uint32_t> it(0);
+    hipcub::TransformInputIterator<bool, TripBit, const uint8_t *> fl(sorted ? e->ev_out_s.p : e->ev_out.p, TripBit());
+    uint32_t *o = e->trip_idx.p;
+    unsigned long long *ns = e->scalars.p + 4;
+    cub_call(e, [&](void *tmp, size_t &bytes) {
+      return hipcub::DeviceSelect::Flagged(tmp, bytes, it, fl, o, ns, (int)n_ev, st);
+    });
     unsigned long long nt = 0;
     HIP_OK(hipMemcpyAsync(&nt, e->scalars.p + 4, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     n_trips = nt;
     if (n_trips) {
+      const uint32_t *trip_ev = e->trip_idx.p;
+      if (sorted) {
+        e->trip_ev.ensure(n_trips); e->trip_ev2.ensure(n_trips);
+        hipLaunchKernelGGL(k_trip_events, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_idx.p, e->ev_rec2.p,
+                           e->trip_ev.p);
+        uint32_t *ki = e->trip_ev.p, *ko = e->trip_ev2.p;
+        const int bits = std::max(1, bit_width(n_ev));
+        cub_call(e, [&](void *tmp, size_t &bytes) {
+          return hipcub::DeviceRadixSort::SortKeys(tmp, bytes, ki, ko, (int)n_trips, 0, bits, st);
+        });
+        trip_ev = e->trip_ev2.p;
+      }
       e->d_trips.ensure(n_trips);
-      hipLaunchKernelGGL(k_build_trips, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_idx.p, e->ev_el.p,
+      hipLaunchKernelGGL(k_build_trips, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, trip_ev, e->ev_el.p,
                          e->ev_rule.p, e->nl.p, L, B.rules, e->d_trips.p);
       HIP_OK(hipGetLastError());
       e->trips.resize(n_trips);
       HIP_OK(hipMemcpyAsync(e->trips.data(), e->d_trips.p, n_trips * sizeof(bjx_trip), hipMemcpyDeviceToHost, st));
     }
     if (flags & BJX_COPY_RESULTS) {
+      if (sorted)
+        hipLaunchKernelGGL(k_unsort, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_rec2.p, e->ev_out_s.p, e->ev_out.p);
       hipLaunchKernelGGL(k_scatter_rl, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_res.p, e->ev_out.p, e->rl_out.p);
       HIP_OK(hipGetLastError());
     }
@@ -2989,7 +3025,7 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
   if (!match_phase(e, rs, bytes, n, now_ns, flags, out)) return;
   if (e->bc.n_ev)
     rate_limit_stage(e, e->bind, local_evsrc(e), e->bc.n_el, e->bc.el_bytes, e->bc.n_ev, e->ev_el.p, e->ev_rule.p);
-  finish_phase(e, flags, out);
+  finish_phase(e, flags, out, true);
 }
 
 extern "C" int bjx_process_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns,
@@ -3148,7 +3184,8 @@ extern "C" int bjx_apply_events(bjx_engine *e, const bjx_ruleset *rs, const bjx_
     E.bytes = d_bytes; E.nl = nullptr; E.ip_off = nullptr; E.ip_pos = e->rx_pos.p; E.ip_len = e->rx_len.p;
     E.ip_hash = e->rx_hash.p; E.ts = e->rx_ts.p; E.counts = nullptr; E.n = n_lines;
     rate_limit_stage(e, B, E, n_lines, n_bytes, n_ev, e->rx_ev_el.p, d_events);
-    HIP_OK(hipMemcpyAsync(d_out, e->ev_out.p, n_ev, hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(k_unsort, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_rec2.p, e->ev_out_s.p, d_out);
+    HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(st));
     return BJX_OK;
   });
@@ -3171,7 +3208,7 @@ extern "C" int bjx_finish_batch(bjx_engine *e, const uint8_t *d_outcomes, uint32
     out->consumed_bytes = c.consumed;
     out->n_results = c.n_res;
     out->n_events = c.n_ev;
-    finish_phase(e, flags, out);
+    finish_phase(e, flags, out, false);
     e->partitioned = false;
     return BJX_OK;
   });
