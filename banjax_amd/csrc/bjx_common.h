@@ -64,9 +64,10 @@ inline uint32_t ld4(const uint8_t *p) {
 }
 #ifdef __HIPCC__
 __device__ __forceinline__ uint32_t ld4(const uint8_t *p) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
-  const uint32_t sh = (uint32_t)(a & 3);
+  // align by pointer arithmetic on p itself (no integer round trip), so the
+  // compiler keeps p's address space: ds_read for LDS, global_load for HBM
+  const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(p - sh);
   return sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
 }
 #endif

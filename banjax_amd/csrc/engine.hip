@@ -148,6 +148,32 @@ __device__ __forceinline__ bool bytes_eq(const uint8_t *a, const uint8_t *b, uin
   return true;
 }
 
+// Inline IP key (IpSlot.key16): bytes 0..14 zero padded, byte 15 = min(len, 255).
+// Equal keys <=> equal IPs when len <= 15 (every IPv4 text); longer IPs
+// compare their bytes in the arena.  Word loads; the caller keeps 3 bytes of
+// readable slack past ip + 15 (a log line always continues past its IP).
+__device__ __forceinline__ uint4 ip_key16(const uint8_t *ip, uint32_t len) {
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t lo = 4u * k;
+    const uint32_t m = len <= lo ? 0u : (len >= lo + 4 ? 0xFFFFFFFFu : (1u << (8 * (len - lo))) - 1u);
+    w[k] = m ? ld4(ip + lo) & m : 0u;
+  }
+  w[3] = (w[3] & 0x00FFFFFFu) | ((len < 255 ? len : 255u) << 24);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+// the same key from bytes that may end at ip + len (exchanged IP pools)
+__device__ __forceinline__ uint4 ip_key16_bytes(const uint8_t *ip, uint32_t len) {
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (uint32_t k = 0; k < len && k < 15; ++k) w[k >> 2] |= (uint32_t)ip[k] << (8 * (k & 3));
+  w[3] |= (len < 255 ? len : 255u) << 24;
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ bool key16_eq(const uint4 &a, const uint4 &b) {
+  return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+}
+
 // host string -> host id (per_site_regexes_with_rates key / skip host / allow-list site)
 __device__ int32_t host_lookup(const Bind &B, const uint8_t *h, uint32_t n) {
   if (B.n_hd == 0) return -1;
@@ -296,6 +322,7 @@ __device__ void parse_and_match(const Bind &B, const uint8_t *__restrict__ p, ui
   L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
   L.host_id[j] = hid;
   L.ip_hash[j] = hash_bytes(p + ip_off, ip_len);
+  L.ip16[j] = ip_key16(p + ip_off, ip_len);
   if (!SLOW) {
     if (parse_float_fast(p, sp1, &f) != 0) {
       // rare: exotic timestamp token -> general ParseFloat kernel
@@ -887,9 +914,8 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
 // first four spaces of the line [p, p + n): 16 B aligned loads, SWAR compare
 __device__ __forceinline__ uint32_t find_spaces(const uint8_t *p, uint32_t n, uint32_t &sp0, uint32_t &sp1,
                                                 uint32_t &sp2, uint32_t &sp3) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint4 *base = reinterpret_cast<const uint4 *>(a & ~(uintptr_t)15);
-  const uint32_t skip = (uint32_t)(a & 15);
+  const uint32_t skip = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15);
+  const uint4 *base = reinterpret_cast<const uint4 *>(p - skip);  // keeps p's address space
   uint32_t ns = 0;
   for (uint32_t c = 0; c * 16 < n + skip && ns < 4; ++c) {
     const uint4 v = base[c];
@@ -936,6 +962,9 @@ struct LinesArgs {
 // consumeLine up to the rule loop for line j (bytes at base + (s - origin)):
 // SplitN header, parseTimestamp fast path, host lookup, CheckIsAllowed,
 // OldLine, then the rule decisions from the scan pass's literal hits.
+// STAGED: base is the wave's LDS span (a distinct instantiation, so the
+// compiler cannot merge the two call sites into one generic-pointer copy)
+template <bool STAGED>
 __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const LinesArgs &A, const uint8_t *base,
                                           uint64_t origin, uint64_t s, uint32_t n, uint64_t j, const JobSink &S) {
   const Lines &L = A.L;
@@ -962,6 +991,7 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
     L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
     L.host_id[j] = hid;
     L.ip_hash[j] = hash_bytes(p + ip_off, ip_len);
+    L.ip16[j] = ip_key16(p + ip_off, ip_len);
     const int64_t tsn = ns_from_seconds(f);
     L.ts[j] = tsn;
     uint8_t fl = 0;
@@ -1055,8 +1085,8 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
       const uint64_t s = j ? A.nl[j - 1] + 1 : 0;
       const uint32_t n = (uint32_t)(A.nl[j] - s);
       // two inlined copies: LDS addressing for staged waves, global otherwise
-      if (staged) line_body(B, TB, A, span, b16, s, n, j, S);
-      else line_body(B, TB, A, A.buf, 0, s, n, j, S);
+      if (staged) line_body<true>(B, TB, A, span, b16, s, n, j, S);
+      else line_body<false>(B, TB, A, A.buf, 0, s, n, j, S);
     }
     // ---- append this wave's DFA jobs (one global atomic per 64 lines)
     wave_sync();
@@ -1082,6 +1112,9 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
 // the rule's bit and adds to the line's result / event counts.
 constexpr uint32_t kDfaLdsEntries = 8192;  // u16 transitions staged per block (16 KB)
 
+// STAGED: tr / ac point into LDS (a distinct instantiation keeps the call
+// sites apart, so each keeps its address space instead of generic loads)
+template <bool STAGED>
 __device__ __forceinline__ bool dfa_text(const Bind &B, const DevRule &R, const uint16_t *tr, const uint8_t *ac,
                                          const uint8_t *__restrict__ buf, uint64_t n_buf, uint64_t t0, uint32_t len) {
   const uint32_t ncls = R.ncls;
@@ -1162,12 +1195,16 @@ __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restric
   const uint32_t key = jkey[t];
   const uint32_t r = key & 0xFFFFFF, pos = key >> 24;
   const uint64_t j = jline[t];
-  const DevRule R = staged ? R0 : B.rules[r];
-  const uint16_t *tr = staged ? s_tr : B.trans + R.trans_off;
-  const uint8_t *ac = staged ? s_ac : B.ascii_cls + (size_t)r * 128;
   const uint64_t s = j ? nl[j - 1] + 1 : 0;
   const uint64_t rs = s + L.rest_off[j];
-  if (!dfa_text(B, R, tr, ac, buf, n_buf, rs, (uint32_t)(nl[j] - rs))) return;
+  bool m;
+  if (staged) {
+    m = dfa_text<true>(B, R0, s_tr, s_ac, buf, n_buf, rs, (uint32_t)(nl[j] - rs));
+  } else {
+    const DevRule R = B.rules[r];
+    m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, buf, n_buf, rs, (uint32_t)(nl[j] - rs));
+  }
+  if (!m) return;
   const int32_t hid = L.host_id[j];
   const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
   const bool skip = (B.sc_skip[2 * sc + (pos >> 6)] >> (pos & 63)) & 1;
@@ -1256,6 +1293,8 @@ __global__ __launch_bounds__(kBlock) void k_ip_claim(EvSrc E, State S, uint32_t 
   const uint64_t h = E.ip_hash[i];
   const uint32_t len = E.ip_len[i];
   const uint8_t *ip = ev_ip(E, i);
+  const bool inl = len <= 15;
+  const uint4 k16 = !inl ? make_uint4(0, 0, 0, 0) : E.ip16 ? E.ip16[i] : ip_key16_bytes(ip, len);
   uint64_t s = h & S.ip_mask;
   for (;;) {
     uint64_t cur = S.ip[s].hash;
@@ -1272,8 +1311,9 @@ __global__ __launch_bounds__(kBlock) void k_ip_claim(EvSrc E, State S, uint32_t 
         el_id[i] = kNewIp;
         return;
       }
-      const uint32_t id = S.ip[s].id;  // created by an earlier batch: its bytes are in the arena
-      if (S.ip_len[id] == len && bytes_eq(S.arena + S.ip_off[id], ip, len)) {
+      // created by an earlier batch: short IPs compare inline, long ones in the arena
+      const uint32_t id = S.ip[s].id;
+      if (inl ? key16_eq(S.ip[s].key16, k16) : (S.ip_len[id] == len && bytes_eq(S.arena + S.ip_off[id], ip, len))) {
         el_slot[i] = (uint32_t)s;
         el_id[i] = id;
         return;
@@ -1298,6 +1338,7 @@ __global__ __launch_bounds__(kBlock) void k_ip_commit(EvSrc E, State S, uint32_t
     S.ip_off[id] = off;
     S.ip_len[id] = len;
     S.ip[s].id = id;
+    S.ip[s].key16 = E.ip16 ? E.ip16[i] : ip_key16_bytes(ip, len);
     el_id[i] = id | kFirstIp;
   } else if (E.ip_len[f] != len || !bytes_eq(ev_ip(E, f), ip, len)) {
     const uint64_t k = atomicAdd((unsigned long long *)&S.counters[3], 1ull);
@@ -1329,6 +1370,7 @@ __global__ void k_ip_collide(EvSrc E, State S, uint32_t epoch, uint32_t *__restr
         S.ip[s].hash = h;
         S.ip[s].id = id;
         S.ip[s].born = epoch;
+        S.ip[s].key16 = E.ip16 ? E.ip16[i] : ip_key16_bytes(ip, len);
         S.ip_first[s] = i;
         el_slot[i] = (uint32_t)s;
         el_id[i] = id | kFirstIp;
@@ -1509,7 +1551,7 @@ __global__ void k_rehash_ip(uint64_t old_cap, const IpSlot *__restrict__ o, IpSl
   uint64_t j = o[i].hash & nmask;
   for (;;) {
     const unsigned long long prev = atomicCAS((unsigned long long *)&nt[j].hash, 0ull, (unsigned long long)o[i].hash);
-    if (prev == 0) { nt[j].id = o[i].id; nt[j].born = o[i].born; return; }
+    if (prev == 0) { nt[j].id = o[i].id; nt[j].born = o[i].born; nt[j].key16 = o[i].key16; return; }
     j = (j + 1) & nmask;
   }
 }
@@ -1695,7 +1737,8 @@ struct HostBuf {
       if (p) (void)hipHostFree(p);
       p = nullptr;
       cap = 0;
-      const size_t c = want < 1024 ? 1024 : want + want / 4;
+      // geometric growth: a pinned (re)allocation stalls the batch for ~0.1 ms/MB
+      const size_t c = want < 1024 ? 1024 : std::max(want + want / 2, 2 * cap);
       HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&p), c * sizeof(T), hipHostMallocDefault));
       cap = c;
     }
@@ -1870,6 +1913,7 @@ struct bjx_engine {
   DevBuf<uint32_t> l_ipoff, l_iplen, l_hoff, l_hlen, l_roff, slow_list;
   DevBuf<int32_t> l_hid;
   DevBuf<uint64_t> l_cand;
+  DevBuf<uint4> l_ip16;
   DevBuf<uint32_t> long_list;
   DevBuf<uint32_t> jline, jkey, jline2, jkey2;
   uint64_t last_jobs = 0;
@@ -2612,7 +2656,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
     b->release();
   e->rx_ts.release(); e->trip_idx.release(); e->d_trips.release();
   e->d_results.release(); e->q_out.release();
-  e->long_list.release(); e->jline.release(); e->jkey.release(); e->jline2.release(); e->jkey2.release(); e->l_cand.release(); e->l_ccnt.release();
+  e->long_list.release(); e->l_ip16.release(); e->jline.release(); e->jkey.release(); e->jline2.release(); e->jkey2.release(); e->l_cand.release(); e->l_ccnt.release();
   (void)hipEventDestroy(e->ev0); (void)hipEventDestroy(e->ev1); (void)hipEventDestroy(e->evm0); (void)hipEventDestroy(e->evm1);
   for (auto &x : e->ph) (void)hipEventDestroy(x);
   (void)hipStreamDestroy(e->stream);
@@ -2784,14 +2828,14 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   e->l_masks.ensure(n_lines * B.mask_words);
   e->l_ipoff.ensure(n_lines); e->l_iplen.ensure(n_lines); e->l_hoff.ensure(n_lines); e->l_hlen.ensure(n_lines);
   e->l_roff.ensure(n_lines); e->l_hid.ensure(n_lines); e->l_flags.ensure(n_lines); e->slow_list.ensure(n_lines);
-  e->long_list.ensure(n_lines); e->l_ccnt.ensure(n_lines);
+  e->long_list.ensure(n_lines); e->l_ccnt.ensure(n_lines); e->l_ip16.ensure(n_lines);
   e->l_cand.ensure(B.any_prefilter ? n_lines * kCandSlots : 1);
   e->scalars.ensure(16);
   Lines L;
   L.ts = e->l_ts.p; L.ip_hash = e->l_iph.p; L.ip_off = e->l_ipoff.p; L.ip_len = e->l_iplen.p; L.host_off = e->l_hoff.p;
   L.host_len = e->l_hlen.p; L.rest_off = e->l_roff.p; L.host_id = e->l_hid.p; L.flags = e->l_flags.p;
   L.counts = e->l_counts.p; L.masks = e->l_masks.p;
-  L.cand_cnt = e->l_ccnt.p; L.cand = e->l_cand.p;
+  L.cand_cnt = e->l_ccnt.p; L.cand = e->l_cand.p; L.ip16 = e->l_ip16.p;
   e->jline.ensure(std::max<uint64_t>(e->jline.n, n_lines + (1u << 20)));
   e->jkey.ensure(e->jline.n);
   HIP_OK(hipMemsetAsync(e->scalars.p, 0, 16 * sizeof(unsigned long long), st));
@@ -2927,7 +2971,7 @@ static EvSrc local_evsrc(bjx_engine *e) {
   const BatchCtx &c = e->bc;
   EvSrc E;
   E.bytes = c.buf; E.nl = e->nl.p; E.ip_off = c.L.ip_off; E.ip_pos = nullptr; E.ip_len = c.L.ip_len;
-  E.ip_hash = c.L.ip_hash; E.ts = c.L.ts; E.counts = c.L.counts; E.n = c.n_lines;
+  E.ip_hash = c.L.ip_hash; E.ts = c.L.ts; E.counts = c.L.counts; E.ip16 = c.L.ip16; E.n = c.n_lines;
   return E;
 }
 
@@ -3182,7 +3226,7 @@ extern "C" int bjx_apply_events(bjx_engine *e, const bjx_ruleset *rs, const bjx_
     if (chk[0] != n_ev || chk[1]) throw BjxError(BJX_ERR_ARG, "received event records are inconsistent");
     EvSrc E;
     E.bytes = d_bytes; E.nl = nullptr; E.ip_off = nullptr; E.ip_pos = e->rx_pos.p; E.ip_len = e->rx_len.p;
-    E.ip_hash = e->rx_hash.p; E.ts = e->rx_ts.p; E.counts = nullptr; E.n = n_lines;
+    E.ip_hash = e->rx_hash.p; E.ts = e->rx_ts.p; E.counts = nullptr; E.ip16 = nullptr; E.n = n_lines;
     rate_limit_stage(e, B, E, n_lines, n_bytes, n_ev, e->rx_ev_el.p, d_events);
     hipLaunchKernelGGL(k_unsort, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_rec2.p, e->ev_out_s.p, d_out);
     HIP_OK(hipGetLastError());

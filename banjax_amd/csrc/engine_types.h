@@ -137,6 +137,7 @@ struct Lines {
   uint8_t *flags;
   uint64_t *counts;    // (n_results << 32) | n_events per line, then scanned in place
   uint64_t *masks;     // mask_words per line
+  uint4 *ip16;         // key16 of the line's IP (see IpSlot)
   uint32_t *cand_cnt;  // literal hits recorded by the scan pass
   uint64_t *cand;      // kCandSlots per line: (literal start << 24) | verified | literal id
 };
@@ -152,6 +153,7 @@ struct IpSlot {
   uint64_t hash;  // 0 = empty
   uint32_t id;    // dense IP id (arena index)
   uint32_t born;  // epoch of creation (0 only while being claimed)
+  uint4 key16;    // IP bytes 0..14 zero padded, byte 15 = min(len, 255): IPs of <= 15 bytes compare inline
 };
 //   State table: open addressing on key = ((ip_id + 1) << 24) | name_id,
 //   one 32 B slot per probe (NumHitsAndIntervalStart, rate_limit.go:165-168).
@@ -196,6 +198,7 @@ struct EvSrc {
   const uint64_t *ip_hash;
   const int64_t *ts;
   const uint64_t *counts;  // local batch: low 32 bits = events of line i; nullptr: every record has events
+  const uint4 *ip16;       // local batch: per-line key16 of the IP; nullptr: built from the bytes
   uint64_t n;
 };
 
