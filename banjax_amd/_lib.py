@@ -140,6 +140,8 @@ def lib():
     L.bjx_debug_phase_ms.argtypes = [vp, C.POINTER(C.c_double), sz]
     L.bjx_debug_scan_stats.restype = sz
     L.bjx_debug_scan_stats.argtypes = [vp, C.POINTER(C.c_uint64), sz]
+    L.bjx_debug_set_claim_budget.restype = C.c_int
+    L.bjx_debug_set_claim_budget.argtypes = [vp, C.c_uint64]
     L.bjx_debug_set_ip_hash_mask.restype = C.c_int
     L.bjx_debug_set_ip_hash_mask.argtypes = [vp, C.c_uint64]
     L.bjx_engine_last_error.restype = C.c_char_p

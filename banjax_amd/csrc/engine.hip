@@ -1286,8 +1286,11 @@ __device__ __forceinline__ bool ev_has(const EvSrc &E, uint64_t i) {
 constexpr uint32_t kNewIp = 0xFFFFFFFFu;   // el_id: IP created in this batch, id not known to this line
 constexpr uint32_t kFirstIp = 0x80000000u; // el_id: this line is the first event line of a new IP
 
+// budget: new slots this launch may claim (keeps the table under its load
+// factor); past it the launch sets counters[5] and the host rolls back, grows
+// the table and claims again.
 __global__ __launch_bounds__(kBlock) void k_ip_claim(EvSrc E, State S, uint32_t epoch, uint32_t *__restrict__ el_slot,
-                                                     uint32_t *__restrict__ el_id) {
+                                                     uint32_t *__restrict__ el_id, uint64_t budget) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= E.n || !ev_has(E, i)) return;
   const uint64_t h = E.ip_hash[i];
@@ -1299,8 +1302,17 @@ __global__ __launch_bounds__(kBlock) void k_ip_claim(EvSrc E, State S, uint32_t 
   for (;;) {
     uint64_t cur = S.ip[s].hash;
     if (cur == 0) {
+      // claims counted as they succeed; once the budget is spent nobody claims
+      // (overshoot <= lanes in flight, far below the table's free quarter)
+      if (__hip_atomic_load(&S.counters[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= budget) {
+        atomicOr((unsigned long long *)&S.counters[5], 1ull);
+        return;
+      }
       cur = atomicCAS((unsigned long long *)&S.ip[s].hash, 0ull, (unsigned long long)h);
-      if (cur == 0) cur = h;
+      if (cur == 0) {
+        cur = h;
+        if (atomicAdd((unsigned long long *)&S.counters[4], 1ull) >= budget) atomicOr((unsigned long long *)&S.counters[5], 1ull);
+      }
     }
     if (cur == h) {
       uint32_t b = S.ip[s].born;
@@ -1394,7 +1406,8 @@ __global__ void k_ip_collide(EvSrc E, State S, uint32_t epoch, uint32_t *__restr
 __global__ __launch_bounds__(kBlock) void k_st_claim(EvSrc E, uint64_t n_ev, const uint32_t *__restrict__ ev_el,
                                                      const uint32_t *__restrict__ ev_rule, const uint32_t *__restrict__ el_slot,
                                                      const uint32_t *__restrict__ el_id, const DevRule *__restrict__ rules,
-                                                     State S, uint32_t *__restrict__ ev_st, EvRec *__restrict__ ev_rec) {
+                                                     State S, uint32_t *__restrict__ ev_st, EvRec *__restrict__ ev_rec,
+                                                     uint64_t budget) {
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n_ev) return;
   const uint32_t i = ev_el[k];
@@ -1408,6 +1421,10 @@ __global__ __launch_bounds__(kBlock) void k_st_claim(EvSrc E, uint64_t n_ev, con
   for (;;) {
     uint64_t cur = S.st[q].key;
     if (cur == 0) {
+      if (__hip_atomic_load(&S.counters[6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= budget) {  // see k_ip_claim
+        atomicOr((unsigned long long *)&S.counters[7], 1ull);
+        break;
+      }
       cur = atomicCAS((unsigned long long *)&S.st[q].key, 0ull, (unsigned long long)key);
       if (cur == 0) { claimed = true; break; }
     }
@@ -1420,10 +1437,13 @@ __global__ __launch_bounds__(kBlock) void k_st_claim(EvSrc E, uint64_t n_ev, con
   rec.rule = r | (first ? 0x80000000u : 0u);
   rec.ev = (uint32_t)k;
   ev_rec[k] = rec;
-  // table load (counters[2]): one atomic per wave
+  // table load (counters[2]) and this launch's claims (counters[6], budget): one atomic pair per wave
   const uint64_t won = __ballot(claimed);
-  if (won && (threadIdx.x & 63) == (uint32_t)(__ffsll((unsigned long long)won) - 1))
+  if (won && (threadIdx.x & 63) == (uint32_t)(__ffsll((unsigned long long)won) - 1)) {
     atomicAdd((unsigned long long *)&S.counters[2], (unsigned long long)__popcll(won));
+    if (atomicAdd((unsigned long long *)&S.counters[6], (unsigned long long)__popcll(won)) + __popcll(won) > budget)
+      atomicOr((unsigned long long *)&S.counters[7], 1ull);
+  }
 }
 
 // run heads of the slot-sorted events
@@ -1542,6 +1562,27 @@ __global__ void k_build_results(uint64_t n, const uint64_t *__restrict__ res_seq
 __global__ void k_final_flags(uint64_t n, uint8_t *__restrict__ f) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) f[i] &= (kLineError | kLineOld | kLineExempt);
+}
+
+// undo one batch's claims (table overflow): its slots were empty before the
+// batch and no earlier key's probe chain runs through them
+__global__ void k_ip_rollback(uint64_t cap, State S, uint32_t epoch) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap) return;
+  const IpSlot v = S.ip[i];
+  if (v.hash != 0 && (v.born == epoch || v.born == 0)) {
+    S.ip[i] = IpSlot{};
+    S.ip_first[i] = 0xFFFFFFFFu;
+  }
+}
+__global__ void k_st_rollback(uint64_t cap, State S) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap) return;
+  const bool live = S.st[i].key != 0 && S.st[i].valid != 0;
+  if (S.st[i].key != 0 && !live) S.st[i] = StSlot{};
+  const uint64_t m = __ballot(live);
+  if (m && (threadIdx.x & 63) == (uint32_t)(__ffsll((unsigned long long)m) - 1))
+    atomicAdd((unsigned long long *)&S.counters[2], (unsigned long long)__popcll(m));
 }
 
 // rehash (table growth)
@@ -1902,6 +1943,7 @@ struct bjx_engine {
   uint64_t ip_cap = 0, st_cap = 0;
   uint32_t epoch = 0;  // batch counter (IpSlot.born)
   uint64_t dbg_hash_mask = 0;  // bjx_debug_set_ip_hash_mask
+  uint64_t dbg_budget = 0;     // bjx_debug_set_claim_budget (0 = off)
   uint64_t host_counters[3] = {0, 0, 0};
 
   // batch workspace
@@ -2538,32 +2580,57 @@ void read_counters(bjx_engine *e) {
   HIP_OK(hipStreamSynchronize(e->stream));
 }
 
-// grow tables so that `new_ips` more IPs, `new_bytes` more arena bytes and
-// `new_states` more states fit under a 3/4 load factor (every probe loop
-// then terminates: a table is never full)
+// rehash the IP table into one that holds `want` IPs under a 3/4 load factor
+void grow_ip(bjx_engine *e, uint64_t want) {
+  State &S = e->S;
+  const uint64_t n_ips = e->host_counters[0];
+  const uint64_t cap = next_pow2(want * 4 / 3 + 1024);
+  if (cap <= e->ip_cap) return;
+  IpSlot *nt; uint32_t *nf; uint64_t *noff; uint32_t *nlen;
+  HIP_OK(hipMalloc(&nt, cap * sizeof(IpSlot)));
+  HIP_OK(hipMalloc(&nf, cap * 4));
+  HIP_OK(hipMalloc(&noff, cap * 8));
+  HIP_OK(hipMalloc(&nlen, cap * 4));
+  HIP_OK(hipMemsetAsync(nt, 0, cap * sizeof(IpSlot), e->stream));
+  HIP_OK(hipMemsetAsync(nf, 0xFF, cap * 4, e->stream));
+  HIP_OK(hipMemcpyAsync(noff, S.ip_off, n_ips * 8, hipMemcpyDeviceToDevice, e->stream));
+  HIP_OK(hipMemcpyAsync(nlen, S.ip_len, n_ips * 4, hipMemcpyDeviceToDevice, e->stream));
+  hipLaunchKernelGGL(k_rehash_ip, dim3(grid_for(e->ip_cap)), dim3(kBlock), 0, e->stream, e->ip_cap, S.ip, nt, cap - 1);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipStreamSynchronize(e->stream));
+  (void)hipFree(S.ip); (void)hipFree(S.ip_first); (void)hipFree(S.ip_off); (void)hipFree(S.ip_len);
+  S.ip = nt; S.ip_first = nf; S.ip_off = noff; S.ip_len = nlen;
+  S.ip_mask = cap - 1;
+  e->ip_cap = cap;
+}
+
+// rehash the state table into one that holds `want` states under a 3/4 load factor
+void grow_st(bjx_engine *e, uint64_t want) {
+  State &S = e->S;
+  const uint64_t cap = next_pow2(want * 4 / 3 + 1024);
+  if (cap <= e->st_cap) return;
+  StSlot *nt;
+  HIP_OK(hipMalloc(&nt, cap * sizeof(StSlot)));
+  HIP_OK(hipMemsetAsync(nt, 0, cap * sizeof(StSlot), e->stream));
+  hipLaunchKernelGGL(k_rehash_st, dim3(grid_for(e->st_cap)), dim3(kBlock), 0, e->stream, e->st_cap, S.st, nt, cap - 1);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipStreamSynchronize(e->stream));
+  (void)hipFree(S.st);
+  S.st = nt;
+  S.st_mask = cap - 1;
+  e->st_cap = cap;
+}
+
+// Tables sized for the steady state, not for every batch's worst case: the
+// IP and state tables keep room for `new_ips` / `new_states` more entries
+// (claims beyond that roll back and grow, see rate_limit_stage); the arena
+// always fits the batch's IP bytes.  Small tables keep the random probes in
+// cache and the state-slot sort short.
 void ensure_capacity(bjx_engine *e, uint64_t new_ips, uint64_t new_bytes, uint64_t new_states) {
   read_counters(e);
   State &S = e->S;
   const uint64_t n_ips = e->host_counters[0], used = e->host_counters[1], n_st = e->host_counters[2];
-  if ((n_ips + new_ips) * 4 > e->ip_cap * 3) {
-    const uint64_t cap = next_pow2((n_ips + new_ips) * 2 + 1024);
-    IpSlot *nt; uint32_t *nf; uint64_t *noff; uint32_t *nlen;
-    HIP_OK(hipMalloc(&nt, cap * sizeof(IpSlot)));
-    HIP_OK(hipMalloc(&nf, cap * 4));
-    HIP_OK(hipMalloc(&noff, cap * 8));
-    HIP_OK(hipMalloc(&nlen, cap * 4));
-    HIP_OK(hipMemsetAsync(nt, 0, cap * sizeof(IpSlot), e->stream));
-    HIP_OK(hipMemsetAsync(nf, 0xFF, cap * 4, e->stream));
-    HIP_OK(hipMemcpyAsync(noff, S.ip_off, n_ips * 8, hipMemcpyDeviceToDevice, e->stream));
-    HIP_OK(hipMemcpyAsync(nlen, S.ip_len, n_ips * 4, hipMemcpyDeviceToDevice, e->stream));
-    hipLaunchKernelGGL(k_rehash_ip, dim3(grid_for(e->ip_cap)), dim3(kBlock), 0, e->stream, e->ip_cap, S.ip, nt, cap - 1);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipStreamSynchronize(e->stream));
-    (void)hipFree(S.ip); (void)hipFree(S.ip_first); (void)hipFree(S.ip_off); (void)hipFree(S.ip_len);
-    S.ip = nt; S.ip_first = nf; S.ip_off = noff; S.ip_len = nlen;
-    S.ip_mask = cap - 1;
-    e->ip_cap = cap;
-  }
+  if ((n_ips + new_ips) * 4 > e->ip_cap * 3) grow_ip(e, 2 * (n_ips + new_ips));
   if (used + new_bytes > S.arena_cap) {
     const uint64_t cap = std::max<uint64_t>(S.arena_cap * 2, used + new_bytes + (1 << 20));
     uint8_t *na;
@@ -2574,19 +2641,7 @@ void ensure_capacity(bjx_engine *e, uint64_t new_ips, uint64_t new_bytes, uint64
     S.arena = na;
     S.arena_cap = cap;
   }
-  if ((n_st + new_states) * 4 > e->st_cap * 3) {
-    const uint64_t cap = next_pow2((n_st + new_states) * 2 + 1024);
-    StSlot *nt;
-    HIP_OK(hipMalloc(&nt, cap * sizeof(StSlot)));
-    HIP_OK(hipMemsetAsync(nt, 0, cap * sizeof(StSlot), e->stream));
-    hipLaunchKernelGGL(k_rehash_st, dim3(grid_for(e->st_cap)), dim3(kBlock), 0, e->stream, e->st_cap, S.st, nt, cap - 1);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipStreamSynchronize(e->stream));
-    (void)hipFree(S.st);
-    S.st = nt;
-    S.st_mask = cap - 1;
-    e->st_cap = cap;
-  }
+  if ((n_st + new_states) * 4 > e->st_cap * 3) grow_st(e, 2 * (n_st + new_states));
 }
 
 template <typename F>
@@ -2621,8 +2676,10 @@ extern "C" int bjx_engine_create(int device, const bjx_engine_options *opts, bjx
     HIP_OK(hipEventCreate(&e->evm0));
     HIP_OK(hipEventCreate(&e->evm1));
     for (auto &x : e->ph) HIP_OK(hipEventCreate(&x));
-    uint64_t ipc = opts && opts->ip_capacity ? next_pow2(opts->ip_capacity) : (1ull << 20);
-    uint64_t stc = opts && opts->state_capacity ? next_pow2(opts->state_capacity) : (1ull << 22);
+    // >= 4M slots: a quarter of the table stays free for the claims in flight
+    // when a launch spends its budget (see k_ip_claim)
+    uint64_t ipc = std::max<uint64_t>(opts && opts->ip_capacity ? next_pow2(opts->ip_capacity) : 0, 1ull << 22);
+    uint64_t stc = std::max<uint64_t>(opts && opts->state_capacity ? next_pow2(opts->state_capacity) : 0, 1ull << 22);
     uint64_t ar = opts && opts->ip_arena_bytes ? opts->ip_arena_bytes : (64ull << 20);
     alloc_state(e.get(), ipc, stc, ar);
     *out = e.release();
@@ -2706,17 +2763,34 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
                              const uint32_t *ev_el, const uint32_t *ev_rule) {
   hipStream_t st = e->stream;
   if (E.n >= 0x7FFFFFFFull || n_ev >= 0xFFFFFFFFull) throw BjxError(BJX_ERR_ARG, "batch too large (2^31 lines / 2^32 events)");
-  ensure_capacity(e, n_el, el_bytes, n_ev);
+  read_counters(e);
+  ensure_capacity(e, std::min<uint64_t>(n_el, std::max<uint64_t>(1u << 18, e->host_counters[0] / 8)), el_bytes,
+                  std::min<uint64_t>(n_ev, std::max<uint64_t>(1u << 20, e->host_counters[2] / 8)));
   if (e->host_counters[0] + n_el >= 0x7FFFFFFFull) throw BjxError(BJX_ERR_CAPACITY, "more than 2^31 distinct IPs");
   if (++e->epoch == 0) ++e->epoch;  // 0 marks a slot being claimed
   const uint32_t epoch = e->epoch;
   e->el_slot.ensure(E.n); e->el_id.ensure(E.n); e->coll.ensure(E.n);
   e->ev_st.ensure(n_ev); e->ev_st2.ensure(n_ev); e->ev_rec.ensure(n_ev); e->ev_rec2.ensure(n_ev);
   e->ev_out.ensure(n_ev); e->ev_out_s.ensure(n_ev); e->run_flag.ensure(n_ev); e->run_heads.ensure(n_ev);
-  HIP_OK(hipMemsetAsync(e->S.counters + 3, 0, 8, st));
   mark(e, 5);
-  hipLaunchKernelGGL(k_ip_claim, dim3(grid_for(E.n)), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p);
-  HIP_OK(hipGetLastError());
+  for (int attempt = 0;; ++attempt) {
+    const uint64_t n_ips = e->host_counters[0];
+    HIP_OK(hipMemsetAsync(e->S.counters + 3, 0, 3 * 8, st));
+    uint64_t budget = e->ip_cap * 3 / 4 - n_ips;
+    const bool forced = e->dbg_budget && attempt == 0 && e->dbg_budget < budget;  // test hook
+    if (forced) budget = e->dbg_budget;
+    hipLaunchKernelGGL(k_ip_claim, dim3(grid_for(E.n)), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p,
+                       budget);
+    HIP_OK(hipGetLastError());
+    uint64_t ovf = 0;
+    HIP_OK(hipMemcpyAsync(&ovf, e->S.counters + 5, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (!ovf) break;
+    // more new IPs than the table had room for: undo, grow, claim again
+    hipLaunchKernelGGL(k_ip_rollback, dim3(grid_for(e->ip_cap)), dim3(kBlock), 0, st, e->ip_cap, e->S, epoch);
+    HIP_OK(hipGetLastError());
+    if (!forced) grow_ip(e, attempt >= 2 ? n_ips + n_el : std::min<uint64_t>(n_ips + n_el, 4 * (e->ip_cap * 3 / 4)));
+  }
   hipLaunchKernelGGL(k_ip_commit, dim3(grid_for(E.n)), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p,
                      e->coll.p);
   HIP_OK(hipGetLastError());
@@ -2734,9 +2808,30 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
     hipLaunchKernelGGL(k_ip_collide, dim3(1), dim3(64), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p, e->coll.p, n_coll);
     HIP_OK(hipGetLastError());
   }
-  hipLaunchKernelGGL(k_st_claim, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, E, n_ev, ev_el, ev_rule, e->el_slot.p,
-                     e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_rec.p);
-  HIP_OK(hipGetLastError());
+  for (int attempt = 0;; ++attempt) {
+    read_counters(e);
+    const uint64_t n_st = e->host_counters[2];
+    HIP_OK(hipMemsetAsync(e->S.counters + 6, 0, 2 * 8, st));
+    uint64_t budget = e->st_cap * 3 / 4 - n_st;
+    const bool forced = e->dbg_budget && attempt == 0 && e->dbg_budget < budget;  // test hook
+    if (forced) budget = e->dbg_budget;
+    hipLaunchKernelGGL(k_st_claim, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, E, n_ev, ev_el, ev_rule, e->el_slot.p,
+                       e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_rec.p, budget);
+    HIP_OK(hipGetLastError());
+    uint64_t ovf = 0;
+    HIP_OK(hipMemcpyAsync(&ovf, e->S.counters + 7, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (!ovf) break;
+    // more new (ip, rule name) states than the table had room for: undo this
+    // batch's claims, recount, grow, claim again
+    HIP_OK(hipMemsetAsync(e->S.counters + 2, 0, 8, st));
+    hipLaunchKernelGGL(k_st_rollback, dim3(grid_for(e->st_cap)), dim3(kBlock), 0, st, e->st_cap, e->S);
+    HIP_OK(hipGetLastError());
+    read_counters(e);
+    if (!forced)
+      grow_st(e, attempt >= 2 ? e->host_counters[2] + n_ev
+                              : std::min<uint64_t>(e->host_counters[2] + n_ev, 4 * (e->st_cap * 3 / 4)));
+  }
   mark(e, 6);
   {
     uint32_t *ki = e->ev_st.p, *ko = e->ev_st2.p;
@@ -3369,6 +3464,12 @@ extern "C" int bjx_debug_set_ip_hash_mask(bjx_engine *e, uint64_t mask) {
   if (!e) return BJX_ERR_ARG;
   std::lock_guard<std::mutex> g(e->mu);
   e->dbg_hash_mask = mask;
+  return BJX_OK;
+}
+extern "C" int bjx_debug_set_claim_budget(bjx_engine *e, uint64_t max_new) {
+  if (!e) return BJX_ERR_ARG;
+  std::lock_guard<std::mutex> g(e->mu);
+  e->dbg_budget = max_new;
   return BJX_OK;
 }
 extern "C" size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap) {

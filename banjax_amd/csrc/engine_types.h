@@ -170,7 +170,8 @@ struct State {
   uint32_t *ip_len;
   uint8_t *arena;
   StSlot *st;
-  uint64_t *counters;  // [0] ips, [1] arena bytes, [2] states, [3] hash-collision lines (per batch)
+  uint64_t *counters;  // [0] ips, [1] arena bytes, [2] states; per batch: [3] hash-collision lines,
+                       // [4]/[5] IP slots claimed / over budget, [6]/[7] state slots claimed / over budget
   uint64_t ip_mask;
   uint64_t st_mask;
   uint64_t arena_cap;

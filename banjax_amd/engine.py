@@ -160,6 +160,10 @@ class Engine:
         """Test hook: IP hashes become (hash & mask) | 1 (0 = off)."""
         self._check(_lib.lib().bjx_debug_set_ip_hash_mask(self._h, mask), "debug_set_ip_hash_mask")
 
+    def debug_set_claim_budget(self, max_new: int):
+        """Test hook: cap the first claim launch per table and batch (0 = off)."""
+        self._check(_lib.lib().bjx_debug_set_claim_budget(self._h, max_new), "debug_set_claim_budget")
+
     def state_clear(self):
         self._check(_lib.lib().bjx_state_clear(self._h), "state_clear")
 

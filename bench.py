@@ -118,7 +118,7 @@ def main():
     torch.cuda.synchronize()
     cfg = Config.from_yaml(w.rules_yaml)
     rs = Ruleset(cfg)
-    eng = Engine(local, ip_capacity=1 << 22, state_capacity=1 << 26, ip_arena_bytes=256 << 20)
+    eng = Engine(local, ip_arena_bytes=256 << 20)  # IP / state tables size themselves to the stream
     eng.set_decision_lists(cfg.decision_entries)
     now = w.now_ns(first, n_lines)
 

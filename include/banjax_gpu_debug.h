@@ -28,6 +28,9 @@ size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap);
 /* Test hook: IP hashes become (hash & mask) | 1 (0 = off), so distinct IPs
    share 64-bit hashes and the exact collision path of the IP table runs. */
 int bjx_debug_set_ip_hash_mask(bjx_engine *e, uint64_t mask);
+/* Test hook: the first claim launch of each table in a batch may add at most
+   max_new entries (0 = off), forcing the roll-back / re-claim path. */
+int bjx_debug_set_claim_budget(bjx_engine *e, uint64_t max_new);
 #ifdef __cplusplus
 }
 #endif

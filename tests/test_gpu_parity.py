@@ -484,3 +484,25 @@ def test_sharded_engines_match_single_process(wl, world):
             assert [h for h in have if h is not None] == ([exp] if exp is not None else [])
     for e in engines:
         e.close()
+
+
+@pytest.mark.parametrize("budget", [1, 97, 5000])
+def test_table_overflow_rollback(engine, budget):
+    """The IP and state tables claim at most `budget` new entries in a batch's
+    first claim launch (test hook): every batch overflows, rolls its claims
+    back and claims again - results stay bit-exact across batches."""
+    w = W.scaled(W.CFG5, 24_000, n_ips=8_000)
+    engine.debug_set_claim_budget(budget)
+    try:
+        pair = Pair(w.rules_yaml, engine)
+        ips = set()
+        for b in range(3):
+            data = w.host_lines(b * 8_000, 8_000)
+            for ln in data.split(b"\n")[:200]:
+                parts = ln.split(b" ")
+                if len(parts) > 2:
+                    ips.add(parts[1].decode())
+            pair.feed(data, w.now_ns(b * 8_000, 8_000))
+        pair.compare_state(sorted(ips)[:60])
+    finally:
+        engine.debug_set_claim_budget(0)
