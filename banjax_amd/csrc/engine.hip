@@ -481,6 +481,21 @@ __device__ __forceinline__ Tabs make_tabs(const uint8_t *base, const ImgLayout &
 }
 
 // host id from the open-addressing host table
+// host id from the inline host slots (per-line pass): one 64 B probe per step
+__device__ __forceinline__ int32_t host_lookup_slots(const Bind &B, const uint8_t *h, uint32_t n) {
+  if (B.n_hd == 0) return -1;
+  const uint64_t hh = hash_bytes(h, n);
+  const uint32_t tag = (uint32_t)(hh >> 32) | 1u;
+  uint32_t s = (uint32_t)hh & (B.ht_cap - 1);
+  for (;;) {
+    const HostSlot *e = B.hslot + s;
+    const uint32_t t = e->tag;
+    if (t == 0) return -1;
+    if (t == tag && e->len == n && bytes_eq(n <= 48 ? e->inl : B.hd_bytes + e->off, h, n)) return e->id;
+    s = (s + 1) & (B.ht_cap - 1);
+  }
+}
+
 __device__ __forceinline__ int32_t host_lookup_ht(const Bind &B, const Tabs &T, const uint8_t *h, uint32_t n) {
   if (B.n_hd == 0) return -1;
   const uint64_t hh = hash_bytes(h, n);
@@ -957,6 +972,7 @@ struct LinesArgs {
   uint32_t *jline, *jkey;
   unsigned long long *job_count;
   uint64_t job_cap;
+  uint32_t span_bytes;  // LDS staging per wave (0 = read lines from HBM)
 };
 
 // consumeLine up to the rule loop for line j (bytes at base + (s - origin)):
@@ -964,9 +980,12 @@ struct LinesArgs {
 // OldLine, then the rule decisions from the scan pass's literal hits.
 // STAGED: base is the wave's LDS span (a distinct instantiation, so the
 // compiler cannot merge the two call sites into one generic-pointer copy)
+// cc / cv: the line's scan-pass hit count and hit slots, loaded by the caller
+// ahead of the staging barrier
 template <bool STAGED>
 __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const LinesArgs &A, const uint8_t *base,
-                                          uint64_t origin, uint64_t s, uint32_t n, uint64_t j, const JobSink &S) {
+                                          uint64_t origin, uint64_t s, uint32_t n, uint64_t j, const JobSink &S,
+                                          uint32_t cc, const uint64_t (&cv)[kCandSlots]) {
   const Lines &L = A.L;
   const uint8_t *p = base + (s - origin);
   uint32_t sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
@@ -977,7 +996,7 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
     L.flags[j] = kLineError;
     L.counts[j] = 0;
   } else if (parse_float_fast(p, sp0, &f) != 0 ||
-             (hid = (A.dbg & 8) ? -1 : host_lookup_ht(B, TB, p + sp2 + 1, sp3 - sp2 - 1),
+             (hid = (A.dbg & 8) ? -1 : host_lookup_slots(B, p + sp2 + 1, sp3 - sp2 - 1),
               (hid >= 0 ? B.site_off[hid + 1] - B.site_off[hid] : 0u) + B.n_global > 128)) {
     // exotic timestamp token or > 128 applicable rules: the per-line fallback
     L.flags[j] = kLineSlowTs;
@@ -1002,12 +1021,13 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
       L.counts[j] = 0;
     } else {
       // literal hits of the scan pass inside rest (unverified ones checked here)
-      const uint32_t cc = B.any_prefilter ? L.cand_cnt[j] : 0u;
       uint64_t lits = 0;
       uint32_t nlit = 0;
       const uint64_t rs = s + rest_off;
-      for (uint32_t c = 0; c < cc && c < (uint32_t)kCandSlots; ++c) {
-        const uint64_t v = L.cand[j * kCandSlots + c];
+#pragma unroll
+      for (uint32_t c = 0; c < (uint32_t)kCandSlots; ++c) {
+        if (c >= cc) break;
+        const uint64_t v = cv[c];
         const uint32_t lit = (uint32_t)(v & 0x7FFFFF);
         const uint64_t q = v >> 24;
         if (q < rs) continue;
@@ -1048,7 +1068,7 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
   // this wave's 64 lines, staged whole in LDS with coalesced 16 B loads when
   // they span at most kSpanBytes (otherwise read from HBM per lane)
   uint8_t *span = s_dyn + ((IMG_LDS ? B.img_bytes : 0) + 15u & ~15u) + (kBlock / 64) * (kWaveJobs * 8 + 16) +
-                  wave * (kSpanBytes + 32);
+                  wave * (A.span_bytes + 32);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + wave * 64u; base < A.n_lines; base += stride) {
     const uint64_t j = base + lane;
@@ -1056,7 +1076,23 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
     const uint64_t s0 = base ? A.nl[base - 1] + 1 : 0;
     const uint64_t s1 = A.nl[jl];
     const uint64_t b16 = s0 & ~15ull;
-    const bool staged = s1 + 16 - b16 <= kSpanBytes && !(A.dbg & 4);  // 16 B of slack for word-wise over-reads
+    const bool staged = s1 + 16 - b16 <= A.span_bytes && !(A.dbg & 4);  // 16 B of slack for word-wise over-reads
+    // per-line loads that do not depend on the staged bytes go out first
+    uint64_t s = 0, cv[kCandSlots];
+    uint32_t n = 0, cc = 0;
+    if (j < A.n_lines) {
+      s = j ? A.nl[j - 1] + 1 : 0;
+      n = (uint32_t)(A.nl[j] - s);
+      if (B.any_prefilter) {
+        cc = L.cand_cnt[j];
+        const ulonglong2 *cp = reinterpret_cast<const ulonglong2 *>(L.cand + j * kCandSlots);
+#pragma unroll
+        for (int k = 0; k < kCandSlots / 2; ++k) {
+          const ulonglong2 w = cp[k];
+          cv[2 * k] = w.x; cv[2 * k + 1] = w.y;
+        }
+      }
+    }
     if (staged) {
       const uint32_t n16 = (uint32_t)((s1 + 16 - b16 + 15) >> 4);
       for (uint32_t i = lane; i < n16; i += 64) {
@@ -1082,11 +1118,9 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
       wave_sync();
     }
     if (j < A.n_lines) {
-      const uint64_t s = j ? A.nl[j - 1] + 1 : 0;
-      const uint32_t n = (uint32_t)(A.nl[j] - s);
       // two inlined copies: LDS addressing for staged waves, global otherwise
-      if (staged) line_body<true>(B, TB, A, span, b16, s, n, j, S);
-      else line_body<false>(B, TB, A, A.buf, 0, s, n, j, S);
+      if (staged) line_body<true>(B, TB, A, span, b16, s, n, j, S, cc, cv);
+      else line_body<false>(B, TB, A, A.buf, 0, s, n, j, S, cc, cv);
     }
     // ---- append this wave's DFA jobs (one global atomic per 64 lines)
     wave_sync();
@@ -2307,6 +2341,18 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     ht[2 * slot] = (uint32_t)(hd[i].first >> 32) | 1u;
     ht[2 * slot + 1] = i;
   }
+  std::vector<HostSlot> hslot(ht_cap);
+  memset(hslot.data(), 0, hslot.size() * sizeof(HostSlot));
+  for (uint32_t i = 0; i < hd.size(); ++i) {
+    uint32_t slot = (uint32_t)hd[i].first & (ht_cap - 1);
+    while (hslot[slot].tag) slot = (slot + 1) & (ht_cap - 1);
+    HostSlot &hs = hslot[slot];
+    hs.tag = (uint32_t)(hd[i].first >> 32) | 1u;
+    hs.id = (int32_t)hd[i].second;
+    hs.len = hd_len[i];
+    hs.off = hd_off[i];
+    memcpy(hs.inl, hd_bytes.data() + hd_off[i], std::min<uint32_t>(hd_len[i], 48));
+  }
   std::vector<int32_t> host_scope(n_hosts, -1);
   for (auto &s : scope_of_site) host_scope[hosts[s.first]] = s.second;
   std::vector<uint64_t> skip;
@@ -2478,7 +2524,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
          o_rl = bb.add(rule_lits), o_img = bb.add(img), o_lro = bb.add(lr_off), o_lrg = bb.add(lr_gend),
          o_lre = bb.add(lr_ent), o_lrh = bb.add(lr_host), o_sca = bb.add(sc_always), o_scs = bb.add(sc_skipm),
          o_dso = bb.add(dfa_site_off), o_ds = bb.add(dfa_site), o_dg = bb.add(dfa_glob), o_pso = bb.add(pref_site_off),
-         o_ps = bb.add(pref_site), o_pg = bb.add(pref_glob);
+         o_ps = bb.add(pref_site), o_pg = bb.add(pref_glob), o_hslot = bb.add(hslot);
   e->bind_blob.ensure(bb.bytes.size());
   HIP_OK(hipMemcpy(e->bind_blob.p, bb.bytes.data(), bb.bytes.size(), hipMemcpyHostToDevice));
   uint8_t *base = e->bind_blob.p;
@@ -2497,6 +2543,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.hd_off = reinterpret_cast<const uint32_t *>(base + o_hdoff);
   B.hd_len = reinterpret_cast<const uint32_t *>(base + o_hdlen);
   B.hd_bytes = base + o_hdb;
+  B.hslot = reinterpret_cast<const HostSlot *>(base + o_hslot);
   B.host_scope = reinterpret_cast<const int32_t *>(base + o_hsc);
   B.skip_keys = reinterpret_cast<const uint64_t *>(base + o_skip);
   B.sc_addr_off = reinterpret_cast<const uint32_t *>(base + o_sao);
@@ -2972,7 +3019,9 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     A.slow_list = e->slow_list.p; A.slow_count = e->scalars.p;
     A.jline = e->jline.p; A.jkey = e->jkey.p; A.job_count = e->scalars.p + 11; A.job_cap = std::min(e->jline.n, e->jkey.n);
     const bool img_lds = B.img_bytes <= kLinesImgMax;
-    const uint32_t lds = ((img_lds ? B.img_bytes : 0) + 15u & ~15u) + (kBlock / 64) * (kWaveJobs * 8 + 16 + kSpanBytes + 32);
+    A.span_bytes = getenv("BJX_SPAN_BYTES") ? (uint32_t)atoi(getenv("BJX_SPAN_BYTES")) & ~15u : kSpanBytes;
+    const uint32_t lds = ((img_lds ? B.img_bytes : 0) + 15u & ~15u) +
+                         (kBlock / 64) * (kWaveJobs * 8 + 16 + (A.span_bytes ? A.span_bytes + 32 : 0));
     if (!e->lines_attr) {
       HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_lines<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)kScanLdsMax));

@@ -50,6 +50,16 @@ struct ImgLayout {
   uint32_t gt, ge, ht, hrec, hid, hbytes, lrec, lbytes, lcim, lchk;
 };
 
+// Host dictionary slot for the per-line pass: one probe reads one 64 B line
+// (tag, id and the host bytes inline; longer hosts compare in hd_bytes).
+struct HostSlot {
+  uint32_t tag;   // (hash >> 32) | 1; 0 = empty
+  int32_t id;     // host id
+  uint32_t len;
+  uint32_t off;   // bytes in hd_bytes (hosts longer than 48 B)
+  uint8_t inl[48];
+};
+
 // Everything the per-line kernels need about the current (ruleset, decision
 // lists) pair.  All pointers are device pointers into one blob.
 struct Bind {
@@ -67,6 +77,7 @@ struct Bind {
   const uint32_t *hd_off;
   const uint32_t *hd_len;
   const uint8_t *hd_bytes;
+  const HostSlot *hslot;       // open addressing over the host dictionary, ht_cap slots
   const int32_t *host_scope;   // host id -> allow scope (or -1)
   const uint64_t *skip_keys;   // sorted (rule << 32 | host id)
   const uint32_t *sc_addr_off; // scopes + 1
