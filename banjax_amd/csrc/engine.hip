@@ -1306,7 +1306,8 @@ __global__ __launch_bounds__(kBlock) void k_emit(Bind B, uint64_t n_lines, Lines
 //                 hash collision inside the batch -> k_ip_collide, serial)
 //   k_st_claim    one lane per event: (ip id, rule name) -> state slot, seenIp
 //   radix sort by state slot (stable: reference order inside a slot)
-//   k_apply       one lane per state slot run: the fixed-window automaton
+//   k_apply       one lane per state slot run (runs staged in LDS per block
+//                 of sorted records): the fixed-window automaton
 
 __device__ __forceinline__ uint64_t line_start(const uint64_t *nl, uint64_t line) { return line ? nl[line - 1] + 1 : 0; }
 
@@ -1320,33 +1321,55 @@ __device__ __forceinline__ bool ev_has(const EvSrc &E, uint64_t i) {
 constexpr uint32_t kNewIp = 0xFFFFFFFFu;   // el_id: IP created in this batch, id not known to this line
 constexpr uint32_t kFirstIp = 0x80000000u; // el_id: this line is the first event line of a new IP
 
-// budget: new slots this launch may claim (keeps the table under its load
-// factor); past it the launch sets counters[5] and the host rolls back, grows
-// the table and claims again.
-__global__ __launch_bounds__(kBlock) void k_ip_claim(EvSrc E, State S, uint32_t epoch, uint32_t *__restrict__ el_slot,
-                                                     uint32_t *__restrict__ el_id, uint64_t budget) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= E.n || !ev_has(E, i)) return;
+// Claim budgets: a launch may add at most `budget` entries to a table (keeps
+// it under its load factor).  Claims are counted per shard of blocks
+// (blockIdx % kClaimShards, counters on lines of their own), each shard
+// holding budget / kClaimShards; past it the launch raises the overflow flag,
+// every lane still running leaves, and the host rolls the claims back, grows
+// the table and claims again.  One hot counter would serialise every claim.
+constexpr uint32_t kClaimShards = 64;  // = one wave in k_fold_claims
+constexpr uint32_t kShardBase = 16;    // counters[kShardBase + 16 * shard + {0: IP claims, 1: state claims}]
+constexpr size_t kCounterBytes = (kShardBase + 16 * kClaimShards) * 8;
+
+__device__ __forceinline__ unsigned long long *claim_shard(const State &S, uint32_t which) {
+  return (unsigned long long *)&S.counters[kShardBase + 16 * (blockIdx.x % kClaimShards) + which];
+}
+__device__ __forceinline__ bool flag_set(const State &S, uint32_t f) {
+  return __hip_atomic_load(&S.counters[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+__device__ __forceinline__ void raise_flag(const State &S, uint32_t f) {
+  if (!flag_set(S, f)) atomicOr((unsigned long long *)&S.counters[f], 1ull);
+}
+// adds this wave's successful claims to the block's shard; over the shard's
+// share -> overflow flag (all lanes of the wave call it)
+__device__ __forceinline__ void count_claims(const State &S, uint32_t which, uint32_t ovf_flag, bool claimed, uint64_t shard_budget) {
+  const uint64_t won = __ballot(claimed);
+  if (won && (threadIdx.x & 63) == (uint32_t)(__ffsll((unsigned long long)won) - 1))
+    if (atomicAdd(claim_shard(S, which), (unsigned long long)__popcll(won)) + __popcll(won) > shard_budget)
+      raise_flag(S, ovf_flag);
+}
+
+// one event line -> its IP slot; true if this lane claimed a new slot
+__device__ __forceinline__ bool ip_claim_line(const EvSrc &E, const State &S, uint32_t epoch, uint64_t i,
+                                              uint32_t *__restrict__ el_slot, uint32_t *__restrict__ el_id,
+                                              uint64_t shard_budget) {
   const uint64_t h = E.ip_hash[i];
   const uint32_t len = E.ip_len[i];
   const uint8_t *ip = ev_ip(E, i);
   const bool inl = len <= 15;
   const uint4 k16 = !inl ? make_uint4(0, 0, 0, 0) : E.ip16 ? E.ip16[i] : ip_key16_bytes(ip, len);
   uint64_t s = h & S.ip_mask;
+  bool claimed = false;
   for (;;) {
     uint64_t cur = S.ip[s].hash;
     if (cur == 0) {
-      // claims counted as they succeed; once the budget is spent nobody claims
-      // (overshoot <= lanes in flight, far below the table's free quarter)
-      if (__hip_atomic_load(&S.counters[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= budget) {
-        atomicOr((unsigned long long *)&S.counters[5], 1ull);
-        return;
+      if (flag_set(S, 5)) return false;  // this launch is rolled back anyway
+      if (__hip_atomic_load(claim_shard(S, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= shard_budget) {
+        raise_flag(S, 5);
+        return false;
       }
       cur = atomicCAS((unsigned long long *)&S.ip[s].hash, 0ull, (unsigned long long)h);
-      if (cur == 0) {
-        cur = h;
-        if (atomicAdd((unsigned long long *)&S.counters[4], 1ull) >= budget) atomicOr((unsigned long long *)&S.counters[5], 1ull);
-      }
+      if (cur == 0) { cur = h; claimed = true; }
     }
     if (cur == h) {
       uint32_t b = S.ip[s].born;
@@ -1355,38 +1378,69 @@ __global__ __launch_bounds__(kBlock) void k_ip_claim(EvSrc E, State S, uint32_t 
         atomicMin(&S.ip_first[s], (uint32_t)i);
         el_slot[i] = (uint32_t)s;
         el_id[i] = kNewIp;
-        return;
+        return claimed;
       }
       // created by an earlier batch: short IPs compare inline, long ones in the arena
       const uint32_t id = S.ip[s].id;
       if (inl ? key16_eq(S.ip[s].key16, k16) : (S.ip_len[id] == len && bytes_eq(S.arena + S.ip_off[id], ip, len))) {
         el_slot[i] = (uint32_t)s;
         el_id[i] = id;
-        return;
+        return claimed;
       }
     }
     s = (s + 1) & S.ip_mask;
   }
 }
 
+__global__ __launch_bounds__(kBlock) void k_ip_claim(EvSrc E, State S, uint32_t epoch, uint32_t *__restrict__ el_slot,
+                                                     uint32_t *__restrict__ el_id, uint64_t shard_budget) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool claimed = false;
+  if (i < E.n && ev_has(E, i) && !flag_set(S, 5)) claimed = ip_claim_line(E, S, epoch, i, el_slot, el_id, shard_budget);
+  count_claims(S, 0, 5, claimed, shard_budget);
+}
+
+// exclusive prefix of v over the wave and one atomicAdd of the wave's total
+// on ctr; returns ctr's old value + the prefix (every lane of the wave calls it)
+__device__ __forceinline__ uint64_t wave_alloc(unsigned long long *ctr, uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  unsigned long long base = 0;
+  if (lane == 63 && x) base = atomicAdd(ctr, (unsigned long long)x);
+  base = __shfl(base, 63);
+  return base + (x - v);
+}
+
 __global__ __launch_bounds__(kBlock) void k_ip_commit(EvSrc E, State S, uint32_t epoch, const uint32_t *__restrict__ el_slot,
                                                       uint32_t *__restrict__ el_id, uint32_t *__restrict__ coll) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= E.n || !ev_has(E, i) || el_id[i] != kNewIp) return;  // IPs of earlier batches: settled by k_ip_claim
-  const uint32_t s = el_slot[i];
-  const uint32_t f = S.ip_first[s];
-  const uint32_t len = E.ip_len[i];
-  const uint8_t *ip = ev_ip(E, i);
-  if (f == (uint32_t)i) {
-    const uint32_t id = (uint32_t)atomicAdd((unsigned long long *)&S.counters[0], 1ull);
-    const uint64_t off = atomicAdd((unsigned long long *)&S.counters[1], (unsigned long long)len);
+  // IPs of earlier batches were settled by k_ip_claim
+  const bool act = i < E.n && ev_has(E, i) && el_id[i] == kNewIp;
+  uint32_t s = 0, f = 0, len = 0;
+  const uint8_t *ip = nullptr;
+  if (act) {
+    s = el_slot[i];
+    f = S.ip_first[s];
+    len = E.ip_len[i];
+    ip = ev_ip(E, i);
+  }
+  const bool first = act && f == (uint32_t)i;
+  // ids and arena bytes: one atomic per wave
+  const uint32_t id = (uint32_t)wave_alloc((unsigned long long *)&S.counters[0], first ? 1u : 0u);
+  const uint64_t off = wave_alloc((unsigned long long *)&S.counters[1], first ? len : 0u);
+  if (first) {
     for (uint32_t k = 0; k < len; ++k) S.arena[off + k] = ip[k];
     S.ip_off[id] = off;
     S.ip_len[id] = len;
     S.ip[s].id = id;
     S.ip[s].key16 = E.ip16 ? E.ip16[i] : ip_key16_bytes(ip, len);
     el_id[i] = id | kFirstIp;
-  } else if (E.ip_len[f] != len || !bytes_eq(ev_ip(E, f), ip, len)) {
+  } else if (act && (E.ip_len[f] != len || !bytes_eq(ev_ip(E, f), ip, len))) {
     const uint64_t k = atomicAdd((unsigned long long *)&S.counters[3], 1ull);
     coll[k] = (uint32_t)i;
   }
@@ -1437,13 +1491,11 @@ __global__ void k_ip_collide(EvSrc E, State S, uint32_t epoch, uint32_t *__restr
 
 // event k -> state slot and its sort record.  seenIp is false only for the
 // first event of an IP created in this batch.
-__global__ __launch_bounds__(kBlock) void k_st_claim(EvSrc E, uint64_t n_ev, const uint32_t *__restrict__ ev_el,
-                                                     const uint32_t *__restrict__ ev_rule, const uint32_t *__restrict__ el_slot,
-                                                     const uint32_t *__restrict__ el_id, const DevRule *__restrict__ rules,
-                                                     State S, uint32_t *__restrict__ ev_st, EvRec *__restrict__ ev_rec,
-                                                     uint64_t budget) {
-  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_ev) return;
+__device__ __forceinline__ bool st_claim_event(const EvSrc &E, uint64_t n_ev, uint64_t k, const uint32_t *__restrict__ ev_el,
+                                               const uint32_t *__restrict__ ev_rule, const uint32_t *__restrict__ el_slot,
+                                               const uint32_t *__restrict__ el_id, const DevRule *__restrict__ rules,
+                                               const State &S, uint32_t *__restrict__ ev_st, EvRec *__restrict__ ev_rec,
+                                               uint64_t shard_budget) {
   const uint32_t i = ev_el[k];
   const uint32_t r = ev_rule[k];
   uint32_t id = el_id[i];
@@ -1455,9 +1507,10 @@ __global__ __launch_bounds__(kBlock) void k_st_claim(EvSrc E, uint64_t n_ev, con
   for (;;) {
     uint64_t cur = S.st[q].key;
     if (cur == 0) {
-      if (__hip_atomic_load(&S.counters[6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= budget) {  // see k_ip_claim
-        atomicOr((unsigned long long *)&S.counters[7], 1ull);
-        break;
+      if (flag_set(S, 7)) return false;  // see k_ip_claim
+      if (__hip_atomic_load(claim_shard(S, 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= shard_budget) {
+        raise_flag(S, 7);
+        return false;
       }
       cur = atomicCAS((unsigned long long *)&S.st[q].key, 0ull, (unsigned long long)key);
       if (cur == 0) { claimed = true; break; }
@@ -1471,54 +1524,166 @@ __global__ __launch_bounds__(kBlock) void k_st_claim(EvSrc E, uint64_t n_ev, con
   rec.rule = r | (first ? 0x80000000u : 0u);
   rec.ev = (uint32_t)k;
   ev_rec[k] = rec;
-  // table load (counters[2]) and this launch's claims (counters[6], budget): one atomic pair per wave
-  const uint64_t won = __ballot(claimed);
-  if (won && (threadIdx.x & 63) == (uint32_t)(__ffsll((unsigned long long)won) - 1)) {
-    atomicAdd((unsigned long long *)&S.counters[2], (unsigned long long)__popcll(won));
-    if (atomicAdd((unsigned long long *)&S.counters[6], (unsigned long long)__popcll(won)) + __popcll(won) > budget)
-      atomicOr((unsigned long long *)&S.counters[7], 1ull);
-  }
+  return claimed;
 }
 
-// run heads of the slot-sorted events
-__global__ __launch_bounds__(kBlock) void k_run_heads(uint64_t n_ev, const uint32_t *__restrict__ key, uint8_t *__restrict__ f) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < n_ev) f[t] = (t == 0 || key[t] != key[t - 1]) ? 1 : 0;
+__global__ __launch_bounds__(kBlock) void k_st_claim(EvSrc E, uint64_t n_ev, const uint32_t *__restrict__ ev_el,
+                                                     const uint32_t *__restrict__ ev_rule, const uint32_t *__restrict__ el_slot,
+                                                     const uint32_t *__restrict__ el_id, const DevRule *__restrict__ rules,
+                                                     State S, uint32_t *__restrict__ ev_st, EvRec *__restrict__ ev_rec,
+                                                     uint64_t shard_budget) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool claimed = false;
+  if (k < n_ev && !flag_set(S, 7)) claimed = st_claim_event(E, n_ev, k, ev_el, ev_rule, el_slot, el_id, rules, S, ev_st, ev_rec,
+                                                            shard_budget);
+  count_claims(S, 1, 7, claimed, shard_budget);
+}
+
+// state slots claimed by the last k_st_claim -> table load counters[2]; shards cleared
+__global__ void k_fold_claims(State S) {
+  const uint32_t t = threadIdx.x;  // one wave: lane = shard
+  unsigned long long v = S.counters[kShardBase + 16 * t + 1];
+  S.counters[kShardBase + 16 * t] = 0;
+  S.counters[kShardBase + 16 * t + 1] = 0;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+  if (t == 0) S.counters[2] += v;
 }
 
 // The fixed-window automaton of one (ip, rule name) state over its events in
-// reference order (records sorted by slot, stable).  One lane per run,
-// grid-stride over the run heads.  out_sorted[u] = outcome of record u in
-// sorted order (sequential stores): bit0 seenIp, bits1-2 MatchType, bit3
-// Exceeded, bit7 valid.
-__global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const unsigned long long *__restrict__ n_runs_p,
-                                                  const uint32_t *__restrict__ heads, const uint32_t *__restrict__ key,
-                                                  const EvRec *__restrict__ rec, const DevRule *__restrict__ rules,
-                                                  StSlot *__restrict__ st, uint8_t *__restrict__ out_sorted) {
-  const uint64_t n_runs = *n_runs_p;
-  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n_runs; h += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t b = heads[h], e = h + 1 < n_runs ? heads[h + 1] : n_ev;
-    const uint32_t q = key[b];
+// reference order (records sorted by slot, stable).  A block takes kApplyChunk
+// consecutive sorted records, loaded coalesced into LDS with their slots; each
+// run that STARTS in the chunk goes to one lane (long runs to the first lanes,
+// so short-run waves finish early), which walks it from LDS.  The
+// one run that continues past the chunk end is finished by lane 0 over
+// coalesced 256-record windows staged by the whole block.  Records before the
+// chunk's first run head belong to the previous block's run.  out_sorted[u] = outcome of record u in
+// sorted order: bit0 seenIp, bits1-2 MatchType, bit3 Exceeded, bit7 valid.
+constexpr uint32_t kApplyChunk = 2048;
+
+__device__ __forceinline__ uint8_t apply_step(const EvRec &v, const DevRule *__restrict__ rules, uint32_t &pr, int64_t &interval,
+                                              int64_t &limit, bool &valid, int64_t &hits, int64_t &start) {
+  const uint32_t r = v.rule & 0x7FFFFFFFu;
+  const bool seen = (v.rule >> 31) == 0;
+  if (r != pr) { pr = r; interval = rules[r].interval_ns; limit = rules[r].hits; }  // rules sharing a name share the state
+  uint8_t mt;
+  if (!valid) { hits = 1; start = v.ts; mt = BJX_FIRST_TIME; valid = true; }
+  else if (go_sub(v.ts, start) > interval) { mt = BJX_OUTSIDE_INTERVAL; hits = 1; start = v.ts; }
+  else { mt = BJX_INSIDE_INTERVAL; ++hits; }
+  const bool ex = hits > limit;
+  if (ex) hits = 0;
+  return (uint8_t)(0x80 | (seen ? 1 : 0) | (mt << 1) | (ex ? 8 : 0));
+}
+
+__global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const uint32_t *__restrict__ key, const EvRec *__restrict__ rec,
+                                                  const DevRule *__restrict__ rules, StSlot *__restrict__ st,
+                                                  uint8_t *__restrict__ out_sorted) {
+  constexpr uint32_t kPer = kApplyChunk / kBlock;  // positions per thread for the head scan
+  constexpr uint32_t kLongRun = 8;                 // runs at least this long go to the first lanes
+  __shared__ EvRec s_rec[kApplyChunk];
+  __shared__ uint32_t s_key[kApplyChunk + 1];  // s_key[i + 1] = slot of record i; s_key[0] = slot before the chunk
+  __shared__ uint8_t s_out[kApplyChunk];
+  __shared__ uint16_t s_head[kApplyChunk];  // run heads in position order
+  __shared__ uint16_t s_ord[kApplyChunk];   // run indices: long runs from the front, short ones from the back
+  __shared__ uint32_t s_wsum[kBlock / 64], s_front, s_back, s_cont, s_cross, s_cq;
+  __shared__ int64_t s_chits, s_cstart;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t u0 = (uint64_t)blockIdx.x * kApplyChunk;
+  const uint32_t n = (uint32_t)min<uint64_t>(kApplyChunk, n_ev - u0);
+  for (uint32_t i = tid; i < n; i += kBlock) {
+    s_rec[i] = rec[u0 + i];
+    s_key[i + 1] = key[u0 + i];
+  }
+  if (tid == 0) {
+    s_key[0] = u0 ? key[u0 - 1] : 0xFFFFFFFFu;
+    s_cont = u0 + n < n_ev && key[u0 + n] == key[u0 + n - 1];  // the last run goes on past the chunk
+    s_front = 0;
+    s_back = 0;
+    s_cross = 0;
+  }
+  __syncthreads();
+  // run heads, compacted in position order (block scan of per-thread counts)
+  uint32_t fl = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t i = tid * kPer + k;
+    if (i < n && s_key[i + 1] != s_key[i]) fl |= 1u << k;
+  }
+  const uint32_t cnt = __popc(fl);
+  uint32_t x = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) s_wsum[wave] = x;
+  __syncthreads();
+  uint32_t base = x - cnt, nh = 0;
+  for (uint32_t w = 0; w < kBlock / 64; ++w) {
+    if (w < wave) base += s_wsum[w];
+    nh += s_wsum[w];
+  }
+  for (uint32_t k = 0; fl; ++k, fl >>= 1)
+    if (fl & 1) s_head[base++] = (uint16_t)(tid * kPer + k);
+  __syncthreads();
+  // lanes take runs longest-first (roughly): a wave lasts as long as its longest run
+  for (uint32_t h = tid; h < nh; h += kBlock) {
+    const uint32_t len = (h + 1 < nh ? s_head[h + 1] : n) - s_head[h];
+    if (len >= kLongRun || (h + 1 == nh && s_cont)) s_ord[atomicAdd(&s_front, 1u)] = (uint16_t)h;
+    else s_ord[nh - 1 - atomicAdd(&s_back, 1u)] = (uint16_t)h;
+  }
+  __syncthreads();
+  for (uint32_t k = tid; k < nh; k += kBlock) {
+    const uint32_t h = s_ord[k];
+    const uint32_t b = s_head[h], e = h + 1 < nh ? s_head[h + 1] : n;
+    const uint32_t q = s_key[b + 1];
     const StSlot cur = st[q];
     bool valid = cur.valid != 0;
-    int64_t hits = cur.hits, start = cur.start;
-    for (uint64_t u = b; u < e; ++u) {
-      const EvRec v = rec[u];
-      const uint32_t r = v.rule & 0x7FFFFFFFu;
-      const bool seen = (v.rule >> 31) == 0;
-      const int64_t interval = rules[r].interval_ns, limit = rules[r].hits;
-      uint8_t mt;
-      if (!valid) { hits = 1; start = v.ts; mt = BJX_FIRST_TIME; valid = true; }
-      else if (go_sub(v.ts, start) > interval) { mt = BJX_OUTSIDE_INTERVAL; hits = 1; start = v.ts; }
-      else { mt = BJX_INSIDE_INTERVAL; ++hits; }
-      const bool ex = hits > limit;
-      if (ex) hits = 0;
-      out_sorted[u] = (uint8_t)(0x80 | (seen ? 1 : 0) | (mt << 1) | (ex ? 8 : 0));
+    int64_t hits = cur.hits, start = cur.start, interval = 0, limit = 0;
+    uint32_t pr = 0xFFFFFFFFu;
+    EvRec v = s_rec[b];
+    for (uint32_t u = b; u < e; ++u) {
+      EvRec nx;
+      if (u + 1 < e) nx = s_rec[u + 1];  // next record in flight while this one is applied
+      s_out[u] = apply_step(v, rules, pr, interval, limit, valid, hits, start);
+      v = nx;
+    }
+    if (h + 1 == nh && s_cont) {  // continues past the chunk: handed to lane 0 below
+      s_cross = 1; s_cq = q; s_chits = hits; s_cstart = start;
+      continue;
     }
     st[q].hits = hits;
     st[q].start = start;
     st[q].valid = 1;
   }
+  __syncthreads();
+  if (s_cross) {
+    // lane 0 walks the tail over windows of kBlock records (s_rec / s_key reused)
+    const uint32_t q = s_cq;
+    int64_t hits = s_chits, start = s_cstart, interval = 0, limit = 0;
+    bool valid = true;
+    uint32_t pr = 0xFFFFFFFFu;
+    for (uint64_t g = u0 + n;; g += kBlock) {
+      __syncthreads();
+      if (g + tid < n_ev) { s_rec[tid] = rec[g + tid]; s_key[tid] = key[g + tid]; }
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t j = 0;
+        for (; j < kBlock && g + j < n_ev && s_key[j] == q; ++j)
+          out_sorted[g + j] = apply_step(s_rec[j], rules, pr, interval, limit, valid, hits, start);
+        if (j < kBlock || g + j >= n_ev) {
+          st[q].hits = hits;
+          st[q].start = start;
+          st[q].valid = 1;
+          s_cross = 0;
+        }
+      }
+      __syncthreads();
+      if (!s_cross) break;
+    }
+  }
+  // records before the first head belong to the previous block's run
+  for (uint32_t i = (nh ? s_head[0] : n) + tid; i < n; i += kBlock) out_sorted[u0 + i] = s_out[i];
 }
 
 __global__ void k_dbg_mask_hash(uint64_t n, uint64_t *__restrict__ h, uint64_t mask) {
@@ -2003,8 +2168,7 @@ struct bjx_engine {
   DevBuf<uint64_t> res_seq;
   DevBuf<uint32_t> res_rule, ev_el, ev_rule, ev_res, ev_st, ev_st2, ev_idx, ev_idx2, el_slot, coll, trip_idx;
   DevBuf<EvRec> ev_rec, ev_rec2;
-  DevBuf<uint32_t> el_id, run_heads;
-  DevBuf<uint8_t> run_flag;
+  DevBuf<uint32_t> el_id;
   DevBuf<uint8_t> rl_out, ev_out, ev_out_s, trip_flag;
   DevBuf<uint32_t> trip_ev, trip_ev2;
   DevBuf<bjx_trip> d_trips;
@@ -2602,11 +2766,11 @@ void alloc_state(bjx_engine *e, uint64_t ip_cap, uint64_t st_cap, uint64_t arena
   HIP_OK(hipMalloc(&S.ip_len, ip_cap * 4));
   HIP_OK(hipMalloc(&S.arena, arena_cap));
   HIP_OK(hipMalloc(&S.st, st_cap * sizeof(StSlot)));
-  HIP_OK(hipMalloc(&S.counters, 64));
+  HIP_OK(hipMalloc(&S.counters, kCounterBytes));
   HIP_OK(hipMemset(S.ip, 0, ip_cap * sizeof(IpSlot)));
   HIP_OK(hipMemset(S.ip_first, 0xFF, ip_cap * 4));
   HIP_OK(hipMemset(S.st, 0, st_cap * sizeof(StSlot)));
-  HIP_OK(hipMemset(S.counters, 0, 64));
+  HIP_OK(hipMemset(S.counters, 0, kCounterBytes));
   S.ip_mask = ip_cap - 1;
   S.st_mask = st_cap - 1;
   S.arena_cap = arena_cap;
@@ -2753,7 +2917,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   e->scalars.release(); e->res_seq.release(); e->res_rule.release(); e->ev_el.release(); e->ev_rule.release();
   e->ev_res.release(); e->ev_st.release(); e->ev_st2.release(); e->ev_idx.release(); e->ev_idx2.release();
   e->el_slot.release(); e->coll.release(); e->ev_rec.release(); e->ev_rec2.release(); e->el_id.release();
-  e->run_heads.release(); e->run_flag.release();
+
   for (auto *b : {&e->pk_key, &e->pk_key2, &e->pk_line, &e->pk_line2, &e->pack_src, &e->rx_len, &e->rx_ev_el}) b->release();
   for (auto *b : {&e->pk_nev, &e->pk_ipl, &e->pk_evoff, &e->pk_byoff, &e->pk_start, &e->pk_counts, &e->pk_bbase,
                   &e->rx_hash, &e->rx_pos, &e->rx_nev, &e->rx_evoff})
@@ -2818,16 +2982,17 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
   const uint32_t epoch = e->epoch;
   e->el_slot.ensure(E.n); e->el_id.ensure(E.n); e->coll.ensure(E.n);
   e->ev_st.ensure(n_ev); e->ev_st2.ensure(n_ev); e->ev_rec.ensure(n_ev); e->ev_rec2.ensure(n_ev);
-  e->ev_out.ensure(n_ev); e->ev_out_s.ensure(n_ev); e->run_flag.ensure(n_ev); e->run_heads.ensure(n_ev);
+  e->ev_out.ensure(n_ev); e->ev_out_s.ensure(n_ev);
   mark(e, 5);
   for (int attempt = 0;; ++attempt) {
     const uint64_t n_ips = e->host_counters[0];
     HIP_OK(hipMemsetAsync(e->S.counters + 3, 0, 3 * 8, st));
+    HIP_OK(hipMemsetAsync(e->S.counters + kShardBase, 0, kClaimShards * 128, st));
     uint64_t budget = e->ip_cap * 3 / 4 - n_ips;
     const bool forced = e->dbg_budget && attempt == 0 && e->dbg_budget < budget;  // test hook
     if (forced) budget = e->dbg_budget;
     hipLaunchKernelGGL(k_ip_claim, dim3(grid_for(E.n)), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p,
-                       budget);
+                       budget / kClaimShards);
     HIP_OK(hipGetLastError());
     uint64_t ovf = 0;
     HIP_OK(hipMemcpyAsync(&ovf, e->S.counters + 5, 8, hipMemcpyDeviceToHost, st));
@@ -2859,16 +3024,21 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
     read_counters(e);
     const uint64_t n_st = e->host_counters[2];
     HIP_OK(hipMemsetAsync(e->S.counters + 6, 0, 2 * 8, st));
+    HIP_OK(hipMemsetAsync(e->S.counters + kShardBase, 0, kClaimShards * 128, st));
     uint64_t budget = e->st_cap * 3 / 4 - n_st;
     const bool forced = e->dbg_budget && attempt == 0 && e->dbg_budget < budget;  // test hook
     if (forced) budget = e->dbg_budget;
     hipLaunchKernelGGL(k_st_claim, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, E, n_ev, ev_el, ev_rule, e->el_slot.p,
-                       e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_rec.p, budget);
+                       e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_rec.p, budget / kClaimShards);
     HIP_OK(hipGetLastError());
     uint64_t ovf = 0;
     HIP_OK(hipMemcpyAsync(&ovf, e->S.counters + 7, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    if (!ovf) break;
+    if (!ovf) {
+      hipLaunchKernelGGL(k_fold_claims, dim3(1), dim3(kClaimShards), 0, st, e->S);
+      HIP_OK(hipGetLastError());
+      break;
+    }
     // more new (ip, rule name) states than the table had room for: undo this
     // batch's claims, recount, grow, claim again
     HIP_OK(hipMemsetAsync(e->S.counters + 2, 0, 8, st));
@@ -2888,19 +3058,8 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
       return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)n_ev, 0, bits, st);
     });
   }
-  hipLaunchKernelGGL(k_run_heads, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_st2.p, e->run_flag.p);
-  HIP_OK(hipGetLastError());
-  {
-    hipcub::CountingInputIterator<uint32_t> it(0);
-    uint8_t *fl = e->run_flag.p;
-    uint32_t *o = e->run_heads.p;
-    unsigned long long *ns = e->scalars.p + 5;
-    cub_call(e, [&](void *tmp, size_t &bytes) {
-      return hipcub::DeviceSelect::Flagged(tmp, bytes, it, fl, o, ns, (int)n_ev, st);
-    });
-  }
-  hipLaunchKernelGGL(k_apply, dim3(2048), dim3(kBlock), 0, st, n_ev, e->scalars.p + 5, e->run_heads.p, e->ev_st2.p,
-                     e->ev_rec2.p, B.rules, e->S.st, e->ev_out_s.p);
+  hipLaunchKernelGGL(k_apply, dim3((unsigned)((n_ev + kApplyChunk - 1) / kApplyChunk)), dim3(kBlock), 0, st, n_ev,
+                     e->ev_st2.p, e->ev_rec2.p, B.rules, e->S.st, e->ev_out_s.p);
   HIP_OK(hipGetLastError());
 }
 
@@ -3451,7 +3610,7 @@ extern "C" int bjx_state_clear(bjx_engine *e) {
     HIP_OK(hipMemsetAsync(e->S.ip, 0, e->ip_cap * sizeof(IpSlot), e->stream));
     HIP_OK(hipMemsetAsync(e->S.ip_first, 0xFF, e->ip_cap * 4, e->stream));
     HIP_OK(hipMemsetAsync(e->S.st, 0, e->st_cap * sizeof(StSlot), e->stream));
-    HIP_OK(hipMemsetAsync(e->S.counters, 0, 64, e->stream));
+    HIP_OK(hipMemsetAsync(e->S.counters, 0, kCounterBytes, e->stream));
     HIP_OK(hipStreamSynchronize(e->stream));
     return BJX_OK;
   } catch (const BjxError &x) {
@@ -3528,8 +3687,12 @@ extern "C" size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap) {
 }
 extern "C" size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap) {
   if (!e) return 0;
-  for (size_t k = 0; k < 5 && k < cap; ++k) out[k] = e->scan_stats[k];
-  return 5;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (e->S.counters) read_counters(e);
+  const uint64_t v[9] = {e->scan_stats[0], e->scan_stats[1], e->scan_stats[2], e->scan_stats[3], e->scan_stats[4],
+                         e->ip_cap, e->host_counters[0], e->st_cap, e->host_counters[2]};
+  for (size_t k = 0; k < 9 && k < cap; ++k) out[k] = v[k];
+  return 9;
 }
 extern "C" size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t i, char *out, size_t cap) {
   if (!rs || i >= rs->rules.size()) return 0;

@@ -182,7 +182,8 @@ struct State {
   uint8_t *arena;
   StSlot *st;
   uint64_t *counters;  // [0] ips, [1] arena bytes, [2] states; per batch: [3] hash-collision lines,
-                       // [4]/[5] IP slots claimed / over budget, [6]/[7] state slots claimed / over budget
+                       // [5] / [7] IP / state claims over budget; [16 + 16 * shard + 0/1]: claims per
+                       // block shard (engine.hip kClaimShards)
   uint64_t ip_mask;
   uint64_t st_mask;
   uint64_t arena_cap;
