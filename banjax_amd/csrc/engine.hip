@@ -424,7 +424,8 @@ struct ScanArgs {
   Lines L;
   unsigned long long *stats;  // [0] bitset hits, [1] recorded literal hits
   uint32_t shared_bytes;      // per-wave LDS regions start here
-  uint32_t debug_skip;        // timing experiments only (BJX_DEBUG_SKIP): 1 gram phase
+  uint32_t debug_skip;        // timing experiments only (BJX_DEBUG_SKIP, results invalid): 1 gram phase, 2 candidates,
+                              // 4 literal checks of gram table hits, 8 gram table probes
 };
 
 // pass A: '\n' count per wave tile
@@ -684,7 +685,7 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
   uint16_t *ls = reinterpret_cast<uint16_t *>(T + kTileLds);
   uint16_t *le = ls + kLineCap;
   const Lines &L = A.L;
-  uint32_t n_probe = 0, n_hit = 0;
+  uint32_t n_probe = 0, n_hit = 0, n_gram = 0;
 
   const uint64_t nw = (uint64_t)gridDim.x * kScanWaves;
   uint64_t t = (uint64_t)blockIdx.x * kScanWaves + wave;
@@ -813,14 +814,20 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
     // ---- 4-gram prefilter: positions [64 lane, 64 lane + 64) and the last line's halo part
     {
       const uint32_t nxt = *reinterpret_cast<const uint32_t *>(T + lane * 64u + 64u);
-      uint64_t hits = 0;
+      // per position: alignbyte, fold (shift, xor), mul24, word address, LDS
+      // read, bfe (its offset operand uses bits 0-4 only), shift-or
+      const uint8_t *sb = reinterpret_cast<const uint8_t *>(s_bits);
+      uint32_t hlo = 0, hhi = 0;
 #pragma unroll
       for (int k = 0; k < 64; ++k) {
         const uint32_t lo = w[k >> 2], hi = (k >> 2) < 15 ? w[(k >> 2) + 1] : nxt;
         const uint32_t g = (k & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3)) : lo;
-        const uint32_t h = gram_hash(g);
-        hits |= (uint64_t)((s_bits[h >> 5] >> (h & 31)) & 1u) << k;
+        const uint32_t x = gram_fold(g);
+        const uint32_t word = *reinterpret_cast<const uint32_t *>(sb + ((gram_mix(x) >> 11) & ((kGramWords - 1) << 2)));
+        const uint32_t bit = __builtin_amdgcn_ubfe(word, x, 1);  // = gram_hash(g)'s bit
+        if (k < 32) hlo |= bit << k; else hhi |= bit << (k - 32);
       }
+      uint64_t hits = ((uint64_t)hhi << 32) | hlo;
       if (ts0 + lane * 64u + 64u > A.n) hits &= (ts0 + lane * 64u >= A.n) ? 0ull : ((1ull << (A.n - ts0 - lane * 64u)) - 1ull);
       uint32_t hh = 0;  // halo positions of the last started line
       const uint32_t hend = last_in_halo ? hfirst : kWT;
@@ -831,6 +838,7 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
         }
       }
       n_probe += __popcll(hits) + __popc(hh);
+      if (A.debug_skip & 2) { hits = 0; hh = 0; }
       // ---- candidates, lane-compacted: every lane appends its surviving
       // positions (with the started-line index they belong to) to a wave list,
       // then the list is verified one candidate per lane
@@ -874,8 +882,8 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
           const uint32_t p = e & 0xFFFF;
           const int32_t lk = (int32_t)(e >> 16) - 1;
           const uint32_t g = ld4(T + p);
-          if ((g & 0xFF) == '\n') continue;
-          uint32_t slot = (uint32_t)mix64(g) & (B.gt2_cap - 1);
+          if ((g & 0xFF) == '\n' || (A.debug_skip & 8)) continue;
+          uint32_t slot = gram_slot(g, B.gt2_cap);
           uint32_t ol;
           for (;;) {
             ol = gt[2 * slot + 1];
@@ -883,6 +891,8 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
             slot = (slot + 1) & (B.gt2_cap - 1);
           }
           if ((ol & 0xFFFF) == 0) continue;
+          ++n_gram;
+          if (A.debug_skip & 4) continue;
           if (lk < 0 && !open_long) continue;  // the previous tile covered it
           const uint64_t gline = tb + nh + (uint64_t)(int64_t)lk;
           if (gline >= A.n_lines) continue;
@@ -919,10 +929,12 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
   for (int o = 32; o > 0; o >>= 1) {
     n_probe += __shfl_xor(n_probe, o);
     n_hit += __shfl_xor(n_hit, o);
+    n_gram += __shfl_xor(n_gram, o);
   }
   if (lane == 0 && (n_probe | n_hit)) {
     atomicAdd(&A.stats[0], (unsigned long long)n_probe);
     atomicAdd(&A.stats[1], (unsigned long long)n_hit);
+    atomicAdd(&A.stats[2], (unsigned long long)n_gram);
   }
 }
 
@@ -2161,7 +2173,7 @@ struct bjx_engine {
   uint32_t scan_lds[2] = {0, 0};
   bool lines_attr = false;
   DevBuf<uint32_t> l_ccnt;
-  unsigned long long scan_stats[5] = {0, 0, 0, 0, 0};
+  unsigned long long scan_stats[6] = {0, 0, 0, 0, 0, 0};
   uint64_t last_slow = 0;
   DevBuf<uint8_t> l_flags;
   DevBuf<unsigned long long> scalars;  // [0] slow count, [1..2] bounds, [3] selected
@@ -2324,14 +2336,26 @@ static void calibrate_grams(const std::vector<uint8_t> &lit_bytes, const std::ve
     auto it = cnt.find(g);
     if (it != cnt.end()) ++it->second;
   }
+  // window choice: a gram hit costs one check per literal filed under that
+  // gram, so a window costs (sample count + 1) x (literals sharing it).
+  // Start from the rarest window of each literal, then a few rounds of
+  // re-choosing each literal's window against the others' choices.
+  auto variants = [&](size_t id, uint32_t o, uint32_t *out) {
+    uint32_t k = 0;
+    for (uint32_t v = 0; v < 16; ++v) {
+      uint32_t x;
+      if (window_variant(&lit_bytes[lit_off[id] + o], &lit_ci[lit_off[id] + o], v, &x)) out[k++] = x;
+    }
+    return k;
+  };
+  std::vector<std::vector<uint64_t>> wcs(lit_off.size());
   for (size_t id = 0; id < lit_off.size(); ++id) {
-    std::vector<uint64_t> wc;
+    std::vector<uint64_t> &wc = wcs[id];
     for (uint32_t o = 0; o + 4 <= lit_len[id]; ++o) {
+      uint32_t vs[16];
+      const uint32_t k = variants(id, o, vs);
       uint64_t c = 0;
-      for (uint32_t v = 0; v < 16; ++v) {
-        uint32_t x;
-        if (window_variant(&lit_bytes[lit_off[id] + o], &lit_ci[lit_off[id] + o], v, &x)) c += cnt[x];
-      }
+      for (uint32_t i = 0; i < k; ++i) c += cnt[vs[i]];
       wc.push_back(c);
     }
     uint64_t best = ~0ull;
@@ -2341,6 +2365,36 @@ static void calibrate_grams(const std::vector<uint8_t> &lit_bytes, const std::ve
       if (c < best) { best = c; best_o = o; }
     }
     lit_gram[id] = best_o;
+  }
+  std::unordered_map<uint32_t, uint32_t> load;  // gram -> literals filed under it
+  auto file = [&](size_t id, int d) {
+    uint32_t vs[16];
+    const uint32_t k = variants(id, lit_gram[id], vs);
+    for (uint32_t i = 0; i < k; ++i) load[vs[i]] += d;
+  };
+  for (size_t id = 0; id < lit_off.size(); ++id) file(id, 1);
+  for (int round = 0; round < 3; ++round)
+    for (size_t id = 0; id < lit_off.size(); ++id) {
+      file(id, -1);
+      uint64_t best = ~0ull;
+      uint32_t best_o = lit_gram[id];
+      for (uint32_t o = 0; o + 4 <= lit_len[id]; ++o) {
+        uint32_t vs[16];
+        const uint32_t k = variants(id, o, vs);
+        uint64_t c = 0;
+        for (uint32_t i = 0; i < k; ++i) {
+          auto it = load.find(vs[i]);
+          c += (cnt[vs[i]] + 1) * (1 + (it == load.end() ? 0 : it->second));
+        }
+        c = 2 * c + (o == lit_gram[id] ? 0 : 1);  // ties keep the current window
+        if (c < best) { best = c; best_o = o; }
+      }
+      lit_gram[id] = best_o;
+      file(id, 1);
+    }
+  for (size_t id = 0; id < lit_off.size(); ++id) {
+    const std::vector<uint64_t> &wc = wcs[id];
+    const uint32_t best_o = lit_gram[id];
     uint64_t bc = ~0ull;
     for (uint32_t o = 0; o < wc.size(); ++o) {
       if (o == best_o && wc.size() > 1) continue;
@@ -2463,7 +2517,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     for (auto &kv : gmap) {
       const uint32_t h = gram_hash(kv.first);
       gram_bits[h >> 5] |= 1u << (h & 31);
-      uint32_t slot = (uint32_t)mix64(kv.first) & (gt2_cap - 1);
+      uint32_t slot = gram_slot(kv.first, gt2_cap);
       while (gt2[2 * slot + 1] & 0xFFFF) slot = (slot + 1) & (gt2_cap - 1);
       gt2[2 * slot] = kv.first;
       gt2[2 * slot + 1] = ((uint32_t)gt2_ent.size() << 16) | (uint32_t)kv.second.size();
@@ -3208,7 +3262,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   const unsigned long long n_slow = sc4[4], n_jobs = sc4[3];
   e->last_jobs = n_jobs;
   e->scan_stats[0] = sc4[0]; e->scan_stats[1] = sc4[1]; e->scan_stats[2] = n_slow; e->scan_stats[3] = B.img_bytes;
-  e->scan_stats[4] = n_jobs;
+  e->scan_stats[4] = n_jobs; e->scan_stats[5] = sc4[2];
   if (n_jobs) {
     // group the jobs by rule (stable: line order inside a rule), then one lane per job
     e->jline2.ensure(n_jobs); e->jkey2.ensure(n_jobs);
@@ -3689,10 +3743,10 @@ extern "C" size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap)
   if (!e) return 0;
   std::lock_guard<std::mutex> g(e->mu);
   if (e->S.counters) read_counters(e);
-  const uint64_t v[9] = {e->scan_stats[0], e->scan_stats[1], e->scan_stats[2], e->scan_stats[3], e->scan_stats[4],
-                         e->ip_cap, e->host_counters[0], e->st_cap, e->host_counters[2]};
-  for (size_t k = 0; k < 9 && k < cap; ++k) out[k] = v[k];
-  return 9;
+  const uint64_t v[10] = {e->scan_stats[0], e->scan_stats[1], e->scan_stats[2], e->scan_stats[3], e->scan_stats[4],
+                          e->ip_cap, e->host_counters[0], e->st_cap, e->host_counters[2], e->scan_stats[5]};
+  for (size_t k = 0; k < 10 && k < cap; ++k) out[k] = v[k];
+  return 10;
 }
 extern "C" size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t i, char *out, size_t cap) {
   if (!rs || i >= rs->rules.size()) return 0;

@@ -32,10 +32,25 @@ struct DevRule {
 // Full-rate hash (24-bit multiply after folding the top byte in).
 constexpr uint32_t kGramLog2 = 16;
 constexpr uint32_t kGramWords = (1u << kGramLog2) / 32;
-__host__ __device__ inline uint32_t gram_hash(uint32_t g) {
-  const uint32_t x = g ^ (g >> 15);
-  return ((x & 0xFFFFFFu) * 0x2C1B3Bu >> 8) & ((1u << kGramLog2) - 1);
+// 4-gram -> bit of the 64K-bit prefilter set: word = bits 13..23 of a 24 x
+// 24-bit product of the folded gram (one full-rate v_mul_u32_u24 on the
+// device), bit = the folded gram's low 5 bits (a v_bfe offset operand as is)
+__host__ __device__ inline uint32_t gram_fold(uint32_t g) { return g ^ (g >> 15); }
+__host__ __device__ inline uint32_t gram_mix(uint32_t x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __umul24(x, 0x2C1B3Bu);
+#else
+  return (x & 0xFFFFFFu) * 0x2C1B3Bu;
+#endif
 }
+__host__ __device__ inline uint32_t gram_hash(uint32_t g) {
+  const uint32_t x = gram_fold(g);
+  return (((gram_mix(x) >> 13) & 0x7FFu) << 5) | (x & 31u);
+}
+static_assert(kGramLog2 == 16, "gram_hash yields 16 bits");
+// home slot of a gram in the exact gram table (cap a power of two <= 2^18):
+// Fibonacci hashing, high product bits
+__host__ __device__ inline uint32_t gram_slot(uint32_t g, uint32_t cap) { return ((g * 0x9E3779B1u) >> 14) & (cap - 1); }
 constexpr int kCandSlots = 4;  // literal hits kept per line (more = overflow: every literal rule by DFA)
 constexpr uint64_t kCandVerified = 1u << 23;  // hit bytes already checked by the scan pass
 

@@ -136,10 +136,11 @@ class Engine:
     PHASES = ("count", "scan", "resolve", "emit", "capacity", "ip_state_claim", "sort_apply", "trips")
 
     def scan_stats(self):
-        out = (C.c_uint64 * 9)()
-        _lib.lib().bjx_debug_scan_stats(self._h, out, 9)
+        out = (C.c_uint64 * 10)()
+        _lib.lib().bjx_debug_scan_stats(self._h, out, 10)
         return {"gram_bitset_hits": out[0], "literal_hits": out[1], "fallback_lines": out[2], "lookup_image_bytes": out[3],
-                "dfa_jobs": out[4], "ip_table_slots": out[5], "ips": out[6], "state_table_slots": out[7], "states": out[8]}
+                "dfa_jobs": out[4], "ip_table_slots": out[5], "ips": out[6], "state_table_slots": out[7], "states": out[8],
+                "gram_table_hits": out[9]}
 
     def phase_ms(self):
         out = (C.c_double * 8)()

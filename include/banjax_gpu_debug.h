@@ -24,7 +24,8 @@ size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t rule_idx, char *out,
 size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap);
 /* last batch: gram bitset hits, recorded literal hits, lines sent to the per-line
    fallback, lines decided by the long-line pass, DFA jobs; then the state
-   tables: IP slots, IPs, state slots, states (returns the count, 9) */
+   tables: IP slots, IPs, state slots, states; then gram table hits (returns
+   the count, 10) */
 size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap);
 /* Test hook: IP hashes become (hash & mask) | 1 (0 = off), so distinct IPs
    share 64-bit hashes and the exact collision path of the IP table runs. */
