@@ -12,6 +12,7 @@ Prints ONE JSON line on rank 0.  Multi-GPU: launched by torch.distributed.run,
 one rank per GPU.
 """
 import argparse
+import re
 import json
 import os
 import sys
@@ -49,7 +50,9 @@ def pmc_traffic(nbytes):
     import csv
     import glob
     best = None
-    for d in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*"))):
+    def natural(d):  # r01_v10 after r01_v5
+        return [int(x) if x.isdigit() else x for x in re.split(r"(\d+)", d)]
+    for d in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")), key=natural):
         f, wr = os.path.join(d, "cfg3_bench_pmc_fetch.csv"), os.path.join(d, "cfg3_bench_pmc_write.csv")
         if os.path.exists(f) and os.path.exists(wr):
             best = (d, f, wr)
