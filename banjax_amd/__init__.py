@@ -11,9 +11,11 @@ from .config import (ALLOW, CHALLENGE, IPTABLES_BLOCK, NGINX_BLOCK, Config, Conf
 from .engine import BatchOutput, Engine
 from .regex_rate_limiter import (Banner, ConsumeLineResult, DynamicDecisionLists, MockBanner, RateLimitResult,
                                  RegexRateLimiter, RegexRateLimitStates, RuleResult, consume_line)
+from .tailer import LogTailer, TailBatch, TailStopped, run_log_tailer
 
 __all__ = [
     "ALLOW", "CHALLENGE", "NGINX_BLOCK", "IPTABLES_BLOCK", "Config", "ConfigError", "RegexWithRate", "Ruleset",
     "decision_string", "parse_decision", "Engine", "BatchOutput", "Banner", "MockBanner", "DynamicDecisionLists",
     "ConsumeLineResult", "RuleResult", "RateLimitResult", "RegexRateLimiter", "RegexRateLimitStates", "consume_line",
+    "LogTailer", "TailBatch", "TailStopped", "run_log_tailer",
 ]

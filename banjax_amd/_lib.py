@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libbanjax_gpu.so")
 
 OK = 0
 ERR_REGEX, ERR_ARG, ERR_DEVICE, ERR_NOMEM, ERR_TOO_COMPLEX, ERR_CAPACITY, ERR_DECISION = -1, -2, -3, -4, -5, -6, -7
+TAIL_STOPPED, ERR_IO = -8, -9
 INPUT_DEVICE, COPY_RESULTS = 1, 2
 
 
@@ -64,13 +65,24 @@ class EventLine(C.Structure):
                 ("n_events", C.c_uint32), ("_pad", C.c_uint32)]
 
 
+class TailerOptions(C.Structure):
+    _fields_ = [("device", C.c_int32), ("from_start", C.c_int32), ("slots", C.c_uint32), ("poll_ms", C.c_uint32),
+                ("batch_bytes", C.c_uint64)]
+
+
+class TailBatch(C.Structure):
+    _fields_ = [("slot", C.c_uint32), ("reopened", C.c_uint32), ("host_bytes", C.c_void_p),
+                ("device_bytes", C.c_void_p), ("n_bytes", C.c_uint64), ("file_offset", C.c_uint64)]
+
+
 # every symbol include/banjax_gpu.h declares
 EXPORTS = [
     "bjx_abi_version", "bjx_ruleset_compile", "bjx_ruleset_release", "bjx_ruleset_num_rules",
     "bjx_ruleset_rule_info", "bjx_engine_create", "bjx_engine_destroy", "bjx_engine_set_decision_lists",
     "bjx_process_batch", "bjx_state_get", "bjx_state_len", "bjx_state_clear", "bjx_state_dump",
     "bjx_engine_last_error", "bjx_match_batch", "bjx_events_partition", "bjx_events_pack", "bjx_apply_events",
-    "bjx_finish_batch",
+    "bjx_finish_batch", "bjx_tailer_open", "bjx_tailer_next", "bjx_tailer_release", "bjx_tailer_stats",
+    "bjx_tailer_close",
 ]
 
 _lib = None
@@ -144,6 +156,15 @@ def lib():
     L.bjx_debug_set_claim_budget.argtypes = [vp, C.c_uint64]
     L.bjx_debug_set_ip_hash_mask.restype = C.c_int
     L.bjx_debug_set_ip_hash_mask.argtypes = [vp, C.c_uint64]
+    L.bjx_tailer_open.restype = C.c_int
+    L.bjx_tailer_open.argtypes = [C.c_char_p, sz, C.POINTER(TailerOptions), C.POINTER(vp), C.c_char_p, sz]
+    L.bjx_tailer_next.restype = C.c_int
+    L.bjx_tailer_next.argtypes = [vp, C.c_int32, C.POINTER(TailBatch)]
+    L.bjx_tailer_release.restype = C.c_int
+    L.bjx_tailer_release.argtypes = [vp, C.c_uint32]
+    L.bjx_tailer_stats.restype = C.c_int
+    L.bjx_tailer_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.bjx_tailer_close.argtypes = [vp]
     L.bjx_engine_last_error.restype = C.c_char_p
     L.bjx_engine_last_error.argtypes = [vp]
     _lib = L

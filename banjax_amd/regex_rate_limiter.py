@@ -303,11 +303,27 @@ class RegexRateLimiter:
         self.engine.set_decision_lists(cfg.decision_entries)
 
     def consume_lines(self, data: bytes, now_ns: int, want_results: bool = True):
-        """consumeLine for every complete line; returns (results, consumed bytes)."""
+        """consumeLine for every complete line; returns (results, batch output)."""
         out = self.engine.process(self.ruleset, data, now_ns, copy_results=want_results)
+        return self._finish(data, out, now_ns, want_results)
+
+    def consume_device_batch(self, host_view, device_ptr: Optional[int], nbytes: int, now_ns: int,
+                             want_results: bool = True):
+        """consumeLine over a batch already in HBM (the tailer's copy); host_view
+        holds the same bytes for the Banner's log lines.  device_ptr None: host."""
+        if device_ptr is None:
+            out = self.engine.process(self.ruleset, bytes(host_view[:nbytes]), now_ns, copy_results=want_results)
+        else:
+            out = self.engine.process(self.ruleset, None, now_ns, copy_results=want_results, device_ptr=device_ptr,
+                                      nbytes=nbytes)
+        return self._finish(host_view, out, now_ns, want_results)
+
+    def _finish(self, data, out, now_ns: int, want_results: bool):
+        """Banner replay of the trips in reference order (regex_rate_limiter.go:254-266)
+        and, if asked, the ConsumeLineResults."""
         rules = self.ruleset.rules
         for t in out.trips:
-            line = data[t.line_offset:t.line_offset + t.line_len]
+            line = bytes(data[t.line_offset:t.line_offset + t.line_len])
             ip = line[t.ip_off:t.ip_off + t.ip_len]
             host = line[t.host_off:t.host_off + t.host_len]
             rest = line[t.rest_off:]

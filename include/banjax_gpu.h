@@ -16,6 +16,8 @@
  *   bjx_state_get           RegexRateLimitStates.Get           internal/rate_limit.go:81-96
  *   bjx_state_len           RegexRateLimitStates.Len           internal/rate_limit.go:30-35
  *   bjx_state_dump          RegexRateLimitStates.String        internal/rate_limit.go:98-103,204-220
+ *   bjx_tailer_*            tail.TailFile(Follow, SeekEnd) + tailer.Lines in RunLogTailer
+ *                           internal/regex_rate_limiter.go:21-78 (github.com/hpcloud/tail v1.0.0)
  *
  * Ownership: input buffers are borrowed for the duration of a call.  Result
  * arrays are engine-owned and valid until the next bjx_process_batch on the
@@ -47,7 +49,9 @@ enum bjx_status {
   BJX_ERR_NOMEM = -4,
   BJX_ERR_TOO_COMPLEX = -5, /* rule exceeds the engine's automaton limits */
   BJX_ERR_CAPACITY = -6,    /* state tables full (raise bjx_engine_options) */
-  BJX_ERR_DECISION = -7     /* unknown decision string / value */
+  BJX_ERR_DECISION = -7,    /* unknown decision string / value */
+  BJX_TAIL_STOPPED = -8,    /* bjx_tailer_next: the followed file was deleted or renamed (tail stops) */
+  BJX_ERR_IO = -9           /* bjx_tailer: read/open failure other than "not there yet" */
 };
 
 /* Decision, reference internal/decision.go:20-28 */
@@ -213,6 +217,51 @@ int bjx_state_clear(bjx_engine *e);
 /* RegexRateLimitStates.String(): "ip:\n\trule:\n\t\t{hits start}\n" blocks, IPs in
    first-seen order.  Returns the full length (writes at most cap bytes). */
 size_t bjx_state_dump(bjx_engine *e, char *out, size_t cap);
+
+/* ---- Log-tail front end.  Replaces github.com/hpcloud/tail
+   v1.0.0 as RunLogTailer uses it (regex_rate_limiter.go:30-58: Follow, start
+   at EOF) with bulk reads into pinned buffers and batches of complete lines:
+     - a line is the bytes before '\n' ('\r' kept), exactly tail.Line.Text;
+     - a trailing partial line is held until its '\n' arrives (tail seeks back
+       over it and re-reads, same effect);
+     - a missing file is waited for, then followed from its end (MustExist false);
+     - a file that shrinks below the read offset was truncated: it is re-read
+       from offset 0 and the held partial line is dropped (tail's reopen);
+     - a file deleted or renamed away stops the tail (ReOpen false):
+       bjx_tailer_next returns BJX_TAIL_STOPPED once every batch is handed out.
+   A reader thread fills the next pinned slot and issues its host-to-device
+   copy on a copy stream while the caller runs bjx_process_batch on the
+   previous slot (double buffering with slots = 2).  Batch = one config
+   snapshot for all its lines (the reference reads configHolder.Get() per
+   line, :58-59; a reload takes effect at the next batch). */
+typedef struct bjx_tailer bjx_tailer;
+
+typedef struct bjx_tailer_options {
+  int32_t device;        /* GPU that receives each batch (HBM copy); -1 = host framing only */
+  int32_t from_start;    /* 0: first open seeks to EOF (Whence io.SeekEnd, :32-36); 1: offset 0 */
+  uint32_t slots;        /* pinned (+ device) buffers in flight; 0 = 2 */
+  uint32_t poll_ms;      /* wait at EOF before looking again; 0 = 20 */
+  uint64_t batch_bytes;  /* largest batch; 0 = 256 MiB (a longer line grows the slot) */
+} bjx_tailer_options;
+
+typedef struct bjx_tail_batch {
+  uint32_t slot;               /* give back with bjx_tailer_release */
+  uint32_t reopened;           /* the file was truncated and re-read from 0 before this batch */
+  const uint8_t *host_bytes;   /* pinned host copy: trips' line offsets index it */
+  const uint8_t *device_bytes; /* HBM copy, complete: pass to bjx_process_batch with BJX_INPUT_DEVICE (NULL if device = -1) */
+  uint64_t n_bytes;            /* ends with '\n' */
+  uint64_t file_offset;        /* file offset of host_bytes[0] */
+} bjx_tail_batch;
+
+int bjx_tailer_open(const char *path, size_t path_len, const bjx_tailer_options *opts, bjx_tailer **out, char *err,
+                    size_t err_len);
+/* Next batch, oldest first.  Waits up to timeout_ms (< 0: forever).  Returns
+   1 with *out filled, 0 on timeout, BJX_TAIL_STOPPED, or an error code. */
+int bjx_tailer_next(bjx_tailer *t, int32_t timeout_ms, bjx_tail_batch *out);
+int bjx_tailer_release(bjx_tailer *t, uint32_t slot);
+/* bytes read from the file so far / handed out in batches (held partial line = difference) */
+int bjx_tailer_stats(bjx_tailer *t, uint64_t *read_bytes, uint64_t *batched_bytes, uint64_t *batches);
+void bjx_tailer_close(bjx_tailer *t);
 
 /* Last error message of an engine call. */
 const char *bjx_engine_last_error(bjx_engine *e);
