@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libbanjax_gpu.so")
 OK = 0
 ERR_REGEX, ERR_ARG, ERR_DEVICE, ERR_NOMEM, ERR_TOO_COMPLEX, ERR_CAPACITY, ERR_DECISION = -1, -2, -3, -4, -5, -6, -7
 TAIL_STOPPED, ERR_IO = -8, -9
-INPUT_DEVICE, COPY_RESULTS = 1, 2
+INPUT_DEVICE, COPY_RESULTS, EMIT_BANS = 1, 2, 4
 
 
 class Str(C.Structure):
@@ -65,6 +65,22 @@ class EventLine(C.Structure):
                 ("n_events", C.c_uint32), ("_pad", C.c_uint32)]
 
 
+class BanOptions(C.Structure):
+    _fields_ = [("expiring_ttl_ns", C.c_int64), ("tz_offset_s", C.c_int32), ("_pad", C.c_uint32),
+                ("disable_logging", C.POINTER(Str)), ("n_disable_logging", C.c_size_t)]
+
+
+class IpDecision(C.Structure):
+    _fields_ = [("trip_idx", C.c_uint64), ("n_trips", C.c_uint64), ("expires_ns", C.c_int64),
+                ("decision", C.c_int32), ("iptables", C.c_uint32)]
+
+
+class BanBatch(C.Structure):
+    _fields_ = [("n_ips", C.c_uint64), ("ips", C.POINTER(IpDecision)), ("n_trips", C.c_uint64),
+                ("log", C.c_void_p), ("log_bytes", C.c_uint64), ("log_off", C.POINTER(C.c_uint64)),
+                ("log_kind", C.POINTER(C.c_uint8))]
+
+
 class TailerOptions(C.Structure):
     _fields_ = [("device", C.c_int32), ("from_start", C.c_int32), ("slots", C.c_uint32), ("poll_ms", C.c_uint32),
                 ("batch_bytes", C.c_uint64)]
@@ -82,7 +98,7 @@ EXPORTS = [
     "bjx_process_batch", "bjx_state_get", "bjx_state_len", "bjx_state_clear", "bjx_state_dump",
     "bjx_engine_last_error", "bjx_match_batch", "bjx_events_partition", "bjx_events_pack", "bjx_apply_events",
     "bjx_finish_batch", "bjx_tailer_open", "bjx_tailer_next", "bjx_tailer_release", "bjx_tailer_stats",
-    "bjx_tailer_close",
+    "bjx_tailer_close", "bjx_engine_set_ban_options", "bjx_batch_bans",
 ]
 
 _lib = None
@@ -165,6 +181,10 @@ def lib():
     L.bjx_tailer_stats.restype = C.c_int
     L.bjx_tailer_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.bjx_tailer_close.argtypes = [vp]
+    L.bjx_engine_set_ban_options.restype = C.c_int
+    L.bjx_engine_set_ban_options.argtypes = [vp, C.POINTER(BanOptions)]
+    L.bjx_batch_bans.restype = C.c_int
+    L.bjx_batch_bans.argtypes = [vp, C.POINTER(BanBatch)]
     L.bjx_engine_last_error.restype = C.c_char_p
     L.bjx_engine_last_error.argtypes = [vp]
     _lib = L

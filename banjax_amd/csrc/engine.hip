@@ -36,6 +36,7 @@
 #include "bjx_common.h"
 #include "engine_types.h"
 #include "regex_compiler.h"
+#include "bans.h"
 
 using namespace bjx;
 
@@ -1747,6 +1748,115 @@ __global__ void k_build_trips(uint64_t n_trips, const uint32_t *__restrict__ idx
   out[t] = tr;
 }
 
+// ---- trip -> decision emission (bans.h)
+
+// LogRegexBan line length of each trip (entry n_trips: 0, for the exclusive scan)
+__global__ void k_ban_len(BanDev A, uint64_t *__restrict__ len, uint8_t *__restrict__ kind) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > A.n_trips) return;
+  if (t == A.n_trips) { len[t] = 0; return; }
+  JOut<false> o{nullptr, 0};
+  kind[t] = (uint8_t)ban_log_line(A, t, o);
+  len[t] = o.n;
+}
+
+__global__ void k_ban_write(BanDev A, const uint64_t *__restrict__ off, uint8_t *__restrict__ out) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= A.n_trips) return;
+  JOut<true> o{out + off[t], 0};
+  ban_log_line(A, t, o);
+}
+
+__device__ __forceinline__ const uint8_t *trip_ip(const BanDev &A, uint64_t t) {
+  return A.buf + A.trips[t].line_offset + A.trips[t].ip_off;
+}
+
+// per-IP grouping key: hash of the IP bytes (exact grouping below)
+__global__ void k_ban_keys(BanDev A, uint64_t mask, uint64_t *__restrict__ key, uint32_t *__restrict__ val) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= A.n_trips) return;
+  key[t] = hash_bytes(trip_ip(A, t), A.trips[t].ip_len) & mask;  // mask: collision test hook
+  val[t] = (uint32_t)t;
+}
+
+__global__ void k_ban_heads(uint64_t n, const uint64_t *__restrict__ ks, uint32_t *__restrict__ head) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) head[i] = (i == 0 || ks[i] != ks[i - 1]) ? 1u : 0u;
+}
+
+__device__ __forceinline__ bool same_ip(const BanDev &A, uint64_t a, uint64_t b) {
+  const uint32_t n = A.trips[a].ip_len;
+  if (A.trips[b].ip_len != n) return false;
+  const uint8_t *x = trip_ip(A, a), *y = trip_ip(A, b);
+  for (uint32_t k = 0; k < n; ++k)
+    if (x[k] != y[k]) return false;
+  return true;
+}
+
+// (max decision, first trip with it) per hash run: atomicMax of
+// decision << 32 | ~trip; a run whose IP bytes differ (64-bit hash collision)
+// is flagged and regrouped exactly by k_ban_collide
+__global__ void k_ban_reduce(BanDev A, uint64_t n, const uint64_t *__restrict__ ks, const uint32_t *__restrict__ vs,
+                             const uint32_t *__restrict__ seg, uint32_t *__restrict__ seg_first,
+                             unsigned long long *__restrict__ best, uint32_t *__restrict__ cnt, uint32_t *__restrict__ ipt,
+                             uint32_t *__restrict__ coll) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = seg[i] - 1, t = vs[i];
+  const bool head = i == 0 || ks[i] != ks[i - 1];
+  if (head) seg_first[s] = (uint32_t)i;
+  else if (!same_ip(A, t, vs[i - 1])) atomicOr(&coll[s], 1u);
+  const int32_t d = A.trips[t].decision;
+  atomicMax(&best[s], ((unsigned long long)(uint32_t)d << 32) | (0xFFFFFFFFull - t));
+  atomicAdd(&cnt[s], 1u);
+  if (d == 4) atomicOr(&ipt[s], 1u);
+}
+
+__global__ void k_ban_out(uint64_t n_seg, const unsigned long long *__restrict__ best, const uint32_t *__restrict__ cnt,
+                          const uint32_t *__restrict__ ipt, const uint32_t *__restrict__ coll, int64_t expires,
+                          uint8_t *__restrict__ rep_flag, bjx_ip_decision *__restrict__ rep) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_seg || coll[s]) return;
+  const uint32_t t = 0xFFFFFFFFu - (uint32_t)(best[s] & 0xFFFFFFFFull);
+  bjx_ip_decision r;
+  r.trip_idx = t;
+  r.n_trips = cnt[s];
+  r.expires_ns = expires;
+  r.decision = (int32_t)(best[s] >> 32);
+  r.iptables = ipt[s];
+  rep[t] = r;
+  rep_flag[t] = 1;
+}
+
+// hash runs holding more than one IP: one lane per run groups its trips by
+// their bytes (trip order within the run, O(run^2); 64-bit collisions only)
+__global__ void k_ban_collide(BanDev A, uint64_t n, uint64_t n_seg, const uint32_t *__restrict__ vs,
+                              const uint32_t *__restrict__ seg_first, const uint32_t *__restrict__ coll, int64_t expires,
+                              uint8_t *__restrict__ rep_flag, bjx_ip_decision *__restrict__ rep) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_seg || !coll[s]) return;
+  const uint64_t b = seg_first[s], e = s + 1 < n_seg ? seg_first[s + 1] : n;
+  for (uint64_t i = b; i < e; ++i) {
+    bool leader = true;
+    for (uint64_t k = b; k < i && leader; ++k) leader = !same_ip(A, vs[i], vs[k]);
+    if (!leader) continue;
+    uint32_t bt = vs[i], nt = 0, ip4 = 0;
+    int32_t bd = -1;
+    for (uint64_t k = i; k < e; ++k) {
+      const uint32_t t = vs[k];
+      if (k != i && !same_ip(A, vs[i], t)) continue;
+      const int32_t d = A.trips[t].decision;
+      if (d > bd || (d == bd && t < bt)) { bd = d; bt = t; }
+      ++nt;
+      ip4 |= d == 4 ? 1u : 0u;
+    }
+    bjx_ip_decision r;
+    r.trip_idx = bt; r.n_trips = nt; r.expires_ns = expires; r.decision = bd; r.iptables = ip4;
+    rep[bt] = r;
+    rep_flag[bt] = 1;
+  }
+}
+
 __global__ void k_scatter_rl(uint64_t n_ev, const uint32_t *__restrict__ ev_res, const uint8_t *__restrict__ ev_out,
                              uint8_t *__restrict__ rl_out) {
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2119,6 +2229,7 @@ struct BatchCtx {
   uint64_t n_lines = 0, n_res = 0, n_ev = 0;
   uint64_t n_el = 0, el_bytes = 0;  // lines with events, their IP bytes
   uint64_t consumed = 0;
+  int64_t now_ns = 0;
   Lines L{};
   bool live = false;
 };
@@ -2198,6 +2309,25 @@ struct bjx_engine {
   uint32_t pk_parts = 0;
   uint64_t pk_n_ev = 0;
   bool partitioned = false;
+
+  // trip -> decision emission (bjx_engine_set_ban_options / bjx_batch_bans)
+  int64_t ban_ttl_ns = 0;
+  int32_t ban_tz = 0;
+  DevBuf<uint64_t> dl_hash; DevBuf<uint32_t> dl_off, dl_len; DevBuf<uint8_t> dl_bytes;
+  uint32_t n_dl = 0;
+  DevBuf<uint32_t> nm_off; DevBuf<uint8_t> nm_json;
+  size_t nm_built = 0;
+  DevBuf<uint64_t> bn_key, bn_key2, bn_len, bn_off;
+  DevBuf<uint32_t> bn_val, bn_val2, bn_head, bn_seg, bn_first, bn_cnt, bn_ipt, bn_coll;
+  DevBuf<unsigned long long> bn_best;
+  DevBuf<uint8_t> bn_kind, bn_flag, bn_log;
+  DevBuf<bjx_ip_decision> bn_rep, bn_sel;
+  bool ban_emitted = false;
+  uint64_t ban_n_trips = 0;
+  HostBuf<bjx_ip_decision> ban_ips;
+  HostBuf<char> ban_log;
+  HostBuf<uint64_t> ban_off;
+  HostBuf<uint8_t> ban_kind;
 
   // host copies of the last batch
   HostBuf<bjx_trip> trips;
@@ -2977,6 +3107,12 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
                   &e->rx_hash, &e->rx_pos, &e->rx_nev, &e->rx_evoff})
     b->release();
   e->rx_ts.release(); e->trip_idx.release(); e->d_trips.release();
+  for (auto *b : {&e->bn_key, &e->bn_key2, &e->bn_len, &e->bn_off, &e->dl_hash}) b->release();
+  for (auto *b : {&e->bn_val, &e->bn_val2, &e->bn_head, &e->bn_seg, &e->bn_first, &e->bn_cnt, &e->bn_ipt, &e->bn_coll,
+                  &e->dl_off, &e->dl_len, &e->nm_off})
+    b->release();
+  for (auto *b : {&e->bn_kind, &e->bn_flag, &e->bn_log, &e->dl_bytes, &e->nm_json}) b->release();
+  e->bn_best.release(); e->bn_rep.release(); e->bn_sel.release();
   e->d_results.release(); e->q_out.release();
   e->long_list.release(); e->l_ip16.release(); e->jline.release(); e->jkey.release(); e->jline2.release(); e->jkey2.release(); e->l_cand.release(); e->l_ccnt.release();
   (void)hipEventDestroy(e->ev0); (void)hipEventDestroy(e->ev1); (void)hipEventDestroy(e->evm0); (void)hipEventDestroy(e->evm1);
@@ -3319,6 +3455,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   BatchCtx &c = e->bc;
   c.buf = buf; c.n_lines = n_lines; c.n_res = n_res; c.n_ev = n_ev; c.L = L; c.n_el = bnd[0]; c.el_bytes = bnd[1];
   c.consumed = out->consumed_bytes;
+  c.now_ns = now_ns;
   c.live = true;
   return true;
 }
@@ -3332,6 +3469,109 @@ static EvSrc local_evsrc(bjx_engine *e) {
   return E;
 }
 
+// escaped JSON of every interned rule name (LogRegexBan "trigger"), rebuilt
+// when reloads intern new names
+static void ensure_name_json(bjx_engine *e) {
+  if (e->nm_built == e->names.size() && e->nm_off.p) return;
+  std::vector<uint32_t> off;
+  std::vector<uint8_t> js;
+  for (const auto &nm : e->names) {
+    off.push_back((uint32_t)js.size());
+    const uint8_t *b = reinterpret_cast<const uint8_t *>(nm.data());
+    JOut<false> c{nullptr, 0};
+    json_str(c, b, (uint32_t)nm.size());
+    const size_t at = js.size();
+    js.resize(at + c.n);
+    JOut<true> w{js.data() + at, 0};
+    json_str(w, b, (uint32_t)nm.size());
+  }
+  off.push_back((uint32_t)js.size());
+  e->nm_off.ensure(off.size());
+  e->nm_json.ensure(js.size() + 16);
+  HIP_OK(hipMemcpy(e->nm_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+  if (!js.empty()) HIP_OK(hipMemcpy(e->nm_json.p, js.data(), js.size(), hipMemcpyHostToDevice));
+  e->nm_built = e->names.size();
+}
+
+// decision updates (one per tripped IP) and LogRegexBan lines of the batch's
+// n trips (e->d_trips), copied to pinned host buffers (bans.h)
+static void emit_bans(bjx_engine *e, uint64_t n) {
+  hipStream_t st = e->stream;
+  ensure_name_json(e);
+  BanDev A{};
+  A.buf = e->bc.buf; A.trips = e->d_trips.p; A.n_trips = n; A.rules = e->bind.rules;
+  A.name_off = e->nm_off.p; A.name_json = e->nm_json.p;
+  A.dl_hash = e->dl_hash.p; A.dl_off = e->dl_off.p; A.dl_len = e->dl_len.p; A.dl_bytes = e->dl_bytes.p; A.n_dl = e->n_dl;
+  A.tz_offset_s = e->ban_tz;
+  const int64_t expires = (int64_t)((uint64_t)e->bc.now_ns + (uint64_t)e->ban_ttl_ns);
+  // ban-log lines: lengths, offsets, bytes
+  e->bn_len.ensure(n + 1); e->bn_off.ensure(n + 1); e->bn_kind.ensure(n);
+  hipLaunchKernelGGL(k_ban_len, dim3(grid_for(n + 1)), dim3(kBlock), 0, st, A, e->bn_len.p, e->bn_kind.p);
+  HIP_OK(hipGetLastError());
+  {
+    uint64_t *in = e->bn_len.p, *o = e->bn_off.p;
+    cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)(n + 1), st); });
+  }
+  e->ban_off.resize(n + 1);
+  e->ban_kind.resize(n);
+  HIP_OK(hipMemcpyAsync(e->ban_off.data(), e->bn_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(e->ban_kind.data(), e->bn_kind.p, n, hipMemcpyDeviceToHost, st));
+  // per-IP escalation: sort trips by IP hash (stable: trip order within a run)
+  e->bn_key.ensure(n); e->bn_key2.ensure(n); e->bn_val.ensure(n); e->bn_val2.ensure(n); e->bn_head.ensure(n);
+  e->bn_seg.ensure(n);
+  hipLaunchKernelGGL(k_ban_keys, dim3(grid_for(n)), dim3(kBlock), 0, st, A, e->dbg_hash_mask ? e->dbg_hash_mask : ~0ull,
+                     e->bn_key.p, e->bn_val.p);
+  HIP_OK(hipGetLastError());
+  {
+    uint64_t *ki = e->bn_key.p, *ko = e->bn_key2.p;
+    uint32_t *vi = e->bn_val.p, *vo = e->bn_val2.p;
+    cub_call(e, [&](void *tmp, size_t &bytes) {
+      return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)n, 0, 64, st);
+    });
+  }
+  hipLaunchKernelGGL(k_ban_heads, dim3(grid_for(n)), dim3(kBlock), 0, st, n, e->bn_key2.p, e->bn_head.p);
+  {
+    uint32_t *in = e->bn_head.p, *o = e->bn_seg.p;
+    cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceScan::InclusiveSum(tmp, bytes, in, o, (int)n, st); });
+  }
+  uint32_t n_seg = 0;
+  HIP_OK(hipMemcpyAsync(&n_seg, e->bn_seg.p + (n - 1), 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  const uint64_t log_bytes = e->ban_off.data()[n];
+  e->bn_log.ensure(log_bytes + 16);
+  hipLaunchKernelGGL(k_ban_write, dim3(grid_for(n)), dim3(kBlock), 0, st, A, e->bn_off.p, e->bn_log.p);
+  HIP_OK(hipGetLastError());
+  e->ban_log.resize(log_bytes);
+  if (log_bytes) HIP_OK(hipMemcpyAsync(e->ban_log.data(), e->bn_log.p, log_bytes, hipMemcpyDeviceToHost, st));
+  e->bn_first.ensure(n_seg); e->bn_cnt.ensure(n_seg); e->bn_ipt.ensure(n_seg); e->bn_coll.ensure(n_seg);
+  e->bn_best.ensure(n_seg); e->bn_flag.ensure(n); e->bn_rep.ensure(n); e->bn_sel.ensure(n);
+  HIP_OK(hipMemsetAsync(e->bn_cnt.p, 0, n_seg * 4ull, st));
+  HIP_OK(hipMemsetAsync(e->bn_ipt.p, 0, n_seg * 4ull, st));
+  HIP_OK(hipMemsetAsync(e->bn_coll.p, 0, n_seg * 4ull, st));
+  HIP_OK(hipMemsetAsync(e->bn_best.p, 0, n_seg * 8ull, st));
+  HIP_OK(hipMemsetAsync(e->bn_flag.p, 0, n, st));
+  hipLaunchKernelGGL(k_ban_reduce, dim3(grid_for(n)), dim3(kBlock), 0, st, A, n, e->bn_key2.p, e->bn_val2.p, e->bn_seg.p,
+                     e->bn_first.p, e->bn_best.p, e->bn_cnt.p, e->bn_ipt.p, e->bn_coll.p);
+  hipLaunchKernelGGL(k_ban_out, dim3(grid_for(n_seg)), dim3(kBlock), 0, st, (uint64_t)n_seg, e->bn_best.p, e->bn_cnt.p,
+                     e->bn_ipt.p, e->bn_coll.p, expires, e->bn_flag.p, e->bn_rep.p);
+  hipLaunchKernelGGL(k_ban_collide, dim3(grid_for(n_seg)), dim3(kBlock), 0, st, A, n, (uint64_t)n_seg, e->bn_val2.p,
+                     e->bn_first.p, e->bn_coll.p, expires, e->bn_flag.p, e->bn_rep.p);
+  HIP_OK(hipGetLastError());
+  {
+    const bjx_ip_decision *in = e->bn_rep.p;
+    const uint8_t *fl = e->bn_flag.p;
+    bjx_ip_decision *o = e->bn_sel.p;
+    unsigned long long *cnt = e->scalars.p + 5;
+    cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceSelect::Flagged(tmp, bytes, in, fl, o, cnt, (int)n, st); });
+  }
+  unsigned long long n_ips = 0;
+  HIP_OK(hipMemcpyAsync(&n_ips, e->scalars.p + 5, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  e->ban_ips.resize(n_ips);
+  if (n_ips) HIP_OK(hipMemcpyAsync(e->ban_ips.data(), e->bn_sel.p, n_ips * sizeof(bjx_ip_decision), hipMemcpyDeviceToHost, st));
+  e->ban_n_trips = n;
+}
+
 // Trips (reference order) and the optional per-line / RuleResult copies, once
 // e->ev_out holds every local event's Apply outcome (phases 7-8).
 static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, bool sorted) {
@@ -3341,6 +3581,9 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
   const uint64_t n_lines = c.n_lines, n_res = c.n_res, n_ev = c.n_ev;
   const Lines &L = c.L;
   uint64_t n_trips = 0;
+  e->ban_emitted = (flags & BJX_EMIT_BANS) != 0;
+  e->ban_n_trips = 0;
+  e->ban_ips.resize(0); e->ban_log.resize(0); e->ban_off.resize(1); e->ban_off.data()[0] = 0; e->ban_kind.resize(0);
   if (n_ev) {
     mark(e, 7);
     // trips: Exceeded outcomes.  sorted: outcomes in state-slot order (this
@@ -3377,6 +3620,7 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
       HIP_OK(hipGetLastError());
       e->trips.resize(n_trips);
       HIP_OK(hipMemcpyAsync(e->trips.data(), e->d_trips.p, n_trips * sizeof(bjx_trip), hipMemcpyDeviceToHost, st));
+      if (flags & BJX_EMIT_BANS) emit_bans(e, n_trips);
     }
     if (flags & BJX_COPY_RESULTS) {
       if (sorted)
@@ -3611,6 +3855,59 @@ extern "C" int bjx_finish_batch(bjx_engine *e, const uint8_t *d_outcomes, uint32
     out->n_events = c.n_ev;
     finish_phase(e, flags, out, false);
     e->partitioned = false;
+    return BJX_OK;
+  });
+}
+
+extern "C" int bjx_engine_set_ban_options(bjx_engine *e, const bjx_ban_options *o) {
+  if (!o || (o->n_disable_logging && !o->disable_logging)) return BJX_ERR_ARG;
+  return guarded(e, [&]() -> int {
+    e->ban_ttl_ns = o->expiring_ttl_ns;
+    e->ban_tz = o->tz_offset_s;
+    std::vector<std::pair<uint64_t, std::string>> hs;
+    for (size_t i = 0; i < o->n_disable_logging; ++i) {
+      const bjx_str &h = o->disable_logging[i];
+      if (h.len && !h.ptr) return BJX_ERR_ARG;
+      std::string x(h.ptr ? h.ptr : "", h.len);
+      std::vector<uint8_t> pad(x.begin(), x.end());
+      pad.resize(x.size() + 8, 0);
+      hs.emplace_back(hash_bytes(pad.data(), (uint32_t)x.size()), x);
+    }
+    std::sort(hs.begin(), hs.end());
+    hs.erase(std::unique(hs.begin(), hs.end()), hs.end());
+    std::vector<uint64_t> hh;
+    std::vector<uint32_t> off, len;
+    std::vector<uint8_t> by;
+    for (auto &p : hs) {
+      hh.push_back(p.first);
+      off.push_back((uint32_t)by.size());
+      len.push_back((uint32_t)p.second.size());
+      by.insert(by.end(), p.second.begin(), p.second.end());
+    }
+    e->n_dl = (uint32_t)hs.size();
+    e->dl_hash.ensure(hh.size()); e->dl_off.ensure(off.size()); e->dl_len.ensure(len.size()); e->dl_bytes.ensure(by.size() + 16);
+    if (!hs.empty()) {
+      HIP_OK(hipMemcpy(e->dl_hash.p, hh.data(), hh.size() * 8, hipMemcpyHostToDevice));
+      HIP_OK(hipMemcpy(e->dl_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+      HIP_OK(hipMemcpy(e->dl_len.p, len.data(), len.size() * 4, hipMemcpyHostToDevice));
+      if (!by.empty()) HIP_OK(hipMemcpy(e->dl_bytes.p, by.data(), by.size(), hipMemcpyHostToDevice));
+    }
+    return BJX_OK;
+  });
+}
+
+extern "C" int bjx_batch_bans(bjx_engine *e, bjx_ban_batch *out) {
+  if (!out) return BJX_ERR_ARG;
+  return guarded(e, [&]() -> int {
+    memset(out, 0, sizeof *out);
+    if (!e->ban_emitted) throw BjxError(BJX_ERR_ARG, "bjx_batch_bans: the last batch ran without BJX_EMIT_BANS");
+    out->n_ips = e->ban_ips.size();
+    out->ips = out->n_ips ? e->ban_ips.data() : nullptr;
+    out->n_trips = e->ban_n_trips;
+    out->log_bytes = e->ban_n_trips ? e->ban_off.data()[e->ban_n_trips] : 0;
+    out->log = out->log_bytes ? e->ban_log.data() : nullptr;
+    out->log_off = e->ban_off.data();
+    out->log_kind = e->ban_n_trips ? e->ban_kind.data() : nullptr;
     return BJX_OK;
   });
 }

@@ -52,6 +52,34 @@ class BatchOutput:
         return self._results
 
 
+class BanBatch:
+    """Host view of bjx_batch_bans: per-IP decision updates (trip order of
+    their representative trip) and the LogRegexBan lines of the batch."""
+
+    def __init__(self, bb: _lib.BanBatch):
+        import numpy as np
+        self.n_ips = bb.n_ips
+        self.n_trips = bb.n_trips
+        if bb.n_ips:
+            arr = (_lib.IpDecision * bb.n_ips).from_address(C.addressof(bb.ips.contents))
+            self.ips = np.ctypeslib.as_array(arr).copy()
+        else:
+            self.ips = np.zeros(0, dtype=np.dtype(_lib.IpDecision))
+        self.log = C.string_at(bb.log, bb.log_bytes) if bb.log_bytes else b""
+        n = bb.n_trips
+        self.log_off = np.ctypeslib.as_array(bb.log_off, shape=(n + 1,)).copy() if n else np.zeros(1, np.uint64)
+        self.log_kind = np.ctypeslib.as_array(bb.log_kind, shape=(n,)).copy() if n else np.zeros(0, np.uint8)
+
+    def lines(self):
+        """(kind, line without '\\n') per trip that logs (kind 1 Logger, 2 LoggerTemp)."""
+        out = []
+        for t in range(self.n_trips):
+            k = int(self.log_kind[t])
+            if k:
+                out.append((k, self.log[int(self.log_off[t]):int(self.log_off[t + 1]) - 1]))
+        return out
+
+
 class Engine:
     def __init__(self, device: int = 0, ip_capacity: int = 0, state_capacity: int = 0, ip_arena_bytes: int = 0):
         L = _lib.lib()
@@ -82,12 +110,32 @@ class Engine:
             arr[i] = _lib.DecisionEntry(s, dec, ipb)
         self._check(_lib.lib().bjx_engine_set_decision_lists(self._h, arr, len(entries)), "set_decision_lists")
 
+    def set_ban_options(self, expiring_ttl_s: int, disable_logging: Iterable[str] = (), tz_offset_s: int = 0):
+        """Banner settings of the device decision emission (bjx_engine_set_ban_options)."""
+        hosts = [h for h in disable_logging]
+        arr = (_lib.Str * max(1, len(hosts)))()
+        keep = []
+        for i, h in enumerate(hosts):
+            arr[i] = _lib.mkstr(h)
+            keep.append(arr[i])
+        ttl = (int(expiring_ttl_s) * 1_000_000_000) & ((1 << 64) - 1)
+        if ttl >= 1 << 63:
+            ttl -= 1 << 64
+        o = _lib.BanOptions(ttl, tz_offset_s, 0, arr, len(hosts))
+        self._check(_lib.lib().bjx_engine_set_ban_options(self._h, C.byref(o)), "set_ban_options")
+
+    def bans(self) -> BanBatch:
+        """Decision updates and ban-log lines of the last batch (run with emit_bans)."""
+        bb = _lib.BanBatch()
+        self._check(_lib.lib().bjx_batch_bans(self._h, C.byref(bb)), "batch_bans")
+        return BanBatch(bb)
+
     def process(self, rs: Ruleset, data, now_ns: int, copy_results: bool = False, device_ptr: Optional[int] = None,
-                nbytes: Optional[int] = None) -> BatchOutput:
+                nbytes: Optional[int] = None, emit_bans: bool = False) -> BatchOutput:
         """consumeLine over every complete line of `data` (bytes) or of a device
         buffer (device_ptr, nbytes) already resident in HBM."""
         res = _lib.BatchResult()
-        flags = _lib.COPY_RESULTS if copy_results else 0
+        flags = (_lib.COPY_RESULTS if copy_results else 0) | (_lib.EMIT_BANS if emit_bans else 0)
         if device_ptr is not None:
             rc = _lib.lib().bjx_process_batch(self._h, rs.handle, C.c_void_p(device_ptr), nbytes, now_ns,
                                               flags | _lib.INPUT_DEVICE, C.byref(res))
@@ -126,9 +174,9 @@ class Engine:
                                                 C.c_void_p(bytes_ptr), len(src_counts), arr, C.c_void_p(out_ptr)),
                     "apply_events")
 
-    def finish(self, outcomes_ptr: int, copy_results: bool = False) -> BatchOutput:
+    def finish(self, outcomes_ptr: int, copy_results: bool = False, emit_bans: bool = False) -> BatchOutput:
         res = _lib.BatchResult()
-        flags = _lib.COPY_RESULTS if copy_results else 0
+        flags = (_lib.COPY_RESULTS if copy_results else 0) | (_lib.EMIT_BANS if emit_bans else 0)
         self._check(_lib.lib().bjx_finish_batch(self._h, C.c_void_p(outcomes_ptr), flags, C.byref(res)),
                     "finish_batch")
         return BatchOutput(res, copy_results)

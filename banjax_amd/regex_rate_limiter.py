@@ -158,9 +158,9 @@ def _trim_space(s: bytes) -> bytes:
     return s
 
 
-def format_time(ns: int) -> str:
-    """logTime.Format("2006-01-02T15:04:05") in UTC (injected time zone)."""
-    sec = ns // 1_000_000_000
+def format_time(ns: int, tz_offset_s: int = 0) -> str:
+    """logTime.Format("2006-01-02T15:04:05") in a fixed zone (injected; UTC by default)."""
+    sec = ns // 1_000_000_000 + tz_offset_s
     d = _dt.datetime(1970, 1, 1) + _dt.timedelta(seconds=sec)
     return "%04d-%02d-%02dT%02d:%02d:%02d" % (d.year, d.month, d.day, d.hour, d.minute, d.second)
 
@@ -211,6 +211,7 @@ class Banner:
         self.ban_log_temp: List[str] = []  # LoggerTemp lines (disable_logging hosts)
         self.ipset: List[str] = []        # IPs an iptables ban would add (standalone: none)
         self.standalone = True
+        self.tz_offset_s = 0              # local zone of LogRegexBan's timestring (seconds east of UTC)
 
     def ban_or_challenge_ip(self, cfg: Config, ip: str, decision: int, domain: str, now_ns: int):
         expires = (now_ns + cfg.expiring_decision_ttl_seconds * 1_000_000_000) & ((1 << 64) - 1)
@@ -229,7 +230,7 @@ class Banner:
         ua = _trim_space(words[5].split(b"|", 1)[0])
         parts = [
             '"path":' + _go_json_string(words[3]),
-            '"timestring":' + _go_json_string(format_time(log_time_ns).encode()),
+            '"timestring":' + _go_json_string(format_time(log_time_ns, self.tz_offset_s).encode()),
             '"trigger":' + _go_json_string(rule_name.encode()),
             '"client_ua":' + _go_json_string(ua),
             '"client_ip":' + _go_json_string(ip),
@@ -245,6 +246,28 @@ class Banner:
         (self.ban_log_temp if disable else self.ban_log).append(line)
 
 
+    def apply_device_bans(self, cfg: Config, bans, trips, data):
+        """The batch's device-emitted decision updates (one Update per tripped IP,
+        same final lists as the per-trip BanOrChallengeIp replay) and ban-log lines."""
+        for rec in bans.ips:
+            t = trips[int(rec["trip_idx"])]
+            line = bytes(data[t.line_offset:t.line_offset + t.line_len])
+            ip = line[t.ip_off:t.ip_off + t.ip_len].decode("utf-8", "surrogateescape")
+            host = line[t.host_off:t.host_off + t.host_len].decode("utf-8", "surrogateescape")
+            self.decision_lists.update(ip, int(rec["expires_ns"]), int(rec["decision"]), False, host)
+            if rec["iptables"] and ip != "127.0.0.1" and not self.standalone:
+                self.ipset.append(ip)
+        for kind, text in bans.lines():
+            (self.ban_log_temp if kind == 2 else self.ban_log).append(text.decode("utf-8"))
+        if trips:
+            t = trips[-1]
+            line = bytes(data[t.line_offset:t.line_offset + t.line_len])
+            self.last_banned(line[t.ip_off:t.ip_off + t.ip_len].decode("utf-8", "surrogateescape"))
+
+    def last_banned(self, ip: str):
+        pass
+
+
 class MockBanner(Banner):
     """regex_rate_limiter_test.go:27-75: records the last banned IP."""
 
@@ -255,6 +278,9 @@ class MockBanner(Banner):
     def ban_or_challenge_ip(self, cfg, ip, decision, domain, now_ns):
         self.banned_ip = ip
         super().ban_or_challenge_ip(cfg, ip, decision, domain, now_ns)
+
+    def last_banned(self, ip: str):
+        self.banned_ip = ip
 
 
 # ------------------------------------------------------------ the tailer
@@ -286,9 +312,16 @@ class RegexRateLimiter:
     """Owns the config snapshot, its compiled ruleset and the engine; the
     equivalent of RunLogTailer's loop body over a batch of lines."""
 
-    def __init__(self, cfg: Config, engine: Optional[Engine] = None, banner: Optional[Banner] = None):
+    def __init__(self, cfg: Config, engine: Optional[Engine] = None, banner: Optional[Banner] = None,
+                 device_bans: bool = False, tz_offset_s: int = 0):
+        """device_bans: the engine emits one decision update per tripped IP and
+        the formatted ban-log lines (bjx_batch_bans) instead of
+        the per-trip Banner replay on the host."""
         self.engine = engine or Engine()
         self.banner = banner or MockBanner()
+        self.device_bans = device_bans
+        self.tz_offset_s = tz_offset_s
+        self.banner.tz_offset_s = tz_offset_s
         self._seen_names: Dict[str, None] = {}
         self.states = RegexRateLimitStates(self.engine, lambda: list(self._seen_names))
         self.reload(cfg)
@@ -301,10 +334,12 @@ class RegexRateLimiter:
         for r in rs.rules:
             self._seen_names.setdefault(r.rule, None)
         self.engine.set_decision_lists(cfg.decision_entries)
+        self.engine.set_ban_options(cfg.expiring_decision_ttl_seconds,
+                                    [h for h, v in cfg.disable_logging.items() if v], self.tz_offset_s)
 
     def consume_lines(self, data: bytes, now_ns: int, want_results: bool = True):
         """consumeLine for every complete line; returns (results, batch output)."""
-        out = self.engine.process(self.ruleset, data, now_ns, copy_results=want_results)
+        out = self.engine.process(self.ruleset, data, now_ns, copy_results=want_results, emit_bans=self.device_bans)
         return self._finish(data, out, now_ns, want_results)
 
     def consume_device_batch(self, host_view, device_ptr: Optional[int], nbytes: int, now_ns: int,
@@ -312,15 +347,32 @@ class RegexRateLimiter:
         """consumeLine over a batch already in HBM (the tailer's copy); host_view
         holds the same bytes for the Banner's log lines.  device_ptr None: host."""
         if device_ptr is None:
-            out = self.engine.process(self.ruleset, bytes(host_view[:nbytes]), now_ns, copy_results=want_results)
+            out = self.engine.process(self.ruleset, bytes(host_view[:nbytes]), now_ns, copy_results=want_results,
+                                      emit_bans=self.device_bans)
         else:
             out = self.engine.process(self.ruleset, None, now_ns, copy_results=want_results, device_ptr=device_ptr,
-                                      nbytes=nbytes)
+                                      nbytes=nbytes, emit_bans=self.device_bans)
         return self._finish(host_view, out, now_ns, want_results)
 
     def _finish(self, data, out, now_ns: int, want_results: bool):
         """Banner replay of the trips in reference order (regex_rate_limiter.go:254-266)
         and, if asked, the ConsumeLineResults."""
+        rules = self.ruleset.rules
+        if self.device_bans:
+            self.banner.apply_device_bans(self.config, self.engine.bans(), out.trips, data)
+        else:
+            self._replay_trips(data, out, now_ns)
+        if not want_results:
+            return None, out
+        results = [ConsumeLineResult(error=bool(f & LINE_ERROR), old_line=bool(f & LINE_OLD),
+                                     exempted=bool(f & LINE_EXEMPTED)) for f in out.line_flags]
+        for r in out.results:
+            results[r.line_idx].rule_results.append(RuleResult(
+                rule_name=rules[r.rule_idx].rule, regex_match=True, skip_host=bool(r.skip_host),
+                seen_ip=bool(r.seen_ip), rate_limit_result=RateLimitResult(r.match_type, bool(r.exceeded))))
+        return results, out
+
+    def _replay_trips(self, data, out, now_ns: int):
         rules = self.ruleset.rules
         for t in out.trips:
             line = bytes(data[t.line_offset:t.line_offset + t.line_len])
@@ -331,15 +383,6 @@ class RegexRateLimiter:
             self.banner.ban_or_challenge_ip(self.config, ip.decode("utf-8", "surrogateescape"), rule.decision,
                                             host.decode("utf-8", "surrogateescape"), now_ns)
             self.banner.log_regex_ban(self.config, t.ts_ns, ip, rule.rule, rest, rule.decision)
-        if not want_results:
-            return None, out
-        results = [ConsumeLineResult(error=bool(f & LINE_ERROR), old_line=bool(f & LINE_OLD),
-                                     exempted=bool(f & LINE_EXEMPTED)) for f in out.line_flags]
-        for r in out.results:
-            results[r.line_idx].rule_results.append(RuleResult(
-                rule_name=rules[r.rule_idx].rule, regex_match=True, skip_host=bool(r.skip_host),
-                seen_ip=bool(r.seen_ip), rate_limit_result=RateLimitResult(r.match_type, bool(r.exceeded))))
-        return results, out
 
 
 def consume_line(limiter: RegexRateLimiter, text: str, now_ns: int) -> ConsumeLineResult:

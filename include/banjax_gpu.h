@@ -151,7 +151,8 @@ typedef struct bjx_trip {
 
 enum bjx_batch_flags {
   BJX_INPUT_DEVICE = 1,   /* bytes is a device pointer already resident in HBM */
-  BJX_COPY_RESULTS = 2    /* also copy per-line flags and RuleResults to host memory */
+  BJX_COPY_RESULTS = 2,   /* also copy per-line flags and RuleResults to host memory */
+  BJX_EMIT_BANS = 4       /* also build the batch's decision updates and ban-log lines (bjx_batch_bans) */
 };
 
 typedef struct bjx_batch_result {
@@ -265,6 +266,48 @@ void bjx_tailer_close(bjx_tailer *t);
 
 /* Last error message of an engine call. */
 const char *bjx_engine_last_error(bjx_engine *e);
+/* ---- Trip -> decision emission.  Replaces the per-trip
+   host replay of Banner.BanOrChallengeIp -> DynamicDecisionLists.Update
+   (internal/iptables.go:273-294, internal/decision.go:404-439) and
+   Banner.LogRegexBan (internal/iptables.go:179-228) that consumeLine runs for
+   every trip (internal/regex_rate_limiter.go:254-266).
+   Options hold for every later batch run with BJX_EMIT_BANS. */
+typedef struct bjx_ban_options {
+  int64_t expiring_ttl_ns;          /* expiring_decision_ttl_seconds * 1e9 (config.go) */
+  int32_t tz_offset_s;              /* local time zone of LogRegexBan's timestring, seconds east of UTC */
+  uint32_t _pad;
+  const bjx_str *disable_logging;   /* config.DisableLogging hosts set to true (LoggerTemp lines) */
+  size_t n_disable_logging;
+} bjx_ban_options;
+int bjx_engine_set_ban_options(bjx_engine *e, const bjx_ban_options *opts);
+
+/* One per distinct IP that tripped in the batch.  Applying
+   Update(ip, expires_ns, decision, fromBaskerville=false, domain) once per
+   record, with ip / domain (host) taken from trips[trip_idx], leaves the
+   decision lists exactly as the per-trip replay does: the entry changes only
+   when decision beats the one held, and the first trip with the IP's highest
+   decision is the last strict escalation.  iptables: some trip decided
+   IptablesBlock (banIp, which the reference calls per such trip). */
+typedef struct bjx_ip_decision {
+  uint64_t trip_idx;
+  uint64_t n_trips;     /* trips of this IP in the batch */
+  int64_t expires_ns;   /* now_ns + expiring_ttl_ns (Go wrapping add) */
+  int32_t decision;     /* highest decision over the IP's trips */
+  uint32_t iptables;
+} bjx_ip_decision;
+
+typedef struct bjx_ban_batch {
+  uint64_t n_ips;
+  const bjx_ip_decision *ips;   /* host, ordered by trip_idx */
+  uint64_t n_trips;
+  const char *log;              /* host: LogRegexBan lines in trip order, each ending in '\n' */
+  uint64_t log_bytes;
+  const uint64_t *log_off;      /* host, n_trips + 1: trip t's line is log[log_off[t], log_off[t+1]) (empty: < 6 words) */
+  const uint8_t *log_kind;      /* host, n_trips: 0 no line, 1 Logger, 2 LoggerTemp (disable_logging host) */
+} bjx_ban_batch;
+/* The last batch's emission (valid until the next batch; needs BJX_EMIT_BANS). */
+int bjx_batch_bans(bjx_engine *e, bjx_ban_batch *out);
+
 int bjx_abi_version(void);
 
 #ifdef __cplusplus

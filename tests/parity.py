@@ -31,13 +31,13 @@ def oracle_config(cfg: Config) -> O.Config:
 class Pair:
     """An oracle and an engine fed identical batches."""
 
-    def __init__(self, cfg_yaml: str, engine: Engine = None):
+    def __init__(self, cfg_yaml: str, engine: Engine = None, device_bans: bool = False):
         self.cfg = Config.from_yaml(cfg_yaml)
         self.ocfg = oracle_config(self.cfg)
         self.ost = O.State()
         self.engine = engine or Engine()
         self.engine.state_clear()
-        self.lim = RegexRateLimiter(self.cfg, engine=self.engine, banner=MockBanner())
+        self.lim = RegexRateLimiter(self.cfg, engine=self.engine, banner=MockBanner(), device_bans=device_bans)
         self.n_rules = len(self.cfg.all_rules())
 
     def feed(self, data: bytes, now_ns: int, check=True):

@@ -1,0 +1,50 @@
+"""CPU checks of the decision-emission algebra the device relies on (SURVEY.md
+§8 f3; bans.h): for every IP, replaying DynamicDecisionLists.Update
+(internal/decision.go:404-439) once per trip in order leaves the same entry as
+one Update with the IP's highest decision taken from the first trip that
+reached it — whatever entry the IP held before the batch.  Plus the fixed-zone
+timestring of LogRegexBan (internal/iptables.go:189).
+"""
+import datetime as dt
+import random
+
+import pytest
+
+from banjax_amd.regex_rate_limiter import DynamicDecisionLists, format_time
+
+
+def per_ip_records(trips):
+    """What k_ban_reduce / k_ban_out compute: ip -> (first trip with max decision, max decision)."""
+    best = {}
+    for t, (ip, dec, dom) in enumerate(trips):
+        if ip not in best or dec > best[ip][1]:
+            best[ip] = (t, dec)
+    return best
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_one_update_per_ip_equals_per_trip_replay(seed):
+    rnd = random.Random(seed)
+    ips = ["10.0.0.%d" % i for i in range(rnd.randrange(1, 8))]
+    pre = {ip: (rnd.randrange(1, 5), "old.com") for ip in ips if rnd.random() < 0.5}
+    trips = [(rnd.choice(ips), rnd.randrange(1, 5), "d%d.com" % rnd.randrange(4)) for _ in range(rnd.randrange(1, 60))]
+    expires = 123456789
+
+    seq, once = DynamicDecisionLists(), DynamicDecisionLists()
+    for lists in (seq, once):
+        for ip, (d, dom) in pre.items():
+            lists.update(ip, 1, d, True, dom)
+    for ip, dec, dom in trips:
+        seq.update(ip, expires, dec, False, dom)
+    for ip, (t, dec) in sorted(per_ip_records(trips).items(), key=lambda kv: kv[1][0]):
+        once.update(ip, expires, dec, False, trips[t][2])
+    assert seq.expiring == once.expiring
+
+
+@pytest.mark.parametrize("ns,tz", [(1700000000_123456789, 0), (1700000000_999999999, 19800), (-1, 0), (-1_500_000_000, -3600),
+                                   (0, 50400), (951782400_000000000, 0), (4102444799_000000000, -43200)])
+def test_format_time_fixed_zone(ns, tz):
+    sec = ns // 1_000_000_000
+    want = (dt.datetime(1970, 1, 1, tzinfo=dt.timezone.utc) + dt.timedelta(seconds=sec)).astimezone(
+        dt.timezone(dt.timedelta(seconds=tz))).strftime("%Y-%m-%dT%H:%M:%S")
+    assert format_time(ns, tz) == want

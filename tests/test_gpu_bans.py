@@ -1,0 +1,125 @@
+"""GPU parity of the device decision emission: the engine's
+per-IP decision updates and formatted LogRegexBan lines (bjx_batch_bans)
+against the oracle's per-trip Banner replay (internal/iptables.go:179-228,
+273-294; internal/decision.go:404-439), bit-exact: same decision lists
+(decision, expiry, domain), same ban-log lines in trip order, same last
+banned IP.
+"""
+import pytest
+
+import workloads as W
+from banjax_amd import Config, MockBanner, RegexRateLimiter
+from tests.parity import Pair
+from tests.test_gpu_parity import EDGE_CFG, edge_lines
+
+pytestmark = pytest.mark.gpu
+S = 1_000_000_000
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from banjax_amd import Engine
+    e = Engine()
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("name,n,batches", [("cfg1", 200_000, 3), ("cfg3", 100_000, 2), ("cfg5", 60_000, 3)])
+def test_device_bans_match_oracle(engine, name, n, batches):
+    w = W.scaled(W.ALL[name], n, n_ips=min(W.ALL[name].n_ips, n // 10))
+    pair = Pair(w.rules_yaml, engine, device_bans=True)
+    per = n // batches
+    for b in range(batches):
+        pair.feed(w.host_lines(b * per, per), w.now_ns(b * per, per))
+    pair.compare_state()
+
+
+ESC_SITE = r"""  "esc.com":
+    - rule: "esc \"quoted\" <rule> & \u2028 name"
+      regex: 'x'
+      interval: 1
+      hits_per_interval: 0
+      decision: challenge
+    - rule: "esc block"
+      regex: 'BLOCK'
+      interval: 1
+      hits_per_interval: 0
+      decision: iptables_block
+"""
+BAN_CFG = (EDGE_CFG.replace("per_site_regexes_with_rates:\n", "per_site_regexes_with_rates:\n" + ESC_SITE)
+           .replace("expiring_decision_ttl_seconds: 7", "expiring_decision_ttl_seconds: 600\n"
+                    "disable_logging:\n  h.com: true\n  other.com: false"))
+
+
+def ban_lines(t):
+    """Lines whose ban-log fields need every encoding/json escape and every
+    TrimSpace edge (words[3] = path, words[5] up to '|' = UA)."""
+    L = []
+    add = L.append
+    uas = [b"plain ua", b"  padded\t\t", b"quote\" back\\slash", b"<script>&amp;</script>", b"ctl\x01\x08\x0c\x1f\x7f",
+           b"tab\there\rcr", b"bad \xff\xfe utf8", b"sep \xe2\x80\xa8 \xe2\x80\xa9 end", b"\xc2\xa0nbsp\xc2\xa0",
+           b"\xe3\x80\x80ideo\xe3\x80\x80", b"\xc2\x85nel", b"ua | 200", b"| 404", b"trail \xc3", b"\xe2\x80\x8a",
+           b"emoji \xf0\x9f\x98\x80 ok", b"enc \xef\xbf\xbd lit", b"surrogate \xed\xa0\x80"]
+    for i, ua in enumerate(uas):
+        ip = b"7.7.7.%d" % (i % 5)
+        add(b"%d %s GET esc.com GET /p/%d\"<&> HTTP/1.1 %s x" % (t, ip, i, ua))
+        add(b"%d %s GET esc.com GET /BLOCK%d HTTP/1.1 %s" % (t, ip, i, ua))
+        add(b"%d %s GET h.com GET /x%d HTTP/1.1 %s" % (t, ip, i, ua))
+    add(b"%d 7.7.7.9 GET esc.com GET /x" % t)           # < 6 words: no ban-log line
+    add(b"%d 7.7.7.9 GET esc.com GET /x HTTP/1.1" % t)  # exactly 5 words
+    add(b"%d 7.7.7.9 GET esc.com GET /x HTTP/1.1 " % t)  # 6th word empty
+    add(b"%d 127.0.0.1 GET esc.com GET /BLOCK HTTP/1.1 ua" % t)
+    return b"\n".join(L) + b"\n"
+
+
+def test_device_bans_edge(engine):
+    t = 1700000000
+    pair = Pair(BAN_CFG, engine, device_bans=True)
+    data = edge_lines(t)
+    pair.feed(data, t * S)
+    pair.feed(ban_lines(t), t * S + 5)
+    pair.feed(data + ban_lines(t + 1), (t + 1) * S)
+    pair.compare_state()
+    assert pair.lim.banner.ban_log and pair.lim.banner.ban_log_temp
+
+
+@pytest.mark.parametrize("tz", [19800, -36000, 0])
+def test_device_bans_equal_host_replay(engine, tz):
+    """Device emission vs the host Banner replay of the same trips (decision
+    lists incl. ipset with standalone off, ban logs), with a local time zone."""
+    w = W.scaled(W.CFG5, 40_000, n_ips=3_000)
+    cfg = Config.from_yaml(w.rules_yaml.replace("expiring_decision_ttl_seconds: 10", "expiring_decision_ttl_seconds: 3600"))
+    got = {}
+    for dev in (False, True):
+        engine.state_clear()
+        banner = MockBanner()
+        banner.standalone = False
+        lim = RegexRateLimiter(cfg, engine=engine, banner=banner, device_bans=dev, tz_offset_s=tz)
+        for b in range(2):
+            lim.consume_lines(w.host_lines(b * 20_000, 20_000), w.now_ns(b * 20_000, 20_000), want_results=False)
+        lim.consume_lines(ban_lines(1700000000 + 3600 * 24 * 200), (1700000000 + 3600 * 24 * 200) * S,
+                          want_results=False)
+        dl = {ip: (d.decision, d.expires_ns, d.domain, d.from_baskerville)
+              for ip, d in banner.decision_lists.expiring.items()}
+        got[dev] = (dl, banner.ban_log, banner.ban_log_temp, sorted(set(banner.ipset)), banner.banned_ip)
+    assert got[True][0] == got[False][0]
+    assert got[True][1] == got[False][1]
+    assert got[True][2] == got[False][2]
+    assert got[True][3] == got[False][3]
+    assert got[True][4] == got[False][4]
+    assert len(got[True][1]) > 100
+
+
+@pytest.mark.parametrize("mask", [0xFF, 0xFFFF])
+def test_device_bans_hash_collisions(engine, mask):
+    """Tripped IPs forced onto a few hash values (test hook): the exact
+    regrouping (k_ban_collide) keeps one record per distinct IP."""
+    w = W.scaled(W.CFG5, 30_000, n_ips=2_000)
+    engine.debug_set_ip_hash_mask(mask)
+    try:
+        pair = Pair(w.rules_yaml, engine, device_bans=True)
+        for b in range(2):
+            pair.feed(w.host_lines(b * 15_000, 15_000), w.now_ns(b * 15_000, 15_000))
+        pair.compare_state()
+    finally:
+        engine.debug_set_ip_hash_mask(0)
