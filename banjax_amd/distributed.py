@@ -107,9 +107,11 @@ class ThreadExchange:
 
 
 def sharded_batch(engine, rs: Ruleset, now_ns: int, device_ptr: int, nbytes: int, ex,
-                  copy_results: bool = False) -> BatchOutput:
+                  copy_results: bool = False, emit_bans: bool = False) -> BatchOutput:
     """consumeLine over this rank's chunk with IP-sharded rate limiting.
-    Every rank of `ex` must call this for the same batch step."""
+    Every rank of `ex` must call this for the same batch step.  emit_bans: the
+    rank's trips also get device decision emission (engine.bans(); merge the
+    ranks' records with merge_rank_bans)."""
     world, dev = ex.world, ex.device
     engine.match(rs, now_ns, device_ptr, nbytes, copy_results=copy_results)
     send = engine.events_partition(world)
@@ -125,4 +127,37 @@ def sharded_batch(engine, rs: Ruleset, now_ns: int, device_ptr: int, nbytes: int
     out = torch.empty(max(1, sum(c[1] for c in recv)), dtype=torch.uint8, device=dev)
     engine.apply_events(rs, r_lines.data_ptr(), r_events.data_ptr(), r_ipb.data_ptr(), recv, out.data_ptr())
     back = ex.exchange(out, [c[1] for c in recv], [c[1] for c in send])
+    if emit_bans:
+        return engine.finish(back.data_ptr(), copy_results=copy_results, emit_bans=True)
     return engine.finish(back.data_ptr(), copy_results=copy_results)
+
+
+def merge_rank_bans(parts):
+    """One sharded step's decision updates and ban-log lines from every rank's
+    bjx_batch_bans.  parts: per rank, in stream order, (BanBatch, trips, chunk
+    bytes).  Rank r's trips precede rank r+1's in reference order, so per IP
+    the highest decision's first trip is the earliest (rank, trip) reaching
+    it, and the log is the ranks' logs concatenated.  Returns (records in
+    global trip order, [(kind, line)]); a record is (ip, domain, decision,
+    expires_ns, n_trips, iptables)."""
+    best = {}
+    log = []
+    for r, (bans, trips, data) in enumerate(parts):
+        for rec in bans.ips:
+            t = trips[int(rec["trip_idx"])]
+            line = bytes(data[t.line_offset:t.line_offset + t.line_len])
+            ip = line[t.ip_off:t.ip_off + t.ip_len]
+            host = line[t.host_off:t.host_off + t.host_len]
+            key = (r, int(rec["trip_idx"]))
+            d = int(rec["decision"])
+            cur = best.get(ip)
+            if cur is None:
+                best[ip] = [key, host, d, int(rec["expires_ns"]), int(rec["n_trips"]), int(rec["iptables"])]
+                continue
+            if d > cur[2]:
+                cur[0], cur[1], cur[2] = key, host, d
+            cur[4] += int(rec["n_trips"])
+            cur[5] |= int(rec["iptables"])
+        log.extend(bans.lines())
+    recs = sorted(best.items(), key=lambda kv: kv[1][0])
+    return [(ip, v[1], v[2], v[3], v[4], v[5]) for ip, v in recs], log

@@ -97,6 +97,9 @@ def main():
     ap.add_argument("--lines", type=int, default=0, help="lines per GPU (default: workload size)")
     ap.add_argument("--cpu-sample", type=int, default=600_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--bans", type=int, default=0,
+                    help="1: each step also emits the decision updates and ban-log lines of its trips on the device "
+                         "(BJX_EMIT_BANS, copied to pinned host memory); 0: trip list only")
     args = ap.parse_args()
 
     import torch
@@ -123,7 +126,9 @@ def main():
     rs = Ruleset(cfg)
     eng = Engine(local, ip_arena_bytes=256 << 20)  # IP / state tables size themselves to the stream
     eng.set_decision_lists(cfg.decision_entries)
+    eng.set_ban_options(cfg.expiring_decision_ttl_seconds, [h for h, v in cfg.disable_logging.items() if v])
     now = w.now_ns(first, n_lines)
+    bans = bool(args.bans)
 
     ex = None
     if world > 1:
@@ -132,8 +137,8 @@ def main():
 
     def step():
         if ex is None:
-            return eng.process(rs, None, now, device_ptr=data.data_ptr(), nbytes=nbytes)
-        return sharded_batch(eng, rs, now, data.data_ptr(), nbytes, ex)
+            return eng.process(rs, None, now, device_ptr=data.data_ptr(), nbytes=nbytes, emit_bans=bans)
+        return sharded_batch(eng, rs, now, data.data_ptr(), nbytes, ex, emit_bans=bans)
 
     for _ in range(args.warmup):
         step()
@@ -181,6 +186,8 @@ def main():
                 "rule_results_per_step_rank0": o.n_results,
                 "rate_limit_events_per_step_rank0": o.n_events,
                 "trips_per_step_rank0": o.n_trips,
+                "decision_emission": ("device: per-IP decision updates + LogRegexBan JSON lines, in the step"
+                                      if bans else "off (trip list only)"),
                 "device_ms_per_step_rank0": round(dev_ms, 3),
                 "pipeline_GBps_rank0": round(nbytes / (ms_per_step / 1000.0) / 1e9, 1),
                 "phase_ms_last_step_rank0": phases,

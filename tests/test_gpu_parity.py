@@ -430,7 +430,10 @@ def test_sharded_engines_match_single_process(wl, world):
     import torch
 
     from banjax_amd import Ruleset
-    from banjax_amd.distributed import ThreadMesh, sharded_batch
+    from types import SimpleNamespace
+
+    from banjax_amd.distributed import ThreadMesh, merge_rank_bans, sharded_batch
+    from banjax_amd.regex_rate_limiter import DynamicDecisionLists
     n_chunks, per = 2 * world, 8000
     w = W.scaled(W.ALL[wl[0]], per * n_chunks, n_ips=wl[1])
     cfg = Config.from_yaml(w.rules_yaml)
@@ -438,18 +441,22 @@ def test_sharded_engines_match_single_process(wl, world):
     dev = torch.device("cuda", 0)
     engines = [Engine(0) for _ in range(world)]
     mesh = ThreadMesh(world)
-    got, errs = {}, []
+    got, errs, bans = {}, [], {}
 
     def run(r):
         try:
             rs = Ruleset(cfg)
             engines[r].set_decision_lists(cfg.decision_entries)
+            engines[r].set_ban_options(cfg.expiring_decision_ttl_seconds)
             ex = mesh.rank(r, dev)
             for step in range(n_chunks // world):
                 k = step * world + r
                 t = torch.frombuffer(bytearray(chunks[k]), dtype=torch.uint8).to(dev)
                 out = sharded_batch(engines[r], rs, w.now_ns(0, per), t.data_ptr(), len(chunks[k]), ex,
-                                    copy_results=True)
+                                    copy_results=True, emit_bans=True)
+                trips = [SimpleNamespace(line_offset=x.line_offset, line_len=x.line_len, ip_off=x.ip_off,
+                                         ip_len=x.ip_len, host_off=x.host_off, host_len=x.host_len) for x in out.trips]
+                bans[k] = (engines[r].bans(), trips, chunks[k])
                 got[k] = ([[x.line_idx, x.rule_idx, x.rule_pos, x.skip_host, x.seen_ip, x.match_type, x.exceeded]
                            for x in out.results], [(x.line_idx, x.rule_idx) for x in out.trips], bytes(out.line_flags))
         except BaseException as e:  # noqa: BLE001
@@ -474,6 +481,17 @@ def test_sharded_engines_match_single_process(wl, world):
         assert trips == [(r[0], r[1]) for r in exp if r[6]]
         n_trips += len(trips)
     assert n_trips > 0
+    # device decision emission, merged over the ranks of each step
+    dl, blog = DynamicDecisionLists(), []
+    for step in range(n_chunks // world):
+        recs, log = merge_rank_bans([bans[step * world + r] for r in range(world)])
+        for ip, host, d, exp_ns, _, _ in recs:
+            dl.update(ip.decode(), exp_ns, d, False, host.decode())
+        blog += ["%d %s" % (kind - 1, line.decode()) for kind, line in log]
+    assert len(dl.expiring) == st.decisions_len()
+    for ip, d in dl.expiring.items():
+        assert tuple(st.decision(ip)[:3]) == (d.decision, d.expires_ns, d.domain), ip
+    assert blog == [ln for ln in st.ban_log().split("\n") if ln]
     assert sum(e.state_len() for e in engines) == len(st)
     names = sorted(set(r.rule for r in cfg.all_rules()))
     for ln in chunks[0].split(b"\n")[:40]:
