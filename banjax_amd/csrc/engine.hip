@@ -30,6 +30,7 @@
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
+#include <thread>
 #include <vector>
 
 #include "../../include/banjax_gpu.h"
@@ -2154,6 +2155,52 @@ static void set_err(char *err, size_t len, const std::string &m) {
   err[k] = 0;
 }
 
+// Compiled regexes by pattern, process-wide: a reload (ConfigHolder.Reload,
+// config_holder.go:55-66) recompiles only the patterns it has not seen
+// before.  Entries are immutable once published.
+struct RxCacheEntry {
+  int rc = 0;
+  std::string err;
+  CompiledRegex rx;
+};
+static std::mutex g_rx_mu;
+static std::unordered_map<std::string, std::shared_ptr<const RxCacheEntry>> g_rx_cache;
+static constexpr size_t kRxCacheMax = 1u << 16;
+
+// compile every pattern not in the cache, on up to 16 host threads
+static std::vector<std::shared_ptr<const RxCacheEntry>> compile_patterns(const std::vector<std::string> &pats) {
+  std::vector<std::shared_ptr<const RxCacheEntry>> out(pats.size());
+  std::vector<size_t> todo;
+  {
+    std::lock_guard<std::mutex> g(g_rx_mu);
+    std::unordered_map<std::string, size_t> first;
+    for (size_t i = 0; i < pats.size(); ++i) {
+      auto it = g_rx_cache.find(pats[i]);
+      if (it != g_rx_cache.end()) out[i] = it->second;
+      else if (first.emplace(pats[i], i).second) todo.push_back(i);
+    }
+  }
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (size_t k; (k = next.fetch_add(1)) < todo.size();) {
+      auto e = std::make_shared<RxCacheEntry>();
+      e->rc = compile_regex(pats[todo[k]], &e->rx, &e->err);
+      out[todo[k]] = std::move(e);
+    }
+  };
+  const size_t nt = std::min<size_t>({16, std::max(1u, std::thread::hardware_concurrency()), (todo.size() + 7) / 8});
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nt; ++t) th.emplace_back(work);
+  work();
+  for (auto &t : th) t.join();
+  std::lock_guard<std::mutex> g(g_rx_mu);
+  if (g_rx_cache.size() + todo.size() > kRxCacheMax) g_rx_cache.clear();
+  for (size_t i : todo) g_rx_cache.emplace(pats[i], out[i]);
+  for (size_t i = 0; i < pats.size(); ++i)
+    if (!out[i]) out[i] = g_rx_cache.at(pats[i]);
+  return out;
+}
+
 extern "C" int bjx_ruleset_compile(const bjx_rule_spec *global_rules, size_t n_global, const bjx_site_rules *per_site,
                                    size_t n_sites, bjx_ruleset **out, int64_t *err_rule, char *err, size_t err_len) {
   if (!out) return BJX_ERR_ARG;
@@ -2161,24 +2208,36 @@ extern "C" int bjx_ruleset_compile(const bjx_rule_spec *global_rules, size_t n_g
   if (err_rule) *err_rule = -1;
   try {
     auto rs = std::make_unique<bjx_ruleset>();
+    // every rule spec in evaluation order: globals, then each site's rules
+    std::vector<const bjx_rule_spec *> specs;
+    for (size_t i = 0; i < n_global; ++i) specs.push_back(&global_rules[i]);
+    for (size_t s = 0; s < n_sites; ++s)
+      for (size_t k = 0; k < per_site[s].n_rules; ++k) specs.push_back(&per_site[s].rules[k]);
+    std::vector<std::string> pats;
+    for (auto *sp : specs) pats.emplace_back(sp->regex.ptr ? sp->regex.ptr : "", sp->regex.len);
+    const auto compiled = compile_patterns(pats);
+    // the first failing rule in order decides the error, as the sequential
+    // UnmarshalYAML -> regexp.Compile does (config.go:110-113)
+    size_t si = 0;
     auto add = [&](const bjx_rule_spec &s) -> int {
+      const size_t i = si++;
       if (s.decision < BJX_ALLOW || s.decision > BJX_IPTABLES_BLOCK) {
         set_err(err, err_len, "invalid decision value");
         return BJX_ERR_DECISION;
       }
+      const RxCacheEntry &ce = *compiled[i];
+      if (ce.rc != 0) {
+        set_err(err, err_len, ce.err);
+        return ce.rc;
+      }
       bjx_ruleset::Rule r;
       r.name.assign(s.name.ptr ? s.name.ptr : "", s.name.len);
-      r.regex.assign(s.regex.ptr ? s.regex.ptr : "", s.regex.len);
+      r.regex = pats[i];
       r.interval_ns = s.interval_ns;
       r.hits = s.hits_per_interval;
       r.decision = s.decision;
       for (size_t k = 0; k < s.n_hosts_to_skip; ++k) r.skip_hosts.emplace_back(s.hosts_to_skip[k].ptr, s.hosts_to_skip[k].len);
-      std::string e;
-      int rc = compile_regex(r.regex, &r.rx, &e);
-      if (rc != 0) {
-        set_err(err, err_len, e);
-        return rc;
-      }
+      r.rx = ce.rx;
       rs->rules.push_back(std::move(r));
       return 0;
     };

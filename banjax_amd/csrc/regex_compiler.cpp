@@ -150,27 +150,29 @@ const std::vector<Group> &perl_groups() {
   return g;
 }
 const std::vector<Group> &posix_groups() {
-  static std::vector<Group> g;
-  if (g.empty()) {
-    struct B { const char *n; std::vector<int32_t> r; };
-    std::vector<B> base = {
-      {"alnum", {'0', '9', 'A', 'Z', 'a', 'z'}}, {"alpha", {'A', 'Z', 'a', 'z'}}, {"ascii", {0, 0x7F}},
-      {"blank", {'\t', '\t', ' ', ' '}}, {"cntrl", {0, 0x1F, 0x7F, 0x7F}}, {"digit", {'0', '9'}},
-      {"graph", {'!', '~'}}, {"lower", {'a', 'z'}}, {"print", {' ', '~'}},
-      {"punct", {'!', '/', ':', '@', '[', '`', '{', '~'}}, {"space", {'\t', '\r', ' ', ' '}},
-      {"upper", {'A', 'Z'}}, {"word", {'0', '9', 'A', 'Z', '_', '_', 'a', 'z'}}, {"xdigit", {'0', '9', 'A', 'F', 'a', 'f'}},
+  // built once (thread-safe static init: rulesets compile on worker threads)
+  static const std::vector<std::string> names = [] {
+    std::vector<std::string> v;
+    for (const char *n : {"alnum", "alpha", "ascii", "blank", "cntrl", "digit", "graph", "lower", "print", "punct",
+                          "space", "upper", "word", "xdigit"}) {
+      v.push_back(std::string("[:") + n + ":]");
+      v.push_back(std::string("[:^") + n + ":]");
+    }
+    return v;
+  }();
+  static const std::vector<Group> g = [] {
+    const std::vector<std::vector<int32_t>> base = {
+      {'0', '9', 'A', 'Z', 'a', 'z'}, {'A', 'Z', 'a', 'z'}, {0, 0x7F}, {'\t', '\t', ' ', ' '}, {0, 0x1F, 0x7F, 0x7F},
+      {'0', '9'}, {'!', '~'}, {'a', 'z'}, {' ', '~'}, {'!', '/', ':', '@', '[', '`', '{', '~'}, {'\t', '\r', ' ', ' '},
+      {'A', 'Z'}, {'0', '9', 'A', 'Z', '_', '_', 'a', 'z'}, {'0', '9', 'A', 'F', 'a', 'f'},
     };
-    static std::vector<std::string> names;
-    names.reserve(base.size() * 2);
-    for (auto &b : base) {
-      names.push_back(std::string("[:") + b.n + ":]");
-      names.push_back(std::string("[:^") + b.n + ":]");
-    }
+    std::vector<Group> out;
     for (size_t i = 0; i < base.size(); ++i) {
-      g.push_back({names[2 * i].c_str(), 1, base[i].r});
-      g.push_back({names[2 * i + 1].c_str(), -1, base[i].r});
+      out.push_back({names[2 * i].c_str(), 1, base[i]});
+      out.push_back({names[2 * i + 1].c_str(), -1, base[i]});
     }
-  }
+    return out;
+  }();
   return g;
 }
 

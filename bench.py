@@ -123,7 +123,11 @@ def main():
     data, nbytes = w.device_lines(local, first, n_lines)
     torch.cuda.synchronize()
     cfg = Config.from_yaml(w.rules_yaml)
-    rs = Ruleset(cfg)
+    from banjax_amd import _lib
+    _lib.lib()
+    tc = time.perf_counter()
+    rs = Ruleset(cfg)  # cold: first compile of these patterns in this process (reload = cached patterns only)
+    compile_ms = (time.perf_counter() - tc) * 1000.0
     eng = Engine(local, ip_arena_bytes=256 << 20)  # IP / state tables size themselves to the stream
     eng.set_decision_lists(cfg.decision_entries)
     eng.set_ban_options(cfg.expiring_decision_ttl_seconds, [h for h, v in cfg.disable_logging.items() if v])
@@ -180,6 +184,7 @@ def main():
             "config": {
                 "workload": "%s: %s" % (w0.name, w0.description),
                 "rules": len(rs),
+                "ruleset_compile_ms_cold": round(compile_ms, 1),
                 "lines_per_gpu": n_lines,
                 "bytes_per_gpu": nbytes,
                 "distinct_ips": w.n_ips,
