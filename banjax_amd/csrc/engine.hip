@@ -484,17 +484,34 @@ __device__ __forceinline__ Tabs make_tabs(const uint8_t *base, const ImgLayout &
 }
 
 // host id from the open-addressing host table
-// host id from the inline host slots (per-line pass): one 64 B probe per step
+// host id from the inline host slots (per-line pass): each probe step loads
+// the whole 64 B slot at once (four 16 B loads, one round trip) and compares
+// hosts of up to 48 B from registers, so a lookup costs one dependent global
+// access instead of one per 4-byte word
 __device__ __forceinline__ int32_t host_lookup_slots(const Bind &B, const uint8_t *h, uint32_t n) {
   if (B.n_hd == 0) return -1;
   const uint64_t hh = hash_bytes(h, n);
   const uint32_t tag = (uint32_t)(hh >> 32) | 1u;
   uint32_t s = (uint32_t)hh & (B.ht_cap - 1);
   for (;;) {
-    const HostSlot *e = B.hslot + s;
-    const uint32_t t = e->tag;
-    if (t == 0) return -1;
-    if (t == tag && e->len == n && bytes_eq(n <= 48 ? e->inl : B.hd_bytes + e->off, h, n)) return e->id;
+    const uint4 *sp = reinterpret_cast<const uint4 *>(B.hslot + s);
+    const uint4 q0 = sp[0], q1 = sp[1], q2 = sp[2], q3 = sp[3];
+    if (q0.x == 0) return -1;
+    if (q0.x == tag && q0.z == n) {
+      if (n > 48) {
+        if (bytes_eq(B.hd_bytes + q0.w, h, n)) return (int32_t)q0.y;
+      } else {
+        const uint32_t iw[12] = {q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+        uint32_t diff = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 12; ++k) {
+          if (4 * k >= n) break;
+          const uint32_t m = n - 4 * k >= 4 ? 0xFFFFFFFFu : (1u << (8 * (n - 4 * k))) - 1u;
+          diff |= (ld4(h + 4 * k) ^ iw[k]) & m;
+        }
+        if (!diff) return (int32_t)q0.y;
+      }
+    }
     s = (s + 1) & (B.ht_cap - 1);
   }
 }
