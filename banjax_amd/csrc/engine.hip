@@ -601,6 +601,23 @@ __device__ __forceinline__ void dfa_rule(const Bind &B, const Tabs &T, uint32_t 
   else if (rule_match(B, r, rest, rest_len)) set_pos(m0, m1, pos);
 }
 
+// Inline test of an anchored rule's single prefix literal (bind record
+// dfa_*_q: qa = {len, window offset | exact << 8 | equiv << 9, case mask of
+// the 8-byte window}, qb = {window bytes}): 0 = the literal cannot start
+// rest (too long, or the window differs), 1 = the whole literal matched
+// (len <= 8), 2 = undecided (dfa_rule decides).  The window is the literal's
+// tail: per-site literals share their host part with every line of the host.
+__device__ __forceinline__ uint32_t anchor_quick(const uint4 qa, const uint4 qb, const uint8_t *rest, uint32_t rest_len) {
+  if (qa.x == 0) return 2;
+  if (qa.x > rest_len) return 0;
+  const uint32_t o = qa.y & 0xFF, nb = qa.x - o < 8 ? qa.x - o : 8;
+  const uint32_t m0 = nb >= 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1u;
+  const uint32_t m1 = nb >= 8 ? 0xFFFFFFFFu : (nb <= 4 ? 0u : (1u << (8 * (nb - 4))) - 1u);
+  const uint32_t t0 = ld4(rest + o), t1 = nb > 4 ? ld4(rest + o + 4) : 0u;
+  if ((((t0 | qa.z) ^ qb.x) & m0) | (((t1 | qa.w) ^ qb.y) & m1)) return 0;
+  return ((qa.y >> 8) & 1) ? 1u : 2u;
+}
+
 // The applicable rules of one line (per-site[host] then global, YAML order;
 // regex_rate_limiter.go:175-211) decided from the line's verified literal
 // hits.  Writes the match mask (positions < 128) and the result/event counts
@@ -619,10 +636,18 @@ __device__ __forceinline__ void decide_rules(const Bind &B, const Tabs &T, const
   if (hid >= 0 && !(dbg & 1))
     for (uint32_t i = B.dfa_site_off[hid]; i < B.dfa_site_off[hid + 1]; ++i) {
       const uint2 e = B.dfa_site[i];
+      const uint4 qa = B.dfa_site_q[2 * i], qb = B.dfa_site_q[2 * i + 1];
+      const uint32_t qk = anchor_quick(qa, qb, rest, rest_len);
+      if (qk == 0) continue;
+      if (qk == 1 && ((qa.y >> 9) & 1)) { set_pos(m0, m1, e.y); continue; }
       dfa_rule<EMIT>(B, T, e.x, e.y, true, rest, rest_len, m0, m1, j, S);
     }
   for (uint32_t i = 0; i < (dbg & 1 ? 0u : B.n_dfa_glob); ++i) {
     const uint2 e = B.dfa_glob[i];
+    const uint4 qa = B.dfa_glob_q[2 * i], qb = B.dfa_glob_q[2 * i + 1];
+    const uint32_t qk = anchor_quick(qa, qb, rest, rest_len);
+    if (qk == 0) continue;
+    if (qk == 1 && ((qa.y >> 9) & 1)) { set_pos(m0, m1, nsite + e.y); continue; }
     dfa_rule<EMIT>(B, T, e.x, nsite + e.y, true, rest, rest_len, m0, m1, j, S);
   }
   if (ovf) {
@@ -2822,6 +2847,32 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     if (m == kModeAnchored || m == kModeScan) dfa_glob.push_back(make_uint2(g, g));
     else if (m == kModePrefilter) pref_glob.push_back(make_uint2(g, g));
   }
+  // inline anchor tests (anchor_quick) of the dfa_site / dfa_glob entries
+  auto anchor_q = [&](const std::vector<uint2> &ents) {
+    std::vector<uint4> q;
+    for (const uint2 &en : ents) {
+      uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, 0);
+      const DevRule &d = drules[en.x];
+      if (mode_of(en.x) == kModeAnchored && d.anc_len == 1) {
+        const uint32_t lit = rule_lits[d.anc_off], len = lit_len[lit];
+        const uint32_t o = len > 8 ? len - 8 : 0, nb = std::min(8u, len);
+        if (len > 0 && o < 256) {
+          uint8_t bw[8] = {0}, mw[8] = {0};
+          for (uint32_t k = 0; k < nb; ++k) {
+            bw[k] = lit_bytes[lit_off[lit] + o + k];
+            mw[k] = lit_ci[lit_off[lit] + o + k] ? 0x20 : 0;
+          }
+          a.x = len;
+          a.y = o | ((len <= 8 ? 1u : 0u) << 8) | ((d.anc_equiv ? 1u : 0u) << 9);
+          memcpy(&a.z, mw, 4); memcpy(&a.w, mw + 4, 4); memcpy(&b.x, bw, 4); memcpy(&b.y, bw + 4, 4);
+        }
+      }
+      q.push_back(a);
+      q.push_back(b);
+    }
+    return q;
+  };
+  const std::vector<uint4> dfa_site_q = anchor_q(dfa_site), dfa_glob_q = anchor_q(dfa_glob);
   const uint32_t n_lit = (uint32_t)lit_off.size();
   std::vector<std::vector<uint2>> lr_g(n_lit);
   std::vector<std::vector<std::pair<int32_t, uint2>>> lr_s(n_lit);
@@ -2948,6 +2999,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
          o_rl = bb.add(rule_lits), o_img = bb.add(img), o_lro = bb.add(lr_off), o_lrg = bb.add(lr_gend),
          o_lre = bb.add(lr_ent), o_lrh = bb.add(lr_host), o_sca = bb.add(sc_always), o_scs = bb.add(sc_skipm),
          o_dso = bb.add(dfa_site_off), o_ds = bb.add(dfa_site), o_dg = bb.add(dfa_glob), o_pso = bb.add(pref_site_off),
+         o_dsq = bb.add(dfa_site_q), o_dgq = bb.add(dfa_glob_q),
          o_ps = bb.add(pref_site), o_pg = bb.add(pref_glob), o_hslot = bb.add(hslot);
   e->bind_blob.ensure(bb.bytes.size());
   HIP_OK(hipMemcpy(e->bind_blob.p, bb.bytes.data(), bb.bytes.size(), hipMemcpyHostToDevice));
@@ -3009,6 +3061,8 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.dfa_site = reinterpret_cast<const uint2 *>(base + o_ds);
   B.dfa_glob = reinterpret_cast<const uint2 *>(base + o_dg);
   B.n_dfa_glob = (uint32_t)dfa_glob.size();
+  B.dfa_site_q = reinterpret_cast<const uint4 *>(base + o_dsq);
+  B.dfa_glob_q = reinterpret_cast<const uint4 *>(base + o_dgq);
   B.pref_site_off = reinterpret_cast<const uint32_t *>(base + o_pso);
   B.pref_site = reinterpret_cast<const uint2 *>(base + o_ps);
   B.pref_glob = reinterpret_cast<const uint2 *>(base + o_pg);

@@ -148,6 +148,8 @@ struct Bind {
   const uint2 *dfa_site;         // (rule, index)
   const uint2 *dfa_glob;
   uint32_t n_dfa_glob;
+  const uint4 *dfa_site_q;       // per dfa_site / dfa_glob entry: 2 x uint4 inline anchor test (anchor_quick)
+  const uint4 *dfa_glob_q;
   const uint32_t *pref_site_off;
   const uint2 *pref_site;
   const uint2 *pref_glob;
