@@ -57,12 +57,15 @@ def engine():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("device_bans", [False, True], ids=["host_banner", "device_bans"])
 @pytest.mark.parametrize("path", GOLDEN, ids=NAMES)
-def test_engine_reproduces_golden(engine, path):
+def test_engine_reproduces_golden(engine, path, device_bans):
+    """device_bans: the decisions and ban-log lines come from the GPU emission
+    (bjx_batch_bans) instead of the host Banner replay of the trip list."""
     fx = load(path)
     cfg = Config.from_yaml(fx["config_yaml"])
     engine.state_clear()
-    lim = RegexRateLimiter(cfg, engine=engine, banner=MockBanner())
+    lim = RegexRateLimiter(cfg, engine=engine, banner=MockBanner(), device_bans=device_bans)
     for b in fx["batches"]:
         data = base64.b64decode(b["log_b64"])
         _, out = lim.consume_lines(data, b["now_ns"], want_results=True)
