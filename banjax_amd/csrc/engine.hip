@@ -3508,7 +3508,15 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
                                  (int)kScanLdsMax));
       e->lines_attr = true;
     }
-    const unsigned grid = (unsigned)std::min<uint64_t>((n_lines + kBlock - 1) / kBlock, 256 * 8);
+    // one resident wave of blocks (grid-stride loop): a grid of several
+    // "rounds" leaves the last round partly empty
+    int per_cu = 0, n_cu = 0;
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, img_lds ? reinterpret_cast<const void *>(&k_lines<true>) : reinterpret_cast<const void *>(&k_lines<false>),
+        kBlock, lds));
+    HIP_OK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, e->device));
+    const uint64_t resident = (uint64_t)std::max(1, per_cu) * (uint64_t)std::max(1, n_cu);
+    const unsigned grid = (unsigned)std::min<uint64_t>((n_lines + kBlock - 1) / kBlock, resident);
     if (img_lds) hipLaunchKernelGGL(k_lines<true>, dim3(grid), dim3(kBlock), lds, st, B, A);
     else hipLaunchKernelGGL(k_lines<false>, dim3(grid), dim3(kBlock), lds, st, B, A);
     HIP_OK(hipGetLastError());
