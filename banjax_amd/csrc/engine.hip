@@ -1322,6 +1322,10 @@ __global__ __launch_bounds__(kBlock) void k_emit(Bind B, uint64_t n_lines, Lines
     const uint32_t nsite = s_end - s_begin;
     const uint32_t napp = nsite + B.n_global;
     const uint64_t *mask = L.masks + j * B.mask_words;
+    // HostsToSkip of the line's host by rule position (positions < 128; the
+    // per-result binary search only past that)
+    const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
+    const uint64_t k0 = B.sc_skip[2 * sc], k1 = B.sc_skip[2 * sc + 1];
     for (uint32_t w = 0; w * 64 < napp; ++w) {
       uint64_t m = mask[w];
       while (m) {
@@ -1329,7 +1333,7 @@ __global__ __launch_bounds__(kBlock) void k_emit(Bind B, uint64_t n_lines, Lines
         m &= m - 1;
         const uint32_t pos = w * 64 + b;
         const uint32_t r = pos < nsite ? B.site_rules[s_begin + pos] : B.global_rules[pos - nsite];
-        const bool skip = is_skip(B, r, hid);
+        const bool skip = pos < 128 ? (((pos < 64 ? k0 >> pos : k1 >> (pos - 64)) & 1) != 0) : is_skip(B, r, hid);
         res_seq[ro] = (j << 16) | pos;
         res_rule[ro] = r | (skip ? 0x80000000u : 0u);
         if (!skip) { ev_el[eo] = (uint32_t)j; ev_rule[eo] = r; ev_res[eo] = (uint32_t)ro; ++eo; }
