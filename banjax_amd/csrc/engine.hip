@@ -1421,7 +1421,12 @@ __device__ __forceinline__ bool ip_claim_line(const EvSrc &E, const State &S, ui
   uint64_t s = h & S.ip_mask;
   bool claimed = false;
   for (;;) {
-    uint64_t cur = S.ip[s].hash;
+    // the whole 32 B slot in one round trip: hash, id, born, key16.  Fields
+    // changed in this launch (hash, born) are re-read by the CAS paths below;
+    // id and key16 of IPs from earlier batches are settled.
+    const uint4 *sp = reinterpret_cast<const uint4 *>(&S.ip[s]);
+    const uint4 q0 = sp[0], q1 = sp[1];
+    uint64_t cur = ((uint64_t)q0.y << 32) | q0.x;
     if (cur == 0) {
       if (flag_set(S, 5)) return false;  // this launch is rolled back anyway
       if (__hip_atomic_load(claim_shard(S, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= shard_budget) {
@@ -1432,7 +1437,7 @@ __device__ __forceinline__ bool ip_claim_line(const EvSrc &E, const State &S, ui
       if (cur == 0) { cur = h; claimed = true; }
     }
     if (cur == h) {
-      uint32_t b = S.ip[s].born;
+      uint32_t b = q0.w;  // 0 (stale) when the hash came from the CAS: the CAS below decides
       if (b == 0 || b == epoch) b = atomicCAS(&S.ip[s].born, 0u, epoch);
       if (b == 0 || b == epoch) {  // created in this batch: identity checked by k_ip_commit
         atomicMin(&S.ip_first[s], (uint32_t)i);
@@ -1441,8 +1446,8 @@ __device__ __forceinline__ bool ip_claim_line(const EvSrc &E, const State &S, ui
         return claimed;
       }
       // created by an earlier batch: short IPs compare inline, long ones in the arena
-      const uint32_t id = S.ip[s].id;
-      if (inl ? key16_eq(S.ip[s].key16, k16) : (S.ip_len[id] == len && bytes_eq(S.arena + S.ip_off[id], ip, len))) {
+      const uint32_t id = q0.z;
+      if (inl ? key16_eq(q1, k16) : (S.ip_len[id] == len && bytes_eq(S.arena + S.ip_off[id], ip, len))) {
         el_slot[i] = (uint32_t)s;
         el_id[i] = id;
         return claimed;
