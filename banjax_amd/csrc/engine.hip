@@ -1212,19 +1212,21 @@ __device__ __forceinline__ bool dfa_text(const Bind &B, const DevRule &R, const 
   uint64_t a = t0 & ~15ull;
   const uint64_t end = t0 + len;
   uint32_t skip = (uint32_t)(t0 - a);
-  while (a < end) {
-    uint4 v;
-    if (a + 16 <= n_buf) {
-      v = *reinterpret_cast<const uint4 *>(buf + a);
-    } else {
-      uint32_t w[4];
-      for (int k = 0; k < 4; ++k) {
-        uint32_t x = 0;
-        for (int b = 0; b < 4; ++b) x |= (a + 4 * k + b < n_buf ? (uint32_t)buf[a + 4 * k + b] : 0u) << (8 * b);
-        w[k] = x;
-      }
-      v = make_uint4(w[0], w[1], w[2], w[3]);
+  auto load16 = [&](uint64_t p) -> uint4 {
+    if (p + 16 <= n_buf) return *reinterpret_cast<const uint4 *>(buf + p);
+    uint32_t w[4];
+    for (int k = 0; k < 4; ++k) {
+      uint32_t x = 0;
+      for (int b = 0; b < 4; ++b) x |= (p + 4 * k + b < n_buf ? (uint32_t)buf[p + 4 * k + b] : 0u) << (8 * b);
+      w[k] = x;
     }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  };
+  // software-pipelined: the next 16 B are in flight while the DFA steps over
+  // the current ones (each step is a dependent LDS lookup)
+  uint4 v = a < end ? load16(a) : make_uint4(0, 0, 0, 0);
+  while (a < end) {
+    const uint4 vn = a + 16 < end ? load16(a + 16) : make_uint4(0, 0, 0, 0);
     const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
     const uint32_t lim = end - a < 16 ? (uint32_t)(end - a) : 16u;
 #pragma unroll
@@ -1260,6 +1262,7 @@ __device__ __forceinline__ bool dfa_text(const Bind &B, const DevRule &R, const 
     }
     skip = 0;
     a += 16;
+    v = vn;
   }
   return B.accept_end[R.ae_off + st] != 0;
 }
