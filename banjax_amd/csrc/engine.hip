@@ -558,6 +558,14 @@ __device__ __forceinline__ bool literal_at(const Tabs &T, uint32_t lit, const ui
 __device__ __forceinline__ void set_pos(uint64_t &m0, uint64_t &m1, uint32_t pos) {
   if (pos < 64) m0 |= 1ull << pos; else m1 |= 1ull << (pos - 64);
 }
+// home slot of (literal, host) in Bind::lh_tab (cap a power of two)
+__host__ __device__ __forceinline__ uint32_t lit_host_slot(uint32_t lit, uint32_t host, uint32_t cap) {
+  uint32_t x = lit * 0x9E3779B1u ^ (host + 0x7F4A7C15u) * 0x85EBCA77u;
+  x ^= x >> 15;
+  x *= 0x2C1B3C6Du;
+  x ^= x >> 13;
+  return x & (cap - 1);
+}
 __device__ __forceinline__ bool has_pos(uint64_t m0, uint64_t m1, uint32_t pos) {
   return ((pos < 64 ? m0 >> pos : m1 >> (pos - 64)) & 1) != 0;
 }
@@ -678,12 +686,16 @@ __device__ __forceinline__ void decide_rules(const Bind &B, const Tabs &T, const
         else dfa_rule<EMIT>(B, T, x.x, pos, false, rest, rest_len, m0, m1, j, S);
       }
       if (hid < 0 || g == e) continue;
-      uint32_t lo = g, hi = e;  // first site entry of this host
-      while (lo < hi) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (B.lr_host[m] < hid) lo = m + 1; else hi = m;
+      // this host's run of the literal's site entries: one (usually) probe
+      uint32_t sl = lit_host_slot(lit, (uint32_t)hid, B.lh_cap);
+      uint4 run;
+      for (;;) {
+        run = B.lh_tab[sl];
+        if (run.x == 0 || (run.x == lit + 1 && run.y == (uint32_t)hid)) break;
+        sl = (sl + 1) & (B.lh_cap - 1);
       }
-      for (uint32_t i = lo; i < e && B.lr_host[i] == hid; ++i) {
+      if (run.x == 0) continue;
+      for (uint32_t i = run.z; i < run.w; ++i) {
         const uint2 x = B.lr_ent[i];
         if (has_pos(t0, t1, x.y)) continue;
         set_pos(t0, t1, x.y);
@@ -2913,6 +2925,23 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     for (auto &x : lr_s[l]) { lr_ent.push_back(x.second); lr_host.push_back(x.first); }
   }
   lr_off[n_lit] = (uint32_t)lr_ent.size();
+  // (literal, host) -> run of that host's site entries (one probe per hit in
+  // decide_rules instead of a binary search over lr_host)
+  uint32_t lh_n = 0;
+  for (uint32_t l = 0; l < n_lit; ++l)
+    for (uint32_t i = lr_gend[l]; i < lr_off[l + 1]; ++i) lh_n += (i == lr_gend[l] || lr_host[i] != lr_host[i - 1]);
+  uint32_t lh_cap = 16;
+  while (lh_cap < 2 * lh_n) lh_cap <<= 1;
+  std::vector<uint4> lh_tab(lh_cap, make_uint4(0, 0, 0, 0));
+  for (uint32_t l = 0; l < n_lit; ++l)
+    for (uint32_t i = lr_gend[l]; i < lr_off[l + 1];) {
+      uint32_t k = i;
+      while (k < lr_off[l + 1] && lr_host[k] == lr_host[i]) ++k;
+      uint32_t s = lit_host_slot(l, (uint32_t)lr_host[i], lh_cap);
+      while (lh_tab[s].x) s = (s + 1) & (lh_cap - 1);
+      lh_tab[s] = make_uint4(l + 1, (uint32_t)lr_host[i], i, k);
+      i = k;
+    }
 
   // allow scopes (decision.go:278-374): exact maps are last-writer-wins in
   // config order; Allow IPFilters hold every allow entry
@@ -3012,7 +3041,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
          o_lre = bb.add(lr_ent), o_lrh = bb.add(lr_host), o_sca = bb.add(sc_always), o_scs = bb.add(sc_skipm),
          o_dso = bb.add(dfa_site_off), o_ds = bb.add(dfa_site), o_dg = bb.add(dfa_glob), o_pso = bb.add(pref_site_off),
          o_dsq = bb.add(dfa_site_q), o_dgq = bb.add(dfa_glob_q),
-         o_ps = bb.add(pref_site), o_pg = bb.add(pref_glob), o_hslot = bb.add(hslot);
+         o_ps = bb.add(pref_site), o_pg = bb.add(pref_glob), o_hslot = bb.add(hslot), o_lh = bb.add(lh_tab);
   e->bind_blob.ensure(bb.bytes.size());
   HIP_OK(hipMemcpy(e->bind_blob.p, bb.bytes.data(), bb.bytes.size(), hipMemcpyHostToDevice));
   uint8_t *base = e->bind_blob.p;
@@ -3067,6 +3096,8 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.lr_gend = reinterpret_cast<const uint32_t *>(base + o_lrg);
   B.lr_ent = reinterpret_cast<const uint2 *>(base + o_lre);
   B.lr_host = reinterpret_cast<const int32_t *>(base + o_lrh);
+  B.lh_tab = reinterpret_cast<const uint4 *>(base + o_lh);
+  B.lh_cap = lh_cap;
   B.sc_always = reinterpret_cast<const uint64_t *>(base + o_sca);
   B.sc_skip = reinterpret_cast<const uint64_t *>(base + o_scs);
   B.dfa_site_off = reinterpret_cast<const uint32_t *>(base + o_dso);

@@ -138,6 +138,10 @@ struct Bind {
   const uint32_t *lr_gend;
   const uint2 *lr_ent;         // (rule | equiv << 31, index in its site / global list)
   const int32_t *lr_host;
+  // (literal, host) -> that host's run of site entries of the literal:
+  // lh_cap open-addressed slots {lit + 1 (0 = empty), host, begin, end}
+  const uint4 *lh_tab;
+  uint32_t lh_cap;
   // per scope (host id, or n_hosts = no per-site rules): 2-word masks over the
   // applicable-rule positions of ALWAYS rules and of hosts_to_skip hits
   const uint64_t *sc_always;
