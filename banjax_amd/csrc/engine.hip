@@ -631,18 +631,36 @@ __device__ __forceinline__ uint32_t anchor_quick(const uint4 qa, const uint4 qb,
 // hits.  Writes the match mask (positions < 128) and the result/event counts
 // of the rules decided here; rules left to k_dfa add theirs atomically.
 // lits: up to 4 literal ids packed 16 bits each.
+// The per-host words decide_rules needs, loaded together as soon as the host
+// id is known (ahead of the exemption check and the per-line stores, which
+// the compiler cannot move these loads across)
+struct HostRules {
+  uint32_t s_begin, s_end;  // site rules [site_off[hid], site_off[hid + 1])
+  uint32_t d_begin, d_end;  // anchored / no-literal site rules (dfa_site_off)
+  uint64_t a0, a1, k0, k1;  // ALWAYS and hosts_to_skip position masks of the scope
+};
+__device__ __forceinline__ HostRules host_rules(const Bind &B, int32_t hid) {
+  HostRules H;
+  const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
+  H.s_begin = H.s_end = H.d_begin = H.d_end = 0;
+  if (hid >= 0) {
+    H.s_begin = B.site_off[hid]; H.s_end = B.site_off[hid + 1];
+    H.d_begin = B.dfa_site_off[hid]; H.d_end = B.dfa_site_off[hid + 1];
+  }
+  H.a0 = B.sc_always[2 * sc]; H.a1 = B.sc_always[2 * sc + 1];
+  H.k0 = B.sc_skip[2 * sc]; H.k1 = B.sc_skip[2 * sc + 1];
+  return H;
+}
+
 template <bool EMIT>
 __device__ __forceinline__ void decide_rules(const Bind &B, const Tabs &T, const uint8_t *rest, uint32_t rest_len, int32_t hid,
-                             uint64_t lits, uint32_t nlit, bool ovf, uint64_t j, const Lines &L, const JobSink &S,
-                             uint32_t dbg = 0) {
-  const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
-  uint32_t s_begin = 0, s_end = 0;
-  if (hid >= 0) { s_begin = B.site_off[hid]; s_end = B.site_off[hid + 1]; }
-  const uint32_t nsite = s_end - s_begin;
-  uint64_t m0 = B.sc_always[2 * sc], m1 = B.sc_always[2 * sc + 1];
+                             const HostRules &H, uint64_t lits, uint32_t nlit, bool ovf, uint64_t j, const Lines &L,
+                             const JobSink &S, uint32_t dbg = 0) {
+  const uint32_t nsite = H.s_end - H.s_begin;
+  uint64_t m0 = H.a0, m1 = H.a1;
   // anchored / no-literal rules: every line
   if (hid >= 0 && !(dbg & 1))
-    for (uint32_t i = B.dfa_site_off[hid]; i < B.dfa_site_off[hid + 1]; ++i) {
+    for (uint32_t i = H.d_begin; i < H.d_end; ++i) {
       const uint2 e = B.dfa_site[i];
       const uint4 qa = B.dfa_site_q[2 * i], qb = B.dfa_site_q[2 * i + 1];
       const uint32_t qk = anchor_quick(qa, qb, rest, rest_len);
@@ -707,9 +725,8 @@ __device__ __forceinline__ void decide_rules(const Bind &B, const Tabs &T, const
   uint64_t *mask = L.masks + j * B.mask_words;
   mask[0] = m0;
   if (B.mask_words > 1) mask[1] = m1;
-  const uint64_t k0 = B.sc_skip[2 * sc], k1 = B.sc_skip[2 * sc + 1];
   const uint32_t nres = __popcll(m0) + __popcll(m1);
-  const uint32_t nev = __popcll(m0 & ~k0) + __popcll(m1 & ~k1);
+  const uint32_t nev = __popcll(m0 & ~H.k0) + __popcll(m1 & ~H.k1);
   L.counts[j] = ((uint64_t)nres << 32) | nev;
 }
 
@@ -1060,12 +1077,20 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
   const uint32_t ns = find_spaces(p, n, sp0, sp1, sp2, sp3);
   double f;
   int32_t hid = -1;
+  HostRules H;
+  bool slow = false;
+  if (ns >= 4) {
+    slow = parse_float_fast(p, sp0, &f) != 0;
+    if (!slow) {
+      hid = (A.dbg & 8) ? -1 : host_lookup_slots(B, p + sp2 + 1, sp3 - sp2 - 1);
+      H = host_rules(B, hid);
+      slow = (H.s_end - H.s_begin) + B.n_global > 128;
+    }
+  }
   if (ns < 4) {
     L.flags[j] = kLineError;
     L.counts[j] = 0;
-  } else if (parse_float_fast(p, sp0, &f) != 0 ||
-             (hid = (A.dbg & 8) ? -1 : host_lookup_slots(B, p + sp2 + 1, sp3 - sp2 - 1),
-              (hid >= 0 ? B.site_off[hid + 1] - B.site_off[hid] : 0u) + B.n_global > 128)) {
+  } else if (slow) {
     // exotic timestamp token or > 128 applicable rules: the per-line fallback
     L.flags[j] = kLineSlowTs;
     L.counts[j] = 0;
@@ -1104,7 +1129,7 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
           continue;
         lits |= (uint64_t)lit << (16 * nlit++);
       }
-      decide_rules<true>(B, TB, p + rest_off, n - rest_off, hid, lits, (A.dbg & 2) ? 0u : nlit, cc > (uint32_t)kCandSlots, j, L, S,
+      decide_rules<true>(B, TB, p + rest_off, n - rest_off, hid, H, lits, (A.dbg & 2) ? 0u : nlit, cc > (uint32_t)kCandSlots, j, L, S,
                          A.dbg);
     }
   }
