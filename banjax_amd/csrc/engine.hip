@@ -2867,6 +2867,15 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     return (m == kModePrefilter && !use_pref) ? kModeScan : m;
   };
   auto equiv_of = [&](uint32_t r) { return rs->rules[r].rx.pref_equivalent ? 0x80000000u : 0u; };
+  // rules with the same pattern have the same automaton, anchors and literals:
+  // the DFA-side entries below name the first rule of each pattern, so the DFA
+  // jobs (sorted by that id) of, e.g., a per-site rule repeated on every host
+  // form one run and k_dfa stages its transition table once per block
+  std::vector<uint32_t> canon(rs->rules.size());
+  {
+    std::unordered_map<std::string, uint32_t> first;
+    for (uint32_t r = 0; r < (uint32_t)rs->rules.size(); ++r) canon[r] = first.emplace(rs->rules[r].regex, r).first->second;
+  }
   std::vector<uint64_t> sc_always(2 * (n_hosts + 1), 0), sc_skipm(2 * (n_hosts + 1), 0);
   for (uint32_t sc = 0; sc <= n_hosts; ++sc) {
     const uint32_t nsite = sc < n_hosts ? (uint32_t)per_host[sc].size() : 0;
@@ -2885,16 +2894,16 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     for (uint32_t k = 0; k < per_host[h].size(); ++k) {
       const uint32_t r = per_host[h][k];
       const RuleMode m = mode_of(r);
-      if (m == kModeAnchored || m == kModeScan) dfa_site.push_back(make_uint2(r, k));
-      else if (m == kModePrefilter) pref_site.push_back(make_uint2(r, k));
+      if (m == kModeAnchored || m == kModeScan) dfa_site.push_back(make_uint2(canon[r], k));
+      else if (m == kModePrefilter) pref_site.push_back(make_uint2(canon[r], k));
     }
   }
   dfa_site_off[n_hosts] = (uint32_t)dfa_site.size();
   pref_site_off[n_hosts] = (uint32_t)pref_site.size();
   for (uint32_t g = 0; g < rs->n_global; ++g) {
     const RuleMode m = mode_of(g);
-    if (m == kModeAnchored || m == kModeScan) dfa_glob.push_back(make_uint2(g, g));
-    else if (m == kModePrefilter) pref_glob.push_back(make_uint2(g, g));
+    if (m == kModeAnchored || m == kModeScan) dfa_glob.push_back(make_uint2(canon[g], g));
+    else if (m == kModePrefilter) pref_glob.push_back(make_uint2(canon[g], g));
   }
   // inline anchor tests (anchor_quick) of the dfa_site / dfa_glob entries
   auto anchor_q = [&](const std::vector<uint2> &ents) {
@@ -2929,13 +2938,13 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     for (uint32_t g = 0; g < rs->n_global; ++g)
       if (mode_of(g) == kModePrefilter)
         for (uint32_t i = drules[g].lits_off; i < drules[g].lits_off + drules[g].lits_len; ++i)
-          lr_g[rule_lits[i]].push_back(make_uint2(g | equiv_of(g), g));
+          lr_g[rule_lits[i]].push_back(make_uint2(canon[g] | equiv_of(g), g));
     for (uint32_t h = 0; h < n_hosts; ++h)
       for (uint32_t k = 0; k < per_host[h].size(); ++k) {
         const uint32_t r = per_host[h][k];
         if (mode_of(r) != kModePrefilter) continue;
         for (uint32_t i = drules[r].lits_off; i < drules[r].lits_off + drules[r].lits_len; ++i)
-          lr_s[rule_lits[i]].push_back({(int32_t)h, make_uint2(r | equiv_of(r), k)});
+          lr_s[rule_lits[i]].push_back({(int32_t)h, make_uint2(canon[r] | equiv_of(r), k)});
       }
   }
   std::vector<uint32_t> lr_off(n_lit + 1, 0), lr_gend(std::max<uint32_t>(1, n_lit), 0);
