@@ -524,3 +524,40 @@ def test_table_overflow_rollback(engine, budget):
         pair.compare_state(sorted(ips)[:60])
     finally:
         engine.debug_set_claim_budget(0)
+
+
+def test_shared_patterns_across_rules(engine):
+    """Rules that repeat one pattern (on several hosts, and as a global) under
+    different names, limits, decisions and hosts_to_skip: the device runs one
+    automaton per pattern (engine.hip `canon`), while results, state keys and
+    trips stay per rule (regex_rate_limiter.go:175-211, rate_limit.go:37-78)."""
+    pats = [r"(GET|POST) \S+ (GET|POST) \/admin\/", r"(?i)union.+select", r"^GET \S+ GET \/api\/[0-9]+ ",
+            r"\/static\/(js|css)\/", r".*blockme.*"]
+    hosts = ["h%d.example.com" % i for i in range(6)]
+    decs = ["challenge", "nginx_block", "iptables_block"]
+    rnd = random.Random(21)
+    out = ["regexes_with_rates:"]
+    for k, p in enumerate(pats[:3]):
+        out.append("  - rule: 'g%d'\n    regex: '%s'\n    interval: 2\n    hits_per_interval: %d\n    decision: %s\n"
+                   "    hosts_to_skip:\n      h1.example.com: true" % (k, p.replace("'", "''"), k, decs[k % 3]))
+    out.append("per_site_regexes_with_rates:")
+    for hi, h in enumerate(hosts[:5]):
+        out.append("  %s:" % h)
+        for k, p in enumerate(pats):
+            if (hi + k) % 4 == 3:
+                continue
+            out.append("    - rule: '%s'\n      regex: '%s'\n      interval: %d\n      hits_per_interval: %d\n"
+                       "      decision: %s" % ("s%d" % k if hi % 2 else "%s r%d" % (h, k), p.replace("'", "''"),
+                                              1 + hi, (hi * k) % 3, decs[(hi + k) % 3]))
+    pair = Pair("\n".join(out) + "\n", engine)
+    uris = ["/admin/x", "/api/12 ", "/static/js/a.js", "/q?UNION%20x%20select", "/blockme", "/admin", "/api/x", "/"]
+    base = 1700000000
+    for b in range(2):
+        lines = []
+        for j in range(6000):
+            m = rnd.choice(["GET", "POST"])
+            lines.append("%.3f 10.0.%d.%d %s %s %s %s HTTP/1.1 UA-%d\n" % (
+                base + b * 3 + j * 0.0004, rnd.randrange(4), rnd.randrange(8), m, rnd.choice(hosts), m,
+                rnd.choice(uris) + rnd.choice(["", " ", "x"]), j % 7))
+        pair.feed("".join(lines).encode(), (base + b * 3 + 3) * S)
+    pair.compare_state(["10.0.%d.%d" % (a, c) for a in range(4) for c in range(8)])
