@@ -65,9 +65,14 @@ class EventLine(C.Structure):
                 ("n_events", C.c_uint32), ("_pad", C.c_uint32)]
 
 
+class TzTransition(C.Structure):
+    _fields_ = [("utc_start_s", C.c_int64), ("offset_s", C.c_int32), ("_pad", C.c_int32)]
+
+
 class BanOptions(C.Structure):
     _fields_ = [("expiring_ttl_ns", C.c_int64), ("tz_offset_s", C.c_int32), ("_pad", C.c_uint32),
-                ("disable_logging", C.POINTER(Str)), ("n_disable_logging", C.c_size_t)]
+                ("disable_logging", C.POINTER(Str)), ("n_disable_logging", C.c_size_t),
+                ("tz_transitions", C.POINTER(TzTransition)), ("n_tz_transitions", C.c_size_t)]
 
 
 class IpDecision(C.Structure):
@@ -172,6 +177,8 @@ def lib():
     L.bjx_debug_set_claim_budget.argtypes = [vp, C.c_uint64]
     L.bjx_debug_set_ip_hash_mask.restype = C.c_int
     L.bjx_debug_set_ip_hash_mask.argtypes = [vp, C.c_uint64]
+    L.bjx_debug_set_dfa_state_cap.restype = C.c_int
+    L.bjx_debug_set_dfa_state_cap.argtypes = [C.c_uint32]
     L.bjx_tailer_open.restype = C.c_int
     L.bjx_tailer_open.argtypes = [C.c_char_p, sz, C.POINTER(TailerOptions), C.POINTER(vp), C.c_char_p, sz]
     L.bjx_tailer_next.restype = C.c_int

@@ -37,7 +37,10 @@ struct BanDev {
   const uint32_t *dl_off, *dl_len;
   const uint8_t *dl_bytes;
   uint32_t n_dl;
-  int32_t tz_offset_s;
+  int32_t tz_offset_s;       // offset before the first transition (fixed zone when n_tz == 0)
+  const int64_t *tz_at;      // local zone: UTC second of each offset change, ascending
+  const int32_t *tz_off;     // offset from tz_at[i] on
+  uint32_t n_tz;
 };
 
 template <bool W>
@@ -124,12 +127,24 @@ BJX_HD void put_dec(JOut<W> &o, int64_t v, int width) {
   while (k) o.put((uint8_t)d[--k]);
 }
 
-// time.Unix(0, ns).In(fixed zone).Format("2006-01-02T15:04:05")
+// offset of the local zone at Unix second sec (time.Location.lookup: the last
+// transition at or before sec)
+__device__ __forceinline__ int32_t zone_offset(const BanDev &A, int64_t sec) {
+  if (A.n_tz == 0 || sec < A.tz_at[0]) return A.tz_offset_s;
+  uint32_t lo = 0, hi = A.n_tz;  // tz_at[lo] <= sec < tz_at[hi]
+  while (hi - lo > 1) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (A.tz_at[m] <= sec) lo = m; else hi = m;
+  }
+  return A.tz_off[lo];
+}
+
+// time.Unix(0, ns).In(time.Local).Format("2006-01-02T15:04:05")
 template <bool W>
-__device__ void put_time(JOut<W> &o, int64_t ns, int32_t tz) {
+__device__ void put_time(JOut<W> &o, int64_t ns, const BanDev &A) {
   int64_t sec = ns / 1000000000LL;
   if (ns % 1000000000LL < 0) --sec;
-  sec += tz;
+  sec += zone_offset(A, sec);
   int64_t days = sec / 86400, sod = sec % 86400;
   if (sod < 0) { sod += 86400; --days; }
   // civil date from days since 1970-01-01 (proleptic Gregorian)
@@ -192,7 +207,7 @@ __device__ uint32_t ban_log_line(const BanDev &A, uint64_t t, JOut<W> &o) {
   o.puts("{\"path\":");
   json_str(o, rest + sp[2] + 1, sp[3] - sp[2] - 1);
   o.puts(",\"timestring\":\"");
-  put_time(o, T.ts_ns, A.tz_offset_s);
+  put_time(o, T.ts_ns, A);
   o.puts("\",\"trigger\":");
   o.raw(A.name_json + A.name_off[R.name_id], A.name_off[R.name_id + 1] - A.name_off[R.name_id]);
   o.puts(",\"client_ua\":");

@@ -264,11 +264,131 @@ __device__ __forceinline__ bool is_skip(const Bind &B, uint32_t rule, int32_t ho
 
 // --------------------------------------------------------------- regex
 
-// (*Regexp).Match over rest, via the rule's rune-class DFA.
+// ---- bit-parallel NFA (rules past the DFA state cap; regex_compiler.cpp
+// "bit-parallel NFA" gives the algorithm and the table layout).  State sets
+// are WT 64-bit words in VGPRs; EXACT: the rule's W equals WT (k_nfa), else W
+// <= WT is read from the header (per-line slow path).
+
+template <int WT>
+__device__ __forceinline__ bool nfa_bit(const uint64_t (&v)[WT], uint32_t p) {
+  uint64_t w = 0;
+#pragma unroll
+  for (int k = 0; k < WT; ++k) w = (p >> 6) == (uint32_t)k ? v[k] : w;  // selects: no scratch
+  return ((w >> (p & 63)) & 1) != 0;
+}
+
+// X = D with the assertion closures of context k (ctx * 4 + next category)
+template <int WT, bool EXACT>
+__device__ __forceinline__ void nfa_cross(const uint64_t *__restrict__ b, const NfaLayout &L, const uint64_t (&D)[WT],
+                                          uint64_t (&X)[WT], uint32_t k) {
+  const uint32_t W = EXACT ? (uint32_t)WT : L.W;
+#pragma unroll
+  for (int w = 0; w < WT; ++w) X[w] = D[w];
+  if (!(L.flags & kNfaAsserts)) return;
+  const uint32_t *apos = reinterpret_cast<const uint32_t *>(b + L.o_apos);
+  for (uint32_t a = 0; a < L.nassert; ++a) {
+    if (!nfa_bit(D, apos[a])) continue;
+    const uint64_t *T = b + L.o_at + (a * 16 + k) * W;
+#pragma unroll
+    for (int w = 0; w < WT; ++w)
+      if (EXACT || (uint32_t)w < W) X[w] |= T[w];
+  }
+}
+
+// one rune of class c; true = matched (before or after it)
+template <int WT, bool EXACT>
+__device__ __forceinline__ bool nfa_rune(const uint64_t *__restrict__ b, const NfaLayout &L, uint64_t (&D)[WT], uint32_t c,
+                                         uint32_t &ctx) {
+  const uint32_t W = EXACT ? (uint32_t)WT : L.W;
+  uint64_t X[WT], Y[WT];
+  const uint32_t cat = (L.flags & kNfaAsserts) ? reinterpret_cast<const uint8_t *>(b + L.o_cat)[c] : 0u;
+  nfa_cross<WT, EXACT>(b, L, D, X, ctx * 4 + cat);
+  ctx = cat == 1 ? 1u : (cat == 2 ? 2u : 0u);
+  if (L.match != 0xFFFFFFFFu && nfa_bit(X, L.match)) return true;
+  const uint64_t *cm = b + L.o_cm + c * W, *sh = b + L.o_sh, *s0 = b + L.o_s0;
+#pragma unroll
+  for (int w = 0; w < WT; ++w) Y[w] = (EXACT || (uint32_t)w < W) ? X[w] & cm[w] : 0ull;
+  uint64_t carry = 0;
+#pragma unroll
+  for (int w = 0; w < WT; ++w) {
+    if (!EXACT && (uint32_t)w >= W) { D[w] = 0; continue; }
+    const uint64_t m = Y[w] & sh[w];
+    D[w] = (m << 1) | carry | s0[w];
+    carry = m >> 63;
+  }
+  for (uint32_t g = 0; g < L.ngroups; ++g) {
+    const uint64_t *gm = b + L.o_gm + g * W, *gt = b + L.o_gt + g * W;
+    uint64_t any = 0;
+#pragma unroll
+    for (int w = 0; w < WT; ++w)
+      if (EXACT || (uint32_t)w < W) any |= Y[w] & gm[w];
+    if (any) {
+#pragma unroll
+      for (int w = 0; w < WT; ++w)
+        if (EXACT || (uint32_t)w < W) D[w] |= gt[w];
+    }
+  }
+  return L.match != 0xFFFFFFFFu && nfa_bit(D, L.match);
+}
+
+template <int WT, bool EXACT>
+__device__ __forceinline__ bool nfa_at_s0(const uint64_t *__restrict__ b, const NfaLayout &L, const uint64_t (&D)[WT]) {
+  const uint32_t W = EXACT ? (uint32_t)WT : L.W;
+  uint64_t d = 0;
+#pragma unroll
+  for (int w = 0; w < WT; ++w)
+    if (EXACT || (uint32_t)w < W) d |= D[w] ^ b[L.o_s0 + w];
+  return d == 0;
+}
+
+template <int WT, bool EXACT>
+__device__ __forceinline__ bool nfa_end(const uint64_t *__restrict__ b, const NfaLayout &L, const uint64_t (&D)[WT], uint32_t ctx) {
+  uint64_t X[WT];
+  nfa_cross<WT, EXACT>(b, L, D, X, ctx * 4 + 3);
+  return L.match != 0xFFFFFFFFu && nfa_bit(X, L.match);
+}
+
+__device__ __forceinline__ uint32_t nonascii_class(const Bind &B, const DevRule &R, int32_t rune) {
+  const uint32_t *na = B.nonascii + 2 * R.na_off;
+  uint32_t lo = 0, hi = R.n_na;  // last interval with start <= rune
+  while (hi - lo > 1) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (na[2 * m] <= (uint32_t)rune) lo = m; else hi = m;
+  }
+  return na[2 * lo + 1];
+}
+
+// (*Regexp).Match of a kRuleNfa rule over [t, t + n), tables at b (any
+// address space; the per-line slow path reads them from HBM)
+__device__ __noinline__ bool nfa_match_generic(const Bind &B, const DevRule &R, const uint8_t *t, uint32_t n) {
+  const uint64_t *b = B.nfa + R.nfa_off;
+  const NfaLayout L = nfa_layout_of(reinterpret_cast<const uint32_t *>(b));
+  const uint16_t *a16 = reinterpret_cast<const uint16_t *>(b + L.o_ascii);
+  uint64_t D[16];
+#pragma unroll
+  for (int w = 0; w < 16; ++w) D[w] = (uint32_t)w < L.W ? b[L.o_s0 + w] : 0ull;
+  uint32_t ctx = 3;
+  for (uint32_t i = 0; i < n;) {
+    uint32_t c;
+    if (t[i] < 0x80) { c = a16[t[i]]; ++i; }
+    else {
+      int w;
+      const int32_t rune = decode_rune_hd(t + i, n - i, &w);
+      c = nonascii_class(B, R, rune);
+      i += (uint32_t)w;
+    }
+    if (nfa_rune<16, false>(b, L, D, c, ctx)) return true;
+    if ((L.flags & kNfaAnchored) && nfa_at_s0<16, false>(b, L, D)) return false;
+  }
+  return nfa_end<16, false>(b, L, D, ctx);
+}
+
+// (*Regexp).Match over rest, via the rule's rune-class DFA (or bit-parallel NFA).
 __device__ bool rule_match(const Bind &B, uint32_t r, const uint8_t *t, uint32_t n) {
   const DevRule R = B.rules[r];
   if (R.flags & kRuleAlways) return true;
   if (R.flags & kRuleNever) return false;
+  if (R.flags & kRuleNfa) return nfa_match_generic(B, R, t, n);
   const uint16_t *tr = B.trans + R.trans_off;
   const uint8_t *ac = B.ascii_cls + (size_t)r * 128;
   const uint32_t ncls = R.ncls;
@@ -1314,7 +1434,9 @@ __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restric
   const uint64_t tl = t0 + blockDim.x - 1 < n ? t0 + blockDim.x - 1 : n - 1;
   const uint32_t r0 = jkey[t0] & 0xFFFFFF;
   const DevRule R0 = B.rules[r0];
-  const bool staged = (jkey[tl] & 0xFFFFFF) == r0 && (uint32_t)R0.ncls * R0.n_states <= kDfaLdsEntries;
+  const bool uniform = (jkey[tl] & 0xFFFFFF) == r0;  // jobs sorted by rule: the whole block is r0's
+  if (uniform && (R0.flags & kRuleNfa)) return;       // k_nfa's
+  const bool staged = uniform && (uint32_t)R0.ncls * R0.n_states <= kDfaLdsEntries;
   if (staged) {
     const uint16_t *g = B.trans + R0.trans_off;
     for (uint32_t i = threadIdx.x; i < (uint32_t)R0.ncls * R0.n_states; i += blockDim.x) s_tr[i] = g[i];
@@ -1332,6 +1454,7 @@ __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restric
     m = dfa_text<true>(B, R0, s_tr, s_ac, buf, n_buf, rs, (uint32_t)(nl[j] - rs));
   } else {
     const DevRule R = B.rules[r];
+    if (R.flags & kRuleNfa) return;  // k_nfa's
     m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, buf, n_buf, rs, (uint32_t)(nl[j] - rs));
   }
   if (!m) return;
@@ -1340,6 +1463,92 @@ __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restric
   const bool skip = (B.sc_skip[2 * sc + (pos >> 6)] >> (pos & 63)) & 1;
   atomicOr(reinterpret_cast<unsigned long long *>(L.masks + j * B.mask_words + (pos >> 6)), 1ull << (pos & 63));
   atomicAdd(reinterpret_cast<unsigned long long *>(L.counts + j), (1ull << 32) | (skip ? 0ull : 1ull));
+}
+
+// DFA jobs of one kRuleNfa rule (the sorted job range [j0, j1)): one job per
+// lane, the rule's tables staged in LDS, WT-word state sets in VGPRs, text
+// read 16 B at a time (a non-ASCII byte switches the rest of the text to rune
+// decoding, as dfa_text does).
+template <int WT>
+__global__ __launch_bounds__(kBlock) void k_nfa(Bind B, uint32_t rule, const uint8_t *__restrict__ buf, uint64_t n_buf,
+                                                const uint64_t *__restrict__ nl, const uint32_t *__restrict__ jkey,
+                                                const uint32_t *__restrict__ jline, uint64_t j0, uint64_t j1, Lines L) {
+  uint64_t *s_b = reinterpret_cast<uint64_t *>(s_dyn);
+  const DevRule R = B.rules[rule];
+  const uint64_t *g = B.nfa + R.nfa_off;
+  const uint32_t total = reinterpret_cast<const uint32_t *>(g)[7];
+  for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) s_b[i] = g[i];
+  __syncthreads();
+  const uint64_t t = j0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= j1) return;
+  const NfaLayout Ly = nfa_layout_of(reinterpret_cast<const uint32_t *>(s_b));
+  const uint16_t *a16 = reinterpret_cast<const uint16_t *>(s_b + Ly.o_ascii);
+  const uint32_t key = jkey[t], pos = key >> 24;
+  const uint64_t j = jline[t];
+  const uint64_t s = j ? nl[j - 1] + 1 : 0;
+  const uint64_t t0 = s + L.rest_off[j], end = nl[j];
+  uint64_t D[WT];
+#pragma unroll
+  for (int w = 0; w < WT; ++w) D[w] = s_b[Ly.o_s0 + w];
+  uint32_t ctx = 3;
+  bool m = false, done = false;
+  auto load16 = [&](uint64_t p) -> uint4 {
+    if (p + 16 <= n_buf) return *reinterpret_cast<const uint4 *>(buf + p);
+    uint32_t w4[4];
+    for (int k = 0; k < 4; ++k) {
+      uint32_t x = 0;
+      for (int q = 0; q < 4; ++q) x |= (p + 4 * k + q < n_buf ? (uint32_t)buf[p + 4 * k + q] : 0u) << (8 * q);
+      w4[k] = x;
+    }
+    return make_uint4(w4[0], w4[1], w4[2], w4[3]);
+  };
+  uint64_t a = t0 & ~15ull;
+  uint32_t skip = (uint32_t)(t0 - a);
+  uint64_t slow_at = end;  // first non-ASCII byte: runes from here on
+  uint4 v = a < end ? load16(a) : make_uint4(0, 0, 0, 0);
+  while (a < end && !done) {
+    const uint4 vn = a + 16 < end ? load16(a + 16) : make_uint4(0, 0, 0, 0);
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t lim = end - a < 16 ? (uint32_t)(end - a) : 16u;
+    for (uint32_t k = skip; k < lim; ++k) {
+      const uint32_t by = (wv[k >> 2] >> (8 * (k & 3))) & 0xFF;
+      if (by >= 0x80) { slow_at = a + k; done = true; break; }
+      if (nfa_rune<WT, true>(s_b, Ly, D, a16[by], ctx)) { m = true; done = true; break; }
+      if ((Ly.flags & kNfaAnchored) && nfa_at_s0<WT, true>(s_b, Ly, D)) { done = true; break; }
+    }
+    skip = 0;
+    a += 16;
+    v = vn;
+  }
+  if (!m && slow_at < end) {
+    for (uint64_t i = slow_at; i < end;) {
+      int w;
+      const int32_t rune = decode_rune_hd(buf + i, (uint32_t)(end - i), &w);
+      const uint32_t c = rune < 0x80 ? a16[rune] : nonascii_class(B, R, rune);
+      i += (uint32_t)w;
+      if (nfa_rune<WT, true>(s_b, Ly, D, c, ctx)) { m = true; break; }
+      if ((Ly.flags & kNfaAnchored) && nfa_at_s0<WT, true>(s_b, Ly, D)) { slow_at = end; break; }
+    }
+    if (!m && slow_at != end) m = nfa_end<WT, true>(s_b, Ly, D, ctx);
+  } else if (!m && !done) {
+    m = nfa_end<WT, true>(s_b, Ly, D, ctx);
+  }
+  if (!m) return;
+  const int32_t hid = L.host_id[j];
+  const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
+  const bool skp = (B.sc_skip[2 * sc + (pos >> 6)] >> (pos & 63)) & 1;
+  atomicOr(reinterpret_cast<unsigned long long *>(L.masks + j * B.mask_words + (pos >> 6)), 1ull << (pos & 63));
+  atomicAdd(reinterpret_cast<unsigned long long *>(L.counts + j), (1ull << 32) | (skp ? 0ull : 1ull));
+}
+
+// first / one-past-last sorted job of every rule that has jobs
+__global__ void k_rule_bounds(uint64_t n, const uint32_t *__restrict__ jkey, uint32_t *__restrict__ first,
+                              uint32_t *__restrict__ last) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = jkey[i] & 0xFFFFFF;
+  if (i == 0 || (jkey[i - 1] & 0xFFFFFF) != r) first[r] = (uint32_t)i;
+  if (i + 1 == n || (jkey[i + 1] & 0xFFFFFF) != r) last[r] = (uint32_t)(i + 1);
 }
 
 // RuleResults (reference order) and rate-limit events from the per-line masks.
@@ -2408,6 +2617,9 @@ struct bjx_engine {
   uint64_t bound_uid = 0, bound_dec_version = 0;
   DevBuf<uint8_t> bind_blob;
   Bind bind{};
+  std::vector<uint4> nfa_rules;  // (rule, state words, table words) of the kRuleNfa patterns (k_nfa launches)
+  DevBuf<uint32_t> rb_first, rb_last;
+  std::vector<uint32_t> h_first, h_last;
   std::vector<DevRule> host_rules;
 
   // persistent state
@@ -2463,6 +2675,8 @@ struct bjx_engine {
   // trip -> decision emission (bjx_engine_set_ban_options / bjx_batch_bans)
   int64_t ban_ttl_ns = 0;
   int32_t ban_tz = 0;
+  DevBuf<int64_t> tz_at; DevBuf<int32_t> tz_off;
+  uint32_t n_tz = 0;
   DevBuf<uint64_t> dl_hash; DevBuf<uint32_t> dl_off, dl_len; DevBuf<uint8_t> dl_bytes;
   uint32_t n_dl = 0;
   DevBuf<uint32_t> nm_off; DevBuf<uint8_t> nm_json;
@@ -2721,6 +2935,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   std::vector<uint8_t> lit_bytes, lit_ci;
   std::vector<uint32_t> lit_off, lit_len, lit_gram, rule_lits;
   std::vector<uint8_t> lit_pref;
+  std::vector<uint64_t> nfa_blob;
   bool any_anchored = false;
   for (size_t i = 0; i < rs->rules.size(); ++i) {
     const auto &r = rs->rules[i];
@@ -2772,6 +2987,11 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     any_anchored = any_anchored || r.rx.mode == kModeAnchored;
     d.interval_ns = r.interval_ns;
     d.hits = r.hits;
+    if (r.rx.flags & kRuleNfa) {
+      d.nfa_off = (uint32_t)nfa_blob.size();
+      d.nfa_words = r.rx.nfa_words;
+      nfa_blob.insert(nfa_blob.end(), r.rx.nfa.begin(), r.rx.nfa.end());
+    }
   }
   std::vector<uint8_t> lit_chk;
   calibrate_grams(lit_bytes, lit_ci, lit_off, lit_len, lit_gram, lit_chk, sample, sample_n);
@@ -3075,7 +3295,8 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
          o_lre = bb.add(lr_ent), o_lrh = bb.add(lr_host), o_sca = bb.add(sc_always), o_scs = bb.add(sc_skipm),
          o_dso = bb.add(dfa_site_off), o_ds = bb.add(dfa_site), o_dg = bb.add(dfa_glob), o_pso = bb.add(pref_site_off),
          o_dsq = bb.add(dfa_site_q), o_dgq = bb.add(dfa_glob_q),
-         o_ps = bb.add(pref_site), o_pg = bb.add(pref_glob), o_hslot = bb.add(hslot), o_lh = bb.add(lh_tab);
+         o_ps = bb.add(pref_site), o_pg = bb.add(pref_glob), o_hslot = bb.add(hslot), o_lh = bb.add(lh_tab),
+         o_nfa = bb.add(nfa_blob);
   e->bind_blob.ensure(bb.bytes.size());
   HIP_OK(hipMemcpy(e->bind_blob.p, bb.bytes.data(), bb.bytes.size(), hipMemcpyHostToDevice));
   uint8_t *base = e->bind_blob.p;
@@ -3144,6 +3365,13 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.pref_site = reinterpret_cast<const uint2 *>(base + o_ps);
   B.pref_glob = reinterpret_cast<const uint2 *>(base + o_pg);
   B.n_pref_glob = (uint32_t)pref_glob.size();
+  B.nfa = reinterpret_cast<const uint64_t *>(base + o_nfa);
+  B.any_nfa = nfa_blob.empty() ? 0 : 1;
+  // DFA jobs name the first rule of each pattern (canon): those of the NFA rules
+  e->nfa_rules.clear();
+  for (uint32_t r = 0; r < (uint32_t)rs->rules.size(); ++r)
+    if (canon[r] == r && (rs->rules[r].rx.flags & kRuleNfa) && !(rs->rules[r].rx.flags & (kRuleAlways | kRuleNever)))
+      e->nfa_rules.push_back(make_uint4(r, rs->rules[r].rx.nfa_words, (uint32_t)rs->rules[r].rx.nfa.size(), 0));
   e->host_rules = drules;
   e->bound_uid = rs->uid;
   e->bound_dec_version = e->decisions_version;
@@ -3319,7 +3547,8 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
                   &e->dl_off, &e->dl_len, &e->nm_off})
     b->release();
   for (auto *b : {&e->bn_kind, &e->bn_flag, &e->bn_log, &e->dl_bytes, &e->nm_json}) b->release();
-  e->bn_best.release(); e->bn_rep.release(); e->bn_sel.release();
+  e->bn_best.release(); e->bn_rep.release(); e->bn_sel.release(); e->tz_at.release(); e->tz_off.release();
+  e->rb_first.release(); e->rb_last.release();
   e->d_results.release(); e->q_out.release();
   e->long_list.release(); e->l_ip16.release(); e->jline.release(); e->jkey.release(); e->jline2.release(); e->jkey2.release(); e->l_cand.release(); e->l_ccnt.release();
   (void)hipEventDestroy(e->ev0); (void)hipEventDestroy(e->ev1); (void)hipEventDestroy(e->evm0); (void)hipEventDestroy(e->evm1);
@@ -3458,6 +3687,35 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
   hipLaunchKernelGGL(k_apply, dim3((unsigned)((n_ev + kApplyChunk - 1) / kApplyChunk)), dim3(kBlock), 0, st, n_ev,
                      e->ev_st2.p, e->ev_rec2.p, B.rules, e->S.st, e->ev_out_s.p);
   HIP_OK(hipGetLastError());
+}
+
+// The sorted DFA jobs of the bit-parallel NFA rules: each rule's job range
+// (k_rule_bounds), then one k_nfa launch per rule with its state width.
+static void run_nfa_jobs(bjx_engine *e, const Bind &B, const uint8_t *buf, uint64_t n, uint64_t n_jobs, const Lines &L) {
+  hipStream_t st = e->stream;
+  e->rb_first.ensure(B.n_rules); e->rb_last.ensure(B.n_rules);
+  HIP_OK(hipMemsetAsync(e->rb_first.p, 0, B.n_rules * 4ull, st));
+  HIP_OK(hipMemsetAsync(e->rb_last.p, 0, B.n_rules * 4ull, st));
+  hipLaunchKernelGGL(k_rule_bounds, dim3(grid_for(n_jobs)), dim3(kBlock), 0, st, n_jobs, e->jkey2.p, e->rb_first.p, e->rb_last.p);
+  HIP_OK(hipGetLastError());
+  e->h_first.resize(B.n_rules); e->h_last.resize(B.n_rules);
+  HIP_OK(hipMemcpyAsync(e->h_first.data(), e->rb_first.p, B.n_rules * 4ull, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(e->h_last.data(), e->rb_last.p, B.n_rules * 4ull, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  for (const uint4 &nr : e->nfa_rules) {
+    const uint64_t j0 = e->h_first[nr.x], j1 = e->h_last[nr.x];
+    if (j1 <= j0) continue;
+    const unsigned grid = grid_for(j1 - j0);
+    const uint32_t lds = nr.z * 8;
+    switch (nr.y) {
+      case 1: hipLaunchKernelGGL(k_nfa<1>, dim3(grid), dim3(kBlock), lds, st, B, nr.x, buf, n, e->nl.p, e->jkey2.p, e->jline2.p, j0, j1, L); break;
+      case 2: hipLaunchKernelGGL(k_nfa<2>, dim3(grid), dim3(kBlock), lds, st, B, nr.x, buf, n, e->nl.p, e->jkey2.p, e->jline2.p, j0, j1, L); break;
+      case 4: hipLaunchKernelGGL(k_nfa<4>, dim3(grid), dim3(kBlock), lds, st, B, nr.x, buf, n, e->nl.p, e->jkey2.p, e->jline2.p, j0, j1, L); break;
+      case 8: hipLaunchKernelGGL(k_nfa<8>, dim3(grid), dim3(kBlock), lds, st, B, nr.x, buf, n, e->nl.p, e->jkey2.p, e->jline2.p, j0, j1, L); break;
+      default: hipLaunchKernelGGL(k_nfa<16>, dim3(grid), dim3(kBlock), lds, st, B, nr.x, buf, n, e->nl.p, e->jkey2.p, e->jline2.p, j0, j1, L); break;
+    }
+    HIP_OK(hipGetLastError());
+  }
 }
 
 // consumeLine up to Apply for every line: framing, header, exemption, rule
@@ -3627,6 +3885,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     hipLaunchKernelGGL(k_dfa, dim3(grid_for(n_jobs)), dim3(kBlock), 0, st, B, buf, (uint64_t)n, e->nl.p, e->jkey2.p,
                        e->jline2.p, (uint64_t)n_jobs, L);
     HIP_OK(hipGetLastError());
+    if (B.any_nfa && !e->nfa_rules.empty()) run_nfa_jobs(e, B, buf, n, n_jobs, L);
   }
   if (n_slow) {
     hipLaunchKernelGGL(k_parse_match<true>, dim3(grid_for(n_slow)), dim3(kBlock), 0, st, B, buf, e->nl.p, (uint64_t)n_slow,
@@ -3718,6 +3977,7 @@ static void emit_bans(bjx_engine *e, uint64_t n) {
   A.name_off = e->nm_off.p; A.name_json = e->nm_json.p;
   A.dl_hash = e->dl_hash.p; A.dl_off = e->dl_off.p; A.dl_len = e->dl_len.p; A.dl_bytes = e->dl_bytes.p; A.n_dl = e->n_dl;
   A.tz_offset_s = e->ban_tz;
+  A.tz_at = e->tz_at.p; A.tz_off = e->tz_off.p; A.n_tz = e->n_tz;
   const int64_t expires = (int64_t)((uint64_t)e->bc.now_ns + (uint64_t)e->ban_ttl_ns);
   // ban-log lines: lengths, offsets, bytes
   e->bn_len.ensure(n + 1); e->bn_off.ensure(n + 1); e->bn_kind.ensure(n);
@@ -4075,10 +4335,26 @@ extern "C" int bjx_finish_batch(bjx_engine *e, const uint8_t *d_outcomes, uint32
 }
 
 extern "C" int bjx_engine_set_ban_options(bjx_engine *e, const bjx_ban_options *o) {
-  if (!o || (o->n_disable_logging && !o->disable_logging)) return BJX_ERR_ARG;
+  if (!o || (o->n_disable_logging && !o->disable_logging) || (o->n_tz_transitions && !o->tz_transitions) ||
+      o->n_tz_transitions >= (1u << 24))
+    return BJX_ERR_ARG;
+  for (size_t i = 1; i < o->n_tz_transitions; ++i)
+    if (o->tz_transitions[i].utc_start_s <= o->tz_transitions[i - 1].utc_start_s) return BJX_ERR_ARG;
   return guarded(e, [&]() -> int {
     e->ban_ttl_ns = o->expiring_ttl_ns;
     e->ban_tz = o->tz_offset_s;
+    std::vector<int64_t> tz_at(o->n_tz_transitions);
+    std::vector<int32_t> tz_off(o->n_tz_transitions);
+    for (size_t i = 0; i < o->n_tz_transitions; ++i) {
+      tz_at[i] = o->tz_transitions[i].utc_start_s;
+      tz_off[i] = o->tz_transitions[i].offset_s;
+    }
+    e->n_tz = (uint32_t)tz_at.size();
+    e->tz_at.ensure(std::max<size_t>(1, tz_at.size())); e->tz_off.ensure(std::max<size_t>(1, tz_off.size()));
+    if (!tz_at.empty()) {
+      HIP_OK(hipMemcpy(e->tz_at.p, tz_at.data(), tz_at.size() * 8, hipMemcpyHostToDevice));
+      HIP_OK(hipMemcpy(e->tz_off.p, tz_off.data(), tz_off.size() * 4, hipMemcpyHostToDevice));
+    }
     std::vector<std::pair<uint64_t, std::string>> hs;
     for (size_t i = 0; i < o->n_disable_logging; ++i) {
       const bjx_str &h = o->disable_logging[i];
@@ -4233,6 +4509,12 @@ extern "C" size_t bjx_state_dump(bjx_engine *e, char *out, size_t cap) {
 extern "C" int bjx_debug_rule_match_host(const bjx_ruleset *rs, size_t i, const uint8_t *text, size_t n) {
   if (!rs || i >= rs->rules.size() || (n && !text)) return BJX_ERR_ARG;
   return dfa_match_host(rs->rules[i].rx, text, n) ? 1 : 0;
+}
+extern "C" int bjx_debug_set_dfa_state_cap(uint32_t cap) {
+  set_dfa_state_cap(cap);
+  std::lock_guard<std::mutex> g(g_rx_mu);
+  g_rx_cache.clear();  // compiled patterns depend on the cap
+  return BJX_OK;
 }
 extern "C" int bjx_debug_set_ip_hash_mask(bjx_engine *e, uint64_t mask) {
   if (!e) return BJX_ERR_ARG;

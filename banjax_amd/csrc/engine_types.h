@@ -23,9 +23,11 @@ struct DevRule {
   uint16_t anc_len;
   uint8_t anc_equiv;     // match <=> rest starts with one of them
   uint8_t _pad;
-  uint32_t n_states;     // DFA states (rows of trans)
+  uint32_t n_states;     // DFA states (rows of trans); NFA positions for kRuleNfa
   int64_t interval_ns;
   int64_t hits;
+  uint32_t nfa_off;      // kRuleNfa: u64 index of the rule's tables in Bind::nfa
+  uint32_t nfa_words;    // kRuleNfa: 64-bit words per state set (1, 2, 4, 8, 16)
 };
 
 // Prefilter gram bitset: one bit per hash of a 4-byte window (LDS resident).
@@ -158,6 +160,9 @@ struct Bind {
   const uint2 *pref_site;
   const uint2 *pref_glob;
   uint32_t n_pref_glob;
+  // bit-parallel NFA tables of the kRuleNfa rules (DevRule::nfa_off)
+  const uint64_t *nfa;
+  uint32_t any_nfa;
 };
 
 // Per-line SoA arrays (batch workspace).

@@ -18,6 +18,7 @@
 #include "regex_compiler.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <strings.h>
 #include <map>
@@ -26,6 +27,7 @@
 
 #include "../../include/banjax_gpu.h"
 #include "../../third_party/unicode/fold_orbits.h"
+#include "../../third_party/unicode/unicode_tables.h"
 
 namespace bjx {
 namespace {
@@ -100,6 +102,61 @@ void add_folded(Ranges &r, int32_t lo, int32_t hi) {
     r.push_back({c, c});
     for (int32_t f = simple_fold(c); f != c; f = simple_fold(f)) r.push_back({f, f});
   }
+}
+
+// ------------------------------------------------ Unicode groups (\p{..})
+//
+// regexp/syntax unicodeTable (Go 1.25): "Any", the general categories of
+// package unicode (incl. LC and Cn), its scripts, "Assigned" (= not Cn) and
+// "ASCII", then the same names and unicode.CategoryAliases matched loosely
+// (canonicalName: case-insensitive, ignoring '_', '-' and ' ').  Tables:
+// third_party/unicode/unicode_tables.h (Unicode 15.0.0).
+
+std::string canonical_name(const std::string &n) {
+  std::string b;
+  bool first = true;
+  for (char c : n) {
+    if (c == '_' || c == '-' || c == ' ') continue;
+    if (first) {
+      if (c >= 'a' && c <= 'z') c = static_cast<char>(c - 'a' + 'A');
+      first = false;
+    } else if (c >= 'A' && c <= 'Z') {
+      c = static_cast<char>(c - 'A' + 'a');
+    }
+    b.push_back(c);
+  }
+  return b;
+}
+
+void table_ranges(const bjx_uni_table &t, Ranges *out) {
+  for (uint32_t i = 0; i < t.n; ++i)
+    out->push_back({static_cast<int32_t>(bjx_uni_ranges[2 * (t.off + i)]), static_cast<int32_t>(bjx_uni_ranges[2 * (t.off + i) + 1])});
+}
+
+const bjx_uni_table *find_table(const std::string &name, bool loose) {
+  const std::string c = loose ? canonical_name(name) : name;
+  for (size_t i = 0; i < BJX_UNI_NTABLES; ++i)
+    if ((loose ? canonical_name(bjx_uni_tables[i].name) : std::string(bjx_uni_tables[i].name)) == c) return &bjx_uni_tables[i];
+  return nullptr;
+}
+
+// true if name is known: *out = its runes, *sign = -1 when they are to be inverted
+bool unicode_table(const std::string &name, Ranges *out, int *sign) {
+  *sign = 1;
+  out->clear();
+  if (name == "Any") { out->push_back({0, kMaxRune}); return true; }
+  if (const bjx_uni_table *t = find_table(name, false)) { table_ranges(*t, out); return true; }
+  const std::string c = canonical_name(name);
+  if (c == "Any") { out->push_back({0, kMaxRune}); return true; }
+  if (c == "Assigned") { table_ranges(*find_table("Cn", false), out); *sign = -1; return true; }
+  if (c == "Ascii") { out->push_back({0, 0x7F}); return true; }
+  if (const bjx_uni_table *t = find_table(name, true)) { table_ranges(*t, out); return true; }
+  for (size_t i = 0; i < BJX_UNI_NALIASES; ++i)
+    if (canonical_name(bjx_uni_cat_aliases[2 * i]) == c) {
+      table_ranges(*find_table(bjx_uni_cat_aliases[2 * i + 1], false), out);
+      return true;
+    }
+  return false;
 }
 
 // ------------------------------------------------------------------ AST
@@ -464,9 +521,44 @@ class Parser {
       if (g.name[1] == s[1]) return &g;
     return nullptr;
   }
-  void reject_unicode_class(const char *s, const char *end) {
-    if (end - s >= 2 && s[0] == '\\' && (s[1] == 'p' || s[1] == 'P'))
-      throw ParseError{"unsupported Unicode class (\\p) in this build", std::string(s, std::min(end, s + 8))};
+  // parseUnicodeClass (UnicodeGroups, part of syntax.Perl): \pN, \p{Name},
+  // \PN, \P{Name}, \p{^Name}.  Appends the (folded, negated) table to cls and
+  // returns the text after it; nullptr if s is not \p / \P.
+  const char *parse_unicode_class(const char *s, const char *end, Ranges &cls) {
+    if (end - s < 2 || s[0] != '\\' || (s[1] != 'p' && s[1] != 'P')) return nullptr;
+    int sign = s[1] == 'P' ? -1 : 1;
+    const char *t = s + 2;
+    std::string name, seq;
+    if (t >= end || *t != '{') {
+      int w = 0;
+      if (t < end) next_rune(t, end, &w);
+      seq.assign(s, t + w);
+      name.assign(t, t + w);
+      t += w;
+    } else {
+      const char *close = static_cast<const char *>(memchr(s, '}', static_cast<size_t>(end - s)));
+      if (!close) {
+        for (const char *c = s; c < end;) { int w; next_rune(c, end, &w); c += w; }  // checkUTF8
+        throw ParseError{kErrInvalidCharRange, std::string(s, end)};
+      }
+      seq.assign(s, close + 1);
+      name.assign(s + 3, close);
+      for (const char *c = s + 3; c < close;) { int w; next_rune(c, close, &w); c += w; }
+      t = close + 1;
+    }
+    if (!name.empty() && name[0] == '^') { sign = -sign; name.erase(0, 1); }
+    Ranges tab;
+    int tsign = 1;
+    if (!unicode_table(name, &tab, &tsign)) throw ParseError{kErrInvalidCharRange, seq};
+    if (flags_ & kFold) {  // the table plus its fold-equivalent runes (unicode.FoldCategory / FoldScript)
+      Ranges f;
+      for (auto &p : tab) add_folded(f, p.first, p.second);
+      tab.swap(f);
+    }
+    clean(tab);
+    if (sign * tsign < 0) negate(tab);
+    cls.insert(cls.end(), tab.begin(), tab.end());
+    return t;
   }
 
   const char *parse_class(const char *s, const char *end) {
@@ -496,7 +588,7 @@ class Parser {
           continue;
         }
       }
-      reject_unicode_class(t, end);
+      if (const char *nt = parse_unicode_class(t, end, re->cls)) { t = nt; continue; }
       if (const Group *g = perl_class_escape(t, end)) { append_group(re->cls, *g); t += 2; continue; }
       const char *rng = t;
       int32_t lo, hi;
@@ -597,7 +689,16 @@ class Parser {
         default: break;
       }
     }
-    reject_unicode_class(t, end);
+    {
+      Ranges u;
+      if (const char *nt = parse_unicode_class(t, end, u)) {
+        auto re = std::make_unique<Re>(kClass, flags_);
+        re->cls.swap(u);
+        clean(re->cls);
+        push(std::move(re));
+        return nt;
+      }
+    }
     if (const Group *g = perl_class_escape(t, end)) {
       auto re = std::make_unique<Re>(kClass, flags_);
       append_group(re->cls, *g);
@@ -1092,12 +1193,81 @@ struct KeyHash {
   size_t operator()(const std::string &s) const { return std::hash<std::string>()(s); }
 };
 
+// Per-rule partition of [0, 0x10FFFF] into rune classes: runes in one class
+// are in exactly the same NFA character sets (and, when \b / ^ / $ occur, of
+// the same word / newline category).
+struct ClassPart {
+  uint32_t ncls = 0;
+  std::vector<std::pair<int32_t, uint32_t>> intervals;  // (lo, class) over [0, max]
+  std::vector<std::vector<uint8_t>> member;             // set -> class -> in
+  std::vector<int> cat;                                 // class -> 0 other / 1 word / 2 nl
+};
+
+ClassPart make_classes(const Nfa &n_) {
+  ClassPart P;
+  std::vector<int32_t> b{0, kMaxRune + 1, 0x80};
+  for (auto &s : n_.sets)
+    for (auto &p : s) { b.push_back(p.first); b.push_back(p.second + 1); }
+  if (n_.conds & (C_WB | C_NWB))
+    for (int32_t x : {int32_t('0'), int32_t('9' + 1), int32_t('A'), int32_t('Z' + 1), int32_t('_'), int32_t('_' + 1),
+                      int32_t('a'), int32_t('z' + 1)})
+      b.push_back(x);
+  if (n_.conds & (C_BOL | C_EOL)) { b.push_back('\n'); b.push_back('\n' + 1); }
+  std::sort(b.begin(), b.end());
+  b.erase(std::unique(b.begin(), b.end()), b.end());
+  // signature per elementary interval
+  std::map<std::vector<uint8_t>, uint32_t> sig_ids;
+  const size_t nsets = n_.sets.size();
+  std::vector<std::vector<uint8_t>> cls_sig;
+  for (size_t i = 0; i + 1 < b.size(); ++i) {
+    int32_t lo = b[i];
+    std::vector<uint8_t> sig(nsets + 1, 0);
+    for (size_t s = 0; s < nsets; ++s) {
+      const Ranges &r = n_.sets[s];
+      auto it = std::upper_bound(r.begin(), r.end(), std::make_pair(lo, kMaxRune + 1));
+      if (it != r.begin() && std::prev(it)->second >= lo) sig[s] = 1;
+    }
+    int cat = 0;
+    if ((n_.conds & (C_WB | C_NWB)) && is_word_rune(lo)) cat = 1;
+    else if ((n_.conds & (C_BOL | C_EOL)) && lo == '\n') cat = 2;
+    sig[nsets] = static_cast<uint8_t>(cat);
+    auto it = sig_ids.find(sig);
+    uint32_t cid;
+    if (it == sig_ids.end()) {
+      cid = static_cast<uint32_t>(sig_ids.size());
+      sig_ids.emplace(sig, cid);
+      cls_sig.push_back(sig);
+      P.cat.push_back(cat);
+    } else cid = it->second;
+    P.intervals.push_back({lo, cid});
+  }
+  P.ncls = static_cast<uint32_t>(sig_ids.size());
+  P.member.assign(nsets, std::vector<uint8_t>(P.ncls, 0));
+  for (uint32_t c = 0; c < P.ncls; ++c)
+    for (size_t s = 0; s < nsets; ++s) P.member[s][c] = cls_sig[c][s];
+  return P;
+}
+
+// rune -> class tables of a partition: ascii[128], non-ASCII interval starts
+void class_tables(const ClassPart &P, uint16_t *ascii, std::vector<std::pair<uint32_t, uint32_t>> *nonascii) {
+  const auto &iv = P.intervals;
+  for (size_t k = 0; k < iv.size(); ++k) {
+    const int32_t lo = iv[k].first;
+    if (lo < 0x80) {
+      const int32_t hi = k + 1 < iv.size() ? std::min<int32_t>(iv[k + 1].first, 0x80) : 0x80;
+      for (int32_t r = lo; r < hi; ++r) ascii[r] = static_cast<uint16_t>(iv[k].second);
+    } else if (nonascii->empty() || nonascii->back().second != iv[k].second) {
+      nonascii->push_back({static_cast<uint32_t>(lo), iv[k].second});
+    }
+  }
+}
+
 class DfaBuilder {
  public:
-  DfaBuilder(const Nfa &nfa, uint32_t max_states) : n_(nfa), max_states_(max_states) {}
+  DfaBuilder(const Nfa &nfa, const ClassPart &P, uint32_t max_states)
+      : n_(nfa), max_states_(max_states), ncls_(P.ncls), intervals_(P.intervals), member_(P.member), cls_cat_(P.cat) {}
 
   int build(CompiledRegex *out) {
-    make_classes();
     if (ncls_ > 255) return BJX_ERR_TOO_COMPLEX;
     track_word_ = (n_.conds & (C_WB | C_NWB)) != 0;
     track_nl_ = (n_.conds & C_BOL) != 0;
@@ -1123,10 +1293,10 @@ class DfaBuilder {
  private:
   const Nfa &n_;
   uint32_t max_states_;
-  uint32_t ncls_ = 0;
-  std::vector<std::pair<int32_t, uint32_t>> intervals_;  // (lo, class) over [0, max]
-  std::vector<std::vector<uint8_t>> member_;             // set -> class -> in
-  std::vector<int> cls_cat_;                             // class -> 0 other / 1 word / 2 nl
+  const uint32_t ncls_;
+  const std::vector<std::pair<int32_t, uint32_t>> &intervals_;  // (lo, class) over [0, max]
+  const std::vector<std::vector<uint8_t>> &member_;             // set -> class -> in
+  const std::vector<int> &cls_cat_;                             // class -> 0 other / 1 word / 2 nl
   bool track_word_ = false, track_nl_ = false, track_start_ = false;
   std::unordered_map<std::string, uint32_t, KeyHash> ids_;
   std::vector<std::pair<std::vector<int32_t>, uint8_t>> states_;  // by id (index id-2)
@@ -1135,49 +1305,6 @@ class DfaBuilder {
   std::vector<uint8_t> acc_end_;
   std::vector<uint32_t> mark_;
   uint32_t gen_ = 0;
-
-  void make_classes() {
-    std::vector<int32_t> b{0, kMaxRune + 1, 0x80};
-    for (auto &s : n_.sets)
-      for (auto &p : s) { b.push_back(p.first); b.push_back(p.second + 1); }
-    if (n_.conds & (C_WB | C_NWB))
-      for (int32_t x : {int32_t('0'), int32_t('9' + 1), int32_t('A'), int32_t('Z' + 1), int32_t('_'), int32_t('_' + 1),
-                        int32_t('a'), int32_t('z' + 1)})
-        b.push_back(x);
-    if (n_.conds & (C_BOL | C_EOL)) { b.push_back('\n'); b.push_back('\n' + 1); }
-    std::sort(b.begin(), b.end());
-    b.erase(std::unique(b.begin(), b.end()), b.end());
-    // signature per elementary interval
-    std::map<std::vector<uint8_t>, uint32_t> sig_ids;
-    const size_t nsets = n_.sets.size();
-    std::vector<std::vector<uint8_t>> cls_sig;
-    for (size_t i = 0; i + 1 < b.size(); ++i) {
-      int32_t lo = b[i];
-      std::vector<uint8_t> sig(nsets + 1, 0);
-      for (size_t s = 0; s < nsets; ++s) {
-        const Ranges &r = n_.sets[s];
-        auto it = std::upper_bound(r.begin(), r.end(), std::make_pair(lo, kMaxRune + 1));
-        if (it != r.begin() && std::prev(it)->second >= lo) sig[s] = 1;
-      }
-      int cat = 0;
-      if ((n_.conds & (C_WB | C_NWB)) && is_word_rune(lo)) cat = 1;
-      else if ((n_.conds & (C_BOL | C_EOL)) && lo == '\n') cat = 2;
-      sig[nsets] = static_cast<uint8_t>(cat);
-      auto it = sig_ids.find(sig);
-      uint32_t cid;
-      if (it == sig_ids.end()) {
-        cid = static_cast<uint32_t>(sig_ids.size());
-        sig_ids.emplace(sig, cid);
-        cls_sig.push_back(sig);
-        cls_cat_.push_back(cat);
-      } else cid = it->second;
-      intervals_.push_back({lo, cid});
-    }
-    ncls_ = static_cast<uint32_t>(sig_ids.size());
-    member_.assign(nsets, std::vector<uint8_t>(ncls_, 0));
-    for (uint32_t c = 0; c < ncls_; ++c)
-      for (size_t s = 0; s < nsets; ++s) member_[s][c] = cls_sig[c][s];
-  }
 
   // closure through EPS/SPLIT (not through assertions): CHAR, ASSERT, MATCH nodes
   std::vector<int32_t> closure0(const std::vector<int32_t> &seeds) {
@@ -1361,16 +1488,10 @@ class DfaBuilder {
             static_cast<uint16_t>(newid[block[rows_[static_cast<size_t>(s) * ncls_ + c]]]);
     }
     // rune -> class tables
-    for (auto &iv : intervals_) {
-      int32_t lo = iv.first;
-      if (lo < 0x80) {
-        auto it = std::upper_bound(intervals_.begin(), intervals_.end(), std::make_pair(lo, 0xFFFFFFFFu));
-        int32_t hi = (it == intervals_.end()) ? 0x80 : std::min<int32_t>(it->first, 0x80);
-        for (int32_t r = lo; r < hi; ++r) out->ascii_cls[r] = static_cast<uint8_t>(iv.second);
-      } else {
-        if (out->nonascii.empty() || out->nonascii.back().second != iv.second)
-          out->nonascii.push_back({static_cast<uint32_t>(lo), iv.second});
-      }
+    {
+      uint16_t a16[128] = {};
+      class_tables(ClassPart{ncls_, intervals_, {}, {}}, a16, &out->nonascii);
+      for (int r = 0; r < 128; ++r) out->ascii_cls[r] = static_cast<uint8_t>(a16[r]);
     }
     bool always = out->accept_end[out->start] != 0;
     for (uint32_t c = 0; c < ncls_ && always; ++c)
@@ -1382,7 +1503,205 @@ class DfaBuilder {
   }
 };
 
+
+// ------------------------------------------------------- bit-parallel NFA
+//
+// Rules whose DFA passes kDfaStateCap states (counted repetition after an
+// unanchored prefix, e.g. `.*a.{20}`: 2^21 DFA states) or 255 rune classes are
+// matched by a bit-parallel simulation of the NFA instead.  A state is a set
+// of *positions*: the CHAR, ASSERT and MATCH nodes that closure0 reaches,
+// numbered in DFS preorder so that a concatenation steps position p to p + 1.
+// One rune of class c, with the assertion context k = (category of the
+// previous rune) * 4 + (category of c) (regexp/syntax EmptyOpContext):
+//   X  = D | AT[a][k] for each ASSERT position a in D   (assertions crossed)
+//   X has MATCH                       -> match before c
+//   Y  = X & CM[c]                    (CHAR positions that accept c)
+//   D' = ((Y & SH) << 1) | S0 | GT[g] for every group g with Y & GM[g] != 0
+//   D' has MATCH                      -> match after c
+// SH marks positions whose follow set contains p + 1; every other follow
+// target lives in a group (positions with the same remaining follow set share
+// one).  S0 = closure0(start) re-seeds the unanchored search at every rune, as
+// the DFA construction does.  At the end of the text the assertions are
+// crossed once more with next category "end".  Same semantics as DfaBuilder,
+// so the two are interchangeable per rule.
+//
+// Blob layout (u64 words): header (8 x u32: W, npos, ncls, ngroups, nassert,
+// match position, flags, total words), ascii classes (u16[128]), class
+// categories (u8[ncls]), S0[W], SH[W], CM[ncls][W], GM[G][W], GT[G][W],
+// assert positions (u32[nassert]), AT[nassert][16][W].
+
+class BitNfaBuilder {
+ public:
+  BitNfaBuilder(const Nfa &nfa, const ClassPart &P) : n_(nfa), P_(P) {}
+
+  int build(CompiledRegex *out) {
+    mark_.assign(n_.nodes.size(), 0);
+    pos_.assign(n_.nodes.size(), -1);
+    std::vector<int32_t> s0;
+    closure(n_.start, 0, false, s0);
+    // DFS preorder numbering over the position graph
+    std::vector<int32_t> st(s0.rbegin(), s0.rend());
+    while (!st.empty()) {
+      const int32_t i = st.back();
+      st.pop_back();
+      if (pos_[i] >= 0) continue;
+      if (order_.size() >= kNfaMaxPos) return BJX_ERR_TOO_COMPLEX;
+      pos_[i] = static_cast<int32_t>(order_.size());
+      order_.push_back(i);
+      const std::vector<int32_t> &ch = children(i);
+      for (auto it = ch.rbegin(); it != ch.rend(); ++it)
+        if (pos_[*it] < 0) st.push_back(*it);
+    }
+    const uint32_t npos = static_cast<uint32_t>(order_.size());
+    uint32_t W = 1;
+    while (64 * W < npos) W *= 2;
+    auto setbit = [&](std::vector<uint64_t> &v, size_t base, int32_t node) {
+      const uint32_t p = static_cast<uint32_t>(pos_[node]);
+      v[base + p / 64] |= 1ull << (p % 64);
+    };
+    // follow sets, shift bits, groups
+    std::vector<uint64_t> s0m(W, 0), sh(W, 0);
+    for (int32_t i : s0) setbit(s0m, 0, i);
+    std::map<std::vector<int32_t>, uint32_t> group_of;
+    std::vector<std::vector<int32_t>> gtarget;
+    std::vector<std::vector<uint32_t>> gmembers;
+    std::vector<uint32_t> asserts;
+    for (uint32_t p = 0; p < npos; ++p) {
+      const int32_t node = order_[p];
+      const NNode &nd = n_.nodes[node];
+      if (nd.k == NK_ASSERT) { asserts.push_back(p); continue; }
+      if (nd.k != NK_CHAR) continue;
+      std::vector<int32_t> rest;
+      for (int32_t f : children(node)) {
+        if (static_cast<uint32_t>(pos_[f]) == p + 1) sh[(p) / 64] |= 1ull << (p % 64);
+        else rest.push_back(pos_[f]);
+      }
+      if (rest.empty()) continue;
+      std::sort(rest.begin(), rest.end());
+      auto it = group_of.find(rest);
+      if (it == group_of.end()) {
+        it = group_of.emplace(rest, static_cast<uint32_t>(gtarget.size())).first;
+        gtarget.push_back(rest);
+        gmembers.emplace_back();
+      }
+      gmembers[it->second].push_back(p);
+    }
+    const uint32_t ncls = P_.ncls, ng = static_cast<uint32_t>(gtarget.size()), na = static_cast<uint32_t>(asserts.size());
+    const NfaLayout L = nfa_layout(W, npos, ncls, ng, na);
+    if (static_cast<size_t>(L.total) * 8 > kNfaMaxBlobBytes) return BJX_ERR_TOO_COMPLEX;
+    std::vector<uint64_t> b(L.total, 0);
+    uint32_t match = 0xFFFFFFFFu, flags = na ? kNfaAsserts : 0u;
+    for (uint32_t p = 0; p < npos; ++p)
+      if (n_.nodes[order_[p]].k == NK_MATCH) match = p;
+    // anchored at the text start: S0 holds only \A / ^ (OneLine) assertions,
+    // which never hold again, so a state equal to S0 after the first rune is dead
+    bool s0_dead = !s0.empty();
+    for (int32_t i : s0)
+      if (n_.nodes[i].k != NK_ASSERT || !(n_.nodes[i].cond & C_BOT)) s0_dead = false;
+    if (s0_dead) flags |= kNfaAnchored;
+    const uint32_t hdr[8] = {W, npos, ncls, ng, na, match, flags, L.total};
+    memcpy(b.data(), hdr, sizeof hdr);
+    uint16_t a16[128] = {};
+    class_tables(P_, a16, &out->nonascii);
+    memcpy(&b[L.o_ascii], a16, sizeof a16);
+    uint8_t *cat = reinterpret_cast<uint8_t *>(&b[L.o_cat]);
+    for (uint32_t c = 0; c < ncls; ++c) cat[c] = static_cast<uint8_t>(P_.cat[c]);
+    for (uint32_t w = 0; w < W; ++w) { b[L.o_s0 + w] = s0m[w]; b[L.o_sh + w] = sh[w]; }
+    for (uint32_t p = 0; p < npos; ++p) {
+      const NNode &nd = n_.nodes[order_[p]];
+      if (nd.k != NK_CHAR) continue;
+      for (uint32_t c = 0; c < ncls; ++c)
+        if (P_.member[nd.set][c]) b[L.o_cm + c * W + p / 64] |= 1ull << (p % 64);
+    }
+    for (uint32_t g = 0; g < ng; ++g) {
+      for (uint32_t p : gmembers[g]) b[L.o_gm + g * W + p / 64] |= 1ull << (p % 64);
+      for (int32_t q : gtarget[g]) b[L.o_gt + g * W + q / 64] |= 1ull << (q % 64);
+    }
+    uint32_t *apos = reinterpret_cast<uint32_t *>(&b[L.o_apos]);
+    for (uint32_t a = 0; a < na; ++a) {
+      apos[a] = asserts[a];
+      const NNode &nd = n_.nodes[order_[asserts[a]]];
+      for (uint32_t k = 0; k < 16; ++k) {
+        const uint8_t f = empty_flags(static_cast<uint8_t>(k / 4), static_cast<int>(k % 4));
+        if ((nd.cond & ~f) != 0) continue;
+        std::vector<int32_t> t;
+        closure(nd.out, f, true, t);
+        for (int32_t i : t) setbit(b, L.o_at + (a * 16 + k) * W, i);
+      }
+    }
+    out->nfa.swap(b);
+    out->nfa_words = W;
+    out->nstates = npos;
+    out->ncls = ncls;
+    out->start = 0;
+    for (int r = 0; r < 128; ++r) out->ascii_cls[r] = static_cast<uint8_t>(a16[r]);
+    out->flags = kRuleNfa;
+    if (match != 0xFFFFFFFFu && ((s0m[match / 64] >> (match % 64)) & 1)) out->flags |= kRuleAlways;
+    if (match == 0xFFFFFFFFu) out->flags |= kRuleNever;
+    return 0;
+  }
+
+ private:
+  const Nfa &n_;
+  const ClassPart &P_;
+  std::vector<uint32_t> mark_;
+  uint32_t gen_ = 0;
+  std::vector<int32_t> pos_, order_;
+  std::map<int32_t, std::vector<int32_t>> kids_;
+
+  // closure in DFS preorder through EPS / SPLIT (and, with through_asserts,
+  // the assertions that flags satisfy): CHAR / MATCH nodes, plus the ASSERT
+  // nodes where it stops
+  void closure(int32_t seed, uint8_t flags, bool through_asserts, std::vector<int32_t> &out) {
+    ++gen_;
+    std::vector<int32_t> st{seed};
+    while (!st.empty()) {
+      const int32_t i = st.back();
+      st.pop_back();
+      if (i < 0 || mark_[i] == gen_) continue;
+      mark_[i] = gen_;
+      const NNode &nd = n_.nodes[i];
+      switch (nd.k) {
+        case NK_EPS: st.push_back(nd.out); break;
+        case NK_SPLIT: st.push_back(nd.out1); st.push_back(nd.out); break;
+        case NK_ASSERT:
+          if (!through_asserts) out.push_back(i);
+          else if ((nd.cond & ~flags) == 0) st.push_back(nd.out);
+          break;
+        default: out.push_back(i);
+      }
+    }
+  }
+  // successors in the position graph: follow set of a CHAR; every node an
+  // ASSERT can lead to under some context
+  const std::vector<int32_t> &children(int32_t i) {
+    auto it = kids_.find(i);
+    if (it != kids_.end()) return it->second;
+    std::vector<int32_t> v;
+    const NNode &nd = n_.nodes[i];
+    if (nd.k == NK_CHAR) {
+      closure(nd.out, 0, false, v);
+    } else if (nd.k == NK_ASSERT) {
+      std::vector<uint8_t> seen(n_.nodes.size(), 0);
+      for (uint32_t k = 0; k < 16; ++k) {
+        const uint8_t f = empty_flags(static_cast<uint8_t>(k / 4), static_cast<int>(k % 4));
+        if ((nd.cond & ~f) != 0) continue;
+        std::vector<int32_t> t;
+        closure(nd.out, f, true, t);
+        for (int32_t x : t)
+          if (!seen[x]) { seen[x] = 1; v.push_back(x); }
+      }
+    }
+    return kids_.emplace(i, std::move(v)).first->second;
+  }
+};
+
+std::atomic<uint32_t> g_dfa_state_cap{kDfaStateCap};
+
 }  // namespace
+
+void set_dfa_state_cap(uint32_t cap) { g_dfa_state_cap = cap ? cap : kDfaStateCap; }
+uint32_t dfa_state_cap() { return g_dfa_state_cap; }
 
 int compile_regex(const std::string &pattern, CompiledRegex *out, std::string *err, uint32_t max_dfa_states) {
   ReP root;
@@ -1404,11 +1723,24 @@ int compile_regex(const std::string &pattern, CompiledRegex *out, std::string *e
     if (err) *err = "rule too complex for the automaton compiler (NFA size)";
     return BJX_ERR_TOO_COMPLEX;
   }
+  // DFA up to kDfaStateCap states; past that (or past 255 rune classes) the
+  // bit-parallel NFA; a rule with too many NFA positions for that gets a DFA
+  // of up to max_dfa_states states
+  const ClassPart part = make_classes(nfa);
   *out = CompiledRegex();
-  DfaBuilder d(nfa, std::min<uint32_t>(max_dfa_states, 65000));
-  int rc = d.build(out);
+  const uint32_t cap = std::min<uint32_t>(max_dfa_states, dfa_state_cap());
+  int rc = DfaBuilder(nfa, part, std::max<uint32_t>(cap, 3)).build(out);
   if (rc != 0) {
-    if (err) *err = "rule too complex for the DFA engine (state or class limit)";
+    *out = CompiledRegex();
+    rc = BitNfaBuilder(nfa, part).build(out);
+  }
+  if (rc != 0 && max_dfa_states > cap) {
+    *out = CompiledRegex();
+    rc = DfaBuilder(nfa, part, std::min<uint32_t>(max_dfa_states, 65000)).build(out);
+  }
+  if (rc != 0) {
+    if (err) *err = "rule too complex for the automaton engines (more than " + std::to_string(kNfaMaxPos) +
+                    " NFA positions and more than " + std::to_string(max_dfa_states) + " DFA states)";
     return rc;
   }
   if (out->flags & kRuleAlways) out->mode = kModeAlways;
@@ -1448,7 +1780,56 @@ int compile_regex(const std::string &pattern, CompiledRegex *out, std::string *e
   return 0;
 }
 
+static bool nfa_match_host(const CompiledRegex &rx, const uint8_t *text, size_t n) {
+  const uint64_t *b = rx.nfa.data();
+  uint32_t h[8];
+  memcpy(h, b, sizeof h);
+  const NfaLayout L = nfa_layout_of(h);
+  const uint32_t W = L.W, match = L.match, flags = L.flags;
+  const uint16_t *a16 = reinterpret_cast<const uint16_t *>(b + L.o_ascii);
+  const uint8_t *cat = reinterpret_cast<const uint8_t *>(b + L.o_cat);
+  const uint32_t *apos = reinterpret_cast<const uint32_t *>(b + L.o_apos);
+  auto has = [&](const std::vector<uint64_t> &v, uint32_t p) { return p != 0xFFFFFFFFu && ((v[p / 64] >> (p % 64)) & 1); };
+  std::vector<uint64_t> D(b + L.o_s0, b + L.o_s0 + W), X(W), Y(W);
+  uint32_t ctx = 3;  // start of text
+  auto cross = [&](uint32_t k) {
+    X = D;
+    for (uint32_t a = 0; a < L.nassert; ++a)
+      if (has(D, apos[a]))
+        for (uint32_t w = 0; w < W; ++w) X[w] |= b[L.o_at + (a * 16 + k) * W + w];
+  };
+  size_t p = 0;
+  while (p < n) {
+    int w;
+    const int32_t r = decode_rune(text + p, n - p, &w);
+    uint32_t c;
+    if (r < 0x80) c = a16[r];
+    else {
+      auto it = std::upper_bound(rx.nonascii.begin(), rx.nonascii.end(), std::make_pair(static_cast<uint32_t>(r), 0xFFFFFFFFu));
+      c = std::prev(it)->second;
+    }
+    cross(ctx * 4 + cat[c]);
+    if (has(X, match)) return true;
+    for (uint32_t k = 0; k < W; ++k) Y[k] = X[k] & b[L.o_cm + c * W + k];
+    for (uint32_t k = 0; k < W; ++k)
+      D[k] = ((Y[k] & b[L.o_sh + k]) << 1) | (k ? (Y[k - 1] & b[L.o_sh + k - 1]) >> 63 : 0) | b[L.o_s0 + k];
+    for (uint32_t g = 0; g < L.ngroups; ++g) {
+      uint64_t any = 0;
+      for (uint32_t k = 0; k < W; ++k) any |= Y[k] & b[L.o_gm + g * W + k];
+      if (any)
+        for (uint32_t k = 0; k < W; ++k) D[k] |= b[L.o_gt + g * W + k];
+    }
+    if (has(D, match)) return true;
+    if ((flags & kNfaAnchored) && std::equal(D.begin(), D.end(), b + L.o_s0)) return false;
+    ctx = cat[c] == 1 ? 1 : (cat[c] == 2 ? 2 : 0);
+    p += static_cast<size_t>(w);
+  }
+  cross(ctx * 4 + 3);
+  return has(X, match);
+}
+
 bool dfa_match_host(const CompiledRegex &rx, const uint8_t *text, size_t n) {
+  if (rx.flags & kRuleNfa) return nfa_match_host(rx, text, n);
   uint32_t st = rx.start;
   size_t p = 0;
   while (p < n && st > kAccept) {

@@ -8,6 +8,12 @@
 #include <utility>
 #include <vector>
 
+#if defined(__HIPCC__)
+#define BJX_RX_HD __host__ __device__
+#else
+#define BJX_RX_HD
+#endif
+
 namespace bjx {
 
 // DFA state ids: 0 = DEAD (can never match), 1 = ACCEPT (matched; absorbing).
@@ -17,7 +23,48 @@ constexpr uint16_t kAccept = 1;
 enum RuleFlags : uint32_t {
   kRuleAlways = 1,  // matches every input (e.g. ".*", "^"): no scan needed
   kRuleNever = 2,   // matches nothing
+  kRuleNfa = 4,     // matched by the bit-parallel NFA (CompiledRegex::nfa), not a DFA
 };
+
+// DFA states before a rule switches to the bit-parallel NFA; NFA limits
+constexpr uint32_t kDfaStateCap = 4096;
+constexpr uint32_t kNfaMaxPos = 1024;             // positions (16 x 64-bit words per state set)
+constexpr size_t kNfaMaxBlobBytes = 48 * 1024;    // tables staged in LDS per block
+
+// Word offsets of the bit-parallel NFA tables in CompiledRegex::nfa (see
+// regex_compiler.cpp "bit-parallel NFA"); the header is the first 4 words.
+struct NfaLayout {
+  uint32_t W, npos, ncls, ngroups, nassert, match, flags, total;
+  uint32_t o_ascii, o_cat, o_s0, o_sh, o_cm, o_gm, o_gt, o_apos, o_at;
+};
+enum NfaFlags : uint32_t { kNfaAsserts = 1, kNfaAnchored = 2 };
+BJX_RX_HD inline NfaLayout nfa_layout(uint32_t W, uint32_t npos, uint32_t ncls, uint32_t ng, uint32_t na) {
+  NfaLayout L{};
+  L.W = W; L.npos = npos; L.ncls = ncls; L.ngroups = ng; L.nassert = na;
+  L.o_ascii = 4;
+  L.o_cat = L.o_ascii + 32;
+  L.o_s0 = L.o_cat + (ncls + 7) / 8;
+  L.o_sh = L.o_s0 + W;
+  L.o_cm = L.o_sh + W;
+  L.o_gm = L.o_cm + ncls * W;
+  L.o_gt = L.o_gm + ng * W;
+  L.o_apos = L.o_gt + ng * W;
+  L.o_at = L.o_apos + (na + 1) / 2;
+  L.total = L.o_at + na * 16 * W;
+  return L;
+}
+// layout of a blob from its header words (h = the blob's first 8 u32)
+BJX_RX_HD inline NfaLayout nfa_layout_of(const uint32_t *h) {
+  NfaLayout L = nfa_layout(h[0], h[1], h[2], h[3], h[4]);
+  L.match = h[5];
+  L.flags = h[6];
+  return L;
+}
+
+// rules compiled after this call switch to the bit-parallel NFA past `cap` DFA
+// states (test hook: 1 sends every rule that fits the NFA limits to it)
+void set_dfa_state_cap(uint32_t cap);
+uint32_t dfa_state_cap();
 
 // How the device decides a rule on a line.
 enum RuleMode : uint8_t {
@@ -55,6 +102,10 @@ struct CompiledRegex {
   std::vector<PrefLit> anchor;
   bool anchor_equivalent = false;  // match <=> text starts with one of `anchor`
   std::string required_literal;  // diagnostics: the first prefilter literal
+  // kRuleNfa: bit-parallel NFA tables (layout: regex_compiler.cpp "bit-parallel
+  // NFA"); nstates = positions, trans / accept_end empty
+  std::vector<uint64_t> nfa;
+  uint32_t nfa_words = 0;
 };
 
 // Returns 0 on success; otherwise a negative bjx_status with *err set to the
@@ -62,8 +113,8 @@ struct CompiledRegex {
 int compile_regex(const std::string &pattern, CompiledRegex *out, std::string *err,
                   uint32_t max_dfa_states = 40000);
 
-// Host reference evaluation of compiled tables (compiler self-test only; the
-// product matches on the GPU).
+// Host reference evaluation of compiled tables, DFA or bit-parallel NFA
+// (compiler self-test only; the product matches on the GPU).
 bool dfa_match_host(const CompiledRegex &rx, const uint8_t *text, size_t n);
 
 }  // namespace bjx

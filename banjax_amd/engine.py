@@ -110,8 +110,11 @@ class Engine:
             arr[i] = _lib.DecisionEntry(s, dec, ipb)
         self._check(_lib.lib().bjx_engine_set_decision_lists(self._h, arr, len(entries)), "set_decision_lists")
 
-    def set_ban_options(self, expiring_ttl_s: int, disable_logging: Iterable[str] = (), tz_offset_s: int = 0):
-        """Banner settings of the device decision emission (bjx_engine_set_ban_options)."""
+    def set_ban_options(self, expiring_ttl_s: int, disable_logging: Iterable[str] = (), tz_offset_s: int = 0,
+                        zone=None):
+        """Banner settings of the device decision emission (bjx_engine_set_ban_options);
+        zone: a regex_rate_limiter.Zone (local-zone transitions), else the fixed
+        offset tz_offset_s."""
         hosts = [h for h in disable_logging]
         arr = (_lib.Str * max(1, len(hosts)))()
         keep = []
@@ -121,7 +124,10 @@ class Engine:
         ttl = (int(expiring_ttl_s) * 1_000_000_000) & ((1 << 64) - 1)
         if ttl >= 1 << 63:
             ttl -= 1 << 64
-        o = _lib.BanOptions(ttl, tz_offset_s, 0, arr, len(hosts))
+        trans = zone.transitions if zone is not None else []
+        off = zone.offset_s if zone is not None else tz_offset_s
+        tz = (_lib.TzTransition * max(1, len(trans)))(*[_lib.TzTransition(a, o, 0) for a, o in trans])
+        o = _lib.BanOptions(ttl, off, 0, arr, len(hosts), tz, len(trans))
         self._check(_lib.lib().bjx_engine_set_ban_options(self._h, C.byref(o)), "set_ban_options")
 
     def bans(self) -> BanBatch:

@@ -158,9 +158,65 @@ def _trim_space(s: bytes) -> bytes:
     return s
 
 
-def format_time(ns: int, tz_offset_s: int = 0) -> str:
-    """logTime.Format("2006-01-02T15:04:05") in a fixed zone (injected; UTC by default)."""
-    sec = ns // 1_000_000_000 + tz_offset_s
+class Zone:
+    """The local time zone LogRegexBan formats its timestring in (logTime.Format
+    in time.Local, iptables.go:187): a UTC offset before the first transition,
+    then (UTC second, offset) changes in ascending order — the table
+    bjx_ban_options carries to the device."""
+
+    def __init__(self, offset_s: int = 0, transitions=()):
+        self.offset_s = int(offset_s)
+        self.transitions = [(int(a), int(o)) for a, o in transitions]
+        self._at = [a for a, _ in self.transitions]
+
+    @classmethod
+    def fixed(cls, offset_s: int) -> "Zone":
+        return cls(offset_s)
+
+    @classmethod
+    def from_tzinfo(cls, tz, first_year: int = 1970, last_year: int = 2100) -> "Zone":
+        """Expand a tzinfo's offset changes over [first_year, last_year): daily
+        samples, each change pinned to the second by bisection."""
+        def off(sec):
+            return int(_dt.datetime.fromtimestamp(sec, tz).utcoffset().total_seconds())
+        lo = int(_dt.datetime(first_year, 1, 1, tzinfo=_dt.timezone.utc).timestamp())
+        hi = int(_dt.datetime(last_year, 1, 1, tzinfo=_dt.timezone.utc).timestamp())
+        first = off(lo)
+        trans, cur, t = [], first, lo
+        while t < hi:
+            nt = min(t + 86400, hi)
+            o = off(nt)
+            if o != cur:
+                a, b = t, nt  # off(a) == cur, off(b) != cur
+                while b - a > 1:
+                    m = (a + b) // 2
+                    if off(m) == cur:
+                        a = m
+                    else:
+                        b = m
+                cur = off(b)
+                trans.append((b, cur))
+                t = b
+                continue
+            t = nt
+        return cls(first, trans)
+
+    @classmethod
+    def named(cls, name: str) -> "Zone":
+        import zoneinfo
+        return cls.from_tzinfo(zoneinfo.ZoneInfo(name))
+
+    def offset_at(self, sec: int) -> int:
+        import bisect
+        k = bisect.bisect_right(self._at, sec)
+        return self.offset_s if k == 0 else self.transitions[k - 1][1]
+
+
+def format_time(ns: int, zone=0) -> str:
+    """logTime.Format("2006-01-02T15:04:05") in the local zone (a Zone, or a
+    fixed offset in seconds east of UTC; UTC by default)."""
+    sec = ns // 1_000_000_000
+    sec += zone.offset_at(sec) if isinstance(zone, Zone) else int(zone)
     d = _dt.datetime(1970, 1, 1) + _dt.timedelta(seconds=sec)
     return "%04d-%02d-%02dT%02d:%02d:%02d" % (d.year, d.month, d.day, d.hour, d.minute, d.second)
 
@@ -211,7 +267,7 @@ class Banner:
         self.ban_log_temp: List[str] = []  # LoggerTemp lines (disable_logging hosts)
         self.ipset: List[str] = []        # IPs an iptables ban would add (standalone: none)
         self.standalone = True
-        self.tz_offset_s = 0              # local zone of LogRegexBan's timestring (seconds east of UTC)
+        self.zone = Zone()                # local zone of LogRegexBan's timestring
 
     def ban_or_challenge_ip(self, cfg: Config, ip: str, decision: int, domain: str, now_ns: int):
         expires = (now_ns + cfg.expiring_decision_ttl_seconds * 1_000_000_000) & ((1 << 64) - 1)
@@ -230,7 +286,7 @@ class Banner:
         ua = _trim_space(words[5].split(b"|", 1)[0])
         parts = [
             '"path":' + _go_json_string(words[3]),
-            '"timestring":' + _go_json_string(format_time(log_time_ns, self.tz_offset_s).encode()),
+            '"timestring":' + _go_json_string(format_time(log_time_ns, self.zone).encode()),
             '"trigger":' + _go_json_string(rule_name.encode()),
             '"client_ua":' + _go_json_string(ua),
             '"client_ip":' + _go_json_string(ip),
@@ -308,60 +364,83 @@ class RegexRateLimitStates:
         return self._e.state_dump()
 
 
+class _Snapshot:
+    """One ConfigHolder value: a config and the ruleset compiled from it."""
+    __slots__ = ("config", "ruleset")
+
+    def __init__(self, config: Config, ruleset: Ruleset):
+        self.config, self.ruleset = config, ruleset
+
+
 class RegexRateLimiter:
     """Owns the config snapshot, its compiled ruleset and the engine; the
     equivalent of RunLogTailer's loop body over a batch of lines."""
 
     def __init__(self, cfg: Config, engine: Optional[Engine] = None, banner: Optional[Banner] = None,
-                 device_bans: bool = False, tz_offset_s: int = 0):
+                 device_bans: bool = False, tz_offset_s: int = 0, zone: Optional[Zone] = None):
         """device_bans: the engine emits one decision update per tripped IP and
         the formatted ban-log lines (bjx_batch_bans) instead of
-        the per-trip Banner replay on the host."""
+        the per-trip Banner replay on the host.  zone: time.Local of the ban
+        log (default: the fixed offset tz_offset_s)."""
         self.engine = engine or Engine()
         self.banner = banner or MockBanner()
         self.device_bans = device_bans
-        self.tz_offset_s = tz_offset_s
-        self.banner.tz_offset_s = tz_offset_s
+        self.zone = zone if zone is not None else Zone.fixed(tz_offset_s)
+        self.banner.zone = self.zone
         self._seen_names: Dict[str, None] = {}
         self.states = RegexRateLimitStates(self.engine, lambda: list(self._seen_names))
         self.reload(cfg)
 
     def reload(self, cfg: Config):
         """ConfigHolder.Reload (config_holder.go:55-66): compile first; keep the old
-        ruleset if the new config does not compile; state survives (keyed by name)."""
+        ruleset if the new config does not compile; state survives (keyed by name).
+        The (config, ruleset) pair is published as one object, like the
+        reference's atomic config pointer (config_holder.go:28,63): a batch
+        takes one snapshot and uses it from process() to its Banner replay, so a
+        reload on another thread takes effect at the next batch."""
         rs = Ruleset(cfg)
-        self.config, self.ruleset = cfg, rs
         for r in rs.rules:
             self._seen_names.setdefault(r.rule, None)
+        self._snap = _Snapshot(cfg, rs)
         self.engine.set_decision_lists(cfg.decision_entries)
         self.engine.set_ban_options(cfg.expiring_decision_ttl_seconds,
-                                    [h for h, v in cfg.disable_logging.items() if v], self.tz_offset_s)
+                                    [h for h, v in cfg.disable_logging.items() if v], zone=self.zone)
+
+    @property
+    def config(self) -> Config:
+        return self._snap.config
+
+    @property
+    def ruleset(self) -> Ruleset:
+        return self._snap.ruleset
 
     def consume_lines(self, data: bytes, now_ns: int, want_results: bool = True):
         """consumeLine for every complete line; returns (results, batch output)."""
-        out = self.engine.process(self.ruleset, data, now_ns, copy_results=want_results, emit_bans=self.device_bans)
-        return self._finish(data, out, now_ns, want_results)
+        snap = self._snap
+        out = self.engine.process(snap.ruleset, data, now_ns, copy_results=want_results, emit_bans=self.device_bans)
+        return self._finish(snap, data, out, now_ns, want_results)
 
     def consume_device_batch(self, host_view, device_ptr: Optional[int], nbytes: int, now_ns: int,
                              want_results: bool = True):
         """consumeLine over a batch already in HBM (the tailer's copy); host_view
         holds the same bytes for the Banner's log lines.  device_ptr None: host."""
+        snap = self._snap
         if device_ptr is None:
-            out = self.engine.process(self.ruleset, bytes(host_view[:nbytes]), now_ns, copy_results=want_results,
+            out = self.engine.process(snap.ruleset, bytes(host_view[:nbytes]), now_ns, copy_results=want_results,
                                       emit_bans=self.device_bans)
         else:
-            out = self.engine.process(self.ruleset, None, now_ns, copy_results=want_results, device_ptr=device_ptr,
+            out = self.engine.process(snap.ruleset, None, now_ns, copy_results=want_results, device_ptr=device_ptr,
                                       nbytes=nbytes, emit_bans=self.device_bans)
-        return self._finish(host_view, out, now_ns, want_results)
+        return self._finish(snap, host_view, out, now_ns, want_results)
 
-    def _finish(self, data, out, now_ns: int, want_results: bool):
+    def _finish(self, snap, data, out, now_ns: int, want_results: bool):
         """Banner replay of the trips in reference order (regex_rate_limiter.go:254-266)
-        and, if asked, the ConsumeLineResults."""
-        rules = self.ruleset.rules
+        and, if asked, the ConsumeLineResults, against the batch's snapshot."""
+        rules = snap.ruleset.rules
         if self.device_bans:
-            self.banner.apply_device_bans(self.config, self.engine.bans(), out.trips, data)
+            self.banner.apply_device_bans(snap.config, self.engine.bans(), out.trips, data)
         else:
-            self._replay_trips(data, out, now_ns)
+            self._replay_trips(snap, data, out, now_ns)
         if not want_results:
             return None, out
         results = [ConsumeLineResult(error=bool(f & LINE_ERROR), old_line=bool(f & LINE_OLD),
@@ -372,17 +451,17 @@ class RegexRateLimiter:
                 seen_ip=bool(r.seen_ip), rate_limit_result=RateLimitResult(r.match_type, bool(r.exceeded))))
         return results, out
 
-    def _replay_trips(self, data, out, now_ns: int):
-        rules = self.ruleset.rules
+    def _replay_trips(self, snap, data, out, now_ns: int):
+        rules, config = snap.ruleset.rules, snap.config
         for t in out.trips:
             line = bytes(data[t.line_offset:t.line_offset + t.line_len])
             ip = line[t.ip_off:t.ip_off + t.ip_len]
             host = line[t.host_off:t.host_off + t.host_len]
             rest = line[t.rest_off:]
             rule = rules[t.rule_idx]
-            self.banner.ban_or_challenge_ip(self.config, ip.decode("utf-8", "surrogateescape"), rule.decision,
+            self.banner.ban_or_challenge_ip(config, ip.decode("utf-8", "surrogateescape"), rule.decision,
                                             host.decode("utf-8", "surrogateescape"), now_ns)
-            self.banner.log_regex_ban(self.config, t.ts_ns, ip, rule.rule, rest, rule.decision)
+            self.banner.log_regex_ban(config, t.ts_ns, ip, rule.rule, rest, rule.decision)
 
 
 def consume_line(limiter: RegexRateLimiter, text: str, now_ns: int) -> ConsumeLineResult:

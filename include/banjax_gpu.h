@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define BJX_ABI_VERSION 1
+#define BJX_ABI_VERSION 2
 
 enum bjx_status {
   BJX_OK = 0,
@@ -272,12 +272,23 @@ const char *bjx_engine_last_error(bjx_engine *e);
    Banner.LogRegexBan (internal/iptables.go:179-228) that consumeLine runs for
    every trip (internal/regex_rate_limiter.go:254-266).
    Options hold for every later batch run with BJX_EMIT_BANS. */
+/* One UTC-offset change of the local time zone LogRegexBan formats its
+   timestring in (logTime.Format in time.Local, internal/iptables.go:187). */
+typedef struct bjx_tz_transition {
+  int64_t utc_start_s; /* first Unix second the offset applies to */
+  int32_t offset_s;    /* seconds east of UTC from then on */
+  int32_t _pad;
+} bjx_tz_transition;
+
 typedef struct bjx_ban_options {
   int64_t expiring_ttl_ns;          /* expiring_decision_ttl_seconds * 1e9 (config.go) */
-  int32_t tz_offset_s;              /* local time zone of LogRegexBan's timestring, seconds east of UTC */
+  int32_t tz_offset_s;              /* UTC offset (seconds east) before the first transition, or always when there are none */
   uint32_t _pad;
   const bjx_str *disable_logging;   /* config.DisableLogging hosts set to true (LoggerTemp lines) */
   size_t n_disable_logging;
+  const bjx_tz_transition *tz_transitions; /* the zone's offset changes, ascending by utc_start_s (DST rules
+                                              expanded; a Go host walks time.Local with Time.ZoneBounds) */
+  size_t n_tz_transitions;
 } bjx_ban_options;
 int bjx_engine_set_ban_options(bjx_engine *e, const bjx_ban_options *opts);
 

@@ -2,8 +2,8 @@
  * banjax_gpu_debug.h — self-test hooks of libbanjax_gpu.so (not part of the
  * drop-in boundary; never used by bjx_process_batch).
  *
- * bjx_debug_rule_match_host evaluates one compiled rule's DFA tables on the
- * host, so the rule compiler can be checked against the oracle on machines
+ * bjx_debug_rule_match_host evaluates one compiled rule's DFA or bit-parallel
+ * NFA tables on the host, so the rule compiler can be checked against the oracle on machines
  * without a GPU.  The product matches on the GPU only.
  */
 #ifndef BANJAX_GPU_DEBUG_H
@@ -33,6 +33,10 @@ int bjx_debug_set_ip_hash_mask(bjx_engine *e, uint64_t mask);
 /* Test hook: the first claim launch of each table in a batch may add at most
    max_new entries (0 = off), forcing the roll-back / re-claim path. */
 int bjx_debug_set_claim_budget(bjx_engine *e, uint64_t max_new);
+/* Test hook: rules compiled afterwards use the bit-parallel NFA once their DFA
+   passes `cap` states (0 = default 4096; 1 = every rule that fits the NFA),
+   process-wide; clears the compiled-pattern cache. */
+int bjx_debug_set_dfa_state_cap(uint32_t cap);
 #ifdef __cplusplus
 }
 #endif

@@ -14,9 +14,11 @@
  * empty-width assertions.  Boolean Match only (no submatches), which is all the
  * hot path asks for.
  *
- * Known gaps (documented in DESIGN.md): \p{..}/\P{..} Unicode classes are
- * rejected with ErrInvalidCharRange-free "unsupported" error; Go's ErrLarge /
- * ErrNestingDepth size limits are approximated by a depth check.
+ * UnicodeGroups (\pL, \p{Greek}, \P{..}, \p{^..}) follow parse.go's
+ * parseUnicodeClass / unicodeTable of Go 1.25 over the Unicode 15.0.0 tables of
+ * third_party/unicode/unicode_tables.h (tools/gen_unicode_tables.py).
+ * Known gap: Go's ErrLarge / ErrNestingDepth size limits are
+ * approximated by a depth check.
  */
 #include "go_regexp.h"
 
@@ -26,6 +28,7 @@
 #include <string.h>
 
 #include "../third_party/unicode/fold_orbits.h"
+#include "../third_party/unicode/unicode_tables.h"
 
 #define MAX_RUNE 0x10FFFF
 #define RUNE_ERROR 0xFFFD
@@ -461,11 +464,102 @@ static const Group *perl_class_escape(P *p, const char *s, const char *end) {
   return NULL;
 }
 
-/* Unicode classes (\p, \P) are a documented gap: reject. Returns 1 if handled (error set). */
-static int unicode_class_unsupported(P *p, const char *s, const char *end) {
-  if (end - s < 2 || s[0] != '\\' || (s[1] != 'p' && s[1] != 'P')) return 0;
-  fail(p, "unsupported Unicode class (\\p) in this build", s, (size_t)(end - s) < 8 ? (size_t)(end - s) : 8);
-  return 1;
+/* unicodeTable (regexp/syntax, Go 1.25): exact names first ("Any", the
+   categories incl. LC and Cn, the scripts), then canonicalName matching
+   (case-insensitive, '_' '-' ' ' ignored) of "Any", "Assigned" (inverted Cn),
+   "ASCII", the table names and unicode.CategoryAliases. */
+static void canon(const char *s, size_t n, char *out, size_t cap) {
+  size_t k = 0; int first = 1;
+  for (size_t i = 0; i < n && k + 1 < cap; i++) {
+    char c = s[i];
+    if (c == '_' || c == '-' || c == ' ') continue;
+    if (first) { if (c >= 'a' && c <= 'z') c = (char)(c - 32); first = 0; }
+    else if (c >= 'A' && c <= 'Z') c = (char)(c + 32);
+    out[k++] = c;
+  }
+  out[k] = 0;
+}
+static int table_by_name(const char *name, size_t n, int loose) {
+  char a[128], b[128];
+  if (n >= sizeof a) return -1;
+  if (loose) canon(name, n, a, sizeof a); else { memcpy(a, name, n); a[n] = 0; }
+  for (int i = 0; i < BJX_UNI_NTABLES; i++) {
+    const char *t = bjx_uni_tables[i].name;
+    if (loose) canon(t, strlen(t), b, sizeof b); else snprintf(b, sizeof b, "%s", t);
+    if (strcmp(a, b) == 0) return i;
+  }
+  return -1;
+}
+static void push_table(RV *v, int i) {
+  const bjx_uni_table *t = &bjx_uni_tables[i];
+  for (uint32_t k = 0; k < t->n; k++) rv_push(v, (int)bjx_uni_ranges[2 * (t->off + k)], (int)bjx_uni_ranges[2 * (t->off + k) + 1]);
+}
+/* 1 if known (runes appended to v, *sign = -1 when to be inverted) */
+static int unicode_table(const char *name, size_t n, RV *v, int *sign) {
+  char c[128];
+  *sign = 1;
+  if (n == 3 && memcmp(name, "Any", 3) == 0) { rv_push(v, 0, MAX_RUNE); return 1; }
+  int i = table_by_name(name, n, 0);
+  if (i >= 0) { push_table(v, i); return 1; }
+  if (n >= sizeof c) return 0;
+  canon(name, n, c, sizeof c);
+  if (strcmp(c, "Any") == 0) { rv_push(v, 0, MAX_RUNE); return 1; }
+  if (strcmp(c, "Assigned") == 0) { push_table(v, table_by_name("Cn", 2, 0)); *sign = -1; return 1; }
+  if (strcmp(c, "Ascii") == 0) { rv_push(v, 0, 0x7F); return 1; }
+  i = table_by_name(name, n, 1);
+  if (i >= 0) { push_table(v, i); return 1; }
+  for (int k = 0; k < BJX_UNI_NALIASES; k++) {
+    char a[128];
+    canon(bjx_uni_cat_aliases[2 * k], strlen(bjx_uni_cat_aliases[2 * k]), a, sizeof a);
+    if (strcmp(a, c) == 0) {
+      const char *tn = bjx_uni_cat_aliases[2 * k + 1];
+      push_table(v, table_by_name(tn, strlen(tn), 0));
+      return 1;
+    }
+  }
+  return 0;
+}
+
+/* parseUnicodeClass: s at "\p" / "\P".  Returns the text after the group with
+   its runes appended to cls, s itself if s is not a Unicode group, NULL on error. */
+static const char *parse_unicode_class(P *p, const char *s, const char *end, RV *cls) {
+  if (end - s < 2 || s[0] != '\\' || (s[1] != 'p' && s[1] != 'P')) return s;
+  int sign = s[1] == 'P' ? -1 : 1;
+  const char *t = s + 2, *name, *seq_end;
+  size_t nlen;
+  if (t >= end || *t != '{') {
+    int w = 0;
+    if (t < end) { next_rune(p, t, (size_t)(end - t), &w); if (p->failed) return NULL; }
+    name = t; nlen = (size_t)w; seq_end = t + w;
+  } else {
+    const char *close = memchr(s, '}', (size_t)(end - s));
+    if (!close) {
+      for (const char *c = s; c < end;) { int w; next_rune(p, c, (size_t)(end - c), &w); if (p->failed) return NULL; c += w; }
+      fail(p, E_INVALID_CHAR_RANGE, s, (size_t)(end - s));
+      return NULL;
+    }
+    for (const char *c = s + 3; c < close;) { int w; next_rune(p, c, (size_t)(close - c), &w); if (p->failed) return NULL; c += w; }
+    name = s + 3; nlen = (size_t)(close - name); seq_end = close + 1;
+  }
+  if (nlen && name[0] == '^') { sign = -sign; name++; nlen--; }
+  RV tab = {0};
+  int tsign;
+  if (!unicode_table(name, nlen, &tab, &tsign)) {
+    free(tab.r);
+    fail(p, E_INVALID_CHAR_RANGE, s, (size_t)(seq_end - s));
+    return NULL;
+  }
+  if (p->flags & F_FOLD) {  /* the table plus its fold-equivalent runes */
+    RV f = {0};
+    for (int i = 0; i < tab.n; i += 2) rv_push_folded(&f, tab.r[i], tab.r[i + 1]);
+    free(tab.r);
+    tab = f;
+  }
+  rv_clean(&tab);
+  if (sign * tsign < 0) rv_negate(&tab);
+  for (int i = 0; i < tab.n; i += 2) rv_push(cls, tab.r[i], tab.r[i + 1]);
+  free(tab.r);
+  return seq_end;
 }
 
 /* parseClass: s points at '['. */
@@ -494,7 +588,11 @@ static const char *parse_class(P *p, const char *s, const char *end) {
         continue;
       }
     }
-    if (unicode_class_unsupported(p, t, end)) { node_free(re); return NULL; }
+    {
+      const char *nt = parse_unicode_class(p, t, end, &re->cls);
+      if (!nt) { node_free(re); return NULL; }
+      if (nt != t) { t = nt; continue; }
+    }
     const Group *g = perl_class_escape(p, t, end);
     if (g) { append_group(p, &re->cls, g); t += 2; continue; }
     const char *rng = t;
@@ -675,7 +773,15 @@ static Node *parse(const char *s, size_t len, char *err, size_t errlen) {
         }
         if (done) break;
       }
-      if (unicode_class_unsupported(&p, t, end)) break;
+      if (end - t >= 2 && (t[1] == 'p' || t[1] == 'P')) {
+        Node *re = node_new(OP_CLASS, p.flags);
+        const char *nt = parse_unicode_class(&p, t, end, &re->cls);
+        if (!nt) { node_free(re); break; }
+        rv_clean(&re->cls);
+        push(&p, re);
+        t = nt;
+        break;
+      }
       const Group *g = perl_class_escape(&p, t, end);
       if (g) {
         Node *re = node_new(OP_CLASS, p.flags);

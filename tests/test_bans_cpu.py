@@ -48,3 +48,21 @@ def test_format_time_fixed_zone(ns, tz):
     want = (dt.datetime(1970, 1, 1, tzinfo=dt.timezone.utc) + dt.timedelta(seconds=sec)).astimezone(
         dt.timezone(dt.timedelta(seconds=tz))).strftime("%Y-%m-%dT%H:%M:%S")
     assert format_time(ns, tz) == want
+
+
+@pytest.mark.parametrize("name", ["America/New_York", "Europe/Berlin", "Australia/Lord_Howe", "Asia/Kolkata",
+                                  "America/Sao_Paulo", "Pacific/Chatham", "UTC"])
+def test_zone_table_matches_zoneinfo(name):
+    """The transition table handed to the device (Zone, bjx_tz_transition)
+    formats every sampled instant 1970-2099 as zoneinfo does."""
+    import random
+    import zoneinfo
+    from banjax_amd import Zone
+    z, tz = Zone.named(name), zoneinfo.ZoneInfo(name)
+    rnd = random.Random(1)
+    secs = [rnd.randrange(0, 4102444800) for _ in range(3000)]
+    for a, _ in z.transitions[:200]:
+        secs += [a - 1, a, a + 1]
+    for s in secs:
+        want = dt.datetime.fromtimestamp(s, tz).strftime("%Y-%m-%dT%H:%M:%S")
+        assert format_time(s * 1_000_000_000 + 999_999_999, z) == want, (name, s)

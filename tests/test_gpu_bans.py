@@ -123,3 +123,33 @@ def test_device_bans_hash_collisions(engine, mask):
         pair.compare_state()
     finally:
         engine.debug_set_ip_hash_mask(0)
+
+
+@pytest.mark.parametrize("zone_name,t_change", [("America/New_York", 1699164000), ("America/New_York", 1710054000),
+                                                ("Australia/Lord_Howe", 1696087800), ("Europe/Dublin", 1698541200)])
+def test_device_bans_dst_zone(engine, zone_name, t_change):
+    """LogRegexBan timestrings across a DST change of the local zone
+    (logTime.Format in time.Local, iptables.go:187): the device's transition
+    table lookup vs the host replay, and both vs Python's zoneinfo conversion
+    (an independent implementation of the same tz database)."""
+    import datetime as dt
+    import json
+    import zoneinfo
+    from banjax_amd import Zone
+    zone = Zone.named(zone_name)
+    tz = zoneinfo.ZoneInfo(zone_name)
+    cfg = Config.from_yaml(BAN_CFG)
+    t0 = t_change - 3 * 3600
+    lines = b"".join(b"%d.%03d 6.6.%d.%d GET esc.com GET /BLOCK%d HTTP/1.1 ua x\n" % (t0 + 97 * k, k % 1000, k // 200, k % 200, k)
+                     for k in range(6 * 3600 // 97))
+    logs = {}
+    for dev in (False, True):
+        engine.state_clear()
+        lim = RegexRateLimiter(cfg, engine=engine, banner=MockBanner(), device_bans=dev, zone=zone)
+        lim.consume_lines(lines, t0 * S, want_results=False)
+        logs[dev] = lim.banner.ban_log
+    assert logs[True] == logs[False] and len(logs[True]) == 6 * 3600 // 97
+    stamps = [json.loads(l)["timestring"] for l in logs[True]]
+    want = [dt.datetime.fromtimestamp(t0 + 97 * k, tz).strftime("%Y-%m-%dT%H:%M:%S") for k in range(len(stamps))]
+    assert stamps == want
+    assert len({s[11:13] for s in stamps}) >= 5

@@ -1,0 +1,114 @@
+"""GPU parity of the rules the round-1 engine refused (VERDICT r01 "What's
+missing" 1, 2): Unicode groups and rules past the DFA state cap, matched on the
+device by the bit-parallel NFA kernel (k_nfa) — against the oracle's Pike VM
+(restating Go regexp, reference internal/config.go:110 and
+internal/regex_rate_limiter.go:234), bit-exact on every consumeLine output."""
+import random
+
+import pytest
+
+import workloads as W
+from banjax_amd import Engine, _lib
+from oracle import oracle as O
+from tests.parity import Pair
+from tests.test_gpu_parity import EDGE_CFG, edge_lines
+
+pytestmark = pytest.mark.gpu
+S = 1_000_000_000
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = Engine()
+    yield e
+    e.close()
+
+
+@pytest.fixture
+def forced_nfa():
+    L = _lib.lib()
+    assert L.bjx_debug_set_dfa_state_cap(1) == 0
+    yield
+    L.bjx_debug_set_dfa_state_cap(0)
+
+
+NFA_RULES = [r".*a.{20}", r"(a|b)*a(a|b){16}", r"GET \S+ GET .*(wp-admin|xmlrpc).{0,40}token", r"\pL\pN",
+             r"\p{Greek}+", r"\PN{3}x", r"(?i)\p{Lu}{2}", r"\bz.{24}\b", r"^GET \S+ GET /a.{18}$", r"(?m)^x.{12}$",
+             r"(?i)straße.{10}", r"\p{Cyrillic}.{30}\p{Greek}"]
+
+
+def _rules_yaml(pats, limit=3):
+    y = ["regexes_with_rates:"]
+    for i, p in enumerate(pats):
+        y.append("  - rule: 'n%d'\n    regex: '%s'\n    interval: 5\n    hits_per_interval: %d\n    decision: challenge"
+                 % (i, p.replace("'", "''"), limit))
+    return "\n".join(y) + "\n"
+
+
+def _lines(rnd, n):
+    frags = [b"a", b"b", b"ab", b"GET ", b"x", b" ", b"wp-admin", b"xmlrpc", b"token", b"/", b"\xce\xbb", b"\xce\x9b",
+             b"5", b"\xd9\xa3", b"\xc3\xa9", b"\xff", b"A", b"aaaaaaaa", b"bbbbbbbb", b"-", b"z", b"STRASSE",
+             b"\xd0\x96", b"Q" * 20, b"\xe2\x84\xaa", b"\r"]
+    out = []
+    for j in range(n):
+        body = b"".join(rnd.choice(frags) for _ in range(rnd.randrange(0, 40)))
+        if j % 7 == 0:
+            body = b"/a" + b"q" * 18
+        if j % 11 == 0:
+            body = b"/x GET /wp-admin/" + b"q" * rnd.randrange(30, 45) + b"token"
+        out.append(b"1700000000.%03d 10.0.%d.%d GET h%d.com GET " % (j % 1000, j % 7, j % 50, j % 5) + body)
+    return b"\n".join(out) + b"\n"
+
+
+def test_nfa_rules_match_oracle(engine):
+    rs_yaml = _rules_yaml(NFA_RULES)
+    pair = Pair(rs_yaml, engine)
+    n_nfa = sum(1 for i in range(len(pair.lim.ruleset)) if pair.lim.ruleset.rule_info(i)[2] & 4)
+    assert n_nfa >= 3
+    rnd = random.Random(8)
+    pair.feed(_lines(rnd, 4000), 1700000000 * S)
+    pair.feed(_lines(rnd, 4000), 1700000001 * S)
+    pair.compare_state(["10.0.1.1", "10.0.3.7"])
+
+
+def test_forced_nfa_edge_lines(engine, forced_nfa):
+    """Every edge-case rule (\\b, ^ / $, (?i) with non-ASCII folds, negated
+    classes) through k_nfa / the per-line NFA path."""
+    t = 1700000000
+    pair = Pair(EDGE_CFG, engine)
+    data = edge_lines(t)
+    pair.feed(data, t * S)
+    pair.feed(data, (t + 1) * S)
+    pair.compare_state(["1.2.3.4", "3.3.3.3", "4.4.4.4", "8.8.8.8"])
+
+
+@pytest.mark.parametrize("name,n_lines", [("cfg1", 60_000), ("cfg3", 60_000), ("cfg4", 800)])
+def test_forced_nfa_workloads(engine, forced_nfa, name, n_lines):
+    """BASELINE workloads with every non-trivial rule on the bit-parallel NFA."""
+    w = W.scaled(W.ALL[name], n_lines, n_ips=n_lines // 3 + 1)
+    pair = Pair(w.rules_yaml, engine)
+    half = n_lines // 2
+    pair.feed(w.host_lines(0, half), w.now_ns(0, half))
+    pair.feed(w.host_lines(half, n_lines - half), w.now_ns(half, n_lines - half))
+    pair.compare_state()
+
+
+def test_forced_nfa_regex_corpus(engine, forced_nfa):
+    rnd = random.Random(5)
+    atoms = [r"a", r"b", r"\d", r"\w", r"\W", r"\s", r".", r"[a-c]", r"[^ab]", r"(?i:K)", r"\b", r"\B", r"^", r"$",
+             r"é", r"\x{FFFD}", r"(a|bc)", r"x?", r"y+", r"z*", r"[[:upper:]]", r"\.", r" ", r"\pL", r"\p{Greek}"]
+    pats = []
+    for _ in range(60):
+        p = "".join(rnd.choice(atoms) for _ in range(rnd.randrange(1, 6)))
+        if rnd.random() < 0.3 and not p.endswith(("?", "+", "*", "}")):
+            p += "{1,3}"
+        if O.compile_error(p) is None:
+            pats.append(p)
+    pair = Pair(_rules_yaml(pats, 1000000), engine)
+    alpha = [b"a", b"b", b"c", b"K", b"k", b"1", b" ", b"_", b".", b"\xc3\xa9", b"\xff", b"\xe2\x84\xaa", b"-", b"x",
+             b"y", b"z", b"\r", b"\xce\xbb"]
+    lines = []
+    for j in range(3000):
+        body = b"".join(rnd.choice(alpha) for _ in range(rnd.randrange(0, 14)))
+        lines.append(b"1700000000 9.9.9.%d GET h%d.com " % (j % 250, j % 7) + body)
+    pair.feed(b"\n".join(lines) + b"\n", 1700000000 * S)
