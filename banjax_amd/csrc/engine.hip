@@ -534,7 +534,41 @@ constexpr uint32_t kWaveLds = kTileLds + kLineCap * (2 + 2) + kCandList * 4 + kL
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kScanLdsMax = 160 * 1024;  // gfx950 LDS per CU (one scan block per CU)
 constexpr uint32_t kLinesImgMax = 16 * 1024;  // k_lines copies the lookup image to LDS up to this size
+constexpr uint32_t kRulesImgMax = 48 * 1024;  // k_rules likewise (no line staging: 3+ blocks per CU)
 constexpr uint32_t kSpanBytes = 12 * 1024;    // k_lines: bytes of 64 lines staged per wave
+
+// first four spaces of the line [p, p + n): 16 B aligned loads, SWAR compare
+__device__ __forceinline__ uint32_t find_spaces(const uint8_t *p, uint32_t n, uint32_t &sp0, uint32_t &sp1,
+                                                uint32_t &sp2, uint32_t &sp3) {
+  const uint32_t skip = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15);
+  const uint4 *base = reinterpret_cast<const uint4 *>(p - skip);  // keeps p's address space
+  uint32_t ns = 0;
+  for (uint32_t c = 0; c * 16 < n + skip && ns < 4; ++c) {
+    const uint4 v = base[c];
+    // 16-bit mask of the spaces of this chunk inside [p, p + n)
+    uint32_t m16 = 0;
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t x = wv[k] ^ 0x20202020u;
+      const uint32_t hb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+      m16 |= (((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u)) << (4 * k);
+    }
+    const int32_t lo = (int32_t)skip - (int32_t)(c * 16), hi = lo + (int32_t)n;  // valid chunk bytes [lo, hi)
+    if (lo > 0) m16 &= ~((1u << lo) - 1u);
+    if (hi < 16) m16 &= hi > 0 ? (1u << hi) - 1u : 0u;
+    while (m16 && ns < 4) {  // selects, not an indexed store: no scratch
+      const uint32_t pos = c * 16 + (uint32_t)__ffs(m16) - 1 - skip;
+      m16 &= m16 - 1;
+      sp0 = ns == 0 ? pos : sp0;
+      sp1 = ns == 1 ? pos : sp1;
+      sp2 = ns == 2 ? pos : sp2;
+      sp3 = ns == 3 ? pos : sp3;
+      ++ns;
+    }
+  }
+  return ns;
+}
 
 struct ScanArgs {
   const uint8_t *buf;
@@ -548,6 +582,8 @@ struct ScanArgs {
   uint32_t shared_bytes;      // per-wave LDS regions start here
   uint32_t debug_skip;        // timing experiments only (BJX_DEBUG_SKIP, results invalid): 1 gram phase, 2 candidates,
                               // 4 literal checks of gram table hits, 8 gram table probes
+  uint32_t hdr;               // 1: parse the headers of the lines that start in each tile (scan_header)
+  int64_t now_ns;
 };
 
 // pass A: '\n' count per wave tile
@@ -774,8 +810,8 @@ __device__ __forceinline__ HostRules host_rules(const Bind &B, int32_t hid) {
 
 template <bool EMIT>
 __device__ __forceinline__ void decide_rules(const Bind &B, const Tabs &T, const uint8_t *rest, uint32_t rest_len, int32_t hid,
-                             const HostRules &H, uint64_t lits, uint32_t nlit, bool ovf, uint64_t j, const Lines &L,
-                             const JobSink &S, uint32_t dbg = 0) {
+                             const HostRules &H, uint64_t lits, uint64_t lpos, uint32_t nlit, bool ovf, uint64_t j,
+                             const Lines &L, const JobSink &S, uint32_t dbg = 0) {
   const uint32_t nsite = H.s_end - H.s_begin;
   uint64_t m0 = H.a0, m1 = H.a1;
   // anchored / no-literal rules: every line
@@ -813,9 +849,9 @@ __device__ __forceinline__ void decide_rules(const Bind &B, const Tabs &T, const
       const uint32_t lit = (uint32_t)(lits >> (16 * c)) & 0xFFFF;
       bool dup = false;
       for (uint32_t d = 0; d < c; ++d) dup = dup || ((uint32_t)(lits >> (16 * d)) & 0xFFFF) == lit;
-      if (dup) continue;
       const uint32_t b = B.lr_off[lit], g = B.lr_gend[lit], e = B.lr_off[lit + 1];
-      for (uint32_t i = b; i < g; ++i) {
+      if (dup && g == e) continue;  // site runs are revisited: their full-literal checks are per hit
+      for (uint32_t i = dup ? g : b; i < g; ++i) {
         const uint2 x = B.lr_ent[i];
         const uint32_t pos = nsite + x.y;
         if (has_pos(t0, t1, pos)) continue;
@@ -833,12 +869,25 @@ __device__ __forceinline__ void decide_rules(const Bind &B, const Tabs &T, const
         sl = (sl + 1) & (B.lh_cap - 1);
       }
       if (run.x == 0) continue;
+      const uint32_t hp = (uint32_t)(lpos >> (16 * c)) & 0xFFFF;  // hit offset in rest (0xFFFF: unknown)
       for (uint32_t i = run.z; i < run.w; ++i) {
         const uint2 x = B.lr_ent[i];
         if (has_pos(t0, t1, x.y)) continue;
+        const uint32_t full = B.lr_full[i];
+        if (full != kNone && (x.x >> 31) && hp != 0xFFFF) {
+          // host-split literal of an equivalent rule: matched iff the full
+          // literal surrounds one of its piece's hits (every hit is recorded:
+          // no overflow here); undecided until one does
+          const uint32_t fl = full >> 8, off = full & 0xFF;
+          if (hp >= off && hp - off + lit_len_of(T, fl) <= rest_len && literal_at(T, fl, rest + (hp - off))) {
+            set_pos(t0, t1, x.y);
+            set_pos(m0, m1, x.y);
+          }
+          continue;
+        }
         set_pos(t0, t1, x.y);
-        if (x.x >> 31) set_pos(m0, m1, x.y);
-        else dfa_rule<EMIT>(B, T, x.x, x.y, false, rest, rest_len, m0, m1, j, S);
+        if ((x.x >> 31) && full == kNone) set_pos(m0, m1, x.y);
+        else dfa_rule<EMIT>(B, T, x.x & 0x7FFFFFFFu, x.y, false, rest, rest_len, m0, m1, j, S);
       }
     }
   }
@@ -857,6 +906,42 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+
+// consumeLine up to the rule loop for one line, from the scan tile in LDS
+// (regex_rate_limiter.go:120-172): SplitN header, parseTimestamp fast path,
+// host id (LDS host table), CheckIsAllowed, OldLine.  A line whose header runs
+// past the window or whose timestamp needs the general ParseFloat keeps
+// kLineTodo and goes to k_lines.  complete: the line's '\n' is in the window.
+template <bool IMG_LDS>
+__device__ __forceinline__ void scan_header(const Bind &B, const Tabs &TB, const ScanArgs &A, const uint8_t *p, uint32_t n,
+                                            bool complete, uint64_t j) {
+  const Lines &L = A.L;
+  uint32_t sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
+  const uint32_t ns = find_spaces(p, n, sp0, sp1, sp2, sp3);
+  if (ns < 4) {
+    if (complete) { L.flags[j] = kLineError; L.counts[j] = 0; }
+    return;
+  }
+  double f;
+  if (parse_float_fast(p, sp0, &f) != 0) return;
+  const uint32_t ip_off = sp0 + 1, ip_len = sp1 - sp0 - 1;
+  const uint32_t rest_off = sp1 + 1, host_off = sp2 + 1, host_len = sp3 - sp2 - 1;
+  const int32_t hid = host_lookup_ht(B, TB, p + host_off, host_len);
+  const bool exempt = B.any_allow && check_is_allowed(B, hid, p + ip_off, ip_len);
+  L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
+  L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
+  L.host_id[j] = hid;
+  L.ip_hash[j] = hash_bytes(p + ip_off, ip_len);
+  L.ip16[j] = ip_key16(p + ip_off, ip_len);
+  const int64_t tsn = ns_from_seconds(f);
+  L.ts[j] = tsn;
+  uint8_t fl = 0;
+  if (go_sub(A.now_ns, tsn) > 10000000000LL) fl = kLineOld;
+  else if (exempt) fl = kLineExempt;
+  L.flags[j] = fl;
+  if (fl) L.counts[j] = 0;
+}
+
 
 template <bool IMG_LDS>
 __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_scan(Bind B, ScanArgs A) {
@@ -994,15 +1079,26 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
         ++r;
       }
     }
-    if (!B.any_prefilter || (A.debug_skip & 1)) continue;
     if (lane == 0 && head) ls[0] = 0;
     const bool last_in_halo = n_st && !last_nl && hfirst != kNone;
     const bool last_long = n_st && !last_nl && hfirst == kNone;
     if (lane == 0 && last_in_halo && n_st - 1 < kLineCap) le[n_st - 1] = (uint16_t)hfirst;
+    wave_sync();
+    // ---- headers of the lines that start in this tile (one lane per line)
+    if (A.hdr) {
+      const uint32_t n_hl = min(n_st, kLineCap);
+      for (uint32_t k = lane; k < n_hl; k += 64) {
+        const uint64_t gline = tb + nh + k;
+        if (gline >= A.n_lines) continue;
+        const bool complete = k + 1 < n_st || !last_long;
+        const uint32_t b0 = ls[k], e0 = complete ? (uint32_t)le[k] : kWT + kHalo;
+        scan_header<IMG_LDS>(B, TB, A, T + b0, e0 - b0, complete, gline);
+      }
+    }
+    if (!B.any_prefilter || (A.debug_skip & 1)) continue;
     // the line open at the tile start is long iff it started before the previous
     // tile (that tile has no '\n') or runs past the previous tile's halo
     const bool open_long = !head && (p0 == kNone || p0 >= kHalo || tb == A.tile_base[t - 1]);
-    wave_sync();
 
     // ---- 4-gram prefilter: positions [64 lane, 64 lane + 64) and the last line's halo part
     {
@@ -1131,39 +1227,6 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
   }
 }
 
-// first four spaces of the line [p, p + n): 16 B aligned loads, SWAR compare
-__device__ __forceinline__ uint32_t find_spaces(const uint8_t *p, uint32_t n, uint32_t &sp0, uint32_t &sp1,
-                                                uint32_t &sp2, uint32_t &sp3) {
-  const uint32_t skip = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15);
-  const uint4 *base = reinterpret_cast<const uint4 *>(p - skip);  // keeps p's address space
-  uint32_t ns = 0;
-  for (uint32_t c = 0; c * 16 < n + skip && ns < 4; ++c) {
-    const uint4 v = base[c];
-    // 16-bit mask of the spaces of this chunk inside [p, p + n)
-    uint32_t m16 = 0;
-    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t x = wv[k] ^ 0x20202020u;
-      const uint32_t hb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
-      m16 |= (((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u)) << (4 * k);
-    }
-    const int32_t lo = (int32_t)skip - (int32_t)(c * 16), hi = lo + (int32_t)n;  // valid chunk bytes [lo, hi)
-    if (lo > 0) m16 &= ~((1u << lo) - 1u);
-    if (hi < 16) m16 &= hi > 0 ? (1u << hi) - 1u : 0u;
-    while (m16 && ns < 4) {  // selects, not an indexed store: no scratch
-      const uint32_t pos = c * 16 + (uint32_t)__ffs(m16) - 1 - skip;
-      m16 &= m16 - 1;
-      sp0 = ns == 0 ? pos : sp0;
-      sp1 = ns == 1 ? pos : sp1;
-      sp2 = ns == 2 ? pos : sp2;
-      sp3 = ns == 3 ? pos : sp3;
-      ++ns;
-    }
-  }
-  return ns;
-}
-
 struct LinesArgs {
   uint32_t dbg;  // timing experiments only (BJX_DEBUG_LINES): 1 no anchored checks, 2 no literal hits, 4 unstaged, 8 no host lookup
   const uint8_t *buf;
@@ -1178,6 +1241,8 @@ struct LinesArgs {
   unsigned long long *job_count;
   uint64_t job_cap;
   uint32_t span_bytes;  // LDS staging per wave (0 = read lines from HBM)
+  const uint32_t *list; // non-null: process only these lines (n_list of them), unstaged
+  uint64_t n_list;
 };
 
 // consumeLine up to the rule loop for line j (bytes at base + (s - origin)):
@@ -1234,7 +1299,7 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
       L.counts[j] = 0;
     } else {
       // literal hits of the scan pass inside rest (unverified ones checked here)
-      uint64_t lits = 0;
+      uint64_t lits = 0, lpos = 0;
       uint32_t nlit = 0;
       const uint64_t rs = s + rest_off;
 #pragma unroll
@@ -1247,10 +1312,11 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
         if (!(v & kCandVerified) &&
             (q + lit_len_of(TB, lit) > s + n || !literal_at(TB, lit, base + (q - origin))))
           continue;
+        lpos |= (uint64_t)(q - rs < 0xFFFF ? (uint32_t)(q - rs) : 0xFFFFu) << (16 * nlit);
         lits |= (uint64_t)lit << (16 * nlit++);
       }
-      decide_rules<true>(B, TB, p + rest_off, n - rest_off, hid, H, lits, (A.dbg & 2) ? 0u : nlit, cc > (uint32_t)kCandSlots, j, L, S,
-                         A.dbg);
+      decide_rules<true>(B, TB, p + rest_off, n - rest_off, hid, H, lits, lpos, (A.dbg & 2) ? 0u : nlit,
+                         cc > (uint32_t)kCandSlots, j, L, S, A.dbg);
     }
   }
 }
@@ -1283,13 +1349,14 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
   uint8_t *span = s_dyn + ((IMG_LDS ? B.img_bytes : 0) + 15u & ~15u) + (kBlock / 64) * (kWaveJobs * 8 + 16) +
                   wave * (A.span_bytes + 32);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + wave * 64u; base < A.n_lines; base += stride) {
-    const uint64_t j = base + lane;
+  const uint64_t n_work = A.list ? A.n_list : A.n_lines;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + wave * 64u; base < n_work; base += stride) {
+    const uint64_t j = A.list ? (base + lane < n_work ? A.list[base + lane] : A.n_lines) : base + lane;
     const uint64_t jl = min(base + 63, A.n_lines - 1);
     const uint64_t s0 = base ? A.nl[base - 1] + 1 : 0;
     const uint64_t s1 = A.nl[jl];
     const uint64_t b16 = s0 & ~15ull;
-    const bool staged = s1 + 16 - b16 <= A.span_bytes && !(A.dbg & 4);  // 16 B of slack for word-wise over-reads
+    const bool staged = !A.list && s1 + 16 - b16 <= A.span_bytes && !(A.dbg & 4);  // 16 B of slack for word-wise over-reads
     // per-line loads that do not depend on the staged bytes go out first
     uint64_t s = 0, cv[kCandSlots];
     uint32_t n = 0, cc = 0;
@@ -1334,6 +1401,97 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
       // two inlined copies: LDS addressing for staged waves, global otherwise
       if (staged) line_body<true>(B, TB, A, span, b16, s, n, j, S, cc, cv);
       else line_body<false>(B, TB, A, A.buf, 0, s, n, j, S, cc, cv);
+    }
+    // ---- append this wave's DFA jobs (one global atomic per 64 lines)
+    wave_sync();
+    const uint32_t nj = min(*S.cnt, kWaveJobs);
+    if (nj) {
+      unsigned long long jb = 0;
+      if (lane == 0) jb = atomicAdd(A.job_count, (unsigned long long)nj);
+      jb = __shfl(jb, 0);
+      for (uint32_t i = lane; i < nj; i += 64)
+        if (jb + i < A.job_cap) { A.jline[jb + i] = S.lds[i].x; A.jkey[jb + i] = S.lds[i].y; }
+    }
+    wave_sync();
+    if (lane == 0) *S.cnt = 0;
+    wave_sync();
+  }
+}
+
+// Rule decisions of the lines whose header the scan pass parsed (one lane per
+// line, regex_rate_limiter.go:175-211): host rules, anchored checks against
+// the line in HBM, the scan's literal hits; undecided (line, rule) pairs become
+// DFA jobs.  kLineTodo lines (and lines with more than 128 applicable rules)
+// are listed for k_lines.
+struct RulesArgs {
+  const uint8_t *buf;
+  const uint64_t *nl;
+  uint64_t n_lines;
+  Lines L;
+  uint32_t *todo;
+  unsigned long long *todo_count;
+  uint32_t *jline, *jkey;
+  unsigned long long *job_count;
+  uint64_t job_cap;
+};
+
+template <bool IMG_LDS>
+__global__ __launch_bounds__(kBlock) void k_rules(Bind B, RulesArgs A) {
+  uint8_t *s_img = s_dyn;
+  if (IMG_LDS) {
+    for (uint32_t i = threadIdx.x; i < B.img_bytes / 16; i += blockDim.x)
+      reinterpret_cast<uint4 *>(s_img)[i] = reinterpret_cast<const uint4 *>(B.img)[i];
+    __syncthreads();
+  }
+  const Tabs TB = make_tabs(IMG_LDS ? s_img : B.img, B.il);
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  JobSink S;
+  S.lds = reinterpret_cast<uint2 *>(s_dyn + ((IMG_LDS ? B.img_bytes : 0) + 15u & ~15u) + wave * (kWaveJobs * 8 + 16));
+  S.cnt = reinterpret_cast<uint32_t *>(S.lds + kWaveJobs);
+  S.jline = A.jline;
+  S.jkey = A.jkey;
+  S.count = A.job_count;
+  S.cap = A.job_cap;
+  if (lane == 0) *S.cnt = 0;
+  wave_sync();
+  const Lines &L = A.L;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + wave * 64u; base < A.n_lines; base += stride) {
+    const uint64_t j = base + lane;
+    if (j < A.n_lines) {
+      const uint8_t fl = L.flags[j];
+      if (fl & kLineTodo) {
+        push_list(A.todo, A.todo_count, j);
+      } else if (fl == 0) {
+        const int32_t hid = L.host_id[j];
+        const HostRules H = host_rules(B, hid);
+        if ((H.s_end - H.s_begin) + B.n_global > 128) {
+          L.flags[j] = kLineTodo;  // the per-line kernel sends it to the general path
+          push_list(A.todo, A.todo_count, j);
+        } else {
+          const uint64_t s = j ? A.nl[j - 1] + 1 : 0;
+          const uint32_t n = (uint32_t)(A.nl[j] - s);
+          const uint32_t ro = L.rest_off[j];
+          uint64_t lits = 0, lpos = 0;
+          uint32_t nlit = 0, cc = 0;
+          if (B.any_prefilter) {
+            cc = L.cand_cnt[j];
+            const uint64_t rs = s + ro;
+#pragma unroll
+            for (uint32_t c = 0; c < (uint32_t)kCandSlots; ++c) {
+              if (c >= cc) break;
+              const uint64_t v = L.cand[j * kCandSlots + c];
+              const uint32_t lit = (uint32_t)(v & 0x7FFFFF);
+              const uint64_t q = v >> 24;
+              if (q < rs) continue;
+              if (!(v & kCandVerified) && (q + lit_len_of(TB, lit) > s + n || !literal_at(TB, lit, A.buf + q))) continue;
+              lpos |= (uint64_t)(q - rs < 0xFFFF ? (uint32_t)(q - rs) : 0xFFFFu) << (16 * nlit);
+              lits |= (uint64_t)lit << (16 * nlit++);
+            }
+          }
+          decide_rules<true>(B, TB, A.buf + s + ro, n - ro, hid, H, lits, lpos, nlit, cc > (uint32_t)kCandSlots, j, L, S);
+        }
+      }
     }
     // ---- append this wave's DFA jobs (one global atomic per 64 lines)
     wave_sync();
@@ -2642,7 +2800,7 @@ struct bjx_engine {
   DevBuf<uint4> l_ip16;
   DevBuf<uint32_t> long_list;
   DevBuf<uint32_t> jline, jkey, jline2, jkey2;
-  uint64_t last_jobs = 0;
+  uint64_t last_jobs = 0, last_todo = 0;
   uint32_t scan_lds[2] = {0, 0};
   bool lines_attr = false;
   DevBuf<uint32_t> l_ccnt;
@@ -2899,6 +3057,43 @@ static void calibrate_grams(const std::vector<uint8_t> &lit_bytes, const std::ve
   }
 }
 
+// The longest piece (>= 4 bytes) of a prefilter literal left when every
+// occurrence of host h is cut out (ASCII-case-insensitive where the literal
+// is); *off = its offset in the literal.  Any piece of a required literal is a
+// required literal too, so the prefilter stays sound.
+static bool split_at_host(const PrefLit &pl, const std::string &h, PrefLit *piece, uint32_t *off) {
+  const size_t n = pl.s.size(), m = h.size();
+  if (m == 0 || m > n) return false;
+  auto at = [&](size_t i) {
+    for (size_t k = 0; k < m; ++k) {
+      const uint8_t c = (uint8_t)h[k];
+      const uint8_t lc = (c >= 'A' && c <= 'Z') ? (uint8_t)(c | 0x20) : c;
+      if (pl.ci[i + k] ? (uint8_t)pl.s[i + k] != lc : (uint8_t)pl.s[i + k] != c) return false;
+    }
+    return true;
+  };
+  size_t best_b = 0, best_n = 0, b = 0;
+  bool cut = false;
+  for (size_t i = 0; i + m <= n;) {
+    if (at(i)) {
+      if (i - b > best_n) { best_b = b; best_n = i - b; }
+      b = i + m;
+      i = b;
+      cut = true;
+    } else {
+      ++i;
+    }
+  }
+  if (!cut) return false;
+  if (n - b > best_n) { best_b = b; best_n = n - b; }
+  if (best_n < 4 || best_b > 255) return false;
+  piece->s = pl.s.substr(best_b, best_n);
+  piece->ci = pl.ci.substr(best_b, best_n);
+  piece->gram_off = pl.gram_off >= best_b && pl.gram_off + 4 <= best_b + best_n ? pl.gram_off - (uint32_t)best_b : 0;
+  *off = (uint32_t)best_b;
+  return true;
+}
+
 void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, size_t sample_n) {
   if (e->bound_uid == rs->uid && e->bound_dec_version == e->decisions_version) return;
   // host dictionary: per-site hosts, skip hosts, allow-list sites
@@ -2936,6 +3131,10 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   std::vector<uint32_t> lit_off, lit_len, lit_gram, rule_lits;
   std::vector<uint8_t> lit_pref;
   std::vector<uint64_t> nfa_blob;
+  std::vector<uint32_t> rule_full;  // per rule_lits entry: (full literal << 8 | piece offset) of a host-split literal
+  std::vector<const std::string *> site_host(rs->rules.size(), nullptr);
+  for (auto &st : rs->sites)
+    for (uint32_t r : st.second) site_host[r] = &st.first;
   bool any_anchored = false;
   for (size_t i = 0; i < rs->rules.size(); ++i) {
     const auto &r = rs->rules[i];
@@ -2977,11 +3176,27 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     };
     d.lits_off = (uint32_t)rule_lits.size();
     if (r.rx.mode == kModePrefilter)
-      for (auto &pl : r.rx.pref) rule_lits.push_back(intern_lit(pl, true));
+      for (auto &pl : r.rx.pref) {
+        // a per-site rule's literal that spells its own host (e.g. "GET <host> GET
+        // /wp-login.php HTTP/") is filed under its longest host-free piece: the
+        // piece is shared by every host's copy of the rule (one gram, one
+        // verification), the line's host id picks the rule (lh_tab), and the full
+        // literal is checked around the hit in k_lines
+        PrefLit piece;
+        uint32_t off = 0;
+        if (site_host[i] && split_at_host(pl, *site_host[i], &piece, &off)) {
+          const uint32_t full = intern_lit(pl, false);
+          rule_lits.push_back(intern_lit(piece, true));
+          rule_full.push_back((full << 8) | off);
+        } else {
+          rule_lits.push_back(intern_lit(pl, true));
+          rule_full.push_back(kNone);
+        }
+      }
     d.lits_len = (uint16_t)(rule_lits.size() - d.lits_off);
     d.anc_off = (uint32_t)rule_lits.size();
     if (r.rx.mode == kModeAnchored)
-      for (auto &pl : r.rx.anchor) rule_lits.push_back(intern_lit(pl, false));
+      for (auto &pl : r.rx.anchor) { rule_lits.push_back(intern_lit(pl, false)); rule_full.push_back(kNone); }
     d.anc_len = (uint16_t)(rule_lits.size() - d.anc_off);
     d.anc_equiv = r.rx.anchor_equivalent ? 1 : 0;
     any_anchored = any_anchored || r.rx.mode == kModeAnchored;
@@ -3153,7 +3368,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   const std::vector<uint4> dfa_site_q = anchor_q(dfa_site), dfa_glob_q = anchor_q(dfa_glob);
   const uint32_t n_lit = (uint32_t)lit_off.size();
   std::vector<std::vector<uint2>> lr_g(n_lit);
-  std::vector<std::vector<std::pair<int32_t, uint2>>> lr_s(n_lit);
+  std::vector<std::vector<std::pair<int32_t, uint3>>> lr_s(n_lit);
   if (use_pref) {
     for (uint32_t g = 0; g < rs->n_global; ++g)
       if (mode_of(g) == kModePrefilter)
@@ -3164,19 +3379,24 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
         const uint32_t r = per_host[h][k];
         if (mode_of(r) != kModePrefilter) continue;
         for (uint32_t i = drules[r].lits_off; i < drules[r].lits_off + drules[r].lits_len; ++i)
-          lr_s[rule_lits[i]].push_back({(int32_t)h, make_uint2(canon[r] | equiv_of(r), k)});
+          lr_s[rule_lits[i]].push_back({(int32_t)h, make_uint3(canon[r] | equiv_of(r), k, rule_full[i])});
       }
   }
   std::vector<uint32_t> lr_off(n_lit + 1, 0), lr_gend(std::max<uint32_t>(1, n_lit), 0);
   std::vector<uint2> lr_ent;
+  std::vector<uint32_t> lr_full;
   std::vector<int32_t> lr_host;
   for (uint32_t l = 0; l < n_lit; ++l) {
     lr_off[l] = (uint32_t)lr_ent.size();
-    for (auto &x : lr_g[l]) { lr_ent.push_back(x); lr_host.push_back(-1); }
+    for (auto &x : lr_g[l]) { lr_ent.push_back(x); lr_host.push_back(-1); lr_full.push_back(kNone); }
     lr_gend[l] = (uint32_t)lr_ent.size();
     std::stable_sort(lr_s[l].begin(), lr_s[l].end(),
-                     [](const std::pair<int32_t, uint2> &a, const std::pair<int32_t, uint2> &b) { return a.first < b.first; });
-    for (auto &x : lr_s[l]) { lr_ent.push_back(x.second); lr_host.push_back(x.first); }
+                     [](const std::pair<int32_t, uint3> &a, const std::pair<int32_t, uint3> &b) { return a.first < b.first; });
+    for (auto &x : lr_s[l]) {
+      lr_ent.push_back(make_uint2(x.second.x, x.second.y));
+      lr_full.push_back(x.second.z);
+      lr_host.push_back(x.first);
+    }
   }
   lr_off[n_lit] = (uint32_t)lr_ent.size();
   // (literal, host) -> run of that host's site entries (one probe per hit in
@@ -3296,7 +3516,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
          o_dso = bb.add(dfa_site_off), o_ds = bb.add(dfa_site), o_dg = bb.add(dfa_glob), o_pso = bb.add(pref_site_off),
          o_dsq = bb.add(dfa_site_q), o_dgq = bb.add(dfa_glob_q),
          o_ps = bb.add(pref_site), o_pg = bb.add(pref_glob), o_hslot = bb.add(hslot), o_lh = bb.add(lh_tab),
-         o_nfa = bb.add(nfa_blob);
+         o_nfa = bb.add(nfa_blob), o_lrf = bb.add(lr_full);
   e->bind_blob.ensure(bb.bytes.size());
   HIP_OK(hipMemcpy(e->bind_blob.p, bb.bytes.data(), bb.bytes.size(), hipMemcpyHostToDevice));
   uint8_t *base = e->bind_blob.p;
@@ -3351,6 +3571,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.lr_gend = reinterpret_cast<const uint32_t *>(base + o_lrg);
   B.lr_ent = reinterpret_cast<const uint2 *>(base + o_lre);
   B.lr_host = reinterpret_cast<const int32_t *>(base + o_lrh);
+  B.lr_full = reinterpret_cast<const uint32_t *>(base + o_lrf);
   B.lh_tab = reinterpret_cast<const uint4 *>(base + o_lh);
   B.lh_cap = lh_cap;
   B.sc_always = reinterpret_cast<const uint64_t *>(base + o_sca);
@@ -3796,6 +4017,14 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   e->jkey.ensure(e->jline.n);
   HIP_OK(hipMemsetAsync(e->scalars.p, 0, 16 * sizeof(unsigned long long), st));
   if (B.any_prefilter) HIP_OK(hipMemsetAsync(e->l_ccnt.p, 0, n_lines * 4, st));
+  // BJX_SCAN_HEADER=1: the scan pass parses the header of every line that fits
+  // its window and k_rules decides their rules (the others keep kLineTodo for
+  // k_lines).  Off by default: measured slower at cfg3 (profiles/r02_v2: scan
+  // +19 ms, k_rules 24.8 ms against k_lines 30.4 ms), the rule decisions'
+  // reads of line bytes from HBM outweigh the saved staging.
+  static const bool scan_hdr_env = getenv("BJX_SCAN_HEADER") && atoi(getenv("BJX_SCAN_HEADER")) == 1;
+  const bool scan_hdr = scan_hdr_env;
+  if (scan_hdr) HIP_OK(hipMemsetAsync(e->l_flags.p, kLineTodo, n_lines, st));
   mark(e, 1);
 
   // ---- the scan kernel (the hot, HBM-bound kernel): line framing + literal hits
@@ -3805,6 +4034,8 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     A.buf = buf; A.n = n; A.n_tiles = n_tiles; A.n_lines = n_lines; A.tile_base = e->tile_base.p; A.nl = e->nl.p;
     A.L = L; A.stats = e->scalars.p + 8;
     A.debug_skip = getenv("BJX_DEBUG_SKIP") ? (uint32_t)atoi(getenv("BJX_DEBUG_SKIP")) : 0u;
+    A.hdr = scan_hdr ? 1u : 0u;
+    A.now_ns = now_ns;
     // block-shared LDS: gram bitset, the lookup image when it fits, then 16 wave regions
     const uint32_t fixed = kGramWords * 4 + kScanWaves * kWaveLds;
     const bool img_lds = fixed + B.img_bytes <= kScanLdsMax;
@@ -3824,37 +4055,62 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   }
   mark(e, 2);
 
-  // ---- per-line pass (header, host, exemption, rule decisions) -> DFA jobs
+  // ---- rule decisions (k_rules) for the lines the scan parsed; k_lines does
+  // the rest (header past the scan window, exotic timestamps, > 128 rules)
   unsigned long long sc4[5] = {0, 0, 0, 0, 0};
+  int n_cu = 0;
+  HIP_OK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, e->device));
+  if (!e->lines_attr) {
+    for (const void *f : {reinterpret_cast<const void *>(&k_lines<true>), reinterpret_cast<const void *>(&k_lines<false>),
+                          reinterpret_cast<const void *>(&k_rules<true>), reinterpret_cast<const void *>(&k_rules<false>)})
+      HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScanLdsMax));
+    e->lines_attr = true;
+  }
+  // one resident wave of blocks (grid-stride loops): a grid of several
+  // "rounds" leaves the last round partly empty
+  auto resident_grid = [&](const void *fn, uint32_t lds, uint64_t work) {
+    int per_cu = 0;
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds));
+    const uint64_t resident = (uint64_t)std::max(1, per_cu) * (uint64_t)std::max(1, n_cu);
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((work + kBlock - 1) / kBlock, resident));
+  };
   for (int attempt = 0;; ++attempt) {
     LinesArgs A;
     A.buf = buf; A.n = n; A.nl = e->nl.p; A.n_lines = n_lines; A.L = L; A.now_ns = now_ns;
     A.dbg = getenv("BJX_DEBUG_LINES") ? (uint32_t)atoi(getenv("BJX_DEBUG_LINES")) : 0u;
     A.slow_list = e->slow_list.p; A.slow_count = e->scalars.p;
     A.jline = e->jline.p; A.jkey = e->jkey.p; A.job_count = e->scalars.p + 11; A.job_cap = std::min(e->jline.n, e->jkey.n);
-    const bool img_lds = B.img_bytes <= kLinesImgMax;
     A.span_bytes = getenv("BJX_SPAN_BYTES") ? (uint32_t)atoi(getenv("BJX_SPAN_BYTES")) & ~15u : kSpanBytes;
-    const uint32_t lds = ((img_lds ? B.img_bytes : 0) + 15u & ~15u) +
-                         (kBlock / 64) * (kWaveJobs * 8 + 16 + (A.span_bytes ? A.span_bytes + 32 : 0));
-    if (!e->lines_attr) {
-      HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_lines<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)kScanLdsMax));
-      HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_lines<false>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)kScanLdsMax));
-      e->lines_attr = true;
+    A.list = nullptr; A.n_list = 0;
+    unsigned long long n_todo = 0;
+    if (scan_hdr) {
+      RulesArgs R;
+      R.buf = buf; R.nl = e->nl.p; R.n_lines = n_lines; R.L = L; R.todo = e->long_list.p; R.todo_count = e->scalars.p + 12;
+      R.jline = A.jline; R.jkey = A.jkey; R.job_count = A.job_count; R.job_cap = A.job_cap;
+      const bool img_lds = B.img_bytes <= kRulesImgMax;
+      const uint32_t lds = ((img_lds ? B.img_bytes : 0) + 15u & ~15u) + (kBlock / 64) * (kWaveJobs * 8 + 16);
+      const void *fn = img_lds ? reinterpret_cast<const void *>(&k_rules<true>) : reinterpret_cast<const void *>(&k_rules<false>);
+      const unsigned grid = resident_grid(fn, lds, n_lines);
+      if (img_lds) hipLaunchKernelGGL(k_rules<true>, dim3(grid), dim3(kBlock), lds, st, B, R);
+      else hipLaunchKernelGGL(k_rules<false>, dim3(grid), dim3(kBlock), lds, st, B, R);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(&n_todo, e->scalars.p + 12, 8, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      A.list = e->long_list.p;
+      A.n_list = n_todo;
+      A.span_bytes = 0;
     }
-    // one resident wave of blocks (grid-stride loop): a grid of several
-    // "rounds" leaves the last round partly empty
-    int per_cu = 0, n_cu = 0;
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, img_lds ? reinterpret_cast<const void *>(&k_lines<true>) : reinterpret_cast<const void *>(&k_lines<false>),
-        kBlock, lds));
-    HIP_OK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, e->device));
-    const uint64_t resident = (uint64_t)std::max(1, per_cu) * (uint64_t)std::max(1, n_cu);
-    const unsigned grid = (unsigned)std::min<uint64_t>((n_lines + kBlock - 1) / kBlock, resident);
-    if (img_lds) hipLaunchKernelGGL(k_lines<true>, dim3(grid), dim3(kBlock), lds, st, B, A);
-    else hipLaunchKernelGGL(k_lines<false>, dim3(grid), dim3(kBlock), lds, st, B, A);
-    HIP_OK(hipGetLastError());
+    if (!scan_hdr || n_todo) {
+      const bool img_lds = B.img_bytes <= kLinesImgMax;
+      const uint32_t lds = ((img_lds ? B.img_bytes : 0) + 15u & ~15u) +
+                           (kBlock / 64) * (kWaveJobs * 8 + 16 + (A.span_bytes ? A.span_bytes + 32 : 0));
+      const void *fn = img_lds ? reinterpret_cast<const void *>(&k_lines<true>) : reinterpret_cast<const void *>(&k_lines<false>);
+      const unsigned grid = resident_grid(fn, lds, A.list ? A.n_list : n_lines);
+      if (img_lds) hipLaunchKernelGGL(k_lines<true>, dim3(grid), dim3(kBlock), lds, st, B, A);
+      else hipLaunchKernelGGL(k_lines<false>, dim3(grid), dim3(kBlock), lds, st, B, A);
+      HIP_OK(hipGetLastError());
+    }
+    e->last_todo = n_todo;
     HIP_OK(hipMemcpyAsync(&last_nl, e->nl.p + (n_lines - 1), 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(sc4, e->scalars.p + 8, 32, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(sc4 + 4, e->scalars.p, 8, hipMemcpyDeviceToHost, st));
@@ -3865,7 +4121,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     e->jline.ensure(sc4[3] + (1u << 20));
     e->jkey.ensure(sc4[3] + (1u << 20));
     HIP_OK(hipMemsetAsync(e->scalars.p, 0, 8, st));
-    HIP_OK(hipMemsetAsync(e->scalars.p + 11, 0, 8, st));
+    HIP_OK(hipMemsetAsync(e->scalars.p + 11, 0, 16, st));
   }
   out->consumed_bytes = last_nl + 1;
   const unsigned long long n_slow = sc4[4], n_jobs = sc4[3];

@@ -139,6 +139,7 @@ struct Bind {
   const uint32_t *lr_off;
   const uint32_t *lr_gend;
   const uint2 *lr_ent;         // (rule | equiv << 31, index in its site / global list)
+  const uint32_t *lr_full;     // per lr_ent: host-split literal (full literal << 8 | piece offset), or ~0
   const int32_t *lr_host;
   // (literal, host) -> that host's run of site entries of the literal:
   // lh_cap open-addressed slots {lit + 1 (0 = empty), host, begin, end}
@@ -243,6 +244,7 @@ struct EvSrc {
 
 enum LineFlagBits : uint8_t {
   kLineError = 1, kLineOld = 2, kLineExempt = 4,
+  kLineTodo = 0x20,       // header not parsed by the scan pass: the per-line kernel (k_lines) does the line
   kLineSlowTs = 0x40,     // per-line fallback kernel (timestamp / long header)
   kLineLong = 0x80,       // line ends past the scan window: rules decided by k_resolve_long
 };

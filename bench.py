@@ -196,6 +196,7 @@ def main():
                 "device_ms_per_step_rank0": round(dev_ms, 3),
                 "pipeline_GBps_rank0": round(nbytes / (ms_per_step / 1000.0) / 1e9, 1),
                 "phase_ms_last_step_rank0": phases,
+                "scan_stats_last_step_rank0": eng.scan_stats(),
                 "parallelism": ("dp%d: chunk-sharded match, IP-hash-sharded rate-limit state, RCCL all-to-all of "
                                 "event records" % world) if world > 1 else "dp1",
             },

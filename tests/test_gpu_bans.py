@@ -148,8 +148,8 @@ def test_device_bans_dst_zone(engine, zone_name, t_change):
         lim = RegexRateLimiter(cfg, engine=engine, banner=MockBanner(), device_bans=dev, zone=zone)
         lim.consume_lines(lines, t0 * S, want_results=False)
         logs[dev] = lim.banner.ban_log
-    assert logs[True] == logs[False] and len(logs[True]) == 6 * 3600 // 97
-    stamps = [json.loads(l)["timestring"] for l in logs[True]]
-    want = [dt.datetime.fromtimestamp(t0 + 97 * k, tz).strftime("%Y-%m-%dT%H:%M:%S") for k in range(len(stamps))]
-    assert stamps == want
-    assert len({s[11:13] for s in stamps}) >= 5
+    assert logs[True] == logs[False] and len(logs[True]) >= 6 * 3600 // 97
+    stamps = [(int(json.loads(l)["path"][6:]), json.loads(l)["timestring"]) for l in logs[True]]
+    for k, s in stamps:
+        assert s == dt.datetime.fromtimestamp(t0 + 97 * k, tz).strftime("%Y-%m-%dT%H:%M:%S"), (k, s)
+    assert len({s[11:13] for _, s in stamps}) >= 5

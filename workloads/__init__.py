@@ -21,7 +21,9 @@ class SynthCfg(C.Structure):
                 ("us_per_line", C.c_uint32), ("n_ips", C.c_uint32), ("n_hosts", C.c_uint32),
                 ("other_host_pct", C.c_uint32), ("trigger_permille", C.c_uint32), ("ua_heavy", C.c_uint32),
                 ("ipv6_pct", C.c_uint32), ("ts_decimals", C.c_uint32), ("fixture_hosts", C.c_uint32),
-                ("_pad", C.c_uint32)]
+                ("ip_mode", C.c_uint32), ("zipf_milli", C.c_uint32), ("hot_pct", C.c_uint32), ("_pad", C.c_uint32)]
+
+IP_UNIFORM, IP_ZIPF, IP_DISTINCT = 0, 1, 2
 
 
 def build(force=False):
@@ -66,11 +68,15 @@ class Workload:
     ipv6_pct: int = 2
     us_per_line: int = 10
     fixture_hosts: int = 0
+    ip_mode: int = 0      # IP_UNIFORM / IP_ZIPF / IP_DISTINCT (workloads/synth.hip)
+    zipf_milli: int = 1100
+    hot_pct: int = 0      # share of lines from one DDoS IP (pool index 0)
 
     def synth_cfg(self, first_line=0, n_lines=None) -> SynthCfg:
         return SynthCfg(self.seed, first_line, self.n_lines if n_lines is None else n_lines, T0_MS,
                         self.us_per_line, self.n_ips, self.n_hosts, self.other_host_pct, self.trigger_permille,
-                        self.ua_heavy, self.ipv6_pct, 3, self.fixture_hosts, 0)
+                        self.ua_heavy, self.ipv6_pct, 3, self.fixture_hosts, self.ip_mode, self.zipf_milli,
+                        self.hot_pct, 0)
 
     def host_lines(self, first_line=0, n_lines=None) -> bytes:
         cfg = self.synth_cfg(first_line, n_lines)
@@ -284,8 +290,9 @@ regexes_with_rates:
     decision: iptables_block
 """
 
-CFG1 = Workload("cfg1", "fixtures/banjax-config-test.yaml rules over 1M synthetic nginx lines", FIXTURE_RULES,
-                seed=1, n_lines=1_000_000, n_ips=100_000, n_hosts=32, trigger_permille=10, fixture_hosts=1)
+CFG1 = Workload("cfg1", "fixtures/banjax-config-test.yaml rules over 1M synthetic nginx lines, IPs Zipf(1.1) over 100k",
+                FIXTURE_RULES, seed=1, n_lines=1_000_000, n_ips=100_000, n_hosts=32, trigger_permille=10,
+                fixture_hosts=1, ip_mode=1)
 CFG2 = Workload("cfg2", "100 global rules (TestPerSiteRegexStress shape + banjax-config.yaml globals), 100M lines, 1M IPs",
                 stress_global_rules(100) + "expiring_decision_ttl_seconds: 10\n",
                 seed=2, n_lines=100_000_000, n_ips=1_000_000, n_hosts=100)
@@ -295,10 +302,14 @@ CFG3 = Workload("cfg3", "1k per-site rules (100 hosts x 10, host-filtered) + 6 g
 CFG4 = Workload("cfg4", "UA-heavy 2-8 KB lines, user-agent regexes (fixtures/banjax-config-test-ua.yaml style)",
                 UA_RULES + "expiring_decision_ttl_seconds: 10\n",
                 seed=4, n_lines=2_000_000, n_ips=100_000, n_hosts=32, ua_heavy=1)
-CFG5 = Workload("cfg5", "DDoS burst: 100M distinct IPs, high trip rate", DDOS_RULES + "expiring_decision_ttl_seconds: 10\n",
-                seed=5, n_lines=100_000_000, n_ips=100_000_000, n_hosts=32, trigger_permille=50)
+CFG5 = Workload("cfg5", "DDoS burst: 100M distinct IPs (one line each), high trip rate",
+                DDOS_RULES + "expiring_decision_ttl_seconds: 10\n",
+                seed=5, n_lines=100_000_000, n_ips=100_000_000, n_hosts=32, trigger_permille=50, ip_mode=2)
+CFG5H = Workload("cfg5h", "DDoS hot key: one IP sends 25% of 100M lines, the rest Zipf(1.1) over 10M IPs",
+                 DDOS_RULES + "expiring_decision_ttl_seconds: 10\n",
+                 seed=6, n_lines=100_000_000, n_ips=10_000_000, n_hosts=32, trigger_permille=50, ip_mode=1, hot_pct=25)
 
-ALL = {w.name: w for w in (CFG1, CFG2, CFG3, CFG4, CFG5)}
+ALL = {w.name: w for w in (CFG1, CFG2, CFG3, CFG4, CFG5, CFG5H)}
 
 
 def scaled(w: Workload, n_lines: int, n_ips=None) -> Workload:

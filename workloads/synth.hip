@@ -25,6 +25,9 @@ struct SynthCfg {
   uint32_t ipv6_pct;
   uint32_t ts_decimals;   // 3 = nginx $msec
   uint32_t fixture_hosts; // 1: host 0 = localhost:8081, host 1 = example.com
+  uint32_t ip_mode;       // IP pool draw: 0 uniform, 1 Zipf(zipf_milli / 1000), 2 distinct (line i -> pool index i mod n_ips, permuted)
+  uint32_t zipf_milli;    // Zipf exponent x 1000 (ip_mode 1)
+  uint32_t hot_pct;       // DDoS hot key: this share of lines comes from pool index 0 (any ip_mode)
   uint32_t _pad;
 };
 
@@ -169,8 +172,31 @@ HD void render(const SynthCfg &cfg, uint64_t i, W &w) {
     w.u0(frac, d);
   }
   w.c(' ');
-  // $remote_addr: uniform over the pool, unique text per pool index
-  const uint32_t idx = r.below(cfg.n_ips);
+  // $remote_addr: pool index per ip_mode, unique text per pool index
+  uint32_t idx;
+  const uint64_t rip = r.next();
+  if (cfg.hot_pct && (rip >> 40) % 100 < cfg.hot_pct) {
+    idx = 0;
+  } else if (cfg.ip_mode == 1) {
+    // Zipf(s)-shaped rank by the continuous inverse CDF: P(rank <= k) ~ (k^(1-s) - 1) / (N^(1-s) - 1)
+    const double s_ = cfg.zipf_milli / 1000.0, e = 1.0 - s_;
+    const double u = (double)(rip >> 11) * (1.0 / 9007199254740992.0);
+    const double hn = pow((double)cfg.n_ips + 1.0, e) - 1.0;
+    double k = pow(1.0 + u * hn, 1.0 / e);
+    uint64_t kk = (uint64_t)k;
+    if (kk < 1) kk = 1;
+    if (kk > cfg.n_ips) kk = cfg.n_ips;
+    idx = (uint32_t)(kk - 1);
+  } else if (cfg.ip_mode == 2) {
+    // every line its own pool index (a bijection of i mod n_ips): n_ips distinct IPs per n_ips lines
+    uint64_t x = i % cfg.n_ips;
+    uint64_t m = 1;
+    while (m < cfg.n_ips) m <<= 1;
+    do { x = (x * 0x5DEECE66Dull + 0xBull) & (m - 1); } while (x >= cfg.n_ips);  // cycle-walk a full-period LCG mod 2^k
+    idx = (uint32_t)x;
+  } else {
+    idx = (uint32_t)((rip >> 11) % cfg.n_ips);
+  }
   if (r.below(100) < cfg.ipv6_pct) {
     w.s("2001:db8:");
     w.x(idx >> 16, 4); w.c(':'); w.x(idx & 0xFFFF, 4); w.s("::"); w.x((idx * 2654435761u) >> 20, 3);
