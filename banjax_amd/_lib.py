@@ -103,8 +103,13 @@ EXPORTS = [
     "bjx_process_batch", "bjx_state_get", "bjx_state_len", "bjx_state_clear", "bjx_state_dump",
     "bjx_engine_last_error", "bjx_match_batch", "bjx_events_partition", "bjx_events_pack", "bjx_apply_events",
     "bjx_finish_batch", "bjx_tailer_open", "bjx_tailer_next", "bjx_tailer_release", "bjx_tailer_stats",
-    "bjx_tailer_close", "bjx_engine_set_ban_options", "bjx_batch_bans",
+    "bjx_tailer_close", "bjx_engine_set_ban_options", "bjx_batch_bans", "bjx_state_stats_get",
 ]
+
+
+class StateStats(C.Structure):
+    _fields_ = [(k, C.c_uint64) for k in ("ips", "ip_slots", "states", "state_slots", "arena_bytes", "arena_capacity",
+                                            "device_bytes", "rehashes")]
 
 _lib = None
 
@@ -161,6 +166,8 @@ def lib():
     L.bjx_state_get.argtypes = [vp, C.c_char_p, sz, C.c_char_p, sz, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.bjx_state_len.restype = C.c_int64
     L.bjx_state_len.argtypes = [vp]
+    L.bjx_state_stats_get.restype = C.c_int
+    L.bjx_state_stats_get.argtypes = [vp, C.c_void_p]
     L.bjx_state_clear.restype = C.c_int
     L.bjx_state_clear.argtypes = [vp]
     L.bjx_state_dump.restype = sz

@@ -2026,10 +2026,10 @@ __global__ void k_fold_claims(State S) {
 // reference order (records sorted by slot, stable).  A block takes kApplyChunk
 // consecutive sorted records, loaded coalesced into LDS with their slots; each
 // run that STARTS in the chunk goes to one lane (long runs to the first lanes,
-// so short-run waves finish early), which walks it from LDS.  The
-// one run that continues past the chunk end is finished by lane 0 over
-// coalesced 256-record windows staged by the whole block.  Records before the
-// chunk's first run head belong to the previous block's run.  out_sorted[u] = outcome of record u in
+// so short-run waves finish early), which walks it from LDS.  The one run that
+// continues past the chunk end is listed for k_long_runs, which applies it
+// from its head.  Records before the chunk's first run head belong to the
+// previous block's run.  out_sorted[u] = outcome of record u in
 // sorted order: bit0 seenIp, bits1-2 MatchType, bit3 Exceeded, bit7 valid.
 constexpr uint32_t kApplyChunk = 2048;
 
@@ -2049,7 +2049,8 @@ __device__ __forceinline__ uint8_t apply_step(const EvRec &v, const DevRule *__r
 
 __global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const uint32_t *__restrict__ key, const EvRec *__restrict__ rec,
                                                   const DevRule *__restrict__ rules, StSlot *__restrict__ st,
-                                                  uint8_t *__restrict__ out_sorted) {
+                                                  uint8_t *__restrict__ out_sorted, uint64_t *__restrict__ long_heads,
+                                                  unsigned long long *__restrict__ n_long) {
   constexpr uint32_t kPer = kApplyChunk / kBlock;  // positions per thread for the head scan
   constexpr uint32_t kLongRun = 8;                 // runs at least this long go to the first lanes
   __shared__ EvRec s_rec[kApplyChunk];
@@ -2057,8 +2058,7 @@ __global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const uint32_t 
   __shared__ uint8_t s_out[kApplyChunk];
   __shared__ uint16_t s_head[kApplyChunk];  // run heads in position order
   __shared__ uint16_t s_ord[kApplyChunk];   // run indices: long runs from the front, short ones from the back
-  __shared__ uint32_t s_wsum[kBlock / 64], s_front, s_back, s_cont, s_cross, s_cq;
-  __shared__ int64_t s_chits, s_cstart;
+  __shared__ uint32_t s_wsum[kBlock / 64], s_front, s_back, s_cont;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t u0 = (uint64_t)blockIdx.x * kApplyChunk;
   const uint32_t n = (uint32_t)min<uint64_t>(kApplyChunk, n_ev - u0);
@@ -2071,7 +2071,6 @@ __global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const uint32_t 
     s_cont = u0 + n < n_ev && key[u0 + n] == key[u0 + n - 1];  // the last run goes on past the chunk
     s_front = 0;
     s_back = 0;
-    s_cross = 0;
   }
   __syncthreads();
   // run heads, compacted in position order (block scan of per-thread counts)
@@ -2113,6 +2112,10 @@ __global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const uint32_t 
     bool valid = cur.valid != 0;
     int64_t hits = cur.hits, start = cur.start, interval = 0, limit = 0;
     uint32_t pr = 0xFFFFFFFFu;
+    if (h + 1 == nh && s_cont) {  // continues past the chunk: k_long_runs applies it from its head
+      long_heads[atomicAdd(n_long, 1ull)] = u0 + b;
+      continue;
+    }
     EvRec v = s_rec[b];
     for (uint32_t u = b; u < e; ++u) {
       EvRec nx;
@@ -2120,42 +2123,128 @@ __global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const uint32_t 
       s_out[u] = apply_step(v, rules, pr, interval, limit, valid, hits, start);
       v = nx;
     }
-    if (h + 1 == nh && s_cont) {  // continues past the chunk: handed to lane 0 below
-      s_cross = 1; s_cq = q; s_chits = hits; s_cstart = start;
-      continue;
-    }
     st[q].hits = hits;
     st[q].start = start;
     st[q].valid = 1;
   }
   __syncthreads();
-  if (s_cross) {
-    // lane 0 walks the tail over windows of kBlock records (s_rec / s_key reused)
-    const uint32_t q = s_cq;
-    int64_t hits = s_chits, start = s_cstart, interval = 0, limit = 0;
-    bool valid = true;
-    uint32_t pr = 0xFFFFFFFFu;
-    for (uint64_t g = u0 + n;; g += kBlock) {
-      __syncthreads();
-      if (g + tid < n_ev) { s_rec[tid] = rec[g + tid]; s_key[tid] = key[g + tid]; }
-      __syncthreads();
-      if (tid == 0) {
-        uint32_t j = 0;
-        for (; j < kBlock && g + j < n_ev && s_key[j] == q; ++j)
-          out_sorted[g + j] = apply_step(s_rec[j], rules, pr, interval, limit, valid, hits, start);
-        if (j < kBlock || g + j >= n_ev) {
-          st[q].hits = hits;
-          st[q].start = start;
-          st[q].valid = 1;
-          s_cross = 0;
-        }
-      }
-      __syncthreads();
-      if (!s_cross) break;
-    }
-  }
   // records before the first head belong to the previous block's run
   for (uint32_t i = (nh ? s_head[0] : n) + tid; i < n; i += kBlock) out_sorted[u0 + i] = s_out[i];
+}
+
+// One (ip, rule name) state whose sorted run crosses a k_apply chunk (hot
+// keys: a DDoS IP's run can hold a large share of the batch).
+// One block per run, from its head:
+//   * the run end and, over the run, whether every event has the same rule
+//     interval / limit and timestamps never decrease (block reductions);
+//   * if so, the fixed windows of Apply (rate_limit.go:37-78) are found one
+//     after another by a block-parallel search (each round samples kBlock
+//     timestamps, so a window of w events costs log_kBlock(w) rounds), and
+//     every event's outcome follows in closed form: the e-th counted hit of a
+//     window that starts with h0 hits is Exceeded iff (h0 + e) % (limit + 1)
+//     == 0 (every hit when limit < 0), and the hits after it are that residue;
+//   * otherwise (mixed limits, timestamps out of order) thread 0 applies the
+//     events one by one, as k_apply's lanes do.
+__device__ __forceinline__ uint32_t block_min_u32(uint32_t v, uint32_t *s_red) {
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t m = s_red[0];
+  for (uint32_t w = 1; w < kBlock / 64; ++w) m = min(m, s_red[w]);
+  return m;
+}
+
+// smallest i in [lo, hi) with pred(i) (pred monotone: false ... true), else hi
+template <typename P>
+__device__ uint64_t block_first(uint64_t lo, uint64_t hi, P pred, uint32_t *s_red) {
+  while (lo < hi) {
+    const uint64_t stride = (hi - lo + kBlock - 1) / kBlock;
+    const uint64_t p = lo + (uint64_t)threadIdx.x * stride;
+    const bool ok = p < hi && pred(p);
+    const uint32_t f = block_min_u32(ok ? threadIdx.x : (uint32_t)kBlock, s_red);
+    if (f == 0) return lo;
+    if (stride == 1) return f == (uint32_t)kBlock ? hi : lo + f;
+    const uint64_t nlo = lo + (uint64_t)(f - 1) * stride + 1;
+    hi = f == (uint32_t)kBlock ? hi : lo + (uint64_t)f * stride;
+    lo = nlo;
+  }
+  return hi;
+}
+
+constexpr uint64_t kLongSerial = 512;  // runs up to this long: thread 0 walks them
+
+__global__ __launch_bounds__(kBlock) void k_long_runs(uint64_t n_ev, const uint32_t *__restrict__ key,
+                                                      const EvRec *__restrict__ rec, const DevRule *__restrict__ rules,
+                                                      StSlot *__restrict__ st, uint8_t *__restrict__ out_sorted,
+                                                      const uint64_t *__restrict__ heads) {
+  __shared__ uint32_t s_red[kBlock / 64];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t head = heads[blockIdx.x];
+  const uint32_t q = key[head];
+  const uint64_t end = block_first(head + 1, n_ev, [&](uint64_t i) { return key[i] != q; }, s_red);
+  const uint32_t r0 = rec[head].rule & 0x7FFFFFFFu;
+  const int64_t I = rules[r0].interval_ns, Lim = rules[r0].hits;
+  uint32_t bad = 0;
+  if (end - head > kLongSerial)
+    for (uint64_t i = head + 1 + tid; i < end; i += kBlock) {
+      const EvRec v = rec[i];
+      const uint32_t r = v.rule & 0x7FFFFFFFu;
+      if (r != r0 && (rules[r].interval_ns != I || rules[r].hits != Lim)) bad = 1;
+      if (v.ts < rec[i - 1].ts) bad = 1;
+    }
+  const StSlot cur = st[q];
+  if (end - head <= kLongSerial || block_min_u32(bad ? 0u : 1u, s_red) == 0) {
+    if (tid == 0) {
+      bool valid = cur.valid != 0;
+      int64_t hits = cur.hits, start = cur.start, interval = 0, limit = 0;
+      uint32_t pr = 0xFFFFFFFFu;
+      for (uint64_t i = head; i < end; ++i) out_sorted[i] = apply_step(rec[i], rules, pr, interval, limit, valid, hits, start);
+      st[q].hits = hits;
+      st[q].start = start;
+      st[q].valid = 1;
+    }
+    return;
+  }
+  // uniform limits, non-decreasing timestamps: window after window
+  const bool valid = cur.valid != 0;
+  bool cont = valid && go_sub(rec[head].ts, cur.start) <= I;  // the head continues the stored window
+  int64_t T = cont ? cur.start : rec[head].ts;
+  int64_t h0 = cont ? cur.hits : 0;
+  uint8_t first_mt = valid ? BJX_OUTSIDE_INTERVAL : BJX_FIRST_TIME;
+  uint64_t a = head;
+  for (;;) {
+    const int64_t Tw = T;
+    const uint64_t b = block_first(a + 1, end, [&](uint64_t i) { return go_sub(rec[i].ts, Tw) > I; }, s_red);
+    for (uint64_t i = a + tid; i < b; i += kBlock) {
+      const int64_t e = (int64_t)(i - a) + 1;
+      bool ex;
+      if (Lim < 0) ex = true;
+      else if (h0 > Lim) ex = e == 1 || (e - 1) % (Lim + 1) == 0;
+      else ex = (h0 + e) % (Lim + 1) == 0;
+      const uint8_t mt = (!cont && i == a) ? first_mt : (uint8_t)BJX_INSIDE_INTERVAL;
+      const bool seen = (rec[i].rule >> 31) == 0;
+      out_sorted[i] = (uint8_t)(0x80 | (seen ? 1 : 0) | (mt << 1) | (ex ? 8 : 0));
+    }
+    if (b >= end) {
+      if (tid == 0) {
+        const int64_t e = (int64_t)(b - a);
+        int64_t hits;
+        if (Lim < 0) hits = 0;
+        else if (h0 > Lim) hits = (e - 1) % (Lim + 1);
+        else hits = (h0 + e) % (Lim + 1);
+        st[q].hits = hits;
+        st[q].start = Tw;
+        st[q].valid = 1;
+      }
+      return;
+    }
+    a = b;
+    T = rec[b].ts;
+    h0 = 0;
+    cont = false;
+    first_mt = BJX_OUTSIDE_INTERVAL;
+  }
 }
 
 __global__ void k_dbg_mask_hash(uint64_t n, uint64_t *__restrict__ h, uint64_t mask) {
@@ -2783,6 +2872,7 @@ struct bjx_engine {
   // persistent state
   State S{};
   uint64_t ip_cap = 0, st_cap = 0;
+  uint64_t rehashes = 0;
   uint32_t epoch = 0;  // batch counter (IpSlot.born)
   uint64_t dbg_hash_mask = 0;  // bjx_debug_set_ip_hash_mask
   uint64_t dbg_budget = 0;     // bjx_debug_set_claim_budget (0 = off)
@@ -2800,7 +2890,9 @@ struct bjx_engine {
   DevBuf<uint4> l_ip16;
   DevBuf<uint32_t> long_list;
   DevBuf<uint32_t> jline, jkey, jline2, jkey2;
-  uint64_t last_jobs = 0, last_todo = 0;
+  uint64_t last_jobs = 0, last_todo = 0, last_long_runs = 0;
+  DevBuf<uint64_t> long_heads;
+  DevBuf<unsigned long long> long_count;
   uint32_t scan_lds[2] = {0, 0};
   bool lines_attr = false;
   DevBuf<uint32_t> l_ccnt;
@@ -3653,6 +3745,7 @@ void grow_ip(bjx_engine *e, uint64_t want) {
   S.ip = nt; S.ip_first = nf; S.ip_off = noff; S.ip_len = nlen;
   S.ip_mask = cap - 1;
   e->ip_cap = cap;
+  ++e->rehashes;
 }
 
 // rehash the state table into one that holds `want` states under a 3/4 load factor
@@ -3670,6 +3763,7 @@ void grow_st(bjx_engine *e, uint64_t want) {
   S.st = nt;
   S.st_mask = cap - 1;
   e->st_cap = cap;
+  ++e->rehashes;
 }
 
 // Tables sized for the steady state, not for every batch's worst case: the
@@ -3769,7 +3863,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
     b->release();
   for (auto *b : {&e->bn_kind, &e->bn_flag, &e->bn_log, &e->dl_bytes, &e->nm_json}) b->release();
   e->bn_best.release(); e->bn_rep.release(); e->bn_sel.release(); e->tz_at.release(); e->tz_off.release();
-  e->rb_first.release(); e->rb_last.release();
+  e->rb_first.release(); e->rb_last.release(); e->long_heads.release(); e->long_count.release();
   e->d_results.release(); e->q_out.release();
   e->long_list.release(); e->l_ip16.release(); e->jline.release(); e->jkey.release(); e->jline2.release(); e->jkey2.release(); e->l_cand.release(); e->l_ccnt.release();
   (void)hipEventDestroy(e->ev0); (void)hipEventDestroy(e->ev1); (void)hipEventDestroy(e->evm0); (void)hipEventDestroy(e->evm1);
@@ -3905,9 +3999,22 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
       return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)n_ev, 0, bits, st);
     });
   }
-  hipLaunchKernelGGL(k_apply, dim3((unsigned)((n_ev + kApplyChunk - 1) / kApplyChunk)), dim3(kBlock), 0, st, n_ev,
-                     e->ev_st2.p, e->ev_rec2.p, B.rules, e->S.st, e->ev_out_s.p);
+  const uint64_t n_chunks = (n_ev + kApplyChunk - 1) / kApplyChunk;
+  e->long_heads.ensure(n_chunks + 1);
+  e->long_count.ensure(1);
+  HIP_OK(hipMemsetAsync(e->long_count.p, 0, 8, st));
+  hipLaunchKernelGGL(k_apply, dim3((unsigned)n_chunks), dim3(kBlock), 0, st, n_ev, e->ev_st2.p, e->ev_rec2.p, B.rules, e->S.st,
+                     e->ev_out_s.p, e->long_heads.p, e->long_count.p);
   HIP_OK(hipGetLastError());
+  unsigned long long n_long = 0;
+  HIP_OK(hipMemcpyAsync(&n_long, e->long_count.p, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  e->last_long_runs = n_long;
+  if (n_long) {
+    hipLaunchKernelGGL(k_long_runs, dim3((unsigned)n_long), dim3(kBlock), 0, st, n_ev, e->ev_st2.p, e->ev_rec2.p, B.rules,
+                       e->S.st, e->ev_out_s.p, e->long_heads.p);
+    HIP_OK(hipGetLastError());
+  }
 }
 
 // The sorted DFA jobs of the bit-parallel NFA rules: each rule's job range
@@ -4700,6 +4807,27 @@ extern "C" int64_t bjx_state_len(bjx_engine *e) {
   }
 }
 
+extern "C" int bjx_state_stats_get(bjx_engine *e, bjx_state_stats *out) {
+  if (!e || !out) return BJX_ERR_ARG;
+  std::lock_guard<std::mutex> g(e->mu);
+  try {
+    HIP_OK(hipSetDevice(e->device));
+    read_counters(e);
+    out->ips = e->host_counters[0];
+    out->ip_slots = e->ip_cap;
+    out->states = e->host_counters[2];
+    out->state_slots = e->st_cap;
+    out->arena_bytes = e->host_counters[1];
+    out->arena_capacity = e->S.arena_cap;
+    out->device_bytes = e->ip_cap * (sizeof(IpSlot) + 4 + 8 + 4) + e->st_cap * sizeof(StSlot) + e->S.arena_cap;
+    out->rehashes = e->rehashes;
+    return BJX_OK;
+  } catch (const BjxError &x) {
+    e->last_error = x.what();
+    return x.code;
+  }
+}
+
 extern "C" int bjx_state_clear(bjx_engine *e) {
   if (!e) return BJX_ERR_ARG;
   std::lock_guard<std::mutex> g(e->mu);
@@ -4793,10 +4921,11 @@ extern "C" size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap)
   if (!e) return 0;
   std::lock_guard<std::mutex> g(e->mu);
   if (e->S.counters) read_counters(e);
-  const uint64_t v[10] = {e->scan_stats[0], e->scan_stats[1], e->scan_stats[2], e->scan_stats[3], e->scan_stats[4],
-                          e->ip_cap, e->host_counters[0], e->st_cap, e->host_counters[2], e->scan_stats[5]};
-  for (size_t k = 0; k < 10 && k < cap; ++k) out[k] = v[k];
-  return 10;
+  const uint64_t v[12] = {e->scan_stats[0], e->scan_stats[1], e->scan_stats[2], e->scan_stats[3], e->scan_stats[4],
+                          e->ip_cap, e->host_counters[0], e->st_cap, e->host_counters[2], e->scan_stats[5],
+                          e->last_todo, e->last_long_runs};
+  for (size_t k = 0; k < 12 && k < cap; ++k) out[k] = v[k];
+  return 12;
 }
 extern "C" size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t i, char *out, size_t cap) {
   if (!rs || i >= rs->rules.size()) return 0;

@@ -190,11 +190,17 @@ class Engine:
     PHASES = ("count", "scan", "resolve", "emit", "capacity", "ip_state_claim", "sort_apply", "trips")
 
     def scan_stats(self):
-        out = (C.c_uint64 * 10)()
-        _lib.lib().bjx_debug_scan_stats(self._h, out, 10)
+        out = (C.c_uint64 * 12)()
+        _lib.lib().bjx_debug_scan_stats(self._h, out, 12)
         return {"gram_bitset_hits": out[0], "literal_hits": out[1], "fallback_lines": out[2], "lookup_image_bytes": out[3],
                 "dfa_jobs": out[4], "ip_table_slots": out[5], "ips": out[6], "state_table_slots": out[7], "states": out[8],
-                "gram_table_hits": out[9]}
+                "gram_table_hits": out[9], "per_line_kernel_lines": out[10], "long_runs": out[11]}
+
+    def state_stats(self):
+        """Occupancy of the HBM rate-limit tables (bjx_state_stats_get)."""
+        st = _lib.StateStats()
+        self._check(_lib.lib().bjx_state_stats_get(self._h, C.byref(st)), "state_stats")
+        return {k: getattr(st, k) for k, _ in _lib.StateStats._fields_}
 
     def phase_ms(self):
         out = (C.c_double * 8)()

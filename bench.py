@@ -27,7 +27,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 def cpu_baseline(w, sample_lines):
     """Oracle (C restatement of the reference Go path, oracle/) on one host core
-    over the first `sample_lines` lines of the same workload."""
+    over the first `sample_lines` lines of the same workload, plus the N-core
+    IP-sharded variant (oracle/shard_worker.py, one process per core)."""
     from oracle import oracle as O
     from tests.parity import oracle_config
     from banjax_amd import Config
@@ -37,9 +38,43 @@ def cpu_baseline(w, sample_lines):
     t0 = time.perf_counter()
     flags, res, consumed = st.consume(oc, data, w.now_ns(0, sample_lines), cap=sample_lines * 8)
     dt = time.perf_counter() - t0
-    return {"value": round(sample_lines / dt, 1), "unit": "lines/s", "cores": 1, "kind": "port",
-            "sample": "first %d lines of %s (%.1f MB), oracle/bjx_oracle.c single-threaded (the reference path is one "
-                      "goroutine, regex_rate_limiter.go:54-77), %.1f s" % (sample_lines, w.name, len(data) / 1e6, dt)}
+    out = {"value": round(sample_lines / dt, 1), "unit": "lines/s", "cores": 1, "kind": "port",
+           "sample": "first %d lines of %s (%.1f MB), oracle/bjx_oracle.c single-threaded (the reference path is one "
+                     "goroutine, regex_rate_limiter.go:54-77), %.1f s" % (sample_lines, w.name, len(data) / 1e6, dt)}
+    try:
+        out["n_core"] = cpu_baseline_sharded(w, sample_lines)
+    except Exception as e:  # the 1-core figure stands on its own
+        out["n_core"] = {"error": str(e)[:200]}
+    return out
+
+
+def cpu_baseline_sharded(w, sample_lines):
+    """N worker processes (N = the CPUs this process may use, at most 16), each
+    running the oracle over its IP-hash shard of N x sample_lines / 4 lines;
+    throughput = lines / slowest worker."""
+    import subprocess
+    import tempfile
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    n = max(1, min(16, avail))
+    total = sample_lines * n // 4
+    data = w.host_lines(0, total)
+    with tempfile.TemporaryDirectory() as d:
+        dp, yp = os.path.join(d, "sample.log"), os.path.join(d, "rules.yaml")
+        open(dp, "wb").write(data)
+        open(yp, "w").write(w.rules_yaml)
+        env = dict(os.environ, OMP_NUM_THREADS="1")
+        procs = [subprocess.Popen([sys.executable, "-m", "oracle.shard_worker", dp, str(k), str(n),
+                                   str(w.now_ns(0, total)), yp], cwd=ROOT, env=env, stdout=subprocess.PIPE)
+                 for k in range(n)]
+        res = [json.loads(p.communicate()[0].decode().strip().splitlines()[-1]) for p in procs]
+    slowest = max(r["seconds"] for r in res)
+    return {"value": round(sum(r["lines"] for r in res) / slowest, 1), "unit": "lines/s", "cores": n,
+            "host_cpus": os.cpu_count(), "kind": "port",
+            "sample": "first %d lines of %s, IP-hash sharded over %d oracle processes (per-IP order kept), "
+                      "slowest shard %.1f s" % (total, w.name, n, slowest)}
 
 
 def pmc_traffic(nbytes):
@@ -100,6 +135,8 @@ def main():
     ap.add_argument("--bans", type=int, default=0,
                     help="1: each step also emits the decision updates and ban-log lines of its trips on the device "
                          "(BJX_EMIT_BANS, copied to pinned host memory); 0: trip list only")
+    ap.add_argument("--bans-steps", type=int, default=3,
+                    help="after the timed region, steps timed again with decision emission on (reported next to value)")
     args = ap.parse_args()
 
     import torch
@@ -164,6 +201,32 @@ def main():
     dev_ms = sum(o.device_ms for o in outs) / len(outs)
     o = outs[-1]
     phases = eng.phase_ms()
+    stats = eng.scan_stats()
+    state_stats = eng.state_stats()
+    # the same step with the Banner's work on the device too: per-IP decision
+    # updates and every LogRegexBan line, copied to pinned host memory
+    dec = None
+    if args.bans_steps > 0 and not bans:
+        bans = True
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.bans_steps):
+            step()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        el2 = time.perf_counter() - t1
+        if dist:
+            t = torch.tensor([el2], device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el2 = float(t.item())
+        bans = False
+        dec = {"value": round(n_lines * world / (el2 / args.bans_steps), 1), "unit": "lines/s",
+               "ms_per_step": round(el2 * 1000.0 / args.bans_steps, 3), "steps": args.bans_steps,
+               "what": "each step also builds the per-IP DynamicDecisionLists updates and all LogRegexBan JSON lines "
+                       "on the device and copies them to pinned host memory (BJX_EMIT_BANS)"}
     total_lines = n_lines * world
     value = total_lines / (elapsed / args.steps)
     achieved = nbytes / (match_ms / 1000.0) / 1e9
@@ -187,7 +250,8 @@ def main():
                 "ruleset_compile_ms_cold": round(compile_ms, 1),
                 "lines_per_gpu": n_lines,
                 "bytes_per_gpu": nbytes,
-                "distinct_ips": w.n_ips,
+                "distinct_ips": stats["ips"],
+                "ip_pool": w.n_ips,
                 "rule_results_per_step_rank0": o.n_results,
                 "rate_limit_events_per_step_rank0": o.n_events,
                 "trips_per_step_rank0": o.n_trips,
@@ -196,12 +260,20 @@ def main():
                 "device_ms_per_step_rank0": round(dev_ms, 3),
                 "pipeline_GBps_rank0": round(nbytes / (ms_per_step / 1000.0) / 1e9, 1),
                 "phase_ms_last_step_rank0": phases,
-                "scan_stats_last_step_rank0": eng.scan_stats(),
+                "scan_stats_last_step_rank0": stats,
+                "state_tables_rank0": state_stats,
                 "parallelism": ("dp%d: chunk-sharded match, IP-hash-sharded rate-limit state, RCCL all-to-all of "
                                 "event records" % world) if world > 1 else "dp1",
             },
             "roofline": roofline(achieved, match_ms, nbytes, args),
         }
+        mp_ms = phases["count"] + phases["scan"] + phases["resolve"]
+        line["roofline"]["match_pass"] = {
+            "kernels": "k_nl_count_wt + k_scan + k_lines + DFA-job sort + k_dfa / k_nfa (phases count+scan+resolve)",
+            "ms": round(mp_ms, 3), "achieved": round(nbytes / (mp_ms / 1000.0) / 1e9, 1),
+            "frac": round(nbytes / (mp_ms / 1000.0) / 1e9 / HBM_PEAK_GBS, 4)}
+        if dec:
+            line["with_decision_emission"] = dec
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(w, args.cpu_sample)
         print(json.dumps(line), flush=True)

@@ -213,6 +213,22 @@ int bjx_state_get(bjx_engine *e, const char *ip, size_t ip_len, const char *name
                   int64_t *num_hits, int64_t *interval_start_ns);
 /* RegexRateLimitStates.Len(): number of distinct IPs with state. */
 int64_t bjx_state_len(bjx_engine *e);
+/* Occupancy of the persistent rate-limit state in HBM.  The reference never
+   evicts state (rate_limit.go:45-67) and neither does the engine: the tables
+   grow (rehashed on the device, 3/4 load factor) until a batch's growth
+   cannot be allocated, which returns BJX_ERR_CAPACITY; device_bytes lets the
+   host watch that coming (metrics, alongside Len(): config.go:165). */
+typedef struct bjx_state_stats {
+  uint64_t ips;            /* distinct IP strings (RegexRateLimitStates.Len) */
+  uint64_t ip_slots;       /* IP table capacity */
+  uint64_t states;         /* (ip, rule name) states */
+  uint64_t state_slots;    /* state table capacity */
+  uint64_t arena_bytes;    /* IP string bytes stored */
+  uint64_t arena_capacity;
+  uint64_t device_bytes;   /* HBM held by the state tables and the arena */
+  uint64_t rehashes;       /* table growths so far */
+} bjx_state_stats;
+int bjx_state_stats_get(bjx_engine *e, bjx_state_stats *out);
 /* Drop every rate-limit state (a fresh RegexRateLimitStates). */
 int bjx_state_clear(bjx_engine *e);
 /* RegexRateLimitStates.String(): "ip:\n\trule:\n\t\t{hits start}\n" blocks, IPs in

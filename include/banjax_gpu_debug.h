@@ -24,8 +24,9 @@ size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t rule_idx, char *out,
 size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap);
 /* last batch: gram bitset hits, recorded literal hits, lines sent to the per-line
    fallback, lines decided by the long-line pass, DFA jobs; then the state
-   tables: IP slots, IPs, state slots, states; then gram table hits (returns
-   the count, 10) */
+   tables: IP slots, IPs, state slots, states; then gram table hits, lines
+   the per-line kernel took from the scan-header path, rate-limit runs that
+   crossed a k_apply chunk (k_long_runs) (returns the count, 12) */
 size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap);
 /* Test hook: IP hashes become (hash & mask) | 1 (0 = off), so distinct IPs
    share 64-bit hashes and the exact collision path of the IP table runs. */

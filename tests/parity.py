@@ -55,7 +55,8 @@ class Pair:
         assert self.engine.state_len() == len(self.ost), (self.engine.state_len(), len(self.ost))
         for ip in ips or []:
             for n in names:
-                assert self.engine.state_get(ip, n) == self.ost.get(ip, n), (ip, n)
+                g, o = self.engine.state_get(ip, n), self.ost.get(ip, n)
+                assert g == o, (ip, n, g, o)
         dl = self.lim.banner.decision_lists.expiring
         assert len(dl) == self.ost.decisions_len()
         for ip, d in dl.items():
