@@ -8,14 +8,14 @@ Banner / DynamicDecisionLists).
 """
 from .config import (ALLOW, CHALLENGE, IPTABLES_BLOCK, NGINX_BLOCK, Config, ConfigError, RegexWithRate, Ruleset,
                      decision_string, parse_decision)
-from .engine import BatchOutput, Engine
+from .engine import BatchOutput, Engine, Node
 from .regex_rate_limiter import (Banner, ConsumeLineResult, DynamicDecisionLists, MockBanner, RateLimitResult,
                                  RegexRateLimiter, RegexRateLimitStates, RuleResult, Zone, consume_line)
 from .tailer import LogTailer, TailBatch, TailStopped, run_log_tailer
 
 __all__ = [
     "ALLOW", "CHALLENGE", "NGINX_BLOCK", "IPTABLES_BLOCK", "Config", "ConfigError", "RegexWithRate", "Ruleset",
-    "decision_string", "parse_decision", "Engine", "BatchOutput", "Banner", "MockBanner", "DynamicDecisionLists",
+    "decision_string", "parse_decision", "Engine", "Node", "BatchOutput", "Banner", "MockBanner", "DynamicDecisionLists",
     "ConsumeLineResult", "RuleResult", "RateLimitResult", "RegexRateLimiter", "RegexRateLimitStates", "consume_line", "Zone",
     "LogTailer", "TailBatch", "TailStopped", "run_log_tailer",
 ]

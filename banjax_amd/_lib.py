@@ -83,7 +83,7 @@ class IpDecision(C.Structure):
 class BanBatch(C.Structure):
     _fields_ = [("n_ips", C.c_uint64), ("ips", C.POINTER(IpDecision)), ("n_trips", C.c_uint64),
                 ("log", C.c_void_p), ("log_bytes", C.c_uint64), ("log_off", C.POINTER(C.c_uint64)),
-                ("log_kind", C.POINTER(C.c_uint8))]
+                ("log_kind", C.POINTER(C.c_uint8)), ("ip_bytes", C.c_void_p), ("ip_off", C.POINTER(C.c_uint64))]
 
 
 class TailerOptions(C.Structure):
@@ -104,6 +104,10 @@ EXPORTS = [
     "bjx_engine_last_error", "bjx_match_batch", "bjx_events_partition", "bjx_events_pack", "bjx_apply_events",
     "bjx_finish_batch", "bjx_tailer_open", "bjx_tailer_next", "bjx_tailer_release", "bjx_tailer_stats",
     "bjx_tailer_close", "bjx_engine_set_ban_options", "bjx_batch_bans", "bjx_state_stats_get",
+    "bjx_node_create", "bjx_node_destroy", "bjx_node_size", "bjx_node_engine", "bjx_node_last_error", "bjx_node_set_decision_lists",
+    "bjx_node_set_ban_options", "bjx_node_process_batch", "bjx_node_process_chunks", "bjx_node_batch_bans",
+    "bjx_node_state_get", "bjx_node_state_len", "bjx_node_state_dump", "bjx_node_state_stats_get",
+    "bjx_node_state_clear",
 ]
 
 
@@ -201,6 +205,36 @@ def lib():
     L.bjx_batch_bans.argtypes = [vp, C.POINTER(BanBatch)]
     L.bjx_engine_last_error.restype = C.c_char_p
     L.bjx_engine_last_error.argtypes = [vp]
+    L.bjx_node_create.restype = C.c_int
+    L.bjx_node_create.argtypes = [C.POINTER(C.c_int), sz, C.POINTER(EngineOptions), C.POINTER(vp), C.c_char_p, sz]
+    L.bjx_node_destroy.argtypes = [vp]
+    L.bjx_node_size.restype = sz
+    L.bjx_node_size.argtypes = [vp]
+    L.bjx_node_engine.restype = vp
+    L.bjx_node_engine.argtypes = [vp, sz]
+    L.bjx_node_last_error.restype = C.c_char_p
+    L.bjx_node_last_error.argtypes = [vp]
+    L.bjx_node_set_decision_lists.restype = C.c_int
+    L.bjx_node_set_decision_lists.argtypes = [vp, C.POINTER(DecisionEntry), sz]
+    L.bjx_node_set_ban_options.restype = C.c_int
+    L.bjx_node_set_ban_options.argtypes = [vp, C.POINTER(BanOptions)]
+    L.bjx_node_process_batch.restype = C.c_int
+    L.bjx_node_process_batch.argtypes = [vp, vp, vp, sz, C.c_int64, C.c_uint32, C.POINTER(BatchResult)]
+    L.bjx_node_process_chunks.restype = C.c_int
+    L.bjx_node_process_chunks.argtypes = [vp, vp, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_int64, C.c_uint32,
+                                          C.POINTER(BatchResult)]
+    L.bjx_node_batch_bans.restype = C.c_int
+    L.bjx_node_batch_bans.argtypes = [vp, C.POINTER(BanBatch)]
+    L.bjx_node_state_get.restype = C.c_int
+    L.bjx_node_state_get.argtypes = [vp, C.c_char_p, sz, C.c_char_p, sz, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    L.bjx_node_state_len.restype = C.c_int64
+    L.bjx_node_state_len.argtypes = [vp]
+    L.bjx_node_state_dump.restype = sz
+    L.bjx_node_state_dump.argtypes = [vp, C.c_char_p, sz]
+    L.bjx_node_state_stats_get.restype = C.c_int
+    L.bjx_node_state_stats_get.argtypes = [vp, C.c_void_p]
+    L.bjx_node_state_clear.restype = C.c_int
+    L.bjx_node_state_clear.argtypes = [vp]
     _lib = L
     return L
 

@@ -17,7 +17,7 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "--offlo
           "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result"]
 
 TARGETS = {
-    "libbanjax_gpu.so": ["engine.hip", "regex_compiler.cpp", "tailer.cpp"],
+    "libbanjax_gpu.so": ["engine.hip", "regex_compiler.cpp", "tailer.cpp", "node.cpp"],
 }
 
 

@@ -2936,12 +2936,15 @@ struct bjx_engine {
   DevBuf<unsigned long long> bn_best;
   DevBuf<uint8_t> bn_kind, bn_flag, bn_log;
   DevBuf<bjx_ip_decision> bn_rep, bn_sel;
+  DevBuf<uint8_t> bn_ipb;
   bool ban_emitted = false;
   uint64_t ban_n_trips = 0;
   HostBuf<bjx_ip_decision> ban_ips;
   HostBuf<char> ban_log;
   HostBuf<uint64_t> ban_off;
   HostBuf<uint8_t> ban_kind;
+  HostBuf<uint8_t> ban_ipb;
+  HostBuf<uint64_t> ban_ipo;
 
   // host copies of the last batch
   HostBuf<bjx_trip> trips;
@@ -3862,9 +3865,11 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
                   &e->dl_off, &e->dl_len, &e->nm_off})
     b->release();
   for (auto *b : {&e->bn_kind, &e->bn_flag, &e->bn_log, &e->dl_bytes, &e->nm_json}) b->release();
-  e->bn_best.release(); e->bn_rep.release(); e->bn_sel.release(); e->tz_at.release(); e->tz_off.release();
+  e->bn_best.release(); e->bn_rep.release(); e->bn_sel.release(); e->bn_ipb.release(); e->tz_at.release(); e->tz_off.release();
   e->rb_first.release(); e->rb_last.release(); e->long_heads.release(); e->long_count.release();
   e->d_results.release(); e->q_out.release();
+  e->ban_ips.release(); e->ban_log.release(); e->ban_off.release(); e->ban_kind.release(); e->ban_ipb.release();
+  e->ban_ipo.release();
   e->long_list.release(); e->l_ip16.release(); e->jline.release(); e->jkey.release(); e->jline2.release(); e->jkey2.release(); e->l_cand.release(); e->l_ccnt.release();
   (void)hipEventDestroy(e->ev0); (void)hipEventDestroy(e->ev1); (void)hipEventDestroy(e->evm0); (void)hipEventDestroy(e->evm1);
   for (auto &x : e->ph) (void)hipEventDestroy(x);
@@ -4332,6 +4337,23 @@ static void ensure_name_json(bjx_engine *e) {
 
 // decision updates (one per tripped IP) and LogRegexBan lines of the batch's
 // n trips (e->d_trips), copied to pinned host buffers (bans.h)
+// IP bytes of each selected record (bjx_ban_batch.ip_bytes): the Update key
+// for a host that handed device input, and the node's merge key
+__global__ void k_ban_iplen(BanDev A, uint64_t n_ips, const bjx_ip_decision *__restrict__ sel, uint64_t *__restrict__ len) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i <= n_ips) len[i] = i < n_ips ? A.trips[sel[i].trip_idx].ip_len : 0;
+}
+
+__global__ void k_ban_ipcopy(BanDev A, uint64_t n_ips, const bjx_ip_decision *__restrict__ sel,
+                             const uint64_t *__restrict__ off, uint8_t *__restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_ips) return;
+  const uint64_t t = sel[i].trip_idx;
+  const uint8_t *src = trip_ip(A, t);
+  uint8_t *dst = out + off[i];
+  for (uint32_t k = 0, n = A.trips[t].ip_len; k < n; ++k) dst[k] = src[k];
+}
+
 static void emit_bans(bjx_engine *e, uint64_t n) {
   hipStream_t st = e->stream;
   ensure_name_json(e);
@@ -4406,7 +4428,24 @@ static void emit_bans(bjx_engine *e, uint64_t n) {
   HIP_OK(hipMemcpyAsync(&n_ips, e->scalars.p + 5, 8, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
   e->ban_ips.resize(n_ips);
-  if (n_ips) HIP_OK(hipMemcpyAsync(e->ban_ips.data(), e->bn_sel.p, n_ips * sizeof(bjx_ip_decision), hipMemcpyDeviceToHost, st));
+  e->ban_ipo.resize(n_ips + 1);
+  e->ban_ipo.data()[0] = 0;
+  e->ban_ipb.resize(0);
+  if (n_ips) {
+    HIP_OK(hipMemcpyAsync(e->ban_ips.data(), e->bn_sel.p, n_ips * sizeof(bjx_ip_decision), hipMemcpyDeviceToHost, st));
+    uint64_t *len = e->bn_len.p, *off = e->bn_off.p;  // the log offsets are on the host already
+    hipLaunchKernelGGL(k_ban_iplen, dim3(grid_for(n_ips + 1)), dim3(kBlock), 0, st, A, (uint64_t)n_ips, e->bn_sel.p, len);
+    cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, len, off, (int)(n_ips + 1), st); });
+    HIP_OK(hipMemcpyAsync(e->ban_ipo.data(), off, (n_ips + 1) * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    const uint64_t nb = e->ban_ipo.data()[n_ips];
+    e->bn_ipb.ensure(nb + 16);
+    hipLaunchKernelGGL(k_ban_ipcopy, dim3(grid_for(n_ips)), dim3(kBlock), 0, st, A, (uint64_t)n_ips, e->bn_sel.p, off,
+                       e->bn_ipb.p);
+    HIP_OK(hipGetLastError());
+    e->ban_ipb.resize(nb);
+    if (nb) HIP_OK(hipMemcpyAsync(e->ban_ipb.data(), e->bn_ipb.p, nb, hipMemcpyDeviceToHost, st));
+  }
   e->ban_n_trips = n;
 }
 
@@ -4422,6 +4461,7 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
   e->ban_emitted = (flags & BJX_EMIT_BANS) != 0;
   e->ban_n_trips = 0;
   e->ban_ips.resize(0); e->ban_log.resize(0); e->ban_off.resize(1); e->ban_off.data()[0] = 0; e->ban_kind.resize(0);
+  e->ban_ipb.resize(0); e->ban_ipo.resize(1); e->ban_ipo.data()[0] = 0;
   if (n_ev) {
     mark(e, 7);
     // trips: Exceeded outcomes.  sorted: outcomes in state-slot order (this
@@ -4762,6 +4802,8 @@ extern "C" int bjx_batch_bans(bjx_engine *e, bjx_ban_batch *out) {
     out->log = out->log_bytes ? e->ban_log.data() : nullptr;
     out->log_off = e->ban_off.data();
     out->log_kind = e->ban_n_trips ? e->ban_kind.data() : nullptr;
+    out->ip_bytes = e->ban_ipb.size() ? e->ban_ipb.data() : nullptr;
+    out->ip_off = e->ban_ipo.data();
     return BJX_OK;
   });
 }

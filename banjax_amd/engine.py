@@ -3,7 +3,7 @@ batch pipeline of include/banjax_gpu.h."""
 from __future__ import annotations
 
 import ctypes as C
-from typing import Iterable, List, Optional, Tuple
+from typing import Iterable, List, Optional, Sequence, Tuple
 
 from . import _lib
 from .config import Config, Ruleset
@@ -69,6 +69,13 @@ class BanBatch:
         n = bb.n_trips
         self.log_off = np.ctypeslib.as_array(bb.log_off, shape=(n + 1,)).copy() if n else np.zeros(1, np.uint64)
         self.log_kind = np.ctypeslib.as_array(bb.log_kind, shape=(n,)).copy() if n else np.zeros(0, np.uint8)
+        m = bb.n_ips
+        self.ip_off = np.ctypeslib.as_array(bb.ip_off, shape=(m + 1,)).copy() if m else np.zeros(1, np.uint64)
+        self.ip_bytes = C.string_at(bb.ip_bytes, int(self.ip_off[m])) if m and self.ip_off[m] else b""
+
+    def ip(self, r: int) -> bytes:
+        """IP bytes of record r (the Update key)."""
+        return self.ip_bytes[int(self.ip_off[r]):int(self.ip_off[r + 1])]
 
     def lines(self):
         """(kind, line without '\\n') per trip that logs (kind 1 Logger, 2 LoggerTemp)."""
@@ -78,6 +85,33 @@ class BanBatch:
             if k:
                 out.append((k, self.log[int(self.log_off[t]):int(self.log_off[t + 1]) - 1]))
         return out
+
+
+def _decision_entries(entries):
+    entries = list(entries)
+    arr = (_lib.DecisionEntry * max(1, len(entries)))()
+    keep = []
+    for i, (site, dec, ip) in enumerate(entries):
+        s = _lib.Str(None, 0) if site is None else _lib.mkstr(site)
+        ipb = _lib.mkstr(ip)
+        keep.append((s, ipb))
+        arr[i] = _lib.DecisionEntry(s, dec, ipb)
+    return arr, len(entries), keep
+
+
+def _ban_options(expiring_ttl_s, disable_logging, tz_offset_s, zone):
+    hosts = [h for h in disable_logging]
+    arr = (_lib.Str * max(1, len(hosts)))()
+    strs = [_lib.mkstr(h) for h in hosts]
+    for i, x in enumerate(strs):
+        arr[i] = x
+    ttl = (int(expiring_ttl_s) * 1_000_000_000) & ((1 << 64) - 1)
+    if ttl >= 1 << 63:
+        ttl -= 1 << 64
+    trans = zone.transitions if zone is not None else []
+    off = zone.offset_s if zone is not None else tz_offset_s
+    tz = (_lib.TzTransition * max(1, len(trans)))(*[_lib.TzTransition(a, o, 0) for a, o in trans])
+    return _lib.BanOptions(ttl, off, 0, arr, len(hosts), tz, len(trans)), (arr, tz, strs)
 
 
 class Engine:
@@ -100,34 +134,15 @@ class Engine:
 
     def set_decision_lists(self, entries: Iterable[Tuple[Optional[str], int, str]]):
         """StaticDecisionLists from config (decision.go:278-374)."""
-        entries = list(entries)
-        arr = (_lib.DecisionEntry * max(1, len(entries)))()
-        keep = []
-        for i, (site, dec, ip) in enumerate(entries):
-            s = _lib.Str(None, 0) if site is None else _lib.mkstr(site)
-            ipb = _lib.mkstr(ip)
-            keep.append((s, ipb))
-            arr[i] = _lib.DecisionEntry(s, dec, ipb)
-        self._check(_lib.lib().bjx_engine_set_decision_lists(self._h, arr, len(entries)), "set_decision_lists")
+        arr, n, keep = _decision_entries(entries)
+        self._check(_lib.lib().bjx_engine_set_decision_lists(self._h, arr, n), "set_decision_lists")
 
     def set_ban_options(self, expiring_ttl_s: int, disable_logging: Iterable[str] = (), tz_offset_s: int = 0,
                         zone=None):
         """Banner settings of the device decision emission (bjx_engine_set_ban_options);
         zone: a regex_rate_limiter.Zone (local-zone transitions), else the fixed
         offset tz_offset_s."""
-        hosts = [h for h in disable_logging]
-        arr = (_lib.Str * max(1, len(hosts)))()
-        keep = []
-        for i, h in enumerate(hosts):
-            arr[i] = _lib.mkstr(h)
-            keep.append(arr[i])
-        ttl = (int(expiring_ttl_s) * 1_000_000_000) & ((1 << 64) - 1)
-        if ttl >= 1 << 63:
-            ttl -= 1 << 64
-        trans = zone.transitions if zone is not None else []
-        off = zone.offset_s if zone is not None else tz_offset_s
-        tz = (_lib.TzTransition * max(1, len(trans)))(*[_lib.TzTransition(a, o, 0) for a, o in trans])
-        o = _lib.BanOptions(ttl, off, 0, arr, len(hosts), tz, len(trans))
+        o, keep = _ban_options(expiring_ttl_s, disable_logging, tz_offset_s, zone)
         self._check(_lib.lib().bjx_engine_set_ban_options(self._h, C.byref(o)), "set_ban_options")
 
     def bans(self) -> BanBatch:
@@ -238,6 +253,117 @@ class Engine:
         h = getattr(self, "_h", None)
         if h and _lib._lib is not None:
             _lib._lib.bjx_engine_destroy(h)
+        self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+class _NodeEngine(Engine):
+    """A node's engine: closing it is the node's business."""
+
+    def close(self):
+        self._h = None
+
+
+class Node:
+    """The GPUs of one host behind one handle (bjx_node_*): one
+    engine per entry of `devices` (repeats allowed), matching sharded by chunk,
+    RegexRateLimitStates sharded by IP, the exchange done inside the library.
+    Results are in global (reference) order, as one Engine returns them."""
+
+    def __init__(self, devices: Sequence[int], ip_capacity: int = 0, state_capacity: int = 0, ip_arena_bytes: int = 0):
+        L = _lib.lib()
+        h = C.c_void_p()
+        err = C.create_string_buffer(512)
+        devs = (C.c_int * len(devices))(*devices)
+        opts = _lib.EngineOptions(ip_capacity, state_capacity, ip_arena_bytes)
+        rc = L.bjx_node_create(devs, len(devices), C.byref(opts), C.byref(h), err, 512)
+        if rc != _lib.OK:
+            raise _lib.BanjaxGpuError(rc, "bjx_node_create: " + err.value.decode(errors="replace"))
+        self._h = h
+        self.devices = list(devices)
+
+    def __len__(self):
+        return len(self.devices)
+
+    def engine(self, k: int) -> "Engine":
+        """Engine k (stats and debug hooks); owned by the node."""
+        h = _lib.lib().bjx_node_engine(self._h, k)
+        if not h:
+            raise IndexError(k)
+        e = Engine.__new__(_NodeEngine)
+        e._h, e.device, e._node = C.c_void_p(h), self.devices[k], self
+        return e
+
+    def _check(self, rc, what):
+        if rc < 0:
+            msg = _lib.lib().bjx_node_last_error(self._h)
+            raise _lib.BanjaxGpuError(rc, "%s: %s" % (what, (msg or b"").decode(errors="replace")))
+        return rc
+
+    def set_decision_lists(self, entries: Iterable[Tuple[Optional[str], int, str]]):
+        arr, n, keep = _decision_entries(entries)
+        self._check(_lib.lib().bjx_node_set_decision_lists(self._h, arr, n), "node_set_decision_lists")
+
+    def set_ban_options(self, expiring_ttl_s: int, disable_logging: Iterable[str] = (), tz_offset_s: int = 0,
+                        zone=None):
+        o, keep = _ban_options(expiring_ttl_s, disable_logging, tz_offset_s, zone)
+        self._check(_lib.lib().bjx_node_set_ban_options(self._h, C.byref(o)), "node_set_ban_options")
+
+    def process(self, rs: Ruleset, data, now_ns: int, copy_results: bool = False, emit_bans: bool = False) -> BatchOutput:
+        """consumeLine over the complete lines of a host buffer, split over the engines."""
+        res = _lib.BatchResult()
+        flags = (_lib.COPY_RESULTS if copy_results else 0) | (_lib.EMIT_BANS if emit_bans else 0)
+        buf = _lib.b(data)
+        self._check(_lib.lib().bjx_node_process_batch(self._h, rs.handle, C.c_char_p(buf), len(buf), now_ns, flags,
+                                                      C.byref(res)), "node_process_batch")
+        return BatchOutput(res, copy_results)
+
+    def process_chunks(self, rs: Ruleset, chunks: Sequence[Tuple[int, int]], now_ns: int, copy_results: bool = False,
+                       emit_bans: bool = False) -> BatchOutput:
+        """chunks[k] = (device pointer on engine k's GPU, bytes); all but the last end in '\\n'."""
+        res = _lib.BatchResult()
+        flags = (_lib.COPY_RESULTS if copy_results else 0) | (_lib.EMIT_BANS if emit_bans else 0) | _lib.INPUT_DEVICE
+        ptrs = (C.c_void_p * len(chunks))(*[p for p, _ in chunks])
+        lens = (C.c_size_t * len(chunks))(*[n for _, n in chunks])
+        self._check(_lib.lib().bjx_node_process_chunks(self._h, rs.handle, ptrs, lens, now_ns, flags, C.byref(res)),
+                    "node_process_chunks")
+        return BatchOutput(res, copy_results)
+
+    def bans(self) -> BanBatch:
+        bb = _lib.BanBatch()
+        self._check(_lib.lib().bjx_node_batch_bans(self._h, C.byref(bb)), "node_batch_bans")
+        return BanBatch(bb)
+
+    def state_get(self, ip, name):
+        hits, start = C.c_int64(), C.c_int64()
+        ipb, nb = _lib.b(ip), _lib.b(name)
+        rc = self._check(_lib.lib().bjx_node_state_get(self._h, ipb, len(ipb), nb, len(nb), C.byref(hits),
+                                                       C.byref(start)), "node_state_get")
+        return (hits.value, start.value) if rc == 1 else None
+
+    def state_len(self) -> int:
+        return self._check(_lib.lib().bjx_node_state_len(self._h), "node_state_len")
+
+    def state_stats(self):
+        st = _lib.StateStats()
+        self._check(_lib.lib().bjx_node_state_stats_get(self._h, C.byref(st)), "node_state_stats")
+        return {k: getattr(st, k) for k, _ in _lib.StateStats._fields_}
+
+    def state_clear(self):
+        self._check(_lib.lib().bjx_node_state_clear(self._h), "node_state_clear")
+
+    def state_dump(self) -> str:
+        n = _lib.lib().bjx_node_state_dump(self._h, None, 0)
+        buf = C.create_string_buffer(n + 1)
+        _lib.lib().bjx_node_state_dump(self._h, buf, n)
+        return buf.raw[:n].decode(errors="replace")
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h and _lib._lib is not None:
+            _lib._lib.bjx_node_destroy(h)
         self._h = None
 
     def __del__(self):

@@ -137,6 +137,13 @@ def main():
                          "(BJX_EMIT_BANS, copied to pinned host memory); 0: trip list only")
     ap.add_argument("--bans-steps", type=int, default=3,
                     help="after the timed region, steps timed again with decision emission on (reported next to value)")
+    ap.add_argument("--node-engines", type=int, default=0,
+                    help="single process: one bjx_node of this many engines over the visible GPUs (round-robin), "
+                         "e.g. to rehearse the N>1 node path on one GPU")
+    ap.add_argument("--exchange", choices=("node", "rccl"), default="node",
+                    help="N>1: node = rank 0 drives every local GPU through one bjx_node (the library moves the event "
+                         "records over xGMI; the Go host's one-process shape), the other ranks only join the barriers; "
+                         "rccl = every rank drives its own engine and the records move by torch.distributed all-to-all")
     args = ap.parse_args()
 
     import torch
@@ -155,9 +162,23 @@ def main():
     w0 = W.ALL[args.config]
     n_lines = args.lines or w0.n_lines
     w = W.scaled(w0, n_lines, n_ips=w0.n_ips) if args.lines else w0
-    # weak scaling: rank r owns lines [r*n, (r+1)*n) of the workload's stream
+    node_mode = (world > 1 and args.exchange == "node") or args.node_engines > 1
+    drives = not node_mode or rank == 0  # node mode: rank 0 drives every GPU
+    n_parts = world if world > 1 else max(1, args.node_engines)
+    devices = [k % torch.cuda.device_count() for k in range(n_parts)]
+    # weak scaling: GPU r holds lines [r*n, (r+1)*n) of the workload's stream
     first = rank * n_lines
-    data, nbytes = w.device_lines(local, first, n_lines)
+    chunks, keep = [], []
+    if node_mode and drives:
+        for k in range(n_parts):
+            with torch.cuda.device(devices[k]):
+                t, nb = w.device_lines(devices[k], k * n_lines, n_lines)
+                torch.cuda.synchronize()
+            keep.append(t)
+            chunks.append((t.data_ptr(), nb))
+        data, nbytes = keep[0], chunks[0][1]
+    else:
+        data, nbytes = w.device_lines(local, first, n_lines)
     torch.cuda.synchronize()
     cfg = Config.from_yaml(w.rules_yaml)
     from banjax_amd import _lib
@@ -165,30 +186,50 @@ def main():
     tc = time.perf_counter()
     rs = Ruleset(cfg)  # cold: first compile of these patterns in this process (reload = cached patterns only)
     compile_ms = (time.perf_counter() - tc) * 1000.0
-    eng = Engine(local, ip_arena_bytes=256 << 20)  # IP / state tables size themselves to the stream
-    eng.set_decision_lists(cfg.decision_entries)
-    eng.set_ban_options(cfg.expiring_decision_ttl_seconds, [h for h, v in cfg.disable_logging.items() if v])
-    now = w.now_ns(first, n_lines)
+    node = None
+    disable = [h for h, v in cfg.disable_logging.items() if v]
+    if node_mode:
+        if drives:
+            from banjax_amd import Node
+            node = Node(devices, ip_arena_bytes=256 << 20)
+            node.set_decision_lists(cfg.decision_entries)
+            node.set_ban_options(cfg.expiring_decision_ttl_seconds, disable)
+            eng = node.engine(0)
+        now = w.now_ns(0, n_lines * n_parts)
+    else:
+        eng = Engine(local, ip_arena_bytes=256 << 20)  # IP / state tables size themselves to the stream
+        eng.set_decision_lists(cfg.decision_entries)
+        eng.set_ban_options(cfg.expiring_decision_ttl_seconds, disable)
+        now = w.now_ns(first, n_lines)
     bans = bool(args.bans)
 
     ex = None
-    if world > 1:
+    if world > 1 and not node_mode:
         from banjax_amd.distributed import TorchExchange, sharded_batch
         ex = TorchExchange(torch.device("cuda", local))
 
     def step():
+        if node_mode:
+            return node.process_chunks(rs, chunks, now, emit_bans=bans) if drives else None
         if ex is None:
             return eng.process(rs, None, now, device_ptr=data.data_ptr(), nbytes=nbytes, emit_bans=bans)
         return sharded_batch(eng, rs, now, data.data_ptr(), nbytes, ex, emit_bans=bans)
+
+    def sync_all():
+        if node_mode and drives:
+            for d in sorted(set(devices)):
+                torch.cuda.synchronize(d)
+        else:
+            torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         step()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync_all()
     t0 = time.perf_counter()
     outs = [step() for _ in range(args.steps)]
-    torch.cuda.synchronize()
+    sync_all()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -197,12 +238,21 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1000.0 / args.steps
+    if not drives:  # node mode, rank > 0: only the barriers and the max-over-ranks clock
+        if args.bans_steps > 0 and not bans:
+            dist.barrier()
+            dist.barrier()
+            t = torch.tensor([0.0], device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     match_ms = sum(o.match_kernel_ms for o in outs) / len(outs)
     dev_ms = sum(o.device_ms for o in outs) / len(outs)
     o = outs[-1]
     phases = eng.phase_ms()
     stats = eng.scan_stats()
-    state_stats = eng.state_stats()
+    state_stats = node.state_stats() if node else eng.state_stats()
     # the same step with the Banner's work on the device too: per-IP decision
     # updates and every LogRegexBan line, copied to pinned host memory
     dec = None
@@ -210,11 +260,11 @@ def main():
         bans = True
         if dist:
             dist.barrier()
-        torch.cuda.synchronize()
+        sync_all()
         t1 = time.perf_counter()
         for _ in range(args.bans_steps):
             step()
-        torch.cuda.synchronize()
+        sync_all()
         if dist:
             dist.barrier()
         el2 = time.perf_counter() - t1
@@ -223,11 +273,11 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el2 = float(t.item())
         bans = False
-        dec = {"value": round(n_lines * world / (el2 / args.bans_steps), 1), "unit": "lines/s",
+        dec = {"value": round(n_lines * n_parts / (el2 / args.bans_steps), 1), "unit": "lines/s",
                "ms_per_step": round(el2 * 1000.0 / args.bans_steps, 3), "steps": args.bans_steps,
                "what": "each step also builds the per-IP DynamicDecisionLists updates and all LogRegexBan JSON lines "
                        "on the device and copies them to pinned host memory (BJX_EMIT_BANS)"}
-    total_lines = n_lines * world
+    total_lines = n_lines * n_parts
     value = total_lines / (elapsed / args.steps)
     achieved = nbytes / (match_ms / 1000.0) / 1e9
     if rank == 0:
@@ -235,7 +285,8 @@ def main():
             "metric": METRIC,
             "value": round(value, 1),
             "unit": "lines/s",
-            "n_gpus": world,
+            "n_gpus": len(set(devices)),
+            "engines": n_parts,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
@@ -261,9 +312,11 @@ def main():
                 "pipeline_GBps_rank0": round(nbytes / (ms_per_step / 1000.0) / 1e9, 1),
                 "phase_ms_last_step_rank0": phases,
                 "scan_stats_last_step_rank0": stats,
-                "state_tables_rank0": state_stats,
-                "parallelism": ("dp%d: chunk-sharded match, IP-hash-sharded rate-limit state, RCCL all-to-all of "
-                                "event records" % world) if world > 1 else "dp1",
+                "state_tables": state_stats,
+                "parallelism": ("dp%d: chunk-sharded match, IP-hash-sharded rate-limit state, %s" % (
+                    n_parts, "one bjx_node (rank 0) of %d engines moving the event records between GPUs with "
+                    "hipMemcpyPeerAsync" % n_parts if node_mode else "RCCL all-to-all of the event records"))
+                if n_parts > 1 else "dp1",
             },
             "roofline": roofline(achieved, match_ms, nbytes, args),
         }
@@ -274,7 +327,7 @@ def main():
             "frac": round(nbytes / (mp_ms / 1000.0) / 1e9 / HBM_PEAK_GBS, 4)}
         if dec:
             line["with_decision_emission"] = dec
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and n_parts == 1:
             line["cpu_baseline"] = cpu_baseline(w, args.cpu_sample)
         print(json.dumps(line), flush=True)
     if dist:

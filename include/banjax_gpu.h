@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define BJX_ABI_VERSION 2
+#define BJX_ABI_VERSION 3
 
 enum bjx_status {
   BJX_OK = 0,
@@ -331,9 +331,54 @@ typedef struct bjx_ban_batch {
   uint64_t log_bytes;
   const uint64_t *log_off;      /* host, n_trips + 1: trip t's line is log[log_off[t], log_off[t+1]) (empty: < 6 words) */
   const uint8_t *log_kind;      /* host, n_trips: 0 no line, 1 Logger, 2 LoggerTemp (disable_logging host) */
+  const uint8_t *ip_bytes;      /* host: record r's IP (the Update key) is ip_bytes[ip_off[r], ip_off[r+1]) */
+  const uint64_t *ip_off;       /* host, n_ips + 1 */
 } bjx_ban_batch;
 /* The last batch's emission (valid until the next batch; needs BJX_EMIT_BANS). */
 int bjx_batch_bans(bjx_engine *e, bjx_ban_batch *out);
+
+/* ---- Node: the GPUs of one host behind one handle.  The Go
+   host keeps ONE RegexRateLimitStates (rate_limit.go:19-28, created once in
+   banjax.go:80) fed by ONE consumer goroutine (regex_rate_limiter.go:54-77);
+   a node keeps that shape over n_devices engines.  Engine k matches the k-th
+   contiguous chunk of the batch, the rate-limit state is sharded by IP (owner
+   (ip_hash >> 32) % n_devices), and the library moves the event records to
+   their owners and the outcome bytes back itself (device-to-device copies over
+   xGMI, no caller collective).  Results come back in the reference's global
+   order, exactly as one engine over the whole batch returns them. */
+typedef struct bjx_node bjx_node;
+/* devices: HIP device index of each engine (repeats allowed: engines sharing a GPU). */
+int bjx_node_create(const int *devices, size_t n_devices, const bjx_engine_options *opts, bjx_node **out, char *err,
+                    size_t err_len);
+void bjx_node_destroy(bjx_node *n);
+size_t bjx_node_size(const bjx_node *n);
+/* Engine k of the node (its own stats and debug hooks); owned by the node. */
+bjx_engine *bjx_node_engine(bjx_node *n, size_t k);
+const char *bjx_node_last_error(bjx_node *n);
+/* bjx_engine_set_decision_lists / bjx_engine_set_ban_options on every engine. */
+int bjx_node_set_decision_lists(bjx_node *n, const bjx_decision_entry *entries, size_t count);
+int bjx_node_set_ban_options(bjx_node *n, const bjx_ban_options *opts);
+/* consumeLine over the complete lines of a host buffer: split at '\n' into
+   n_devices chunks of about equal size.  line_offset / line_idx in the result
+   are relative to bytes, as bjx_process_batch's. */
+int bjx_node_process_batch(bjx_node *n, const bjx_ruleset *rs, const uint8_t *bytes, size_t len, int64_t now_ns,
+                           uint32_t flags, bjx_batch_result *out);
+/* Same over chunks already resident in HBM: chunks[k] is a device pointer on
+   engine k's GPU (flags must include BJX_INPUT_DEVICE) and every chunk but the
+   last ends in '\n'.  Offsets are relative to the chunks' concatenation. */
+int bjx_node_process_chunks(bjx_node *n, const bjx_ruleset *rs, const uint8_t *const *chunks, const size_t *lens,
+                            int64_t now_ns, uint32_t flags, bjx_batch_result *out);
+/* The last node batch's decision emission (BJX_EMIT_BANS), merged over the
+   engines: one record per IP (highest decision, its first trip), trip_idx
+   into the node batch's trips; log lines in node trip order. */
+int bjx_node_batch_bans(bjx_node *n, bjx_ban_batch *out);
+/* RegexRateLimitStates.Get / Len / String / occupancy over every shard. */
+int bjx_node_state_get(bjx_node *n, const char *ip, size_t ip_len, const char *name, size_t name_len, int64_t *num_hits,
+                       int64_t *interval_start_ns);
+int64_t bjx_node_state_len(bjx_node *n);
+size_t bjx_node_state_dump(bjx_node *n, char *out, size_t cap);
+int bjx_node_state_stats_get(bjx_node *n, bjx_state_stats *out);
+int bjx_node_state_clear(bjx_node *n);
 
 int bjx_abi_version(void);
 

@@ -1,0 +1,128 @@
+"""bjx_node_*: several engines behind one handle, the exchange inside the library.
+
+The engines share GPU 0 here (the box has one GPU; the library takes the
+same-device copy path instead of hipMemcpyPeerAsync).  Every batch is checked
+bit-exact against one oracle over the whole stream: per-line flags, the
+RuleResults and trips in reference order, the merged decision records and
+ban-log lines, and the RegexRateLimitStates spread over the shards.
+"""
+import pytest
+
+import workloads as W
+from banjax_amd import Config, Node
+from banjax_amd.regex_rate_limiter import DynamicDecisionLists
+from oracle import oracle as O
+from tests.parity import oracle_config
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_batch(cfg, st, oc, data, now_ns, out, bans, dl, blog):
+    oflags, ores, _ = st.consume(oc, data, now_ns, cap=(data.count(b"\n") + 1) * (len(cfg.all_rules()) + 1))
+    exp = [[r.line_idx, r.rule_id, r.rule_pos, r.skip_host, r.seen_ip, r.match_type, r.exceeded] for r in ores]
+    assert out.n_lines == data.count(b"\n")
+    assert list(out.line_flags) == oflags
+    got = [[x.line_idx, x.rule_idx, x.rule_pos, x.skip_host, x.seen_ip, x.match_type, x.exceeded] for x in out.results]
+    assert got == exp
+    trips = out.trips
+    assert [(t.line_idx, t.rule_idx) for t in trips] == [(r[0], r[1]) for r in exp if r[6]]
+    for t in trips[:50]:  # offsets are relative to the whole batch
+        line = data[t.line_offset:t.line_offset + t.line_len]
+        assert data[t.line_offset + t.line_len:t.line_offset + t.line_len + 1] == b"\n"
+        assert line.split(b" ")[1] == line[t.ip_off:t.ip_off + t.ip_len]
+    # merged decision records: replay as the Banner does, in trip order
+    assert bans.n_trips == len(trips)
+    prev = -1
+    for r, rec in enumerate(bans.ips):
+        t = trips[int(rec["trip_idx"])]
+        assert int(rec["trip_idx"]) > prev
+        prev = int(rec["trip_idx"])
+        line = data[t.line_offset:t.line_offset + t.line_len]
+        assert bans.ip(r) == line[t.ip_off:t.ip_off + t.ip_len]
+        host = line[t.host_off:t.host_off + t.host_len]
+        dl.update(bans.ip(r).decode(), int(rec["expires_ns"]), int(rec["decision"]), False, host.decode())
+    blog += ["%d %s" % (kind - 1, line.decode()) for kind, line in bans.lines()]
+    return len(trips)
+
+
+@pytest.mark.parametrize("wl,n_engines,device_input", [
+    (("cfg3", 2000), 2, False),
+    (("cfg5", 3000), 3, True),
+    (("cfg1", 500), 4, False),
+    (("cfg3", 2000), 1, True),
+])
+def test_node_matches_one_oracle(wl, n_engines, device_input):
+    import torch
+
+    steps, per = 3, 12_000
+    w = W.scaled(W.ALL[wl[0]], steps * per, n_ips=wl[1])
+    cfg = Config.from_yaml(w.rules_yaml)
+    from banjax_amd import Ruleset
+    rs = Ruleset(cfg)
+    node = Node([0] * n_engines)
+    assert len(node) == n_engines
+    node.set_decision_lists(cfg.decision_entries)
+    node.set_ban_options(cfg.expiring_decision_ttl_seconds)
+    oc = oracle_config(cfg)
+    st = O.State()
+    dl, blog, n_trips = DynamicDecisionLists(), [], 0
+    keep = []
+    for s in range(steps):
+        data = w.host_lines(s * per, per)
+        now = w.now_ns(s * per, per)
+        if device_input:
+            # uneven chunks on line boundaries, each copied to "its" GPU
+            lines = data.split(b"\n")[:-1]
+            cuts = [0] + sorted({(len(lines) * (k + 1)) // (n_engines + 1) for k in range(n_engines - 1)}) + [len(lines)]
+            chunks = []
+            for a, b in zip(cuts, cuts[1:]):
+                blob = b"".join(ln + b"\n" for ln in lines[a:b])
+                t = torch.frombuffer(bytearray(blob or b"\0"), dtype=torch.uint8).to("cuda:0")
+                keep.append(t)
+                chunks.append((t.data_ptr(), len(blob)))
+            out = node.process_chunks(rs, chunks, now, copy_results=True, emit_bans=True)
+        else:
+            out = node.process(rs, data, now, copy_results=True, emit_bans=True)
+        assert out.consumed_bytes == len(data)
+        n_trips += _check_batch(cfg, st, oc, data, now, out, node.bans(), dl, blog)
+    assert n_trips > 0
+    assert len(dl.expiring) == st.decisions_len()
+    for ip, d in dl.expiring.items():
+        assert tuple(st.decision(ip)[:3]) == (d.decision, d.expires_ns, d.domain), ip
+    assert blog == [ln for ln in st.ban_log().split("\n") if ln]
+    # RegexRateLimitStates over the shards: Len, Get, String, occupancy
+    assert node.state_len() == len(st)
+    names = sorted(set(r.rule for r in cfg.all_rules()))
+    first = w.host_lines(0, per).split(b"\n")
+    for ln in first[:60]:
+        ip = ln.split(b" ")[1]
+        for nm in names:
+            assert node.state_get(ip, nm) == st.get(ip, nm), (ip, nm)
+    dump = node.state_dump()
+    assert sum(1 for ln in dump.split("\n") if ln and not ln.startswith("\t")) == len(st)
+    stats = node.state_stats()
+    assert stats["ips"] == len(st) and stats["states"] >= len(st)
+    node.state_clear()
+    assert node.state_len() == 0
+    node.close()
+
+
+def test_node_rejects_chunk_without_newline():
+    import torch
+
+    from banjax_amd import Ruleset
+    from banjax_amd._lib import BanjaxGpuError
+    w = W.scaled(W.CFG3, 1000, n_ips=100)
+    cfg = Config.from_yaml(w.rules_yaml)
+    rs = Ruleset(cfg)
+    node = Node([0, 0])
+    data = w.host_lines(0, 1000)
+    cut = data.index(b"\n", len(data) // 2) - 3  # mid-line
+    a = torch.frombuffer(bytearray(data[:cut]), dtype=torch.uint8).to("cuda:0")
+    b = torch.frombuffer(bytearray(data[cut:]), dtype=torch.uint8).to("cuda:0")
+    with pytest.raises(BanjaxGpuError):
+        node.process_chunks(rs, [(a.data_ptr(), cut), (b.data_ptr(), len(data) - cut)], w.now_ns(0, 1000))
+    # a host batch splits itself on line boundaries, a partial tail is carried
+    out = node.process(rs, data + b"1700000000.000 1.2.3.4 GET", w.now_ns(0, 1000))
+    assert out.consumed_bytes == len(data) and out.n_lines == 1000
+    node.close()
