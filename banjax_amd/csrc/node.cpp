@@ -25,11 +25,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <exception>
 #include <mutex>
 #include <string>
 #include <thread>
-#include <unordered_map>
 #include <vector>
 
 #include "../../include/banjax_gpu.h"
@@ -100,7 +100,7 @@ struct bjx_node {
   std::vector<bjx_ip_decision> ips;
   std::vector<uint8_t> ipb;
   std::vector<uint64_t> ipo;
-  std::string log;
+  std::vector<char> log;
   std::vector<uint64_t> log_off;
   std::vector<uint8_t> log_kind;
 };
@@ -168,35 +168,146 @@ void peer_copy(void *dst, const Part &D, const void *src, const Part &S, size_t 
     hip_ok(hipMemcpyPeerAsync(dst, D.dev, src, S.dev, bytes, D.copy), "hipMemcpyPeerAsync (exchange)");
 }
 
+// fn(i) for i in [0, count) over up to `threads` host threads
+template <typename F>
+void par_for(size_t count, size_t threads, F fn) {
+  threads = std::max<size_t>(1, std::min(threads, count));
+  if (threads == 1) {
+    for (size_t i = 0; i < count; ++i) fn(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> th;
+  th.reserve(threads);
+  for (size_t t = 0; t < threads; ++t)
+    th.emplace_back([&]() {
+      for (size_t i; (i = next.fetch_add(1)) < count;) fn(i);
+    });
+  for (auto &t : th) t.join();
+}
+
+size_t host_threads() {
+  const unsigned hc = std::thread::hardware_concurrency();
+  return std::max<size_t>(1, std::min<size_t>(16, hc ? hc : 1));
+}
+
+uint64_t ip_key(const uint8_t *p, size_t n) {  // FNV-1a, finalised
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (size_t i = 0; i < n; ++i) h = (h ^ p[i]) * 0x100000001b3ull;
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  return h ^ (h >> 33);
+}
+
 // Merge the engines' decision records (bjx_batch_bans, each in its own trip
 // order) into node trip order.  Engine k's trips precede engine k+1's, so per
 // IP the highest decision's first trip is the earliest (k, trip) reaching it
 // (the reference's Update sequence over global trip order,
 // regex_rate_limiter.go:254-263 into decision.go:404-433).
+// Host work, parallel: records are bucketed by a hash of their IP bytes, each
+// bucket merged with its own small table (engine order kept inside a bucket),
+// and the merged records put back in trip order by a radix sort.
 void merge_bans(bjx_node *n, const std::vector<uint64_t> &trip_base) {
-  n->ips.clear(); n->ipb.clear(); n->ipo.assign(1, 0); n->log.clear(); n->log_off.assign(1, 0); n->log_kind.clear();
-  n->ban_trips = 0;
-  struct Rec {
-    bjx_ip_decision d;
-    std::string ip;
-  };
-  std::vector<Rec> recs;
-  std::unordered_map<std::string, size_t> by_ip;
-  for (size_t k = 0; k < n->parts.size(); ++k) {
-    bjx_ban_batch b{};
-    const int rc = bjx_batch_bans(n->parts[k].e, &b);
+  const size_t N = n->parts.size(), T = host_threads();
+  std::vector<bjx_ban_batch> bb(N);
+  for (size_t k = 0; k < N; ++k) {
+    const int rc = bjx_batch_bans(n->parts[k].e, &bb[k]);
     if (rc != BJX_OK) fail(rc, "engine " + std::to_string(k) + ": " + bjx_engine_last_error(n->parts[k].e));
+  }
+  // ban-log lines: the engines' logs back to back
+  std::vector<uint64_t> log_base(N + 1, 0), trip_pos(N + 1, 0);
+  for (size_t k = 0; k < N; ++k) {
+    log_base[k + 1] = log_base[k] + bb[k].log_bytes;
+    trip_pos[k + 1] = trip_pos[k] + bb[k].n_trips;
+  }
+  n->ban_trips = trip_pos[N];
+  n->log.resize(log_base[N]);
+  n->log_off.resize(trip_pos[N] + 1);
+  n->log_off[0] = 0;
+  n->log_kind.resize(trip_pos[N]);
+  {
+    constexpr uint64_t kPiece = 1ull << 22;  // trips (or log bytes) per task
+    std::vector<std::pair<uint32_t, uint64_t>> tasks;  // (engine, first trip / byte), two kinds
+    for (size_t k = 0; k < N; ++k)
+      for (uint64_t t = 0; t < std::max(bb[k].n_trips, bb[k].log_bytes); t += kPiece) tasks.push_back({(uint32_t)k, t});
+    par_for(tasks.size(), T, [&](size_t i) {
+      const size_t k = tasks[i].first;
+      const uint64_t a = tasks[i].second;
+      const bjx_ban_batch &b = bb[k];
+      if (a < b.log_bytes) memcpy(&n->log[log_base[k] + a], b.log + a, std::min(kPiece, b.log_bytes - a));
+      for (uint64_t t = a; t < std::min(a + kPiece, b.n_trips); ++t) {
+        n->log_off[trip_pos[k] + t + 1] = log_base[k] + b.log_off[t + 1];
+        n->log_kind[trip_pos[k] + t] = b.log_kind[t];
+      }
+    });
+  }
+  // per-IP records
+  constexpr size_t kBuckets = 256;
+  struct Item {
+    uint64_t h;
+    uint32_t k, r;
+  };
+  std::vector<std::vector<uint64_t>> hs(N);
+  std::vector<std::vector<uint32_t>> cnt(N, std::vector<uint32_t>(kBuckets, 0));
+  par_for(N, T, [&](size_t k) {
+    const bjx_ban_batch &b = bb[k];
+    hs[k].resize(b.n_ips);
     for (uint64_t r = 0; r < b.n_ips; ++r) {
-      bjx_ip_decision d = b.ips[r];
-      d.trip_idx += trip_base[k];
-      std::string ip(reinterpret_cast<const char *>(b.ip_bytes) + b.ip_off[r], b.ip_off[r + 1] - b.ip_off[r]);
-      auto it = by_ip.find(ip);
-      if (it == by_ip.end()) {
-        by_ip.emplace(ip, recs.size());
-        recs.push_back({d, std::move(ip)});
+      hs[k][r] = ip_key(b.ip_bytes + b.ip_off[r], b.ip_off[r + 1] - b.ip_off[r]);
+      ++cnt[k][hs[k][r] >> 56];
+    }
+  });
+  std::vector<size_t> boff(kBuckets + 1, 0);
+  std::vector<std::vector<size_t>> at(N, std::vector<size_t>(kBuckets));
+  for (size_t q = 0; q < kBuckets; ++q) {
+    size_t o = boff[q];
+    for (size_t k = 0; k < N; ++k) {
+      at[k][q] = o;
+      o += cnt[k][q];
+    }
+    boff[q + 1] = o;
+  }
+  std::vector<Item> items(boff[kBuckets]);
+  par_for(N, T, [&](size_t k) {
+    std::vector<size_t> &a = at[k];
+    for (uint64_t r = 0; r < bb[k].n_ips; ++r) items[a[hs[k][r] >> 56]++] = Item{hs[k][r], (uint32_t)k, (uint32_t)r};
+  });
+  struct Merged {
+    bjx_ip_decision d;
+    uint32_t k, r;  // where the IP bytes are
+  };
+  std::vector<std::vector<Merged>> out(kBuckets);
+  par_for(kBuckets, T, [&](size_t q) {
+    const size_t b0 = boff[q], b1 = boff[q + 1];
+    if (b0 == b1) return;
+    size_t cap = 16;
+    while (cap < 2 * (b1 - b0)) cap <<= 1;
+    std::vector<uint32_t> tab(cap, 0xFFFFFFFFu);
+    std::vector<uint64_t> th;
+    std::vector<Merged> &o = out[q];
+    for (size_t i = b0; i < b1; ++i) {
+      const Item &it = items[i];
+      const bjx_ban_batch &b = bb[it.k];
+      const uint8_t *ip = b.ip_bytes + b.ip_off[it.r];
+      const size_t len = b.ip_off[it.r + 1] - b.ip_off[it.r];
+      bjx_ip_decision d = b.ips[it.r];
+      d.trip_idx += trip_base[it.k];
+      size_t s = it.h & (cap - 1);
+      for (;; s = (s + 1) & (cap - 1)) {
+        const uint32_t m = tab[s];
+        if (m == 0xFFFFFFFFu) break;
+        if (th[m] != it.h) continue;
+        const bjx_ban_batch &c = bb[o[m].k];
+        const size_t clen = c.ip_off[o[m].r + 1] - c.ip_off[o[m].r];
+        if (clen == len && memcmp(c.ip_bytes + c.ip_off[o[m].r], ip, len) == 0) break;
+      }
+      if (tab[s] == 0xFFFFFFFFu) {
+        tab[s] = (uint32_t)o.size();
+        th.push_back(it.h);
+        o.push_back(Merged{d, it.k, it.r});
         continue;
       }
-      bjx_ip_decision &c = recs[it->second].d;
+      bjx_ip_decision &c = o[tab[s]].d;
       if (d.decision > c.decision) {
         c.decision = d.decision;
         c.trip_idx = d.trip_idx;
@@ -204,21 +315,43 @@ void merge_bans(bjx_node *n, const std::vector<uint64_t> &trip_base) {
       c.n_trips += d.n_trips;
       c.iptables |= d.iptables;
     }
-    const uint64_t base = n->log.size();
-    if (b.log_bytes) n->log.append(b.log, b.log_bytes);
-    for (uint64_t t = 0; t < b.n_trips; ++t) {
-      n->log_off.push_back(base + b.log_off[t + 1]);
-      n->log_kind.push_back(b.log_kind[t]);
+  });
+  std::vector<Merged> all;
+  {
+    size_t m = 0;
+    for (auto &v : out) m += v.size();
+    all.reserve(m);
+    for (auto &v : out) all.insert(all.end(), v.begin(), v.end());
+  }
+  // trip order: LSD radix sort on trip_idx (16 bits a pass); trip indices of
+  // distinct IPs are distinct, so stability is not even needed
+  {
+    std::vector<Merged> tmp(all.size());
+    uint64_t maxt = 0;
+    for (auto &x : all) maxt = std::max<uint64_t>(maxt, x.d.trip_idx);
+    for (int shift = 0; shift < 64 && (shift == 0 || (maxt >> shift)); shift += 16) {
+      std::vector<size_t> c(65537, 0);
+      for (auto &x : all) ++c[((x.d.trip_idx >> shift) & 0xFFFF) + 1];
+      for (size_t i = 1; i < c.size(); ++i) c[i] += c[i - 1];
+      for (auto &x : all) tmp[c[(x.d.trip_idx >> shift) & 0xFFFF]++] = x;
+      all.swap(tmp);
     }
-    n->ban_trips += b.n_trips;
   }
-  std::sort(recs.begin(), recs.end(), [](const Rec &a, const Rec &b) { return a.d.trip_idx < b.d.trip_idx; });
-  n->ips.reserve(recs.size());
-  for (auto &r : recs) {
-    n->ips.push_back(r.d);
-    n->ipb.insert(n->ipb.end(), r.ip.begin(), r.ip.end());
-    n->ipo.push_back(n->ipb.size());
+  n->ips.resize(all.size());
+  n->ipo.resize(all.size() + 1);
+  n->ipo[0] = 0;
+  for (size_t i = 0; i < all.size(); ++i) {
+    const bjx_ban_batch &b = bb[all[i].k];
+    n->ips[i] = all[i].d;
+    n->ipo[i + 1] = n->ipo[i] + (b.ip_off[all[i].r + 1] - b.ip_off[all[i].r]);
   }
+  n->ipb.resize(n->ipo[all.size()]);
+  par_for(all.size() ? T : 0, T, [&](size_t t) {
+    for (size_t i = t; i < all.size(); i += T) {
+      const bjx_ban_batch &b = bb[all[i].k];
+      memcpy(n->ipb.data() + n->ipo[i], b.ip_bytes + b.ip_off[all[i].r], n->ipo[i + 1] - n->ipo[i]);
+    }
+  });
 }
 
 void run_batch(bjx_node *n, const bjx_ruleset *rs, const uint8_t *const *chunks, const size_t *lens, int64_t now_ns,
@@ -230,10 +363,7 @@ void run_batch(bjx_node *n, const bjx_ruleset *rs, const uint8_t *const *chunks,
     Part &P = n->parts[0];
     const int rc = bjx_process_batch(P.e, rs, chunks[0], lens[0], now_ns, flags, out);
     if (rc != BJX_OK) fail(rc, std::string("engine 0: ") + bjx_engine_last_error(P.e));
-    if (flags & BJX_EMIT_BANS) {
-      merge_bans(n, std::vector<uint64_t>(1, 0));
-      n->bans = true;
-    }
+    n->bans = (flags & BJX_EMIT_BANS) != 0;  // bjx_node_batch_bans hands out the engine's own
     return;
   }
   // 1. match each chunk
@@ -320,11 +450,9 @@ void run_batch(bjx_node *n, const bjx_ruleset *rs, const uint8_t *const *chunks,
     }
     if (flags & BJX_COPY_RESULTS) {
       if (x.n_lines) n->line_flags.insert(n->line_flags.end(), x.line_flags, x.line_flags + x.n_lines);
-      for (uint64_t i = 0; i < x.n_results; ++i) {
-        bjx_rule_result rr = x.results[i];
-        rr.line_idx += line_base;
-        n->results.push_back(rr);
-      }
+      const size_t r0 = n->results.size();
+      if (x.n_results) n->results.insert(n->results.end(), x.results, x.results + x.n_results);
+      for (size_t i = r0; i < n->results.size(); ++i) n->results[i].line_idx += line_base;
     }
     r.n_lines += x.n_lines;
     r.n_results += x.n_results;
@@ -479,6 +607,11 @@ extern "C" int bjx_node_batch_bans(bjx_node *n, bjx_ban_batch *out) {
   return guarded(n, [&]() -> int {
     memset(out, 0, sizeof *out);
     if (!n->bans) fail(BJX_ERR_ARG, "bjx_node_batch_bans: the last batch ran without BJX_EMIT_BANS");
+    if (n->parts.size() == 1) {
+      const int rc = bjx_batch_bans(n->parts[0].e, out);
+      if (rc != BJX_OK) fail(rc, std::string("engine 0: ") + bjx_engine_last_error(n->parts[0].e));
+      return BJX_OK;
+    }
     out->n_ips = n->ips.size();
     out->ips = out->n_ips ? n->ips.data() : nullptr;
     out->n_trips = n->ban_trips;
