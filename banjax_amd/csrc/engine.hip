@@ -850,6 +850,10 @@ __device__ __forceinline__ void decide_rules(const Bind &B, const Tabs &T, const
       bool dup = false;
       for (uint32_t d = 0; d < c; ++d) dup = dup || ((uint32_t)(lits >> (16 * d)) & 0xFFFF) == lit;
       const uint32_t b = B.lr_off[lit], g = B.lr_gend[lit], e = B.lr_off[lit + 1];
+      // the (literal, host) run's home slot goes out with the literal's bounds:
+      // both depend on the literal id alone
+      uint32_t sl = hid >= 0 ? lit_host_slot(lit, (uint32_t)hid, B.lh_cap) : 0u;
+      uint4 run = hid >= 0 ? B.lh_tab[sl] : make_uint4(0, 0, 0, 0);
       if (dup && g == e) continue;  // site runs are revisited: their full-literal checks are per hit
       for (uint32_t i = dup ? g : b; i < g; ++i) {
         const uint2 x = B.lr_ent[i];
@@ -861,12 +865,9 @@ __device__ __forceinline__ void decide_rules(const Bind &B, const Tabs &T, const
       }
       if (hid < 0 || g == e) continue;
       // this host's run of the literal's site entries: one (usually) probe
-      uint32_t sl = lit_host_slot(lit, (uint32_t)hid, B.lh_cap);
-      uint4 run;
-      for (;;) {
-        run = B.lh_tab[sl];
-        if (run.x == 0 || (run.x == lit + 1 && run.y == (uint32_t)hid)) break;
+      while (!(run.x == 0 || (run.x == lit + 1 && run.y == (uint32_t)hid))) {
         sl = (sl + 1) & (B.lh_cap - 1);
+        run = B.lh_tab[sl];
       }
       if (run.x == 0) continue;
       const uint32_t hp = (uint32_t)(lpos >> (16 * c)) & 0xFFFF;  // hit offset in rest (0xFFFF: unknown)
@@ -891,6 +892,102 @@ __device__ __forceinline__ void decide_rules(const Bind &B, const Tabs &T, const
       }
     }
   }
+  uint64_t *mask = L.masks + j * B.mask_words;
+  mask[0] = m0;
+  if (B.mask_words > 1) mask[1] = m1;
+  const uint32_t nres = __popcll(m0) + __popcll(m1);
+  const uint32_t nev = __popcll(m0 & ~H.k0) + __popcll(m1 & ~H.k1);
+  L.counts[j] = ((uint64_t)nres << 32) | nev;
+}
+
+// ---- rule plans (Bind::plan): the same decisions as decide_rules, from one
+// 32 B entry per rule of the line's scope.  kinds:
+constexpr uint32_t kPlanLit = 0;     // prefilter rule with <= 4 literals: decided by the hits
+constexpr uint32_t kPlanLitAny = 1;  // prefilter rule the entry cannot spell out: a DFA job on any hit
+constexpr uint32_t kPlanAnchor = 2;  // anchored rule: inline window test, anchor literal, DFA
+constexpr uint32_t kPlanScan = 3;    // no literal: a DFA job on every line
+
+template <bool EMIT>
+__device__ __forceinline__ void plan_rule(const Bind &B, const Tabs &T, const uint4 a, const uint4 b, uint32_t pos_base,
+                                          const uint8_t *rest, uint32_t rest_len, uint64_t lits, uint64_t lpos, uint32_t nlit,
+                                          bool ovf, uint64_t &m0, uint64_t &m1, uint64_t j, const JobSink &S) {
+  const uint32_t r = a.x & 0xFFFFFu, pos = pos_base + ((a.x >> 20) & 0x7Fu), kind = (a.x >> 27) & 7u;
+  const bool eq = ((a.x >> 30) & 1u) != 0;
+  if (kind == kPlanScan) {
+    dfa_rule<EMIT>(B, T, r, pos, false, rest, rest_len, m0, m1, j, S);
+    return;
+  }
+  if (kind == kPlanAnchor) {
+    const uint4 qa = make_uint4(a.y, a.z, b.x, b.y), qb = make_uint4(b.z, b.w, 0, 0);
+    const uint32_t qk = anchor_quick(qa, qb, rest, rest_len);
+    if (qk == 0) return;
+    if (qk == 1 && ((qa.y >> 9) & 1)) { set_pos(m0, m1, pos); return; }
+    if (a.w) {  // the rule's single anchor literal, checked here (dfa_rule's anchored branch)
+      if (!((a.w >> 16) <= rest_len && literal_at(T, (a.w & 0xFFFFu) - 1, rest))) return;
+      if (eq) { set_pos(m0, m1, pos); return; }
+      dfa_rule<EMIT>(B, T, r, pos, false, rest, rest_len, m0, m1, j, S);
+      return;
+    }
+    dfa_rule<EMIT>(B, T, r, pos, true, rest, rest_len, m0, m1, j, S);
+    return;
+  }
+  if (ovf) {  // more hits than slots: every literal rule by its automaton
+    dfa_rule<EMIT>(B, T, r, pos, false, rest, rest_len, m0, m1, j, S);
+    return;
+  }
+  if (nlit == 0) return;
+  if (kind == kPlanLitAny) {
+    dfa_rule<EMIT>(B, T, r, pos, false, rest, rest_len, m0, m1, j, S);
+    return;
+  }
+  for (uint32_t c = 0; c < nlit; ++c) {
+    const uint32_t lit = (uint32_t)(lits >> (16 * c)) & 0xFFFFu;
+    if (lit != (a.y & 0xFFFFu) && lit != (a.y >> 16) && lit != (a.z & 0xFFFFu) && lit != (a.z >> 16)) continue;
+    if (a.w != kNone && eq) {
+      // host-split literal of an equivalent rule: matched iff the full literal
+      // surrounds one of its piece's hits; undecided until one does
+      const uint32_t hp = (uint32_t)(lpos >> (16 * c)) & 0xFFFFu;
+      if (hp != 0xFFFFu) {
+        const uint32_t fl = a.w >> 8, off = a.w & 0xFFu;
+        if (hp >= off && hp - off + b.y <= rest_len && literal_at(T, fl, rest + (hp - off))) set_pos(m0, m1, pos);
+        if (has_pos(m0, m1, pos)) return;
+        continue;
+      }
+    }
+    if (eq && a.w == kNone) set_pos(m0, m1, pos);
+    else dfa_rule<EMIT>(B, T, r, pos, false, rest, rest_len, m0, m1, j, S);
+    return;
+  }
+}
+
+// decide_rules over the scope's plan entries: the global entries are uniform
+// across the wave (scalar loads); a host's site entries are loaded four at a
+// time, side by side
+template <bool EMIT>
+__device__ __forceinline__ void decide_plan(const Bind &B, const Tabs &T, const uint8_t *rest, uint32_t rest_len, int32_t hid,
+                                            const HostRules &H, uint64_t lits, uint64_t lpos, uint32_t nlit, bool ovf, uint64_t j,
+                                            const Lines &L, const JobSink &S, uint32_t dbg = 0) {
+  const uint32_t nsite = H.s_end - H.s_begin;
+  uint64_t m0 = H.a0, m1 = H.a1;
+  if (dbg & 32) nlit = 0;  // timing experiments only (BJX_DEBUG_LINES): 16 no site entries, 32 no literal hits
+  if (hid >= 0 && !(dbg & 16)) {
+    const uint32_t pb = B.plan_off[hid], pe = B.plan_off[hid + 1];
+    for (uint32_t i = pb; i < pe; i += 4) {
+      uint4 a[4], b[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool in = i + k < pe;
+        a[k] = in ? B.plan[2 * (i + k)] : make_uint4(0, 0, 0, 0);
+        b[k] = in ? B.plan[2 * (i + k) + 1] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (i + k < pe) plan_rule<EMIT>(B, T, a[k], b[k], 0, rest, rest_len, lits, lpos, nlit, ovf, m0, m1, j, S);
+    }
+  }
+  for (uint32_t i = 0; i < B.n_plan_glob; ++i)
+    plan_rule<EMIT>(B, T, B.plan_glob[2 * i], B.plan_glob[2 * i + 1], nsite, rest, rest_len, lits, lpos, nlit, ovf, m0, m1, j,
+                    S);
   uint64_t *mask = L.masks + j * B.mask_words;
   mask[0] = m0;
   if (B.mask_words > 1) mask[1] = m1;
@@ -1284,17 +1381,13 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
     const uint32_t ip_off = sp0 + 1, ip_len = sp1 - sp0 - 1;
     const uint32_t rest_off = sp1 + 1, host_off = sp2 + 1, host_len = sp3 - sp2 - 1;
     const bool exempt = B.any_allow && check_is_allowed(B, hid, p + ip_off, ip_len);
-    L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
-    L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
-    L.host_id[j] = hid;
-    L.ip_hash[j] = hash_bytes(p + ip_off, ip_len);
-    L.ip16[j] = ip_key16(p + ip_off, ip_len);
     const int64_t tsn = ns_from_seconds(f);
-    L.ts[j] = tsn;
     uint8_t fl = 0;
     if (go_sub(A.now_ns, tsn) > 10000000000LL) fl = kLineOld;
     else if (exempt) fl = kLineExempt;
-    L.flags[j] = fl;
+    // the per-line stores go out after the rule decisions: on gfx9 stores share
+    // vmcnt with loads, so a store issued ahead of decide_rules' dependent
+    // table loads would hold up every one of their waits
     if (fl) {
       L.counts[j] = 0;
     } else {
@@ -1315,9 +1408,21 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
         lpos |= (uint64_t)(q - rs < 0xFFFF ? (uint32_t)(q - rs) : 0xFFFFu) << (16 * nlit);
         lits |= (uint64_t)lit << (16 * nlit++);
       }
-      decide_rules<true>(B, TB, p + rest_off, n - rest_off, hid, H, lits, lpos, (A.dbg & 2) ? 0u : nlit,
-                         cc > (uint32_t)kCandSlots, j, L, S, A.dbg);
+      if (B.use_plan && !(A.dbg & 15))
+        decide_plan<true>(B, TB, p + rest_off, n - rest_off, hid, H, lits, lpos, nlit, cc > (uint32_t)kCandSlots, j, L, S,
+                          A.dbg);
+      else
+        decide_rules<true>(B, TB, p + rest_off, n - rest_off, hid, H, lits, lpos, (A.dbg & 2) ? 0u : nlit,
+                           cc > (uint32_t)kCandSlots, j, L, S, A.dbg);
     }
+    if (A.dbg & 64) return;  // timing experiment: no per-line stores
+    L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
+    L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
+    L.host_id[j] = hid;
+    L.ip_hash[j] = hash_bytes(p + ip_off, ip_len);
+    L.ip16[j] = ip_key16(p + ip_off, ip_len);
+    L.ts[j] = tsn;
+    L.flags[j] = fl;
   }
 }
 
@@ -3512,6 +3617,56 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
       i = k;
     }
 
+  // rule plans (decide_plan): every non-ALWAYS, non-NEVER rule of a scope at
+  // a position < 128, with its decision inputs inline
+  const bool use_plan = rs->rules.size() < (1u << 20) && lit_off.size() < 0xFFFF;
+  auto plan_entry = [&](uint32_t r, uint32_t pos, std::vector<uint4> &out) {
+    const RuleMode m = mode_of(r);
+    if (m == kModeAlways || m == kModeNever) return;
+    const DevRule &d = drules[r];
+    uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, 0);
+    uint32_t kind = kPlanScan, eq = 0;
+    if (m == kModeAnchored) {
+      kind = kPlanAnchor;
+      eq = d.anc_equiv ? 1u : 0u;
+      const std::vector<uint4> q = anchor_q(std::vector<uint2>{make_uint2(r, 0)});
+      a.y = q[0].x; a.z = q[0].y; b.x = q[0].z; b.y = q[0].w; b.z = q[1].x; b.w = q[1].y;
+      a.w = d.anc_len == 1 && lit_len[rule_lits[d.anc_off]] < 0x10000u
+                ? (rule_lits[d.anc_off] + 1) | (lit_len[rule_lits[d.anc_off]] << 16) : 0u;
+    } else if (m == kModePrefilter) {
+      eq = rs->rules[r].rx.pref_equivalent ? 1u : 0u;
+      const uint32_t nl = d.lits_len;
+      bool split = false;
+      for (uint32_t i = 0; i < nl; ++i) split = split || rule_full[d.lits_off + i] != kNone;
+      if (nl == 0 || nl > 4 || (split && nl > 1)) {
+        kind = kPlanLitAny;  // a DFA job on any hit: the automaton decides exactly
+      } else {
+        kind = kPlanLit;
+        uint32_t l[4] = {0xFFFF, 0xFFFF, 0xFFFF, 0xFFFF};
+        for (uint32_t i = 0; i < nl; ++i) l[i] = rule_lits[d.lits_off + i];
+        a.y = l[0] | (l[1] << 16);
+        a.z = l[2] | (l[3] << 16);
+        a.w = split ? rule_full[d.lits_off] : kNone;
+        b.y = split ? lit_len[rule_full[d.lits_off] >> 8] : 0u;
+      }
+    }
+    a.x = canon[r] | (pos << 20) | (kind << 27) | (eq << 30);
+    out.push_back(a);
+    out.push_back(b);
+  };
+  std::vector<uint32_t> plan_off(n_hosts + 1, 0);
+  std::vector<uint4> plan, plan_glob;
+  if (use_plan) {
+    for (uint32_t h = 0; h < n_hosts; ++h) {
+      plan_off[h] = (uint32_t)(plan.size() / 2);
+      for (uint32_t k = 0; k < per_host[h].size() && k < 128; ++k) plan_entry(per_host[h][k], k, plan);
+    }
+    plan_off[n_hosts] = (uint32_t)(plan.size() / 2);
+    for (uint32_t g = 0; g < rs->n_global && g < 128; ++g) plan_entry(g, g, plan_glob);
+  }
+  if (plan.empty()) plan.push_back(make_uint4(0, 0, 0, 0));
+  if (plan_glob.empty()) plan_glob.push_back(make_uint4(0, 0, 0, 0));
+
   // allow scopes (decision.go:278-374): exact maps are last-writer-wins in
   // config order; Allow IPFilters hold every allow entry
   std::vector<std::vector<std::array<uint8_t, 16>>> sc_addrs(n_scopes);
@@ -3611,7 +3766,8 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
          o_dso = bb.add(dfa_site_off), o_ds = bb.add(dfa_site), o_dg = bb.add(dfa_glob), o_pso = bb.add(pref_site_off),
          o_dsq = bb.add(dfa_site_q), o_dgq = bb.add(dfa_glob_q),
          o_ps = bb.add(pref_site), o_pg = bb.add(pref_glob), o_hslot = bb.add(hslot), o_lh = bb.add(lh_tab),
-         o_nfa = bb.add(nfa_blob), o_lrf = bb.add(lr_full);
+         o_nfa = bb.add(nfa_blob), o_lrf = bb.add(lr_full), o_plan = bb.add(plan), o_plo = bb.add(plan_off),
+         o_plg = bb.add(plan_glob);
   e->bind_blob.ensure(bb.bytes.size());
   HIP_OK(hipMemcpy(e->bind_blob.p, bb.bytes.data(), bb.bytes.size(), hipMemcpyHostToDevice));
   uint8_t *base = e->bind_blob.p;
@@ -3669,6 +3825,11 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.lr_full = reinterpret_cast<const uint32_t *>(base + o_lrf);
   B.lh_tab = reinterpret_cast<const uint4 *>(base + o_lh);
   B.lh_cap = lh_cap;
+  B.plan = reinterpret_cast<const uint4 *>(base + o_plan);
+  B.plan_off = reinterpret_cast<const uint32_t *>(base + o_plo);
+  B.plan_glob = reinterpret_cast<const uint4 *>(base + o_plg);
+  B.n_plan_glob = use_plan ? (uint32_t)(plan_glob.size() / 2) : 0u;
+  B.use_plan = use_plan && !getenv("BJX_NO_PLAN") ? 1u : 0u;
   B.sc_always = reinterpret_cast<const uint64_t *>(base + o_sca);
   B.sc_skip = reinterpret_cast<const uint64_t *>(base + o_scs);
   B.dfa_site_off = reinterpret_cast<const uint32_t *>(base + o_dso);

@@ -164,6 +164,17 @@ struct Bind {
   // bit-parallel NFA tables of the kRuleNfa rules (DevRule::nfa_off)
   const uint64_t *nfa;
   uint32_t any_nfa;
+  // rule plans (decide_plan): per rule of a scope that is neither ALWAYS nor
+  // NEVER, one 32 B entry {a, b} holding everything its decision needs (kind,
+  // position, literal ids, host-split full literal, inline anchor test), so a
+  // line loads its host's entries side by side instead of walking the
+  // literal -> rule tables.  Site entries of host h: [plan_off[h],
+  // plan_off[h + 1]); global entries (position = nsite + g): plan_glob.
+  const uint4 *plan;
+  const uint32_t *plan_off;  // n_hosts + 1
+  const uint4 *plan_glob;
+  uint32_t n_plan_glob;
+  uint32_t use_plan;
 };
 
 // Per-line SoA arrays (batch workspace).
