@@ -1950,9 +1950,12 @@ __device__ __forceinline__ bool ip_claim_line(const EvSrc &E, const State &S, ui
     }
     if (cur == h) {
       uint32_t b = q0.w;  // 0 (stale) when the hash came from the CAS: the CAS below decides
-      if (b == 0 || b == epoch) b = atomicCAS(&S.ip[s].born, 0u, epoch);
+      if (b == 0) b = atomicCAS(&S.ip[s].born, 0u, epoch);
       if (b == 0 || b == epoch) {  // created in this batch: identity checked by k_ip_commit
-        atomicMin(&S.ip_first[s], (uint32_t)i);
+        // a hot new IP has every one of its lines here: read before the atomic,
+        // so only lines that can still lower the first index contend for it
+        if (__hip_atomic_load(&S.ip_first[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > (uint32_t)i)
+          atomicMin(&S.ip_first[s], (uint32_t)i);
         el_slot[i] = (uint32_t)s;
         el_id[i] = kNewIp;
         return claimed;
@@ -2279,28 +2282,81 @@ __device__ uint64_t block_first(uint64_t lo, uint64_t hi, P pred, uint32_t *s_re
 
 constexpr uint64_t kLongSerial = 512;  // runs up to this long: thread 0 walks them
 
-__global__ __launch_bounds__(kBlock) void k_long_runs(uint64_t n_ev, const uint32_t *__restrict__ key,
-                                                      const EvRec *__restrict__ rec, const DevRule *__restrict__ rules,
-                                                      StSlot *__restrict__ st, uint8_t *__restrict__ out_sorted,
-                                                      const uint64_t *__restrict__ heads) {
+// Per crossing run (k_apply's long_heads), k_long_* below keep, in LongRuns:
+struct LongRuns {
+  const uint64_t *head;  // first sorted record of the run
+  uint64_t *end;         // one past its last record
+  uint64_t *off;         // exclusive scan of the run lengths (flattened event index)
+  int64_t *t0;           // start of the first window (the stored window when the head continues it)
+  int64_t *h0;           // hits already in that window
+  uint32_t *flags;       // bit0: head continues the stored window; bits1-2: MatchType of the head otherwise;
+                         // bit3: serial (mixed limits or decreasing timestamps); bit4: short (serial)
+  uint64_t *win;         // window start records, off[r] ... off[r] + nwin[r]
+  uint32_t *nwin;
+  uint64_t n;
+};
+
+// 1. run end (block-parallel search), the stored state and the first window
+__global__ __launch_bounds__(kBlock) void k_long_ends(uint64_t n_ev, const uint32_t *__restrict__ key,
+                                                      const EvRec *__restrict__ rec, const StSlot *__restrict__ st,
+                                                      const DevRule *__restrict__ rules, LongRuns R, uint64_t *__restrict__ len) {
   __shared__ uint32_t s_red[kBlock / 64];
-  const uint32_t tid = threadIdx.x;
-  const uint64_t head = heads[blockIdx.x];
+  const uint64_t r = blockIdx.x;
+  const uint64_t head = R.head[r];
   const uint32_t q = key[head];
   const uint64_t end = block_first(head + 1, n_ev, [&](uint64_t i) { return key[i] != q; }, s_red);
-  const uint32_t r0 = rec[head].rule & 0x7FFFFFFFu;
-  const int64_t I = rules[r0].interval_ns, Lim = rules[r0].hits;
-  uint32_t bad = 0;
-  if (end - head > kLongSerial)
-    for (uint64_t i = head + 1 + tid; i < end; i += kBlock) {
-      const EvRec v = rec[i];
-      const uint32_t r = v.rule & 0x7FFFFFFFu;
-      if (r != r0 && (rules[r].interval_ns != I || rules[r].hits != Lim)) bad = 1;
-      if (v.ts < rec[i - 1].ts) bad = 1;
-    }
+  if (threadIdx.x != 0) return;
+  R.end[r] = end;
+  len[r] = end - head;
   const StSlot cur = st[q];
-  if (end - head <= kLongSerial || block_min_u32(bad ? 0u : 1u, s_red) == 0) {
+  const int64_t I = rules[rec[head].rule & 0x7FFFFFFFu].interval_ns;
+  const bool valid = cur.valid != 0;
+  const bool cont = valid && go_sub(rec[head].ts, cur.start) <= I;
+  R.t0[r] = cont ? cur.start : rec[head].ts;
+  R.h0[r] = cont ? cur.hits : 0;
+  R.flags[r] = (cont ? 1u : 0u) | ((uint32_t)(valid ? BJX_OUTSIDE_INTERVAL : BJX_FIRST_TIME) << 1) |
+               (end - head <= kLongSerial ? 16u : 0u);
+}
+
+__device__ __forceinline__ uint64_t long_run_of(const LongRuns &R, uint64_t k) {
+  uint64_t lo = 0, hi = R.n;  // last r with off[r] <= k
+  while (hi - lo > 1) {
+    const uint64_t m = (lo + hi) >> 1;
+    if (R.off[m] <= k) lo = m; else hi = m;
+  }
+  return lo;
+}
+
+// 2. every record of every long run, in parallel: same interval / limit as the
+// head's rule and timestamps that never decrease, or the run is applied serially
+__global__ __launch_bounds__(kBlock) void k_long_check(uint64_t total, const EvRec *__restrict__ rec,
+                                                       const DevRule *__restrict__ rules, LongRuns R) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= total) return;
+  const uint64_t r = long_run_of(R, k);
+  const uint64_t head = R.head[r], i = head + (k - R.off[r]);
+  if (i == head) return;
+  const uint32_t r0 = rec[head].rule & 0x7FFFFFFFu, ri = rec[i].rule & 0x7FFFFFFFu;
+  bool bad = rec[i].ts < rec[i - 1].ts;
+  if (ri != r0) bad = bad || rules[ri].interval_ns != rules[r0].interval_ns || rules[ri].hits != rules[r0].hits;
+  if (bad && !(__hip_atomic_load(&R.flags[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 8u)) atomicOr(&R.flags[r], 8u);
+}
+
+// 3. per run: the serial walk (short or irregular runs), else the window
+// starts one after another (block-parallel search per window) and the final
+// state in closed form
+__global__ __launch_bounds__(kBlock) void k_long_windows(const uint32_t *__restrict__ key, const EvRec *__restrict__ rec,
+                                                         const DevRule *__restrict__ rules, StSlot *__restrict__ st,
+                                                         uint8_t *__restrict__ out_sorted, LongRuns R) {
+  __shared__ uint32_t s_red[kBlock / 64];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t r = blockIdx.x;
+  const uint64_t head = R.head[r], end = R.end[r];
+  const uint32_t q = key[head];
+  const uint32_t fl = R.flags[r];
+  if (fl & 24u) {
     if (tid == 0) {
+      const StSlot cur = st[q];
       bool valid = cur.valid != 0;
       int64_t hits = cur.hits, start = cur.start, interval = 0, limit = 0;
       uint32_t pr = 0xFFFFFFFFu;
@@ -2308,29 +2364,21 @@ __global__ __launch_bounds__(kBlock) void k_long_runs(uint64_t n_ev, const uint3
       st[q].hits = hits;
       st[q].start = start;
       st[q].valid = 1;
+      R.nwin[r] = 0;
     }
     return;
   }
-  // uniform limits, non-decreasing timestamps: window after window
-  const bool valid = cur.valid != 0;
-  bool cont = valid && go_sub(rec[head].ts, cur.start) <= I;  // the head continues the stored window
-  int64_t T = cont ? cur.start : rec[head].ts;
-  int64_t h0 = cont ? cur.hits : 0;
-  uint8_t first_mt = valid ? BJX_OUTSIDE_INTERVAL : BJX_FIRST_TIME;
+  const uint32_t r0 = rec[head].rule & 0x7FFFFFFFu;
+  const int64_t I = rules[r0].interval_ns, Lim = rules[r0].hits;
+  uint64_t *win = R.win + R.off[r];
+  uint32_t nw = 0;
   uint64_t a = head;
+  int64_t T = R.t0[r], h0 = R.h0[r];
   for (;;) {
+    if (tid == 0) win[nw] = a;
+    ++nw;
     const int64_t Tw = T;
     const uint64_t b = block_first(a + 1, end, [&](uint64_t i) { return go_sub(rec[i].ts, Tw) > I; }, s_red);
-    for (uint64_t i = a + tid; i < b; i += kBlock) {
-      const int64_t e = (int64_t)(i - a) + 1;
-      bool ex;
-      if (Lim < 0) ex = true;
-      else if (h0 > Lim) ex = e == 1 || (e - 1) % (Lim + 1) == 0;
-      else ex = (h0 + e) % (Lim + 1) == 0;
-      const uint8_t mt = (!cont && i == a) ? first_mt : (uint8_t)BJX_INSIDE_INTERVAL;
-      const bool seen = (rec[i].rule >> 31) == 0;
-      out_sorted[i] = (uint8_t)(0x80 | (seen ? 1 : 0) | (mt << 1) | (ex ? 8 : 0));
-    }
     if (b >= end) {
       if (tid == 0) {
         const int64_t e = (int64_t)(b - a);
@@ -2341,15 +2389,47 @@ __global__ __launch_bounds__(kBlock) void k_long_runs(uint64_t n_ev, const uint3
         st[q].hits = hits;
         st[q].start = Tw;
         st[q].valid = 1;
+        R.nwin[r] = nw;
       }
       return;
     }
     a = b;
     T = rec[b].ts;
     h0 = 0;
-    cont = false;
-    first_mt = BJX_OUTSIDE_INTERVAL;
   }
+}
+
+// 4. every record of the windowed runs, in parallel: its window (binary
+// search over the run's window starts) and the closed-form outcome
+__global__ __launch_bounds__(kBlock) void k_long_fill(uint64_t total, const EvRec *__restrict__ rec,
+                                                      const DevRule *__restrict__ rules, uint8_t *__restrict__ out_sorted,
+                                                      LongRuns R) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= total) return;
+  const uint64_t r = long_run_of(R, k);
+  const uint32_t fl = R.flags[r];
+  if (fl & 24u) return;  // applied serially
+  const uint64_t head = R.head[r], i = head + (k - R.off[r]);
+  const uint64_t *win = R.win + R.off[r];
+  uint32_t lo = 0, hi = R.nwin[r];  // last window starting at or before i
+  while (hi - lo > 1) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (win[m] <= i) lo = m; else hi = m;
+  }
+  const uint32_t r0 = rec[head].rule & 0x7FFFFFFFu;
+  const int64_t Lim = rules[r0].hits;
+  const bool first_win = lo == 0, cont = first_win && (fl & 1u);
+  const int64_t h0 = first_win ? R.h0[r] : 0;
+  const uint64_t a = win[lo];
+  const int64_t e = (int64_t)(i - a) + 1;
+  bool ex;
+  if (Lim < 0) ex = true;
+  else if (h0 > Lim) ex = e == 1 || (e - 1) % (Lim + 1) == 0;
+  else ex = (h0 + e) % (Lim + 1) == 0;
+  const uint8_t first_mt = first_win ? (uint8_t)((fl >> 1) & 3u) : (uint8_t)BJX_OUTSIDE_INTERVAL;
+  const uint8_t mt = (!cont && i == a) ? first_mt : (uint8_t)BJX_INSIDE_INTERVAL;
+  const bool seen = (rec[i].rule >> 31) == 0;
+  out_sorted[i] = (uint8_t)(0x80 | (seen ? 1 : 0) | (mt << 1) | (ex ? 8 : 0));
 }
 
 __global__ void k_dbg_mask_hash(uint64_t n, uint64_t *__restrict__ h, uint64_t mask) {
@@ -2997,6 +3077,9 @@ struct bjx_engine {
   DevBuf<uint32_t> jline, jkey, jline2, jkey2;
   uint64_t last_jobs = 0, last_todo = 0, last_long_runs = 0;
   DevBuf<uint64_t> long_heads;
+  DevBuf<uint64_t> lr_end, lr_len, lr_off, lr_win;
+  DevBuf<int64_t> lr_t0, lr_h0;
+  DevBuf<uint32_t> lr_flags, lr_nwin;
   DevBuf<unsigned long long> long_count;
   uint32_t scan_lds[2] = {0, 0};
   bool lines_attr = false;
@@ -4028,6 +4111,8 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   for (auto *b : {&e->bn_kind, &e->bn_flag, &e->bn_log, &e->dl_bytes, &e->nm_json}) b->release();
   e->bn_best.release(); e->bn_rep.release(); e->bn_sel.release(); e->bn_ipb.release(); e->tz_at.release(); e->tz_off.release();
   e->rb_first.release(); e->rb_last.release(); e->long_heads.release(); e->long_count.release();
+  e->lr_end.release(); e->lr_len.release(); e->lr_off.release(); e->lr_win.release(); e->lr_t0.release(); e->lr_h0.release();
+  e->lr_flags.release(); e->lr_nwin.release();
   e->d_results.release(); e->q_out.release();
   e->ban_ips.release(); e->ban_log.release(); e->ban_off.release(); e->ban_kind.release(); e->ban_ipb.release();
   e->ban_ipo.release();
@@ -4177,8 +4262,30 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
   HIP_OK(hipStreamSynchronize(st));
   e->last_long_runs = n_long;
   if (n_long) {
-    hipLaunchKernelGGL(k_long_runs, dim3((unsigned)n_long), dim3(kBlock), 0, st, n_ev, e->ev_st2.p, e->ev_rec2.p, B.rules,
-                       e->S.st, e->ev_out_s.p, e->long_heads.p);
+    // runs crossing a k_apply chunk (hot keys): ends, a parallel regularity
+    // check, the window starts per run, then every record in parallel
+    LongRuns R;
+    e->lr_end.ensure(n_long); e->lr_len.ensure(n_long + 1); e->lr_off.ensure(n_long + 1); e->lr_t0.ensure(n_long);
+    e->lr_h0.ensure(n_long); e->lr_flags.ensure(n_long); e->lr_nwin.ensure(n_long);
+    R.head = e->long_heads.p; R.end = e->lr_end.p; R.off = e->lr_off.p; R.t0 = e->lr_t0.p; R.h0 = e->lr_h0.p;
+    R.flags = e->lr_flags.p; R.nwin = e->lr_nwin.p; R.n = n_long; R.win = nullptr;
+    HIP_OK(hipMemsetAsync(e->lr_len.p + n_long, 0, 8, st));
+    hipLaunchKernelGGL(k_long_ends, dim3((unsigned)n_long), dim3(kBlock), 0, st, n_ev, e->ev_st2.p, e->ev_rec2.p, e->S.st,
+                       B.rules, R, e->lr_len.p);
+    HIP_OK(hipGetLastError());
+    {
+      uint64_t *in = e->lr_len.p, *o = e->lr_off.p;
+      cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)(n_long + 1), st); });
+    }
+    uint64_t total = 0;
+    HIP_OK(hipMemcpyAsync(&total, e->lr_off.p + n_long, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    e->lr_win.ensure(total + 1);
+    R.win = e->lr_win.p;
+    hipLaunchKernelGGL(k_long_check, dim3(grid_for(total)), dim3(kBlock), 0, st, total, e->ev_rec2.p, B.rules, R);
+    hipLaunchKernelGGL(k_long_windows, dim3((unsigned)n_long), dim3(kBlock), 0, st, e->ev_st2.p, e->ev_rec2.p, B.rules, e->S.st,
+                       e->ev_out_s.p, R);
+    hipLaunchKernelGGL(k_long_fill, dim3(grid_for(total)), dim3(kBlock), 0, st, total, e->ev_rec2.p, B.rules, e->ev_out_s.p, R);
     HIP_OK(hipGetLastError());
   }
 }

@@ -79,29 +79,15 @@ def cpu_baseline_sharded(w, sample_lines):
 
 def pmc_traffic(nbytes):
     """HBM bytes per k_scan launch from the committed rocprofv3 PMC passes over
-    this same command (profiles/<round>/cfg3_bench_pmc_{fetch,write}.csv):
-    FETCH_SIZE x 2 (gfx950 reports half of a wide streaming read,
-    MI355X_MICROARCH.md "HBM") + WRITE_SIZE, both in KB."""
-    import csv
-    import glob
-    best = None
-    def natural(d):  # r01_v10 after r01_v5
-        return [int(x) if x.isdigit() else x for x in re.split(r"(\d+)", d)]
-    for d in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")), key=natural):
-        f, wr = os.path.join(d, "cfg3_bench_pmc_fetch.csv"), os.path.join(d, "cfg3_bench_pmc_write.csv")
-        if os.path.exists(f) and os.path.exists(wr):
-            best = (d, f, wr)
-    if best is None:
+    this same command (profiles/pmc_traffic.json, written from the pass CSVs
+    under profiles/<round>/ by tools/pmc_session.sh): FETCH_SIZE x 2 (gfx950
+    reports half of a wide streaming read, MI355X_MICROARCH.md "HBM") +
+    WRITE_SIZE, both in KB."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
         return None, None
-
-    def mean(path, counter):
-        v = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-             if "::k_scan<" in r["Kernel_Name"] and r["Counter_Name"] == counter]
-        return sum(v) / len(v) if v else None
-    fe, wb = mean(best[1], "FETCH_SIZE"), mean(best[2], "WRITE_SIZE")
-    if fe is None or wb is None:
-        return None, None
-    return round((2 * fe + wb) * 1024 / 1e9, 3), os.path.relpath(best[0], ROOT)
+    d = json.load(open(path))
+    return d["hbm_gb_per_launch"], d["source"]
 
 
 def roofline(achieved, match_ms, nbytes, args):
@@ -119,7 +105,7 @@ def roofline(achieved, match_ms, nbytes, args):
         "kernel_ms": round(match_ms, 3),
     }
     if src:
-        r["traffic_source"] = src + " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, same command, GB per launch)"
+        r["traffic_source"] = src + ": rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, same command, GB per launch"
     return r
 
 
