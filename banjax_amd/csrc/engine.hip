@@ -1626,9 +1626,10 @@ constexpr uint32_t kDfaLdsEntries = 8192;  // u16 transitions staged per block (
 // sites apart, so each keeps its address space instead of generic loads)
 template <bool STAGED>
 __device__ __forceinline__ bool dfa_text(const Bind &B, const DevRule &R, const uint16_t *tr, const uint8_t *ac,
-                                         const uint8_t *__restrict__ buf, uint64_t n_buf, uint64_t t0, uint32_t len) {
+                                         const uint8_t *__restrict__ buf, uint64_t n_buf, uint64_t t0, uint32_t len,
+                                         uint32_t st0) {
   const uint32_t ncls = R.ncls;
-  uint32_t st = R.start;
+  uint32_t st = st0;
   uint64_t a = t0 & ~15ull;
   const uint64_t end = t0 + len;
   uint32_t skip = (uint32_t)(t0 - a);
@@ -1712,13 +1713,18 @@ __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restric
   const uint64_t j = jline[t];
   const uint64_t s = j ? nl[j - 1] + 1 : 0;
   const uint64_t rs = s + L.rest_off[j];
+  const uint32_t rl = (uint32_t)(nl[j] - rs);
   bool m;
   if (staged) {
-    m = dfa_text<true>(B, R0, s_tr, s_ac, buf, n_buf, rs, (uint32_t)(nl[j] - rs));
+    // anchored prefix literal already matched by k_lines: step in past it
+    const uint32_t sk = R0.skip_len && R0.skip_len <= rl ? R0.skip_len : 0u;
+    m = dfa_text<true>(B, R0, s_tr, s_ac, buf, n_buf, rs + sk, rl - sk, sk ? R0.skip_state : R0.start);
   } else {
     const DevRule R = B.rules[r];
     if (R.flags & kRuleNfa) return;  // k_nfa's
-    m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, buf, n_buf, rs, (uint32_t)(nl[j] - rs));
+    const uint32_t sk = R.skip_len && R.skip_len <= rl ? R.skip_len : 0u;
+    m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, buf, n_buf, rs + sk, rl - sk,
+                        sk ? R.skip_state : R.start);
   }
   if (!m) return;
   const int32_t hid = L.host_id[j];
@@ -2432,6 +2438,37 @@ __global__ __launch_bounds__(kBlock) void k_long_fill(uint64_t total, const EvRe
   out_sorted[i] = (uint8_t)(0x80 | (seen ? 1 : 0) | (mt << 1) | (ex ? 8 : 0));
 }
 
+// ---- BJX_CHECK=1 (debugging aid): invariants of the rate-limit stage
+__device__ __forceinline__ uint32_t ev_line_id(const State &S, const uint32_t *el_slot, const uint32_t *el_id, uint64_t i) {
+  const uint32_t id = el_id[i];
+  return id == kNewIp ? S.ip[el_slot[i]].id : (id & ~kFirstIp);
+}
+// every event line's IP id names the line's IP bytes; every event's state
+// slot holds (that id, its rule's name); every sorted outcome was written
+__global__ void k_check_rl(EvSrc E, uint64_t n_ev, const uint32_t *__restrict__ ev_el, const uint32_t *__restrict__ ev_rule,
+                           const uint32_t *__restrict__ el_slot, const uint32_t *__restrict__ el_id,
+                           const DevRule *__restrict__ rules, State S, const uint32_t *__restrict__ ev_st,
+                           const uint8_t *__restrict__ out_s, unsigned long long *__restrict__ chk) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < E.n && ev_has(E, t)) {
+    const uint32_t id = ev_line_id(S, el_slot, el_id, t);
+    const uint32_t len = E.ip_len[t];
+    if (S.ip_len[id] != len || !bytes_eq(S.arena + S.ip_off[id], ev_ip(E, t), len)) {
+      if (atomicAdd(&chk[0], 1ull) == 0) { chk[1] = t; chk[2] = id; }
+    }
+  }
+  if (t < n_ev) {
+    const uint32_t i = ev_el[t];
+    const uint64_t key = ((uint64_t)(ev_line_id(S, el_slot, el_id, i) + 1) << 24) | rules[ev_rule[t]].name_id;
+    if (S.st[ev_st[t]].key != key) {
+      if (atomicAdd(&chk[3], 1ull) == 0) { chk[4] = t; chk[5] = ev_st[t]; }
+    }
+    if (!(out_s[t] & 0x80)) {
+      if (atomicAdd(&chk[6], 1ull) == 0) chk[7] = t;
+    }
+  }
+}
+
 __global__ void k_dbg_mask_hash(uint64_t n, uint64_t *__restrict__ h, uint64_t mask) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) h[i] = (h[i] & mask) | 1;
@@ -3078,6 +3115,7 @@ struct bjx_engine {
   uint64_t last_jobs = 0, last_todo = 0, last_long_runs = 0;
   DevBuf<uint64_t> long_heads;
   DevBuf<uint64_t> lr_end, lr_len, lr_off, lr_win;
+  DevBuf<unsigned long long> chk;
   DevBuf<int64_t> lr_t0, lr_h0;
   DevBuf<uint32_t> lr_flags, lr_nwin;
   DevBuf<unsigned long long> long_count;
@@ -3489,6 +3527,22 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
       d.nfa_off = (uint32_t)nfa_blob.size();
       d.nfa_words = r.rx.nfa_words;
       nfa_blob.insert(nfa_blob.end(), r.rx.nfa.begin(), r.rx.nfa.end());
+    }
+    // DFA jobs of an anchored rule exist only once its single prefix literal
+    // matched at the start of rest (dfa_rule / plan_rule): when the literal is
+    // case-sensitive ASCII, k_dfa starts past it in the state it leads to
+    if (r.rx.mode == kModeAnchored && r.rx.anchor.size() == 1 && !(r.rx.flags & (kRuleNfa | kRuleAlways | kRuleNever)) &&
+        !getenv("BJX_NO_DFA_SKIP")) {
+      const PrefLit &al = r.rx.anchor[0];
+      bool ok = !al.s.empty() && al.s.size() < 0x10000;
+      uint32_t stt = r.rx.start;
+      for (size_t k = 0; ok && k < al.s.size(); ++k) {
+        const uint8_t c = (uint8_t)al.s[k];
+        if (c >= 0x80 || al.ci[k]) { ok = false; break; }
+        stt = r.rx.trans[(size_t)stt * r.rx.ncls + r.rx.ascii_cls[c]];
+        if (stt <= 1) ok = false;  // decided inside the literal: no skip
+      }
+      if (ok) { d.skip_len = (uint16_t)al.s.size(); d.skip_state = (uint16_t)stt; }
     }
   }
   std::vector<uint8_t> lit_chk;
@@ -4112,7 +4166,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   e->bn_best.release(); e->bn_rep.release(); e->bn_sel.release(); e->bn_ipb.release(); e->tz_at.release(); e->tz_off.release();
   e->rb_first.release(); e->rb_last.release(); e->long_heads.release(); e->long_count.release();
   e->lr_end.release(); e->lr_len.release(); e->lr_off.release(); e->lr_win.release(); e->lr_t0.release(); e->lr_h0.release();
-  e->lr_flags.release(); e->lr_nwin.release();
+  e->lr_flags.release(); e->lr_nwin.release(); e->chk.release();
   e->d_results.release(); e->q_out.release();
   e->ban_ips.release(); e->ban_log.release(); e->ban_off.release(); e->ban_kind.release(); e->ban_ipb.release();
   e->ban_ipo.release();
@@ -4251,6 +4305,8 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
     });
   }
   const uint64_t n_chunks = (n_ev + kApplyChunk - 1) / kApplyChunk;
+  const bool check = getenv("BJX_CHECK") != nullptr;
+  if (check) HIP_OK(hipMemsetAsync(e->ev_out_s.p, 0, n_ev, st));
   e->long_heads.ensure(n_chunks + 1);
   e->long_count.ensure(1);
   HIP_OK(hipMemsetAsync(e->long_count.p, 0, 8, st));
@@ -4287,6 +4343,24 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
                        e->ev_out_s.p, R);
     hipLaunchKernelGGL(k_long_fill, dim3(grid_for(total)), dim3(kBlock), 0, st, total, e->ev_rec2.p, B.rules, e->ev_out_s.p, R);
     HIP_OK(hipGetLastError());
+  }
+  if (check) {
+    e->chk.ensure(8);
+    HIP_OK(hipMemsetAsync(e->chk.p, 0, 64, st));
+    hipLaunchKernelGGL(k_check_rl, dim3(grid_for(std::max<uint64_t>(E.n, n_ev))), dim3(kBlock), 0, st, E, n_ev, ev_el, ev_rule,
+                       e->el_slot.p, e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_out_s.p, e->chk.p);
+    unsigned long long c[8];
+    HIP_OK(hipMemcpyAsync(c, e->chk.p, 64, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (c[0] || c[3] || c[6]) {
+      char msg[512];
+      snprintf(msg, sizeof msg,
+               "BJX_CHECK: %llu event lines with a wrong IP id (first line %llu id %llu), %llu events in a wrong state slot "
+               "(first %llu slot %llu), %llu unwritten outcomes (first %llu); epoch %u, %llu long runs, n_ev %llu",
+               c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], e->epoch, (unsigned long long)n_long, (unsigned long long)n_ev);
+      fprintf(stderr, "%s\n", msg);
+      throw BjxError(BJX_ERR_DEVICE, msg);
+    }
   }
 }
 

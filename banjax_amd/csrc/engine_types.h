@@ -28,6 +28,10 @@ struct DevRule {
   int64_t hits;
   uint32_t nfa_off;      // kRuleNfa: u64 index of the rule's tables in Bind::nfa
   uint32_t nfa_words;    // kRuleNfa: 64-bit words per state set (1, 2, 4, 8, 16)
+  // anchored rule whose single case-sensitive prefix literal is checked before
+  // a DFA job is made: k_dfa starts skip_len bytes in, in state skip_state
+  uint16_t skip_len;
+  uint16_t skip_state;
 };
 
 // Prefilter gram bitset: one bit per hash of a 4-byte window (LDS resident).

@@ -16,6 +16,8 @@
  *   bjx_state_get           RegexRateLimitStates.Get           internal/rate_limit.go:81-96
  *   bjx_state_len           RegexRateLimitStates.Len           internal/rate_limit.go:30-35
  *   bjx_state_dump          RegexRateLimitStates.String        internal/rate_limit.go:98-103,204-220
+ *   bjx_node_*              the same surface over every GPU of the host (one RegexRateLimitStates,
+ *                           banjax.go:80; one consumer goroutine, regex_rate_limiter.go:54-77)
  *   bjx_tailer_*            tail.TailFile(Follow, SeekEnd) + tailer.Lines in RunLogTailer
  *                           internal/regex_rate_limiter.go:21-78 (github.com/hpcloud/tail v1.0.0)
  *
