@@ -1340,6 +1340,21 @@ struct LinesArgs {
   uint32_t span_bytes;  // LDS staging per wave (0 = read lines from HBM)
   const uint32_t *list; // non-null: process only these lines (n_list of them), unstaged
   uint64_t n_list;
+  unsigned long long *prof;  // BJX_PROF_LINES: shader clocks per k_lines segment (k_lines<.., true>)
+};
+
+// k_lines<.., PROF = true>: wave clock (s_memtime) per loop segment, summed
+// over waves: 0 loads + staging, 1 header + timestamp, 2 host lookup, 3 host
+// rule words, 4 rule decisions, 5 per-line stores, 6 DFA-job flush
+struct LinesProf {
+  uint64_t t = 0;
+  uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
+  __device__ __forceinline__ void start() { t = __builtin_amdgcn_s_memtime(); }
+  __device__ __forceinline__ void mark(int k) {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    acc[k] += now - t;
+    t = now;
+  }
 };
 
 // consumeLine up to the rule loop for line j (bytes at base + (s - origin)):
@@ -1349,10 +1364,10 @@ struct LinesArgs {
 // compiler cannot merge the two call sites into one generic-pointer copy)
 // cc / cv: the line's scan-pass hit count and hit slots, loaded by the caller
 // ahead of the staging barrier
-template <bool STAGED>
+template <bool STAGED, bool PROF = false>
 __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const LinesArgs &A, const uint8_t *base,
                                           uint64_t origin, uint64_t s, uint32_t n, uint64_t j, const JobSink &S,
-                                          uint32_t cc, const uint64_t (&cv)[kCandSlots]) {
+                                          uint32_t cc, const uint64_t (&cv)[kCandSlots], LinesProf &P) {
   const Lines &L = A.L;
   const uint8_t *p = base + (s - origin);
   uint32_t sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
@@ -1363,9 +1378,12 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
   bool slow = false;
   if (ns >= 4) {
     slow = parse_float_fast(p, sp0, &f) != 0;
+    if (PROF) P.mark(1);
     if (!slow) {
       hid = (A.dbg & 8) ? -1 : host_lookup_slots(B, p + sp2 + 1, sp3 - sp2 - 1);
+      if (PROF) { __builtin_amdgcn_s_waitcnt(0); P.mark(2); }
       H = host_rules(B, hid);
+      if (PROF) { __builtin_amdgcn_s_waitcnt(0); P.mark(3); }
       slow = (H.s_end - H.s_begin) + B.n_global > 128;
     }
   }
@@ -1415,6 +1433,7 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
         decide_rules<true>(B, TB, p + rest_off, n - rest_off, hid, H, lits, lpos, (A.dbg & 2) ? 0u : nlit,
                            cc > (uint32_t)kCandSlots, j, L, S, A.dbg);
     }
+    if (PROF) { __builtin_amdgcn_s_waitcnt(0); P.mark(4); }
     if (A.dbg & 64) return;  // timing experiment: no per-line stores
     L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
     L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
@@ -1423,14 +1442,16 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
     L.ip16[j] = ip_key16(p + ip_off, ip_len);
     L.ts[j] = tsn;
     L.flags[j] = fl;
+    if (PROF) { __builtin_amdgcn_s_waitcnt(0); P.mark(5); }
   }
 }
 
 // consumeLine up to the rule loop, one lane per line (regex_rate_limiter.go:113-214):
 // SplitN header, parseTimestamp fast path, host lookup, CheckIsAllowed, OldLine,
 // then the rule decisions from the scan pass's literal hits (DFA work to k_dfa).
-template <bool IMG_LDS>
+template <bool IMG_LDS, bool PROF = false>
 __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
+  LinesProf P;
   uint8_t *s_img = s_dyn;
   if (IMG_LDS) {
     for (uint32_t i = threadIdx.x; i < B.img_bytes / 16; i += blockDim.x)
@@ -1456,6 +1477,7 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t n_work = A.list ? A.n_list : A.n_lines;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + wave * 64u; base < n_work; base += stride) {
+    if (PROF) P.start();
     const uint64_t j = A.list ? (base + lane < n_work ? A.list[base + lane] : A.n_lines) : base + lane;
     const uint64_t jl = min(base + 63, A.n_lines - 1);
     const uint64_t s0 = base ? A.nl[base - 1] + 1 : 0;
@@ -1502,11 +1524,13 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
       }
       wave_sync();
     }
+    if (PROF) { __builtin_amdgcn_s_waitcnt(0); P.mark(0); }
     if (j < A.n_lines) {
       // two inlined copies: LDS addressing for staged waves, global otherwise
-      if (staged) line_body<true>(B, TB, A, span, b16, s, n, j, S, cc, cv);
-      else line_body<false>(B, TB, A, A.buf, 0, s, n, j, S, cc, cv);
+      if (staged) line_body<true, PROF>(B, TB, A, span, b16, s, n, j, S, cc, cv, P);
+      else line_body<false, PROF>(B, TB, A, A.buf, 0, s, n, j, S, cc, cv, P);
     }
+    if (PROF) P.t = __builtin_amdgcn_s_memtime();
     // ---- append this wave's DFA jobs (one global atomic per 64 lines)
     wave_sync();
     const uint32_t nj = min(*S.cnt, kWaveJobs);
@@ -1520,7 +1544,10 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
     wave_sync();
     if (lane == 0) *S.cnt = 0;
     wave_sync();
+    if (PROF) { __builtin_amdgcn_s_waitcnt(0); P.mark(6); }
   }
+  if (PROF && lane == 0)
+    for (int k = 0; k < 7; ++k) atomicAdd(&A.prof[k], (unsigned long long)P.acc[k]);
 }
 
 // Rule decisions of the lines whose header the scan pass parsed (one lane per
@@ -4516,6 +4543,8 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   HIP_OK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, e->device));
   if (!e->lines_attr) {
     for (const void *f : {reinterpret_cast<const void *>(&k_lines<true>), reinterpret_cast<const void *>(&k_lines<false>),
+                          reinterpret_cast<const void *>(&k_lines<true, true>),
+                          reinterpret_cast<const void *>(&k_lines<false, true>),
                           reinterpret_cast<const void *>(&k_rules<true>), reinterpret_cast<const void *>(&k_rules<false>)})
       HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScanLdsMax));
     e->lines_attr = true;
@@ -4535,7 +4564,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     A.slow_list = e->slow_list.p; A.slow_count = e->scalars.p;
     A.jline = e->jline.p; A.jkey = e->jkey.p; A.job_count = e->scalars.p + 11; A.job_cap = std::min(e->jline.n, e->jkey.n);
     A.span_bytes = getenv("BJX_SPAN_BYTES") ? (uint32_t)atoi(getenv("BJX_SPAN_BYTES")) & ~15u : kSpanBytes;
-    A.list = nullptr; A.n_list = 0;
+    A.list = nullptr; A.n_list = 0; A.prof = nullptr;
     unsigned long long n_todo = 0;
     if (scan_hdr) {
       RulesArgs R;
@@ -4560,7 +4589,23 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
                            (kBlock / 64) * (kWaveJobs * 8 + 16 + (A.span_bytes ? A.span_bytes + 32 : 0));
       const void *fn = img_lds ? reinterpret_cast<const void *>(&k_lines<true>) : reinterpret_cast<const void *>(&k_lines<false>);
       const unsigned grid = resident_grid(fn, lds, A.list ? A.n_list : n_lines);
-      if (img_lds) hipLaunchKernelGGL(k_lines<true>, dim3(grid), dim3(kBlock), lds, st, B, A);
+      const bool prof = getenv("BJX_PROF_LINES") != nullptr;
+      A.prof = nullptr;
+      if (prof) {  // debugging aid: clock per k_lines segment, printed to stderr
+        e->chk.ensure(8);
+        HIP_OK(hipMemsetAsync(e->chk.p, 0, 64, st));
+        A.prof = e->chk.p;
+        if (img_lds) hipLaunchKernelGGL((k_lines<true, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
+        else hipLaunchKernelGGL((k_lines<false, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
+        unsigned long long c[8];
+        HIP_OK(hipMemcpyAsync(c, e->chk.p, 64, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        double tot = 0;
+        for (int k = 0; k < 7; ++k) tot += (double)c[k];
+        fprintf(stderr, "[bjx] k_lines segments (%% of wave clocks): loads+staging %.1f header %.1f host %.1f host-rules %.1f "
+                "decide %.1f stores %.1f jobs %.1f\n", 100 * c[0] / tot, 100 * c[1] / tot, 100 * c[2] / tot, 100 * c[3] / tot,
+                100 * c[4] / tot, 100 * c[5] / tot, 100 * c[6] / tot);
+      } else if (img_lds) hipLaunchKernelGGL(k_lines<true>, dim3(grid), dim3(kBlock), lds, st, B, A);
       else hipLaunchKernelGGL(k_lines<false>, dim3(grid), dim3(kBlock), lds, st, B, A);
       HIP_OK(hipGetLastError());
     }
