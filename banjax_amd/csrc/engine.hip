@@ -534,6 +534,8 @@ constexpr uint32_t kWaveLds = kTileLds + kLineCap * (2 + 2) + kCandList * 4 + kL
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kScanLdsMax = 160 * 1024;  // gfx950 LDS per CU (one scan block per CU)
 constexpr uint32_t kLinesImgMax = 16 * 1024;  // k_lines copies the lookup image to LDS up to this size
+constexpr uint32_t kLinesHostLdsMax = 6 * 1024;  // k_lines copies the compact host dictionary up to this size
+constexpr uint32_t kLinesBlocksPerCu = 3;       // k_lines' LDS budget: 3 blocks of 4 waves per CU
 constexpr uint32_t kRulesImgMax = 48 * 1024;  // k_rules likewise (no line staging: 3+ blocks per CU)
 constexpr uint32_t kSpanBytes = 12 * 1024;    // k_lines: bytes of 64 lines staged per wave
 
@@ -669,6 +671,30 @@ __device__ __forceinline__ int32_t host_lookup_slots(const Bind &B, const uint8_
       }
     }
     s = (s + 1) & (B.ht_cap - 1);
+  }
+}
+
+// host id from the LDS copy of Bind::hl (k_lines)
+__device__ __forceinline__ int32_t host_lookup_lds(const uint32_t *hl, const uint8_t *h, uint32_t n) {
+  const uint32_t cap = hl[0], nh = hl[1];
+  const uint2 *slots = reinterpret_cast<const uint2 *>(hl + 2);
+  const uint32_t *offs = hl + 2 + 2 * cap;
+  const uint8_t *bytes = reinterpret_cast<const uint8_t *>(hl + 2 + 2 * cap + nh);
+  const uint64_t hh = hash_bytes(h, n);
+  const uint32_t tag = (uint32_t)(hh >> 32) | 1u;
+  uint32_t s = (uint32_t)hh & (cap - 1);
+  for (;;) {
+    const uint2 e = slots[s];
+    if (e.x == 0) return -1;
+    if (e.x == tag && (e.y & 0xFFFFu) == n) {
+      const uint32_t hid = e.y >> 16;
+      const uint8_t *q = bytes + offs[hid];
+      uint32_t diff = 0, i = 0;
+      for (; i + 4 <= n; i += 4) diff |= ld4(h + i) ^ ld4(q + i);
+      if (i < n) diff |= (ld4(h + i) ^ ld4(q + i)) & ((1u << (8 * (n - i))) - 1u);
+      if (!diff) return (int32_t)hid;
+    }
+    s = (s + 1) & (cap - 1);
   }
 }
 
@@ -1364,10 +1390,11 @@ struct LinesProf {
 // compiler cannot merge the two call sites into one generic-pointer copy)
 // cc / cv: the line's scan-pass hit count and hit slots, loaded by the caller
 // ahead of the staging barrier
-template <bool STAGED, bool PROF = false>
+template <bool STAGED, bool PROF = false, bool HOST_LDS = false>
 __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const LinesArgs &A, const uint8_t *base,
                                           uint64_t origin, uint64_t s, uint32_t n, uint64_t j, const JobSink &S,
-                                          uint32_t cc, const uint64_t (&cv)[kCandSlots], LinesProf &P) {
+                                          uint32_t cc, const uint64_t (&cv)[kCandSlots], LinesProf &P,
+                                          const uint32_t *hl) {
   const Lines &L = A.L;
   const uint8_t *p = base + (s - origin);
   uint32_t sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
@@ -1380,7 +1407,8 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
     slow = parse_float_fast(p, sp0, &f) != 0;
     if (PROF) P.mark(1);
     if (!slow) {
-      hid = (A.dbg & 8) ? -1 : host_lookup_slots(B, p + sp2 + 1, sp3 - sp2 - 1);
+      hid = (A.dbg & 8) ? -1
+            : HOST_LDS ? host_lookup_lds(hl, p + sp2 + 1, sp3 - sp2 - 1) : host_lookup_slots(B, p + sp2 + 1, sp3 - sp2 - 1);
       if (PROF) { __builtin_amdgcn_s_waitcnt(0); P.mark(2); }
       H = host_rules(B, hid);
       if (PROF) { __builtin_amdgcn_s_waitcnt(0); P.mark(3); }
@@ -1449,7 +1477,7 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
 // consumeLine up to the rule loop, one lane per line (regex_rate_limiter.go:113-214):
 // SplitN header, parseTimestamp fast path, host lookup, CheckIsAllowed, OldLine,
 // then the rule decisions from the scan pass's literal hits (DFA work to k_dfa).
-template <bool IMG_LDS, bool PROF = false>
+template <bool IMG_LDS, bool PROF = false, bool HOST_LDS = false>
 __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
   LinesProf P;
   uint8_t *s_img = s_dyn;
@@ -1460,8 +1488,15 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
   }
   const Tabs TB = make_tabs(IMG_LDS ? s_img : B.img, B.il);
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // the compact host dictionary after the image (host lookups from LDS)
+  const uint32_t img_al = (IMG_LDS ? B.img_bytes : 0) + 15u & ~15u, hl_al = HOST_LDS ? B.hl_bytes + 15u & ~15u : 0u;
+  uint32_t *s_hl = reinterpret_cast<uint32_t *>(s_dyn + img_al);
+  if (HOST_LDS) {
+    for (uint32_t i = threadIdx.x; i < B.hl_bytes / 4; i += blockDim.x) s_hl[i] = B.hl[i];
+    __syncthreads();
+  }
   JobSink S;
-  S.lds = reinterpret_cast<uint2 *>(s_dyn + ((IMG_LDS ? B.img_bytes : 0) + 15u & ~15u) + wave * (kWaveJobs * 8 + 16));
+  S.lds = reinterpret_cast<uint2 *>(s_dyn + img_al + hl_al + wave * (kWaveJobs * 8 + 16));
   S.cnt = reinterpret_cast<uint32_t *>(S.lds + kWaveJobs);
   S.jline = A.jline;
   S.jkey = A.jkey;
@@ -1472,8 +1507,7 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
   const Lines &L = A.L;
   // this wave's 64 lines, staged whole in LDS with coalesced 16 B loads when
   // they span at most kSpanBytes (otherwise read from HBM per lane)
-  uint8_t *span = s_dyn + ((IMG_LDS ? B.img_bytes : 0) + 15u & ~15u) + (kBlock / 64) * (kWaveJobs * 8 + 16) +
-                  wave * (A.span_bytes + 32);
+  uint8_t *span = s_dyn + img_al + hl_al + (kBlock / 64) * (kWaveJobs * 8 + 16) + wave * (A.span_bytes + 32);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t n_work = A.list ? A.n_list : A.n_lines;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + wave * 64u; base < n_work; base += stride) {
@@ -1527,8 +1561,8 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
     if (PROF) { __builtin_amdgcn_s_waitcnt(0); P.mark(0); }
     if (j < A.n_lines) {
       // two inlined copies: LDS addressing for staged waves, global otherwise
-      if (staged) line_body<true, PROF>(B, TB, A, span, b16, s, n, j, S, cc, cv, P);
-      else line_body<false, PROF>(B, TB, A, A.buf, 0, s, n, j, S, cc, cv, P);
+      if (staged) line_body<true, PROF, HOST_LDS>(B, TB, A, span, b16, s, n, j, S, cc, cv, P, s_hl);
+      else line_body<false, PROF, HOST_LDS>(B, TB, A, A.buf, 0, s, n, j, S, cc, cv, P, s_hl);
     }
     if (PROF) P.t = __builtin_amdgcn_s_memtime();
     // ---- append this wave's DFA jobs (one global atomic per 64 lines)
@@ -3650,6 +3684,36 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     hs.off = hd_off[i];
     memcpy(hs.inl, hd_bytes.data() + hd_off[i], std::min<uint32_t>(hd_len[i], 48));
   }
+  // compact host dictionary for k_lines' LDS (host_lookup_lds)
+  std::vector<uint32_t> hl;
+  {
+    size_t nbytes = 0;
+    bool ok = n_hosts < 0xFFFF;
+    for (uint32_t h = 0; h < n_hosts; ++h) {
+      ok = ok && host_by_id[h].size() < 0xFFFF;
+      nbytes += ((host_by_id[h].size() + 3) & ~size_t(3)) + 4;
+    }
+    const size_t words = 2 + 2 * (size_t)ht_cap + n_hosts + nbytes / 4;
+    if (ok && n_hosts && words * 4 <= kLinesHostLdsMax && !getenv("BJX_NO_HOST_LDS")) {
+      hl.assign(words, 0);
+      hl[0] = ht_cap;
+      hl[1] = n_hosts;
+      for (uint32_t sl = 0; sl < ht_cap; ++sl)
+        if (hslot[sl].tag) {
+          hl[2 + 2 * sl] = hslot[sl].tag;
+          hl[2 + 2 * sl + 1] = ((uint32_t)hslot[sl].id << 16) | hslot[sl].len;
+        }
+      uint8_t *by = reinterpret_cast<uint8_t *>(hl.data() + 2 + 2 * ht_cap + n_hosts);
+      uint32_t o = 0;
+      for (uint32_t h = 0; h < n_hosts; ++h) {
+        hl[2 + 2 * ht_cap + h] = o;
+        memcpy(by + o, host_by_id[h].data(), host_by_id[h].size());
+        o += (uint32_t)(((host_by_id[h].size() + 3) & ~size_t(3)) + 4);
+      }
+    }
+  }
+  const uint32_t hl_bytes = (uint32_t)(hl.size() * 4);
+  if (hl.empty()) hl.push_back(0);
   std::vector<int32_t> host_scope(n_hosts, -1);
   for (auto &s : scope_of_site) host_scope[hosts[s.first]] = s.second;
   std::vector<uint64_t> skip;
@@ -3931,7 +3995,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
          o_dsq = bb.add(dfa_site_q), o_dgq = bb.add(dfa_glob_q),
          o_ps = bb.add(pref_site), o_pg = bb.add(pref_glob), o_hslot = bb.add(hslot), o_lh = bb.add(lh_tab),
          o_nfa = bb.add(nfa_blob), o_lrf = bb.add(lr_full), o_plan = bb.add(plan), o_plo = bb.add(plan_off),
-         o_plg = bb.add(plan_glob);
+         o_plg = bb.add(plan_glob), o_hl = bb.add(hl);
   e->bind_blob.ensure(bb.bytes.size());
   HIP_OK(hipMemcpy(e->bind_blob.p, bb.bytes.data(), bb.bytes.size(), hipMemcpyHostToDevice));
   uint8_t *base = e->bind_blob.p;
@@ -3989,6 +4053,8 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.lr_full = reinterpret_cast<const uint32_t *>(base + o_lrf);
   B.lh_tab = reinterpret_cast<const uint4 *>(base + o_lh);
   B.lh_cap = lh_cap;
+  B.hl = reinterpret_cast<const uint32_t *>(base + o_hl);
+  B.hl_bytes = hl_bytes;
   B.plan = reinterpret_cast<const uint4 *>(base + o_plan);
   B.plan_off = reinterpret_cast<const uint32_t *>(base + o_plo);
   B.plan_glob = reinterpret_cast<const uint4 *>(base + o_plg);
@@ -4545,6 +4611,10 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     for (const void *f : {reinterpret_cast<const void *>(&k_lines<true>), reinterpret_cast<const void *>(&k_lines<false>),
                           reinterpret_cast<const void *>(&k_lines<true, true>),
                           reinterpret_cast<const void *>(&k_lines<false, true>),
+                          reinterpret_cast<const void *>(&k_lines<true, false, true>),
+                          reinterpret_cast<const void *>(&k_lines<false, false, true>),
+                          reinterpret_cast<const void *>(&k_lines<true, true, true>),
+                          reinterpret_cast<const void *>(&k_lines<false, true, true>),
                           reinterpret_cast<const void *>(&k_rules<true>), reinterpret_cast<const void *>(&k_rules<false>)})
       HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScanLdsMax));
     e->lines_attr = true;
@@ -4585,9 +4655,22 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     }
     if (!scan_hdr || n_todo) {
       const bool img_lds = B.img_bytes <= kLinesImgMax;
-      const uint32_t lds = ((img_lds ? B.img_bytes : 0) + 15u & ~15u) +
-                           (kBlock / 64) * (kWaveJobs * 8 + 16 + (A.span_bytes ? A.span_bytes + 32 : 0));
-      const void *fn = img_lds ? reinterpret_cast<const void *>(&k_lines<true>) : reinterpret_cast<const void *>(&k_lines<false>);
+      const bool host_lds = B.hl_bytes != 0;
+      const uint32_t fixed = ((img_lds ? B.img_bytes : 0) + 15u & ~15u) + (host_lds ? B.hl_bytes + 15u & ~15u : 0u) +
+                             (kBlock / 64) * (kWaveJobs * 8 + 16);
+      if (A.span_bytes && !getenv("BJX_SPAN_BYTES")) {
+        // spans take what kLinesBlocksPerCu blocks leave of the CU's LDS
+        // (LDS goes to blocks in granules: 53 KB blocks fit only twice per CU,
+        // measured; stay a 2 KB granule under the share)
+        const uint32_t share = (kScanLdsMax / kLinesBlocksPerCu) & ~2047u;
+        const uint32_t room = share > fixed ? share - fixed : 0u;
+        A.span_bytes = std::min<uint32_t>(kSpanBytes, (room / (kBlock / 64) - 32) & ~15u);
+      }
+      const uint32_t lds = fixed + (kBlock / 64) * (A.span_bytes ? A.span_bytes + 32 : 0);
+      const void *fn = img_lds ? (host_lds ? reinterpret_cast<const void *>(&k_lines<true, false, true>)
+                                           : reinterpret_cast<const void *>(&k_lines<true>))
+                               : (host_lds ? reinterpret_cast<const void *>(&k_lines<false, false, true>)
+                                           : reinterpret_cast<const void *>(&k_lines<false>));
       const unsigned grid = resident_grid(fn, lds, A.list ? A.n_list : n_lines);
       const bool prof = getenv("BJX_PROF_LINES") != nullptr;
       A.prof = nullptr;
@@ -4595,7 +4678,9 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
         e->chk.ensure(8);
         HIP_OK(hipMemsetAsync(e->chk.p, 0, 64, st));
         A.prof = e->chk.p;
-        if (img_lds) hipLaunchKernelGGL((k_lines<true, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
+        if (img_lds && host_lds) hipLaunchKernelGGL((k_lines<true, true, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
+        else if (img_lds) hipLaunchKernelGGL((k_lines<true, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
+        else if (host_lds) hipLaunchKernelGGL((k_lines<false, true, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
         else hipLaunchKernelGGL((k_lines<false, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
         unsigned long long c[8];
         HIP_OK(hipMemcpyAsync(c, e->chk.p, 64, hipMemcpyDeviceToHost, st));
@@ -4605,7 +4690,9 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
         fprintf(stderr, "[bjx] k_lines segments (%% of wave clocks): loads+staging %.1f header %.1f host %.1f host-rules %.1f "
                 "decide %.1f stores %.1f jobs %.1f\n", 100 * c[0] / tot, 100 * c[1] / tot, 100 * c[2] / tot, 100 * c[3] / tot,
                 100 * c[4] / tot, 100 * c[5] / tot, 100 * c[6] / tot);
-      } else if (img_lds) hipLaunchKernelGGL(k_lines<true>, dim3(grid), dim3(kBlock), lds, st, B, A);
+      } else if (img_lds && host_lds) hipLaunchKernelGGL((k_lines<true, false, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
+      else if (img_lds) hipLaunchKernelGGL(k_lines<true>, dim3(grid), dim3(kBlock), lds, st, B, A);
+      else if (host_lds) hipLaunchKernelGGL((k_lines<false, false, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
       else hipLaunchKernelGGL(k_lines<false>, dim3(grid), dim3(kBlock), lds, st, B, A);
       HIP_OK(hipGetLastError());
     }

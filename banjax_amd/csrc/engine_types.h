@@ -174,6 +174,11 @@ struct Bind {
   // line loads its host's entries side by side instead of walking the
   // literal -> rule tables.  Site entries of host h: [plan_off[h],
   // plan_off[h + 1]); global entries (position = nsite + g): plan_glob.
+  // compact host dictionary for LDS (k_lines): {cap, n_hosts}, cap x {tag,
+  // host id << 16 | len}, n_hosts byte offsets, the host bytes (4-byte padded);
+  // hl_bytes = 0 when it does not fit kLinesHostLdsMax
+  const uint32_t *hl;
+  uint32_t hl_bytes;
   const uint4 *plan;
   const uint32_t *plan_off;  // n_hosts + 1
   const uint4 *plan_glob;
