@@ -13,7 +13,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 ARCH = os.environ.get("BJX_OFFLOAD_ARCH", "gfx950")
-COMMON = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "--offload-arch=%s" % ARCH,
+# BJX_PROF=1: also compile the k_lines segment-clock variants (BJX_PROF_LINES)
+PROF = ["-DBJX_PROF"] if os.environ.get("BJX_PROF") == "1" else []
+COMMON = PROF + ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "--offload-arch=%s" % ARCH,
           "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result"]
 
 TARGETS = {
@@ -31,18 +33,32 @@ def _stale(out, srcs):
 
 
 def build(force: bool = False, verbose: bool = False):
+    """Each source compiles to its own object (in parallel, only when stale),
+    then one link: editing engine.hip does not recompile the host-only sources."""
     os.makedirs(LIBDIR, exist_ok=True)
+    objdir = os.path.join(HERE, "build")
+    os.makedirs(objdir, exist_ok=True)
     for out, srcs in TARGETS.items():
         srcs = [os.path.join(CSRC, s) for s in srcs]
         dst = os.path.join(LIBDIR, out)
-        if not force and not _stale(dst, srcs):
-            continue
-        cmd = ["hipcc"] + COMMON + ["-o", dst] + srcs
-        if verbose:
-            print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
+        objs, procs = [], []
+        for s in srcs:
+            o = os.path.join(objdir, os.path.basename(s) + ".o")
+            objs.append(o)
+            if force or _stale(o, [s]):
+                cmd = ["hipcc"] + [f for f in COMMON if f != "-shared"] + ["-c", "-o", o, s]
+                if verbose:
+                    print(" ".join(cmd), flush=True)
+                procs.append((subprocess.Popen(cmd), cmd))
+        for pr, cmd in procs:
+            if pr.wait() != 0:
+                raise subprocess.CalledProcessError(pr.returncode, cmd)
+        if force or procs or _stale(dst, objs):
+            cmd = ["hipcc"] + COMMON + ["-o", dst] + objs
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
     return LIBDIR
-
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)

@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <tuple>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -535,6 +536,7 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kScanLdsMax = 160 * 1024;  // gfx950 LDS per CU (one scan block per CU)
 constexpr uint32_t kLinesImgMax = 16 * 1024;  // k_lines copies the lookup image to LDS up to this size
 constexpr uint32_t kLinesHostLdsMax = 6 * 1024;  // k_lines copies the compact host dictionary up to this size
+constexpr uint32_t kLinesTabLdsMax = 10 * 1024;  // ... and the plan classes after it, up to this size in all
 constexpr uint32_t kLinesBlocksPerCu = 3;       // k_lines' LDS budget: 3 blocks of 4 waves per CU
 constexpr uint32_t kRulesImgMax = 48 * 1024;  // k_rules likewise (no line staging: 3+ blocks per CU)
 constexpr uint32_t kSpanBytes = 12 * 1024;    // k_lines: bytes of 64 lines staged per wave
@@ -1022,6 +1024,134 @@ __device__ __forceinline__ void decide_plan(const Bind &B, const Tabs &T, const 
   L.counts[j] = ((uint64_t)nres << 32) | nev;
 }
 
+// ---- plan classes in LDS (k_lines<.., HOST_LDS>, Bind::lt_*).  Hosts whose
+// site plans are equal once (a) a host-specific literal F = A + host + C
+// becomes a template (A, C) checked around the line's own host field and (b)
+// a host-specific rule becomes "the host's rule at this position" share one
+// class of entries, so a whole per-site rule set sits in a few hundred bytes of
+// LDS next to the host dictionary.
+constexpr uint32_t kPlanLitT = 4;     // kPlanLit whose host-split full literal is a template
+constexpr uint32_t kPlanAnchorT = 5;  // kPlanAnchor whose single anchor literal is a template
+constexpr uint32_t kPlanOwn = 0x80000000u;  // entry word a.x: rule = host's first site rule + position
+
+struct LdsTabs {
+  const uint2 *hinfo;   // per host: {class entry offset | entries << 16, first site rule}
+  const uint4 *cls;     // class entries (2 x uint4 each, as Bind::plan)
+  const uint4 *trec;    // templates: {|A| | |C| << 8 | side << 16, A offset, C offset, 0}
+  const uint8_t *pool;  // template bytes (4-byte padded + 4), each followed by its case mask
+};
+
+// len bytes at text equal the pool string at p (case mask after the padded bytes)
+__device__ __forceinline__ bool pool_eq(const uint8_t *p, uint32_t len, const uint8_t *text) {
+  const uint8_t *cm = p + ((len + 3) & ~3u) + 4;
+  uint32_t i = 0;
+  for (; i + 4 <= len; i += 4)
+    if ((ld4(text + i) | ld4(cm + i)) != ld4(p + i)) return false;
+  if (i < len) {
+    const uint32_t m = (1u << (8 * (len - i))) - 1u;
+    if (((ld4(text + i) | ld4(cm + i)) ^ ld4(p + i)) & m) return false;
+  }
+  return true;
+}
+
+// template t = (A, C) occurs in rest at fs as A + host + C, the host being the
+// line's own host field (host_rel, host_len: the host lookup matched it exactly)
+__device__ __forceinline__ bool tmpl_at(const LdsTabs &LT, uint32_t t, const uint8_t *rest, uint32_t rest_len,
+                                        uint32_t host_rel, uint32_t host_len, int32_t fs) {
+  const uint4 rec = LT.trec[t];
+  const uint32_t la = rec.x & 0xFF, lc = (rec.x >> 8) & 0xFF;
+  if (fs < 0) return false;
+  const uint32_t hs = (uint32_t)fs + la, he = hs + host_len;
+  if (he + lc > rest_len) return false;
+  if (!pool_eq(LT.pool + rec.z, lc, rest + he)) return false;
+  if (!pool_eq(LT.pool + rec.y, la, rest + fs)) return false;
+  if (hs == host_rel) return true;
+  // the host spelled somewhere else in rest: compare with the host field
+  uint32_t diff = 0, i = 0;
+  for (; i + 4 <= host_len; i += 4) diff |= ld4(rest + hs + i) ^ ld4(rest + host_rel + i);
+  if (i < host_len) diff |= (ld4(rest + hs + i) ^ ld4(rest + host_rel + i)) & ((1u << (8 * (host_len - i))) - 1u);
+  return diff == 0;
+}
+
+// one class entry (a, b) of the line's host: template kinds here, the others
+// by plan_rule once an own-rule entry names its rule
+template <bool EMIT>
+__device__ __forceinline__ void plan_rule_lds(const Bind &B, const Tabs &T, const LdsTabs &LT, uint4 a, const uint4 b,
+                                              uint32_t first_rule, const uint8_t *rest, uint32_t rest_len, uint32_t host_rel,
+                                              uint32_t host_len, uint64_t lits, uint64_t lpos, uint32_t nlit, bool ovf,
+                                              uint64_t &m0, uint64_t &m1, uint64_t j, const JobSink &S) {
+  const uint32_t pos = (a.x >> 20) & 0x7Fu, kind = (a.x >> 27) & 7u;
+  if (a.x & kPlanOwn) a.x = (a.x & 0x7FF00000u) | ((first_rule + pos) & 0xFFFFFu);
+  const uint32_t r = a.x & 0xFFFFFu;
+  const bool eq = ((a.x >> 30) & 1u) != 0;
+  if (kind == kPlanAnchorT) {
+    if (!tmpl_at(LT, a.w, rest, rest_len, host_rel, host_len, 0)) return;
+    if (eq) set_pos(m0, m1, pos);
+    else dfa_rule<EMIT>(B, T, r, pos, false, rest, rest_len, m0, m1, j, S);
+    return;
+  }
+  if (kind != kPlanLitT) {
+    plan_rule<EMIT>(B, T, a, b, 0, rest, rest_len, lits, lpos, nlit, ovf, m0, m1, j, S);
+    return;
+  }
+  // the rule requires F = A + host + C; its prefilter literal is the piece A
+  // (side 0: F starts at the hit) or C (side 1: the host ends at the hit)
+  if (ovf) {
+    dfa_rule<EMIT>(B, T, r, pos, false, rest, rest_len, m0, m1, j, S);
+    return;
+  }
+  const uint4 rec = LT.trec[a.w];
+  const uint32_t la = rec.x & 0xFF;
+  const bool side_c = ((rec.x >> 16) & 1u) != 0;
+  for (uint32_t c = 0; c < nlit; ++c) {
+    const uint32_t lit = (uint32_t)(lits >> (16 * c)) & 0xFFFFu;
+    if (lit != (a.y & 0xFFFFu) && lit != (a.y >> 16) && lit != (a.z & 0xFFFFu) && lit != (a.z >> 16)) continue;
+    const uint32_t hp = (uint32_t)(lpos >> (16 * c)) & 0xFFFFu;
+    if (hp == 0xFFFFu) {  // hit offset unknown: the automaton decides
+      dfa_rule<EMIT>(B, T, r, pos, false, rest, rest_len, m0, m1, j, S);
+      return;
+    }
+    const int32_t fs = side_c ? (int32_t)hp - (int32_t)host_len - (int32_t)la : (int32_t)hp;
+    if (!tmpl_at(LT, a.w, rest, rest_len, host_rel, host_len, fs)) continue;
+    if (eq) set_pos(m0, m1, pos);
+    else dfa_rule<EMIT>(B, T, r, pos, false, rest, rest_len, m0, m1, j, S);
+    return;
+  }
+}
+
+// decide_plan with the host's site entries from its LDS class
+template <bool EMIT>
+__device__ __forceinline__ void decide_plan_lds(const Bind &B, const Tabs &T, const LdsTabs &LT, const uint8_t *rest,
+                                                uint32_t rest_len, uint32_t host_rel, uint32_t host_len, int32_t hid,
+                                                const HostRules &H, uint64_t lits, uint64_t lpos, uint32_t nlit, bool ovf,
+                                                uint64_t j, const Lines &L, const JobSink &S) {
+  const uint32_t nsite = H.s_end - H.s_begin;
+  uint64_t m0 = H.a0, m1 = H.a1;
+  if (hid >= 0) {
+    const uint2 hi = LT.hinfo[hid];
+    const uint32_t cb = hi.x & 0xFFFFu, ce = cb + (hi.x >> 16);
+    for (uint32_t i = cb; i < ce; ++i)
+      plan_rule_lds<EMIT>(B, T, LT, LT.cls[2 * i], LT.cls[2 * i + 1], hi.y, rest, rest_len, host_rel, host_len, lits, lpos,
+                          nlit, ovf, m0, m1, j, S);
+  }
+  for (uint32_t i = 0; i < B.n_plan_glob; ++i)
+    plan_rule<EMIT>(B, T, B.plan_glob[2 * i], B.plan_glob[2 * i + 1], nsite, rest, rest_len, lits, lpos, nlit, ovf, m0, m1, j,
+                    S);
+  uint64_t *mask = L.masks + j * B.mask_words;
+  mask[0] = m0;
+  if (B.mask_words > 1) mask[1] = m1;
+  const uint32_t nres = __popcll(m0) + __popcll(m1);
+  const uint32_t nev = __popcll(m0 & ~H.k0) + __popcll(m1 & ~H.k1);
+  L.counts[j] = ((uint64_t)nres << 32) | nev;
+}
+
+// 16 B per lane global -> LDS without a VGPR round trip (gfx950
+// global_load_lds_dwordx4): lane L's bytes land at lds + 16 L (lds wave-uniform)
+__device__ __forceinline__ void glds16(const void *g, void *lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                   (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+}
+
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -1454,7 +1584,15 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
         lpos |= (uint64_t)(q - rs < 0xFFFF ? (uint32_t)(q - rs) : 0xFFFFu) << (16 * nlit);
         lits |= (uint64_t)lit << (16 * nlit++);
       }
-      if (B.use_plan && !(A.dbg & 15))
+      if (HOST_LDS && B.lt_cls && !(A.dbg & 15)) {
+        LdsTabs LT;
+        LT.hinfo = reinterpret_cast<const uint2 *>(hl + B.lt_hinfo);
+        LT.cls = reinterpret_cast<const uint4 *>(hl + B.lt_cls);
+        LT.trec = reinterpret_cast<const uint4 *>(hl + B.lt_trec);
+        LT.pool = reinterpret_cast<const uint8_t *>(hl + B.lt_pool);
+        decide_plan_lds<true>(B, TB, LT, p + rest_off, n - rest_off, host_off - rest_off, host_len, hid, H, lits, lpos, nlit,
+                              cc > (uint32_t)kCandSlots, j, L, S);
+      } else if (B.use_plan && !(A.dbg & 15))
         decide_plan<true>(B, TB, p + rest_off, n - rest_off, hid, H, lits, lpos, nlit, cc > (uint32_t)kCandSlots, j, L, S,
                           A.dbg);
       else
@@ -1536,11 +1674,21 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
     }
     if (staged) {
       const uint32_t n16 = (uint32_t)((s1 + 16 - b16 + 15) >> 4);
-      for (uint32_t i = lane; i < n16; i += 64) {
+      // LDS-DMA: every 1 KB piece of the span in flight at once (the loads
+      // write LDS directly: wave-uniform base + lane x 16 B), one wait
+      for (uint32_t k = 0; k * 64 < n16; ++k) {
+        const uint32_t i = k * 64 + lane;
+        const uint64_t a = b16 + 16ull * i;
+        if (i < n16 && a + 16 <= A.n)
+          glds16(A.buf + a, span + 1024u * k);
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      // the batch's last bytes (zero past the end): one lane writes the tail piece
+      for (uint32_t i = lane; b16 + 16ull * n16 > A.n && i < n16; i += 64) {
         const uint64_t a = b16 + 16ull * i;
         uint4 v;
         if (a + 16 <= A.n) {
-          v = *reinterpret_cast<const uint4 *>(A.buf + a);
+          continue;
         } else {
           uint32_t w[4];
 #pragma unroll
@@ -3712,7 +3860,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
       }
     }
   }
-  const uint32_t hl_bytes = (uint32_t)(hl.size() * 4);
+  uint32_t hl_bytes = (uint32_t)(hl.size() * 4);
   if (hl.empty()) hl.push_back(0);
   std::vector<int32_t> host_scope(n_hosts, -1);
   for (auto &s : scope_of_site) host_scope[hosts[s.first]] = s.second;
@@ -3895,6 +4043,116 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   if (plan.empty()) plan.push_back(make_uint4(0, 0, 0, 0));
   if (plan_glob.empty()) plan_glob.push_back(make_uint4(0, 0, 0, 0));
 
+  // plan classes for k_lines' LDS (decide_plan_lds), appended to the host
+  // dictionary blob when both fit kLinesTabLdsMax
+  uint32_t lt_hinfo = 0, lt_cls = 0, lt_trec = 0, lt_pool = 0;
+  if (use_plan && hl_bytes && n_hosts && !getenv("BJX_NO_PLAN_LDS")) {
+    std::vector<uint2> hinfo(n_hosts, make_uint2(0, 0));
+    std::vector<uint4> cls, trec;
+    std::vector<uint8_t> pool;
+    std::map<std::vector<uint32_t>, uint32_t> cls_ids;
+    std::map<std::tuple<std::string, std::string, std::string, std::string, uint32_t>, uint32_t> tmpl_ids;
+    // F = A + host + C with the host spelled exactly once, case-sensitively:
+    // its template id (side 1: the prefilter piece is C), or -1
+    auto tmpl_of = [&](uint32_t lit, const std::string &h, uint32_t side) -> int32_t {
+      const std::string s((const char *)&lit_bytes[lit_off[lit]], lit_len[lit]);
+      const std::string ci((const char *)&lit_ci[lit_off[lit]], lit_len[lit]);
+      size_t at = std::string::npos, n_at = 0;
+      for (size_t i = 0; i + h.size() <= s.size(); ++i) {
+        bool eq = true, cs = true;
+        for (size_t k = 0; k < h.size() && eq; ++k) {
+          const uint8_t c = (uint8_t)h[k], lc = (c >= 'A' && c <= 'Z') ? (uint8_t)(c | 0x20) : c;
+          eq = ci[i + k] ? (uint8_t)s[i + k] == lc : (uint8_t)s[i + k] == c;
+          cs = cs && !ci[i + k];
+        }
+        if (!eq) continue;
+        ++n_at;
+        at = i;
+        if (!cs) n_at = 99;
+      }
+      if (n_at != 1 || h.empty()) return -1;
+      const std::string A = s.substr(0, at), Aci = ci.substr(0, at), C = s.substr(at + h.size()),
+                        Cci = ci.substr(at + h.size());
+      if (A.size() > 255 || C.size() > 255) return -1;
+      auto key = std::make_tuple(A, Aci, C, Cci, side);
+      auto it = tmpl_ids.find(key);
+      if (it != tmpl_ids.end()) return (int32_t)it->second;
+      auto put_str = [&](const std::string &b, const std::string &m) {
+        const uint32_t off = (uint32_t)pool.size(), pad = (uint32_t)((b.size() + 3) & ~size_t(3)) + 4;
+        pool.resize(off + 2 * pad, 0);
+        for (size_t k = 0; k < b.size(); ++k) {
+          pool[off + k] = (uint8_t)b[k];
+          pool[off + pad + k] = m[k] ? 0x20 : 0;
+        }
+        return off;
+      };
+      const uint32_t oa = put_str(A, Aci), oc = put_str(C, Cci);
+      const uint32_t id = (uint32_t)trec.size();
+      trec.push_back(make_uint4((uint32_t)A.size() | ((uint32_t)C.size() << 8) | (side << 16), oa, oc, 0));
+      tmpl_ids.emplace(key, id);
+      return (int32_t)id;
+    };
+    for (uint32_t h = 0; h < n_hosts; ++h) {
+      std::vector<uint4> ents;
+      const std::string &hn = host_by_id[h];
+      for (uint32_t k = 0; k < per_host[h].size() && k < 128; ++k) {
+        const uint32_t r = per_host[h][k];
+        const size_t at = ents.size();
+        plan_entry(r, k, ents);
+        if (ents.size() == at) continue;
+        uint4 &a = ents[at], &b = ents[at + 1];
+        const uint32_t kind = (a.x >> 27) & 7u;
+        const DevRule &d = drules[r];
+        if (kind == kPlanAnchor && d.anc_len == 1) {
+          const int32_t t = tmpl_of(rule_lits[d.anc_off], hn, 0);
+          if (t >= 0) {
+            a = make_uint4((a.x & ~(7u << 27)) | (kPlanAnchorT << 27), 0, 0, (uint32_t)t);
+            b = make_uint4(0, 0, 0, 0);
+          }
+        } else if (kind == kPlanLit && a.w != kNone) {
+          const uint32_t full = a.w >> 8, off = a.w & 0xFF, piece = rule_lits[d.lits_off];
+          const uint32_t side = off == 0 ? 0u : 1u;
+          const int32_t t = tmpl_of(full, hn, side);
+          // the piece must be all of A (side 0) or all of C (side 1)
+          const bool whole = t >= 0 && (side == 0 ? (trec[t].x & 0xFF) == lit_len[piece]
+                                                  : ((trec[t].x >> 8) & 0xFF) == lit_len[piece] &&
+                                                        off == (trec[t].x & 0xFF) + hn.size());
+          if (whole) {
+            a = make_uint4((a.x & ~(7u << 27)) | (kPlanLitT << 27), a.y, a.z, (uint32_t)t);
+            b = make_uint4(0, 0, 0, 0);
+          }
+        }
+        if (canon[r] == r && r == per_host[h][0] + k) a.x = (a.x & ~0xFFFFFu) | kPlanOwn;
+      }
+      std::vector<uint32_t> key;
+      for (auto &v : ents) { key.push_back(v.x); key.push_back(v.y); key.push_back(v.z); key.push_back(v.w); }
+      auto it = cls_ids.find(key);
+      uint32_t off;
+      if (it != cls_ids.end()) off = it->second;
+      else {
+        off = (uint32_t)(cls.size() / 2);
+        cls.insert(cls.end(), ents.begin(), ents.end());
+        cls_ids.emplace(key, off);
+      }
+      hinfo[h] = make_uint2(off | ((uint32_t)(ents.size() / 2) << 16), per_host[h].empty() ? 0u : per_host[h][0]);
+    }
+    const uint32_t w0 = ((uint32_t)hl.size() + 3) & ~3u, w_hi = w0, w_cls = (w_hi + 2 * n_hosts + 3) & ~3u,
+                   w_tr = w_cls + 4 * (uint32_t)cls.size(), w_pool = w_tr + 4 * (uint32_t)trec.size(),
+                   w_end = w_pool + (uint32_t)((pool.size() + 3) / 4);
+    if (cls.size() / 2 < 0xFFFF && (size_t)w_end * 4 <= kLinesTabLdsMax) {
+      hl.resize(w_end, 0);
+      memcpy(hl.data() + w_hi, hinfo.data(), hinfo.size() * 8);
+      if (!cls.empty()) memcpy(hl.data() + w_cls, cls.data(), cls.size() * 16);
+      if (!trec.empty()) memcpy(hl.data() + w_tr, trec.data(), trec.size() * 16);
+      if (!pool.empty()) memcpy(hl.data() + w_pool, pool.data(), pool.size());
+      hl_bytes = w_end * 4;
+      lt_hinfo = w_hi; lt_cls = w_cls; lt_trec = w_tr; lt_pool = w_pool;
+    }
+    if (getenv("BJX_DEBUG_IMG"))
+      fprintf(stderr, "[bjx] plan classes: %zu entries, %zu templates, pool %zu B, LDS tables %u B (%s)\n", cls.size() / 2,
+              trec.size(), pool.size(), w_end * 4, lt_cls ? "in LDS" : "too large");
+  }
+
   // allow scopes (decision.go:278-374): exact maps are last-writer-wins in
   // config order; Allow IPFilters hold every allow entry
   std::vector<std::vector<std::array<uint8_t, 16>>> sc_addrs(n_scopes);
@@ -3980,6 +4238,10 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   il.lcim = put(cm_al.data(), cm_al.size());
   il.lchk = put(lit_chk.data(), lit_chk.size());
   img.resize((img.size() + 15) & ~size_t(15), 0);
+  if (getenv("BJX_DEBUG_IMG"))
+    fprintf(stderr, "[bjx] image %zu B: gram table %u, gram entries %u, host table %u, literals %zu (recs %u, bytes %zu x2), "
+            "plan %zu entries, lit-rule ents %zu, hosts %zu\n", img.size(), il.ge - il.gt, il.ht - il.ge, il.lrec - il.ht,
+            img.size() - il.lrec, il.lbytes - il.lrec, lb_al.size(), plan.size() / 2, lr_ent.size(), hd.size());
 
   BlobBuilder bb;
   size_t o_rules = bb.add(drules), o_trans = bb.add(trans), o_ae = bb.add(ae), o_ascii = bb.add(ascii),
@@ -4055,6 +4317,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.lh_cap = lh_cap;
   B.hl = reinterpret_cast<const uint32_t *>(base + o_hl);
   B.hl_bytes = hl_bytes;
+  B.lt_hinfo = lt_hinfo; B.lt_cls = lt_cls; B.lt_trec = lt_trec; B.lt_pool = lt_pool;
   B.plan = reinterpret_cast<const uint4 *>(base + o_plan);
   B.plan_off = reinterpret_cast<const uint32_t *>(base + o_plo);
   B.plan_glob = reinterpret_cast<const uint4 *>(base + o_plg);
@@ -4609,12 +4872,14 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   HIP_OK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, e->device));
   if (!e->lines_attr) {
     for (const void *f : {reinterpret_cast<const void *>(&k_lines<true>), reinterpret_cast<const void *>(&k_lines<false>),
+#ifdef BJX_PROF
                           reinterpret_cast<const void *>(&k_lines<true, true>),
                           reinterpret_cast<const void *>(&k_lines<false, true>),
-                          reinterpret_cast<const void *>(&k_lines<true, false, true>),
-                          reinterpret_cast<const void *>(&k_lines<false, false, true>),
                           reinterpret_cast<const void *>(&k_lines<true, true, true>),
                           reinterpret_cast<const void *>(&k_lines<false, true, true>),
+#endif
+                          reinterpret_cast<const void *>(&k_lines<true, false, true>),
+                          reinterpret_cast<const void *>(&k_lines<false, false, true>),
                           reinterpret_cast<const void *>(&k_rules<true>), reinterpret_cast<const void *>(&k_rules<false>)})
       HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScanLdsMax));
     e->lines_attr = true;
@@ -4675,6 +4940,9 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       const bool prof = getenv("BJX_PROF_LINES") != nullptr;
       A.prof = nullptr;
       if (prof) {  // debugging aid: clock per k_lines segment, printed to stderr
+#ifndef BJX_PROF
+        throw BjxError(BJX_ERR_ARG, "BJX_PROF_LINES needs a library built with BJX_PROF=1");
+#else
         e->chk.ensure(8);
         HIP_OK(hipMemsetAsync(e->chk.p, 0, 64, st));
         A.prof = e->chk.p;
@@ -4690,6 +4958,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
         fprintf(stderr, "[bjx] k_lines segments (%% of wave clocks): loads+staging %.1f header %.1f host %.1f host-rules %.1f "
                 "decide %.1f stores %.1f jobs %.1f\n", 100 * c[0] / tot, 100 * c[1] / tot, 100 * c[2] / tot, 100 * c[3] / tot,
                 100 * c[4] / tot, 100 * c[5] / tot, 100 * c[6] / tot);
+#endif
       } else if (img_lds && host_lds) hipLaunchKernelGGL((k_lines<true, false, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
       else if (img_lds) hipLaunchKernelGGL(k_lines<true>, dim3(grid), dim3(kBlock), lds, st, B, A);
       else if (host_lds) hipLaunchKernelGGL((k_lines<false, false, true>), dim3(grid), dim3(kBlock), lds, st, B, A);

@@ -176,9 +176,13 @@ struct Bind {
   // plan_off[h + 1]); global entries (position = nsite + g): plan_glob.
   // compact host dictionary for LDS (k_lines): {cap, n_hosts}, cap x {tag,
   // host id << 16 | len}, n_hosts byte offsets, the host bytes (4-byte padded);
-  // hl_bytes = 0 when it does not fit kLinesHostLdsMax
+  // hl_bytes = 0 when it does not fit kLinesHostLdsMax.  When lt_cls != 0 the
+  // same blob goes on with the plan classes (decide_plan_lds), word offsets:
+  // lt_hinfo (uint2 per host), lt_cls (class entries), lt_trec (templates),
+  // lt_pool (template bytes)
   const uint32_t *hl;
   uint32_t hl_bytes;
+  uint32_t lt_hinfo, lt_cls, lt_trec, lt_pool;
   const uint4 *plan;
   const uint32_t *plan_off;  // n_hosts + 1
   const uint4 *plan_glob;

@@ -3,6 +3,7 @@
 # (k_*): one counter group per run, within gfx950's per-pass slots (8 SQ,
 # 4 TCC: FETCH_SIZE costs 3, WRITE_SIZE 2).  Output: gpurun_out/pmc_<tag>/p<i>/
 #   bash tools/pmc_session.sh <tag> [bench args...]
+# env: PASSES="1 2" (subset of the groups), PMC_REGEX (kernel filter, default k_)
 set -e
 tag=${1:-cur}; shift || true
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -19,8 +20,9 @@ groups=(
 i=0
 for g in "${groups[@]}"; do
   i=$((i+1))
+  case " ${PASSES:-1 2 3 4} " in *" $i "*) ;; *) continue;; esac
   echo "pass $i: $g"
-  timeout -s KILL 150 rocprofv3 --pmc $g --kernel-include-regex "k_" -d "$out/p$i" -o pmc --output-format csv \
+  timeout -s KILL 150 rocprofv3 --pmc $g --kernel-include-regex "${PMC_REGEX:-k_}" -d "$out/p$i" -o pmc --output-format csv \
     -- python3 "$repo/bench.py" --steps 2 --warmup 1 --bans-steps 0 --no-cpu-baseline "$@" > "$out/p$i.log" 2>&1
 done
 echo done
