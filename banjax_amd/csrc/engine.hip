@@ -1648,12 +1648,19 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
   uint8_t *span = s_dyn + img_al + hl_al + (kBlock / 64) * (kWaveJobs * 8 + 16) + wave * (A.span_bytes + 32);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t n_work = A.list ? A.n_list : A.n_lines;
-  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + wave * 64u; base < n_work; base += stride) {
+  // span bounds of the wave's next 64 lines, loaded one iteration ahead
+  auto span_bounds = [&](uint64_t b, uint64_t &a0, uint64_t &a1) {
+    a0 = b ? A.nl[b - 1] + 1 : 0;
+    a1 = A.nl[min(b + 63, A.n_lines - 1)];
+  };
+  uint64_t s0n = 0, s1n = 0;
+  const uint64_t base0 = (uint64_t)blockIdx.x * blockDim.x + wave * 64u;
+  if (!A.list && base0 < n_work) span_bounds(base0, s0n, s1n);
+  for (uint64_t base = base0; base < n_work; base += stride) {
     if (PROF) P.start();
     const uint64_t j = A.list ? (base + lane < n_work ? A.list[base + lane] : A.n_lines) : base + lane;
-    const uint64_t jl = min(base + 63, A.n_lines - 1);
-    const uint64_t s0 = base ? A.nl[base - 1] + 1 : 0;
-    const uint64_t s1 = A.nl[jl];
+    const uint64_t s0 = s0n, s1 = s1n;
+    if (!A.list && base + stride < n_work) span_bounds(base + stride, s0n, s1n);
     const uint64_t b16 = s0 & ~15ull;
     const bool staged = !A.list && s1 + 16 - b16 <= A.span_bytes && !(A.dbg & 4);  // 16 B of slack for word-wise over-reads
     // per-line loads that do not depend on the staged bytes go out first
@@ -2296,22 +2303,29 @@ __device__ __forceinline__ bool st_claim_event(const EvSrc &E, uint64_t n_ev, ui
   uint32_t id = el_id[i];
   const bool first = id != kNewIp && (id & kFirstIp) && (k == 0 || ev_el[k - 1] != i);
   id = id == kNewIp ? S.ip[el_slot[i]].id : (id & ~kFirstIp);
-  const uint64_t key = ((uint64_t)(id + 1) << 24) | rules[r].name_id;
-  uint64_t q = mix64(key) & S.st_mask;
+  const uint32_t nm = rules[r].name_id;
+  const uint64_t key = ((uint64_t)(id + 1) << 24) | nm;
+  const bool hot = nm == S.hot_name && id < S.ip_st_cap;
+  const uint32_t c = hot ? S.ip_st[id] : kNone;
+  uint64_t q = c;
   bool claimed = false;
-  for (;;) {
-    uint64_t cur = S.st[q].key;
-    if (cur == 0) {
-      if (flag_set(S, 7)) return false;  // see k_ip_claim
-      if (__hip_atomic_load(claim_shard(S, 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= shard_budget) {
-        raise_flag(S, 7);
-        return false;
+  if (c == kNone) {
+    q = mix64(key) & S.st_mask;
+    for (;;) {
+      uint64_t cur = S.st[q].key;
+      if (cur == 0) {
+        if (flag_set(S, 7)) return false;  // see k_ip_claim
+        if (__hip_atomic_load(claim_shard(S, 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= shard_budget) {
+          raise_flag(S, 7);
+          return false;
+        }
+        cur = atomicCAS((unsigned long long *)&S.st[q].key, 0ull, (unsigned long long)key);
+        if (cur == 0) { claimed = true; break; }
       }
-      cur = atomicCAS((unsigned long long *)&S.st[q].key, 0ull, (unsigned long long)key);
-      if (cur == 0) { claimed = true; break; }
+      if (cur == key) break;
+      q = (q + 1) & S.st_mask;
     }
-    if (cur == key) break;
-    q = (q + 1) & S.st_mask;
+    if (hot) S.ip_st[id] = (uint32_t)q;
   }
   ev_st[k] = (uint32_t)q;
   EvRec rec;
@@ -4343,6 +4357,15 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     if (canon[r] == r && (rs->rules[r].rx.flags & kRuleNfa) && !(rs->rules[r].rx.flags & (kRuleAlways | kRuleNever)))
       e->nfa_rules.push_back(make_uint4(r, rs->rules[r].rx.nfa_words, (uint32_t)rs->rules[r].rx.nfa.size(), 0));
   e->host_rules = drules;
+  {
+    // the state-slot cache follows the first global rule that matches every line
+    uint32_t hot = kNone;
+    for (uint32_t g = 0; g < rs->n_global && hot == kNone; ++g)
+      if (rs->rules[g].rx.mode == kModeAlways) hot = drules[g].name_id;
+    if (getenv("BJX_NO_SLOT_CACHE") || e->st_cap > (1ull << 32)) hot = kNone;
+    if (hot != e->S.hot_name && e->S.ip_st) HIP_OK(hipMemsetAsync(e->S.ip_st, 0xFF, e->S.ip_st_cap * 4, e->stream));
+    e->S.hot_name = hot;
+  }
   e->bound_uid = rs->uid;
   e->bound_dec_version = e->decisions_version;
 }
@@ -4360,6 +4383,10 @@ void alloc_state(bjx_engine *e, uint64_t ip_cap, uint64_t st_cap, uint64_t arena
   HIP_OK(hipMemset(S.ip_first, 0xFF, ip_cap * 4));
   HIP_OK(hipMemset(S.st, 0, st_cap * sizeof(StSlot)));
   HIP_OK(hipMemset(S.counters, 0, kCounterBytes));
+  HIP_OK(hipMalloc(&S.ip_st, ip_cap * 4));
+  HIP_OK(hipMemset(S.ip_st, 0xFF, ip_cap * 4));
+  S.ip_st_cap = ip_cap;
+  S.hot_name = kNone;
   S.ip_mask = ip_cap - 1;
   S.st_mask = st_cap - 1;
   S.arena_cap = arena_cap;
@@ -4370,7 +4397,7 @@ void alloc_state(bjx_engine *e, uint64_t ip_cap, uint64_t st_cap, uint64_t arena
 void free_state(bjx_engine *e) {
   State &S = e->S;
   for (void *p : {(void *)S.ip, (void *)S.ip_first, (void *)S.ip_off, (void *)S.ip_len, (void *)S.arena, (void *)S.st,
-                  (void *)S.counters})
+                  (void *)S.counters, (void *)S.ip_st})
     if (p) (void)hipFree(p);
   S = State{};
 }
@@ -4401,6 +4428,10 @@ void grow_ip(bjx_engine *e, uint64_t want) {
   (void)hipFree(S.ip); (void)hipFree(S.ip_first); (void)hipFree(S.ip_off); (void)hipFree(S.ip_len);
   S.ip = nt; S.ip_first = nf; S.ip_off = noff; S.ip_len = nlen;
   S.ip_mask = cap - 1;
+  (void)hipFree(S.ip_st);
+  HIP_OK(hipMalloc(&S.ip_st, cap * 4));
+  HIP_OK(hipMemsetAsync(S.ip_st, 0xFF, cap * 4, e->stream));
+  S.ip_st_cap = cap;
   e->ip_cap = cap;
   ++e->rehashes;
 }
@@ -4419,6 +4450,8 @@ void grow_st(bjx_engine *e, uint64_t want) {
   (void)hipFree(S.st);
   S.st = nt;
   S.st_mask = cap - 1;
+  HIP_OK(hipMemsetAsync(S.ip_st, 0xFF, S.ip_st_cap * 4, e->stream));  // slots moved
+  if (cap > (1ull << 32)) S.hot_name = kNone;
   e->st_cap = cap;
   ++e->rehashes;
 }
@@ -4646,6 +4679,7 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
     HIP_OK(hipMemsetAsync(e->S.counters + 2, 0, 8, st));
     hipLaunchKernelGGL(k_st_rollback, dim3(grid_for(e->st_cap)), dim3(kBlock), 0, st, e->st_cap, e->S);
     HIP_OK(hipGetLastError());
+    HIP_OK(hipMemsetAsync(e->S.ip_st, 0xFF, e->S.ip_st_cap * 4, st));  // may name rolled-back slots
     read_counters(e);
     if (!forced)
       grow_st(e, attempt >= 2 ? e->host_counters[2] + n_ev
@@ -5622,6 +5656,7 @@ extern "C" int bjx_state_clear(bjx_engine *e) {
     HIP_OK(hipMemsetAsync(e->S.ip_first, 0xFF, e->ip_cap * 4, e->stream));
     HIP_OK(hipMemsetAsync(e->S.st, 0, e->st_cap * sizeof(StSlot), e->stream));
     HIP_OK(hipMemsetAsync(e->S.counters, 0, kCounterBytes, e->stream));
+    HIP_OK(hipMemsetAsync(e->S.ip_st, 0xFF, e->S.ip_st_cap * 4, e->stream));
     HIP_OK(hipStreamSynchronize(e->stream));
     return BJX_OK;
   } catch (const BjxError &x) {

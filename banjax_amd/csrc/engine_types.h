@@ -238,6 +238,13 @@ struct State {
   uint64_t ip_mask;
   uint64_t st_mask;
   uint64_t arena_cap;
+  // per IP id: state slot of (ip, hot_name) -- the name of the first global
+  // rule that matches every line, whose events are one per line -- so
+  // k_st_claim finds those slots without probing the state table; all ~0
+  // after any rehash / rollback / clear (kNone = not cached, hot_name ~0 = off)
+  uint32_t *ip_st;
+  uint64_t ip_st_cap;
+  uint32_t hot_name;
 };
 
 // One rate-limit event as the sort carries it (16 B): line timestamp, rule
