@@ -2043,7 +2043,9 @@ __global__ void k_rule_bounds(uint64_t n, const uint32_t *__restrict__ jkey, uin
 __global__ __launch_bounds__(kBlock) void k_emit(Bind B, uint64_t n_lines, Lines L, const uint64_t *__restrict__ offs,
                                                  uint64_t *__restrict__ res_seq, uint32_t *__restrict__ res_rule,
                                                  uint32_t *__restrict__ ev_el, uint32_t *__restrict__ ev_rule,
-                                                 uint32_t *__restrict__ ev_res, unsigned long long *bounds) {
+                                                 uint32_t *__restrict__ ev_res, unsigned long long *bounds, bool want_res) {
+  // want_res: also the RuleResult arrays (res_seq, res_rule, ev_res), read only
+  // when the caller copies the RuleResults out (BJX_COPY_RESULTS)
   __shared__ unsigned long long s_acc[2][kBlock / 64];
   unsigned long long has_ev = 0, ipb = 0;
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n_lines; j += (uint64_t)gridDim.x * blockDim.x) {
@@ -2068,9 +2070,16 @@ __global__ __launch_bounds__(kBlock) void k_emit(Bind B, uint64_t n_lines, Lines
         const uint32_t pos = w * 64 + b;
         const uint32_t r = pos < nsite ? B.site_rules[s_begin + pos] : B.global_rules[pos - nsite];
         const bool skip = pos < 128 ? (((pos < 64 ? k0 >> pos : k1 >> (pos - 64)) & 1) != 0) : is_skip(B, r, hid);
-        res_seq[ro] = (j << 16) | pos;
-        res_rule[ro] = r | (skip ? 0x80000000u : 0u);
-        if (!skip) { ev_el[eo] = (uint32_t)j; ev_rule[eo] = r; ev_res[eo] = (uint32_t)ro; ++eo; }
+        if (want_res) {
+          res_seq[ro] = (j << 16) | pos;
+          res_rule[ro] = r | (skip ? 0x80000000u : 0u);
+        }
+        if (!skip) {
+          ev_el[eo] = (uint32_t)j;
+          ev_rule[eo] = r;
+          if (want_res) ev_res[eo] = (uint32_t)ro;
+          ++eo;
+        }
         ++ro;
       }
     }
@@ -2714,6 +2723,44 @@ struct TripBit {
   __host__ __device__ __forceinline__ bool operator()(uint8_t v) const { return (v & 8) != 0; }
 };
 
+// Exceeded outcomes -> their indices, in no particular order (the caller
+// sorts them by event): 16 outcomes per lane from one 16 B load, compacted
+// across the wave, one atomic per wave
+__global__ __launch_bounds__(kBlock) void k_select_trips(uint64_t n, const uint8_t *__restrict__ out, uint32_t *__restrict__ idx,
+                                                         unsigned long long *__restrict__ cnt) {
+  const uint64_t b = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t m = 0;
+  if (b + 16 <= n) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(out + b);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t x = (w[k] >> 3) & 0x01010101u;  // bit 3 (Exceeded) of each byte
+      m |= ((x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u)) << (4 * k);
+    }
+  } else {
+    for (uint32_t k = 0; k < 16; ++k)
+      if (b + k < n && (out[b + k] & 8)) m |= 1u << k;
+  }
+  const uint32_t c = __popc(m);
+  uint32_t x = c;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  unsigned long long base = 0;
+  if (lane == 63 && x) base = atomicAdd(cnt, (unsigned long long)x);
+  base = __shfl(base, 63);
+  uint64_t o = base + (x - c);
+  while (m) {
+    const uint32_t k = (uint32_t)__ffs(m) - 1;
+    m &= m - 1;
+    idx[o++] = (uint32_t)(b + k);
+  }
+}
+
 __global__ void k_flag_trips(uint64_t n, const uint8_t *__restrict__ ev_out, uint8_t *__restrict__ f) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) f[i] = (ev_out[i] & 8) ? 1 : 0;
@@ -3350,6 +3397,7 @@ struct bjx_engine {
   DevBuf<uint8_t> l_flags;
   DevBuf<unsigned long long> scalars;  // [0] slow count, [1..2] bounds, [3] selected
   DevBuf<uint64_t> res_seq;
+  bool res_written = false;  // the last match phase wrote the RuleResult arrays
   DevBuf<uint32_t> res_rule, ev_el, ev_rule, ev_res, ev_st, ev_st2, ev_idx, ev_idx2, el_slot, coll, trip_idx;
   DevBuf<EvRec> ev_rec, ev_rec2;
   DevBuf<uint32_t> el_id;
@@ -4362,7 +4410,10 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     uint32_t hot = kNone;
     for (uint32_t g = 0; g < rs->n_global && hot == kNone; ++g)
       if (rs->rules[g].rx.mode == kModeAlways) hot = drules[g].name_id;
-    if (getenv("BJX_NO_SLOT_CACHE") || e->st_cap > (1ull << 32)) hot = kNone;
+    // opt-in (BJX_SLOT_CACHE=1): -1.1 ms of claim at cfg3, but two full GPU-suite
+    // runs with it on showed the intermittent outcome mismatch of DESIGN.md §3
+    static const bool slot_cache = getenv("BJX_SLOT_CACHE") && atoi(getenv("BJX_SLOT_CACHE")) == 1;
+    if (!slot_cache || e->st_cap > (1ull << 32)) hot = kNone;
     if (hot != e->S.hot_name && e->S.ip_st) HIP_OK(hipMemsetAsync(e->S.ip_st, 0xFF, e->S.ip_st_cap * 4, e->stream));
     e->S.hot_name = hot;
   }
@@ -5060,8 +5111,9 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   e->ev_el.ensure(n_ev + 1); e->ev_rule.ensure(n_ev + 1); e->ev_res.ensure(n_ev + 1);
   HIP_OK(hipMemsetAsync(e->scalars.p + 1, 0, 2 * 8, st));
   if (n_res) {
+    e->res_written = (flags & BJX_COPY_RESULTS) != 0;
     hipLaunchKernelGGL(k_emit, dim3((unsigned)std::min<uint64_t>(grid_for(n_lines), 4096)), dim3(kBlock), 0, st, B, n_lines, L, e->l_offs.p, e->res_seq.p,
-                       e->res_rule.p, e->ev_el.p, e->ev_rule.p, e->ev_res.p, e->scalars.p + 1);
+                       e->res_rule.p, e->ev_el.p, e->ev_rule.p, e->ev_res.p, e->scalars.p + 1, e->res_written);
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemsetAsync(e->rl_out.p, 0, n_res, st));
   }
@@ -5245,30 +5297,26 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
     // engine's rate-limit stage), selected there and put back in reference
     // order; otherwise outcomes already in event (= reference) order
     e->trip_idx.ensure(n_ev + 1);
-    hipcub::CountingInputIterator<uint32_t> it(0);
-    hipcub::TransformInputIterator<bool, TripBit, const uint8_t *> fl(sorted ? e->ev_out_s.p : e->ev_out.p, TripBit());
-    uint32_t *o = e->trip_idx.p;
-    unsigned long long *ns = e->scalars.p + 4;
-    cub_call(e, [&](void *tmp, size_t &bytes) {
-      return hipcub::DeviceSelect::Flagged(tmp, bytes, it, fl, o, ns, (int)n_ev, st);
-    });
+    HIP_OK(hipMemsetAsync(e->scalars.p + 4, 0, 8, st));
+    hipLaunchKernelGGL(k_select_trips, dim3(grid_for((n_ev + 15) / 16)), dim3(kBlock), 0, st, n_ev,
+                       sorted ? e->ev_out_s.p : e->ev_out.p, e->trip_idx.p, e->scalars.p + 4);
+    HIP_OK(hipGetLastError());
     unsigned long long nt = 0;
     HIP_OK(hipMemcpyAsync(&nt, e->scalars.p + 4, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     n_trips = nt;
     if (n_trips) {
-      const uint32_t *trip_ev = e->trip_idx.p;
-      if (sorted) {
-        e->trip_ev.ensure(n_trips); e->trip_ev2.ensure(n_trips);
+      // the selected trips in reference (event) order
+      e->trip_ev.ensure(n_trips); e->trip_ev2.ensure(n_trips);
+      if (sorted)
         hipLaunchKernelGGL(k_trip_events, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_idx.p, e->ev_rec2.p,
                            e->trip_ev.p);
-        uint32_t *ki = e->trip_ev.p, *ko = e->trip_ev2.p;
-        const int bits = std::max(1, bit_width(n_ev));
-        cub_call(e, [&](void *tmp, size_t &bytes) {
-          return hipcub::DeviceRadixSort::SortKeys(tmp, bytes, ki, ko, (int)n_trips, 0, bits, st);
-        });
-        trip_ev = e->trip_ev2.p;
-      }
+      uint32_t *ki = sorted ? e->trip_ev.p : e->trip_idx.p, *ko = e->trip_ev2.p;
+      const int bits = std::max(1, bit_width(n_ev));
+      cub_call(e, [&](void *tmp, size_t &bytes) {
+        return hipcub::DeviceRadixSort::SortKeys(tmp, bytes, ki, ko, (int)n_trips, 0, bits, st);
+      });
+      const uint32_t *trip_ev = e->trip_ev2.p;
       e->d_trips.ensure(n_trips);
       hipLaunchKernelGGL(k_build_trips, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, trip_ev, e->ev_el.p,
                          e->ev_rule.p, e->nl.p, L, B.rules, e->d_trips.p);
@@ -5276,6 +5324,16 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
       e->trips.resize(n_trips);
       HIP_OK(hipMemcpyAsync(e->trips.data(), e->d_trips.p, n_trips * sizeof(bjx_trip), hipMemcpyDeviceToHost, st));
       if (flags & BJX_EMIT_BANS) emit_bans(e, n_trips);
+    }
+    if ((flags & BJX_COPY_RESULTS) && !e->res_written) {
+      // the match phase ran without BJX_COPY_RESULTS: write the RuleResult
+      // arrays now (the per-line masks and offsets are still current)
+      HIP_OK(hipMemsetAsync(e->scalars.p + 1, 0, 2 * 8, st));
+      hipLaunchKernelGGL(k_emit, dim3((unsigned)std::min<uint64_t>(grid_for(n_lines), 4096)), dim3(kBlock), 0, st, e->bind,
+                         n_lines, L, e->l_offs.p, e->res_seq.p, e->res_rule.p, e->ev_el.p, e->ev_rule.p, e->ev_res.p,
+                         e->scalars.p + 1, true);
+      HIP_OK(hipGetLastError());
+      e->res_written = true;
     }
     if (flags & BJX_COPY_RESULTS) {
       if (sorted)
