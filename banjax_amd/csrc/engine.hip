@@ -5705,17 +5705,47 @@ extern "C" int bjx_state_stats_get(bjx_engine *e, bjx_state_stats *out) {
   }
 }
 
+// live keys left in the state / IP tables (bjx_state_clear's check)
+__global__ void k_count_live(const StSlot *__restrict__ st, uint64_t st_cap, const IpSlot *__restrict__ ip, uint64_t ip_cap,
+                             unsigned long long *__restrict__ cnt) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < st_cap && st[i].key != 0) atomicAdd(&cnt[0], 1ull);
+  if (i < ip_cap && ip[i].hash != 0) atomicAdd(&cnt[1], 1ull);
+}
+
 extern "C" int bjx_state_clear(bjx_engine *e) {
   if (!e) return BJX_ERR_ARG;
   std::lock_guard<std::mutex> g(e->mu);
   try {
     HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipDeviceSynchronize());  // nothing of an earlier batch may land after the clear
     HIP_OK(hipMemsetAsync(e->S.ip, 0, e->ip_cap * sizeof(IpSlot), e->stream));
     HIP_OK(hipMemsetAsync(e->S.ip_first, 0xFF, e->ip_cap * 4, e->stream));
     HIP_OK(hipMemsetAsync(e->S.st, 0, e->st_cap * sizeof(StSlot), e->stream));
     HIP_OK(hipMemsetAsync(e->S.counters, 0, kCounterBytes, e->stream));
     HIP_OK(hipMemsetAsync(e->S.ip_st, 0xFF, e->S.ip_st_cap * 4, e->stream));
     HIP_OK(hipStreamSynchronize(e->stream));
+    {
+      // the tables must read back empty: IP ids restart at 0, so a state slot
+      // that survived would be found again by a new IP's key
+      e->chk.ensure(8);
+      HIP_OK(hipMemsetAsync(e->chk.p, 0, 16, e->stream));
+      const uint64_t n = std::max(e->st_cap, e->ip_cap);
+      hipLaunchKernelGGL(k_count_live, dim3(grid_for(n)), dim3(kBlock), 0, e->stream, e->S.st, e->st_cap, e->S.ip, e->ip_cap,
+                         e->chk.p);
+      HIP_OK(hipGetLastError());
+      unsigned long long live[2] = {0, 0};
+      HIP_OK(hipMemcpyAsync(live, e->chk.p, 16, hipMemcpyDeviceToHost, e->stream));
+      HIP_OK(hipStreamSynchronize(e->stream));
+      if (live[0] | live[1]) {
+        fprintf(stderr, "[bjx] state_clear: %llu state slots and %llu IP slots survived the clear; clearing again\n", live[0],
+                live[1]);
+        HIP_OK(hipDeviceSynchronize());
+        HIP_OK(hipMemset(e->S.st, 0, e->st_cap * sizeof(StSlot)));
+        HIP_OK(hipMemset(e->S.ip, 0, e->ip_cap * sizeof(IpSlot)));
+        HIP_OK(hipDeviceSynchronize());
+      }
+    }
     return BJX_OK;
   } catch (const BjxError &x) {
     e->last_error = x.what();

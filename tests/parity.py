@@ -41,12 +41,36 @@ class Pair:
         self.n_rules = len(self.cfg.all_rules())
 
     def feed(self, data: bytes, now_ns: int, check=True):
+        before = self.engine.state_len()
         oflags, ores, oconsumed = self.ost.consume(self.ocfg, data, now_ns,
                                                    cap=(data.count(b"\n") + 1) * (self.n_rules + 1))
         results, out = self.lim.consume_lines(data, now_ns, want_results=True)
         if check:
-            compare_batch(oflags, ores, oconsumed, out)
+            try:
+                compare_batch(oflags, ores, oconsumed, out)
+            except AssertionError:
+                self._explain(data, ores, out, before)
+                raise
         return out
+
+    def _explain(self, data, ores, out, states_before):
+        """Diagnostics for a rate-limit outcome mismatch: every result of the
+        first differing (ip, rule) in this batch, both sides, and both states."""
+        lines = data.split(b"\n")
+        names = [r.rule for r in self.cfg.all_rules()]
+        for k, (g, o) in enumerate(zip(out.results, ores)):
+            if (g.match_type, g.exceeded) == (o.match_type, o.exceeded):
+                continue
+            ip = lines[g.line_idx].split(b" ")[1].decode(errors="replace")
+            name = names[g.rule_idx]
+            seq = [(i, r.line_idx, r.match_type, r.exceeded, ores[i].match_type, ores[i].exceeded)
+                   for i, r in enumerate(out.results) if i < len(ores) and names[r.rule_idx] == name
+                   and lines[r.line_idx].split(b" ")[1].decode(errors="replace") == ip]
+            print("MISMATCH result %d ip=%s rule=%s states before batch gpu=%d; (idx, line, gpu mt, ex, oracle mt, ex): %s"
+                  % (k, ip, name, states_before, seq[:12]), flush=True)
+            print("  gpu state", self.engine.state_get(ip, name), "oracle state", self.ost.get(ip, name),
+                  "gpu len", self.engine.state_len(), "oracle len", len(self.ost), "stats", self.engine.scan_stats(), flush=True)
+            break
 
     def compare_state(self, ips=None):
         """Final RegexRateLimitStates for every (ip, rule name), Len(), and the
