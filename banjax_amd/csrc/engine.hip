@@ -2724,38 +2724,52 @@ struct TripBit {
 };
 
 // Exceeded outcomes -> their indices, in no particular order (the caller
-// sorts them by event): 16 outcomes per lane from one 16 B load, compacted
-// across the wave, one atomic per wave
+// sorts them by event): 64 outcomes per lane (four 16 B loads), compacted
+// across the block, one atomic per block (a per-wave atomic on one counter
+// serialised the kernel)
+constexpr uint32_t kSelPer = 64;
 __global__ __launch_bounds__(kBlock) void k_select_trips(uint64_t n, const uint8_t *__restrict__ out, uint32_t *__restrict__ idx,
                                                          unsigned long long *__restrict__ cnt) {
-  const uint64_t b = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
-  const uint32_t lane = threadIdx.x & 63;
-  uint32_t m = 0;
-  if (b + 16 <= n) {
-    const uint4 v = *reinterpret_cast<const uint4 *>(out + b);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  __shared__ uint32_t s_wsum[kBlock / 64];
+  __shared__ unsigned long long s_base;
+  const uint64_t b = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kSelPer;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t m = 0;
+  if (b + kSelPer <= n) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(out + b);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t x = (w[k] >> 3) & 0x01010101u;  // bit 3 (Exceeded) of each byte
-      m |= ((x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u)) << (4 * k);
+    for (int q = 0; q < 4; ++q) {
+      const uint4 v = src[q];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t x = (w[k] >> 3) & 0x01010101u;  // bit 3 (Exceeded) of each byte
+        m |= (uint64_t)((x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u)) << (16 * q + 4 * k);
+      }
     }
   } else {
-    for (uint32_t k = 0; k < 16; ++k)
-      if (b + k < n && (out[b + k] & 8)) m |= 1u << k;
+    for (uint32_t k = 0; k < kSelPer; ++k)
+      if (b + k < n && (out[b + k] & 8)) m |= 1ull << k;
   }
-  const uint32_t c = __popc(m);
+  const uint32_t c = __popcll(m);
   uint32_t x = c;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t y = __shfl_up(x, d);
     if (lane >= (uint32_t)d) x += y;
   }
-  unsigned long long base = 0;
-  if (lane == 63 && x) base = atomicAdd(cnt, (unsigned long long)x);
-  base = __shfl(base, 63);
-  uint64_t o = base + (x - c);
+  if (lane == 63) s_wsum[wave] = x;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+  for (uint32_t w = 0; w < kBlock / 64; ++w) {
+    before += w < wave ? s_wsum[w] : 0u;
+    tot += s_wsum[w];
+  }
+  if (threadIdx.x == 0) s_base = tot ? atomicAdd(cnt, (unsigned long long)tot) : 0ull;
+  __syncthreads();
+  uint64_t o = s_base + before + (x - c);
   while (m) {
-    const uint32_t k = (uint32_t)__ffs(m) - 1;
+    const uint32_t k = (uint32_t)__ffsll((unsigned long long)m) - 1;
     m &= m - 1;
     idx[o++] = (uint32_t)(b + k);
   }
@@ -5298,7 +5312,7 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
     // order; otherwise outcomes already in event (= reference) order
     e->trip_idx.ensure(n_ev + 1);
     HIP_OK(hipMemsetAsync(e->scalars.p + 4, 0, 8, st));
-    hipLaunchKernelGGL(k_select_trips, dim3(grid_for((n_ev + 15) / 16)), dim3(kBlock), 0, st, n_ev,
+    hipLaunchKernelGGL(k_select_trips, dim3(grid_for((n_ev + kSelPer - 1) / kSelPer)), dim3(kBlock), 0, st, n_ev,
                        sorted ? e->ev_out_s.p : e->ev_out.p, e->trip_idx.p, e->scalars.p + 4);
     HIP_OK(hipGetLastError());
     unsigned long long nt = 0;
