@@ -5129,7 +5129,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     hipLaunchKernelGGL(k_emit, dim3((unsigned)std::min<uint64_t>(grid_for(n_lines), 4096)), dim3(kBlock), 0, st, B, n_lines, L, e->l_offs.p, e->res_seq.p,
                        e->res_rule.p, e->ev_el.p, e->ev_rule.p, e->ev_res.p, e->scalars.p + 1, e->res_written);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipMemsetAsync(e->rl_out.p, 0, n_res, st));
+    if (e->res_written) HIP_OK(hipMemsetAsync(e->rl_out.p, 0, n_res, st));
   }
   mark(e, 4);
   unsigned long long bnd[2] = {0, 0};
@@ -5347,6 +5347,7 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
                          n_lines, L, e->l_offs.p, e->res_seq.p, e->res_rule.p, e->ev_el.p, e->ev_rule.p, e->ev_res.p,
                          e->scalars.p + 1, true);
       HIP_OK(hipGetLastError());
+      HIP_OK(hipMemsetAsync(e->rl_out.p, 0, n_res, st));
       e->res_written = true;
     }
     if (flags & BJX_COPY_RESULTS) {
