@@ -153,3 +153,28 @@ def test_device_bans_dst_zone(engine, zone_name, t_change):
     for k, s in stamps:
         assert s == dt.datetime.fromtimestamp(t0 + 97 * k, tz).strftime("%Y-%m-%dT%H:%M:%S"), (k, s)
     assert len({s[11:13] for _, s in stamps}) >= 5
+
+
+def test_device_bans_records_only(engine):
+    """BJX_BAN_RECORDS_ONLY: the same per-IP decision records as the full
+    emission (decision.go:404-439 replay), no LogRegexBan lines."""
+    from banjax_amd import Ruleset
+    import numpy as np
+    w = W.scaled(W.CFG3, 100_000, n_ips=10_000)
+    cfg = Config.from_yaml(w.rules_yaml)
+    rs = Ruleset(cfg)
+    data, now = w.host_lines(), w.now_ns()
+    got = []
+    for ban_log in (True, False):
+        engine.state_clear()
+        engine.set_decision_lists(cfg.decision_entries)
+        out = engine.process(rs, data, now, emit_bans=True, ban_log=ban_log)
+        bb = engine.bans()
+        got.append((out.n_trips, bb))
+    (nt_full, full), (nt_rec, rec) = got
+    assert nt_full == nt_rec == full.n_trips == rec.n_trips and nt_full > 0
+    assert full.n_ips == rec.n_ips > 0
+    assert np.array_equal(full.ips, rec.ips)
+    assert full.ip_bytes == rec.ip_bytes and np.array_equal(full.ip_off, rec.ip_off)
+    assert len(full.log) > 0 and rec.log == b""
+    assert not rec.log_kind.any() and not rec.log_off.any()
