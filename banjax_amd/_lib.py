@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libbanjax_gpu.so")
 OK = 0
 ERR_REGEX, ERR_ARG, ERR_DEVICE, ERR_NOMEM, ERR_TOO_COMPLEX, ERR_CAPACITY, ERR_DECISION = -1, -2, -3, -4, -5, -6, -7
 TAIL_STOPPED, ERR_IO = -8, -9
-INPUT_DEVICE, COPY_RESULTS, EMIT_BANS = 1, 2, 4
+INPUT_DEVICE, COPY_RESULTS, EMIT_BANS, BAN_RECORDS_ONLY = 1, 2, 4, 8
 
 
 class Str(C.Structure):

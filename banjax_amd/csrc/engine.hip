@@ -5197,7 +5197,7 @@ __global__ void k_ban_ipcopy(BanDev A, uint64_t n_ips, const bjx_ip_decision *__
   for (uint32_t k = 0, n = A.trips[t].ip_len; k < n; ++k) dst[k] = src[k];
 }
 
-static void emit_bans(bjx_engine *e, uint64_t n) {
+static void emit_bans(bjx_engine *e, uint64_t n, bool records_only) {
   hipStream_t st = e->stream;
   ensure_name_json(e);
   BanDev A{};
@@ -5207,18 +5207,23 @@ static void emit_bans(bjx_engine *e, uint64_t n) {
   A.tz_offset_s = e->ban_tz;
   A.tz_at = e->tz_at.p; A.tz_off = e->tz_off.p; A.n_tz = e->n_tz;
   const int64_t expires = (int64_t)((uint64_t)e->bc.now_ns + (uint64_t)e->ban_ttl_ns);
-  // ban-log lines: lengths, offsets, bytes
-  e->bn_len.ensure(n + 1); e->bn_off.ensure(n + 1); e->bn_kind.ensure(n);
-  hipLaunchKernelGGL(k_ban_len, dim3(grid_for(n + 1)), dim3(kBlock), 0, st, A, e->bn_len.p, e->bn_kind.p);
-  HIP_OK(hipGetLastError());
-  {
-    uint64_t *in = e->bn_len.p, *o = e->bn_off.p;
-    cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)(n + 1), st); });
-  }
+  // ban-log lines: lengths, offsets, bytes (BJX_BAN_RECORDS_ONLY: none)
   e->ban_off.resize(n + 1);
   e->ban_kind.resize(n);
-  HIP_OK(hipMemcpyAsync(e->ban_off.data(), e->bn_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipMemcpyAsync(e->ban_kind.data(), e->bn_kind.p, n, hipMemcpyDeviceToHost, st));
+  if (records_only) {
+    memset(e->ban_off.data(), 0, (n + 1) * 8);
+    memset(e->ban_kind.data(), 0, n);
+  } else {
+    e->bn_len.ensure(n + 1); e->bn_off.ensure(n + 1); e->bn_kind.ensure(n);
+    hipLaunchKernelGGL(k_ban_len, dim3(grid_for(n + 1)), dim3(kBlock), 0, st, A, e->bn_len.p, e->bn_kind.p);
+    HIP_OK(hipGetLastError());
+    {
+      uint64_t *in = e->bn_len.p, *o = e->bn_off.p;
+      cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)(n + 1), st); });
+    }
+    HIP_OK(hipMemcpyAsync(e->ban_off.data(), e->bn_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(e->ban_kind.data(), e->bn_kind.p, n, hipMemcpyDeviceToHost, st));
+  }
   // per-IP escalation: sort trips by IP hash (stable: trip order within a run)
   e->bn_key.ensure(n); e->bn_key2.ensure(n); e->bn_val.ensure(n); e->bn_val2.ensure(n); e->bn_head.ensure(n);
   e->bn_seg.ensure(n);
@@ -5241,11 +5246,13 @@ static void emit_bans(bjx_engine *e, uint64_t n) {
   HIP_OK(hipMemcpyAsync(&n_seg, e->bn_seg.p + (n - 1), 4, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
   const uint64_t log_bytes = e->ban_off.data()[n];
-  e->bn_log.ensure(log_bytes + 16);
-  hipLaunchKernelGGL(k_ban_write, dim3(grid_for(n)), dim3(kBlock), 0, st, A, e->bn_off.p, e->bn_log.p);
-  HIP_OK(hipGetLastError());
   e->ban_log.resize(log_bytes);
-  if (log_bytes) HIP_OK(hipMemcpyAsync(e->ban_log.data(), e->bn_log.p, log_bytes, hipMemcpyDeviceToHost, st));
+  if (log_bytes) {
+    e->bn_log.ensure(log_bytes + 16);
+    hipLaunchKernelGGL(k_ban_write, dim3(grid_for(n)), dim3(kBlock), 0, st, A, e->bn_off.p, e->bn_log.p);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(e->ban_log.data(), e->bn_log.p, log_bytes, hipMemcpyDeviceToHost, st));
+  }
   e->bn_first.ensure(n_seg); e->bn_cnt.ensure(n_seg); e->bn_ipt.ensure(n_seg); e->bn_coll.ensure(n_seg);
   e->bn_best.ensure(n_seg); e->bn_flag.ensure(n); e->bn_rep.ensure(n); e->bn_sel.ensure(n);
   HIP_OK(hipMemsetAsync(e->bn_cnt.p, 0, n_seg * 4ull, st));
@@ -5337,7 +5344,7 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
       HIP_OK(hipGetLastError());
       e->trips.resize(n_trips);
       HIP_OK(hipMemcpyAsync(e->trips.data(), e->d_trips.p, n_trips * sizeof(bjx_trip), hipMemcpyDeviceToHost, st));
-      if (flags & BJX_EMIT_BANS) emit_bans(e, n_trips);
+      if (flags & BJX_EMIT_BANS) emit_bans(e, n_trips, (flags & BJX_BAN_RECORDS_ONLY) != 0);
     }
     if ((flags & BJX_COPY_RESULTS) && !e->res_written) {
       // the match phase ran without BJX_COPY_RESULTS: write the RuleResult

@@ -152,11 +152,14 @@ class Engine:
         return BanBatch(bb)
 
     def process(self, rs: Ruleset, data, now_ns: int, copy_results: bool = False, device_ptr: Optional[int] = None,
-                nbytes: Optional[int] = None, emit_bans: bool = False) -> BatchOutput:
+                nbytes: Optional[int] = None, emit_bans: bool = False, ban_log: bool = True) -> BatchOutput:
         """consumeLine over every complete line of `data` (bytes) or of a device
-        buffer (device_ptr, nbytes) already resident in HBM."""
+        buffer (device_ptr, nbytes) already resident in HBM.  emit_bans with
+        ban_log=False: the per-IP decision records only (BJX_BAN_RECORDS_ONLY)."""
         res = _lib.BatchResult()
         flags = (_lib.COPY_RESULTS if copy_results else 0) | (_lib.EMIT_BANS if emit_bans else 0)
+        if emit_bans and not ban_log:
+            flags |= _lib.BAN_RECORDS_ONLY
         if device_ptr is not None:
             rc = _lib.lib().bjx_process_batch(self._h, rs.handle, C.c_void_p(device_ptr), nbytes, now_ns,
                                               flags | _lib.INPUT_DEVICE, C.byref(res))

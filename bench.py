@@ -263,6 +263,20 @@ def main():
                "ms_per_step": round(el2 * 1000.0 / args.bans_steps, 3), "steps": args.bans_steps,
                "what": "each step also builds the per-IP DynamicDecisionLists updates and all LogRegexBan JSON lines "
                        "on the device and copies them to pinned host memory (BJX_EMIT_BANS)"}
+    # the decision records alone (BJX_BAN_RECORDS_ONLY: no LogRegexBan lines
+    # built or copied), single-engine runs
+    rec = None
+    if args.bans_steps > 0 and not args.bans and ex is None and not node_mode and not dist:
+        sync_all()
+        t2 = time.perf_counter()
+        for _ in range(args.bans_steps):
+            eng.process(rs, None, now, device_ptr=data.data_ptr(), nbytes=nbytes, emit_bans=True, ban_log=False)
+        sync_all()
+        el3 = time.perf_counter() - t2
+        rec = {"value": round(n_lines / (el3 / args.bans_steps), 1), "unit": "lines/s",
+               "ms_per_step": round(el3 * 1000.0 / args.bans_steps, 3), "steps": args.bans_steps,
+               "what": "each step also builds the per-IP DynamicDecisionLists updates on the device and copies them "
+                       "to pinned host memory, without the LogRegexBan lines (BJX_EMIT_BANS | BJX_BAN_RECORDS_ONLY)"}
     total_lines = n_lines * n_parts
     value = total_lines / (elapsed / args.steps)
     achieved = nbytes / (match_ms / 1000.0) / 1e9
@@ -313,6 +327,8 @@ def main():
             "frac": round(nbytes / (mp_ms / 1000.0) / 1e9 / HBM_PEAK_GBS, 4)}
         if dec:
             line["with_decision_emission"] = dec
+        if rec:
+            line["with_decision_records_only"] = rec
         if not args.no_cpu_baseline and n_parts == 1:
             line["cpu_baseline"] = cpu_baseline(w, args.cpu_sample)
         print(json.dumps(line), flush=True)

@@ -154,7 +154,9 @@ typedef struct bjx_trip {
 enum bjx_batch_flags {
   BJX_INPUT_DEVICE = 1,   /* bytes is a device pointer already resident in HBM */
   BJX_COPY_RESULTS = 2,   /* also copy per-line flags and RuleResults to host memory */
-  BJX_EMIT_BANS = 4       /* also build the batch's decision updates and ban-log lines (bjx_batch_bans) */
+  BJX_EMIT_BANS = 4,      /* also build the batch's decision updates and ban-log lines (bjx_batch_bans) */
+  BJX_BAN_RECORDS_ONLY = 8 /* with BJX_EMIT_BANS: the per-IP decision records only; no LogRegexBan lines
+                              are built or copied (log_bytes 0, every log_kind 0) */
 };
 
 typedef struct bjx_batch_result {
