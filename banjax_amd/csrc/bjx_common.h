@@ -96,6 +96,29 @@ BJX_HD uint64_t hash_bytes(const uint8_t *p, uint32_t n) {
   return h;
 }
 
+// ------------------------------------------------------------- K-way search
+
+// One narrowing step of a K-way parallel search for the first i in [lo, hi)
+// with pred(i) (pred monotone: false ... true).  The K samples are
+// lo + t * stride (t < K, stride = ceil((hi - lo) / K)); samples at or past hi
+// are not taken.  f = the first sample index whose pred holds, K if none.
+// The answer lies in [lo', hi'], so the search ends (answer hi') once
+// lo' >= hi'.  With no sample true, the next range starts after the last
+// sample taken below hi, which is below lo + (K - 1) * stride when (hi - lo)
+// is not a multiple of stride: starting at lo + (K - 1) * stride + 1 would
+// skip the positions between them (round-2 hot-key outcome mismatch).
+BJX_HD uint64_t search_stride(uint64_t lo, uint64_t hi, uint32_t K) { return (hi - lo + K - 1) / K; }
+BJX_HD void search_narrow(uint64_t &lo, uint64_t &hi, uint64_t stride, uint32_t f, uint32_t K) {
+  if (f == 0) { hi = lo; return; }
+  uint64_t last = f - 1;  // last sample known false
+  if (f < K) hi = lo + (uint64_t)f * stride;
+  else {
+    last = (hi - 1 - lo) / stride;
+    if (last > K - 1) last = K - 1;
+  }
+  lo += last * stride + 1;
+}
+
 // ------------------------------------------------------------- time
 
 // time.Time.Sub for time.Unix(0, ns) values: exact difference saturated to

@@ -2396,7 +2396,7 @@ __device__ __forceinline__ uint8_t apply_step(const EvRec &v, const DevRule *__r
 __global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const uint32_t *__restrict__ key, const EvRec *__restrict__ rec,
                                                   const DevRule *__restrict__ rules, StSlot *__restrict__ st,
                                                   uint8_t *__restrict__ out_sorted, uint64_t *__restrict__ long_heads,
-                                                  unsigned long long *__restrict__ n_long) {
+                                                  unsigned long long *__restrict__ n_long, uint32_t *__restrict__ wcnt) {
   constexpr uint32_t kPer = kApplyChunk / kBlock;  // positions per thread for the head scan
   constexpr uint32_t kLongRun = 8;                 // runs at least this long go to the first lanes
   __shared__ EvRec s_rec[kApplyChunk];
@@ -2474,8 +2474,13 @@ __global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const uint32_t 
     st[q].valid = 1;
   }
   __syncthreads();
-  // records before the first head belong to the previous block's run
-  for (uint32_t i = (nh ? s_head[0] : n) + tid; i < n; i += kBlock) out_sorted[u0 + i] = s_out[i];
+  // records before the first head belong to the previous block's run, those
+  // of a continuing last run to k_long_*: each outcome has exactly one writer
+  const uint32_t s_lo = nh ? s_head[0] : n, s_hi = nh && s_cont ? s_head[nh - 1] : n;
+  for (uint32_t i = s_lo + tid; i < s_hi; i += kBlock) {
+    out_sorted[u0 + i] = s_out[i];
+    if (wcnt) atomicAdd(&wcnt[u0 + i], 1u);
+  }
 }
 
 // One (ip, rule name) state whose sorted run crosses a k_apply chunk (hot
@@ -2505,15 +2510,11 @@ __device__ __forceinline__ uint32_t block_min_u32(uint32_t v, uint32_t *s_red) {
 template <typename P>
 __device__ uint64_t block_first(uint64_t lo, uint64_t hi, P pred, uint32_t *s_red) {
   while (lo < hi) {
-    const uint64_t stride = (hi - lo + kBlock - 1) / kBlock;
+    const uint64_t stride = search_stride(lo, hi, kBlock);
     const uint64_t p = lo + (uint64_t)threadIdx.x * stride;
     const bool ok = p < hi && pred(p);
     const uint32_t f = block_min_u32(ok ? threadIdx.x : (uint32_t)kBlock, s_red);
-    if (f == 0) return lo;
-    if (stride == 1) return f == (uint32_t)kBlock ? hi : lo + f;
-    const uint64_t nlo = lo + (uint64_t)(f - 1) * stride + 1;
-    hi = f == (uint32_t)kBlock ? hi : lo + (uint64_t)f * stride;
-    lo = nlo;
+    search_narrow(lo, hi, stride, f, kBlock);  // uniform across the block
   }
   return hi;
 }
@@ -2532,6 +2533,7 @@ struct LongRuns {
   uint64_t *win;         // window start records, off[r] ... off[r] + nwin[r]
   uint32_t *nwin;
   uint64_t n;
+  uint32_t *wcnt;        // BJX_CHECK: writes per sorted outcome (null otherwise)
 };
 
 // 1. run end (block-parallel search), the stored state and the first window
@@ -2598,7 +2600,10 @@ __global__ __launch_bounds__(kBlock) void k_long_windows(const uint32_t *__restr
       bool valid = cur.valid != 0;
       int64_t hits = cur.hits, start = cur.start, interval = 0, limit = 0;
       uint32_t pr = 0xFFFFFFFFu;
-      for (uint64_t i = head; i < end; ++i) out_sorted[i] = apply_step(rec[i], rules, pr, interval, limit, valid, hits, start);
+      for (uint64_t i = head; i < end; ++i) {
+        out_sorted[i] = apply_step(rec[i], rules, pr, interval, limit, valid, hits, start);
+        if (R.wcnt) atomicAdd(&R.wcnt[i], 1u);
+      }
       st[q].hits = hits;
       st[q].start = start;
       st[q].valid = 1;
@@ -2668,6 +2673,7 @@ __global__ __launch_bounds__(kBlock) void k_long_fill(uint64_t total, const EvRe
   const uint8_t mt = (!cont && i == a) ? first_mt : (uint8_t)BJX_INSIDE_INTERVAL;
   const bool seen = (rec[i].rule >> 31) == 0;
   out_sorted[i] = (uint8_t)(0x80 | (seen ? 1 : 0) | (mt << 1) | (ex ? 8 : 0));
+  if (R.wcnt) atomicAdd(&R.wcnt[i], 1u);
 }
 
 // ---- BJX_CHECK=1 (debugging aid): invariants of the rate-limit stage
@@ -2676,11 +2682,14 @@ __device__ __forceinline__ uint32_t ev_line_id(const State &S, const uint32_t *e
   return id == kNewIp ? S.ip[el_slot[i]].id : (id & ~kFirstIp);
 }
 // every event line's IP id names the line's IP bytes; every event's state
-// slot holds (that id, its rule's name); every sorted outcome was written
+// slot holds (that id, its rule's name); every sorted outcome was written by
+// exactly one writer (wcnt), seenIp false only with FirstTime, and the sorted
+// records' event indices form a permutation (pc: k_check_count over EvRec.ev)
 __global__ void k_check_rl(EvSrc E, uint64_t n_ev, const uint32_t *__restrict__ ev_el, const uint32_t *__restrict__ ev_rule,
                            const uint32_t *__restrict__ el_slot, const uint32_t *__restrict__ el_id,
                            const DevRule *__restrict__ rules, State S, const uint32_t *__restrict__ ev_st,
-                           const uint8_t *__restrict__ out_s, unsigned long long *__restrict__ chk) {
+                           const uint8_t *__restrict__ out_s, const uint32_t *__restrict__ wcnt,
+                           const uint32_t *__restrict__ pc, unsigned long long *__restrict__ chk) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < E.n && ev_has(E, t)) {
     const uint32_t id = ev_line_id(S, el_slot, el_id, t);
@@ -2695,10 +2704,35 @@ __global__ void k_check_rl(EvSrc E, uint64_t n_ev, const uint32_t *__restrict__ 
     if (S.st[ev_st[t]].key != key) {
       if (atomicAdd(&chk[3], 1ull) == 0) { chk[4] = t; chk[5] = ev_st[t]; }
     }
-    if (!(out_s[t] & 0x80)) {
+    const uint8_t o = out_s[t];
+    if (!(o & 0x80)) {
       if (atomicAdd(&chk[6], 1ull) == 0) chk[7] = t;
     }
+    if (wcnt[t] != 1) {  // exactly one writer per sorted outcome
+      if (atomicAdd(&chk[8], 1ull) == 0) chk[9] = t;
+    }
+    if (!(o & 1) && ((o >> 1) & 3) != BJX_FIRST_TIME) {  // seenIp false => FirstTime (rate_limit.go:48-51)
+      if (atomicAdd(&chk[10], 1ull) == 0) chk[11] = t;
+    }
+    if (pc[t] != 1) {  // EvRec.ev over the sorted records is a permutation
+      if (atomicAdd(&chk[12], 1ull) == 0) chk[13] = t;
+    }
   }
+}
+
+// BJX_CHECK: cnt[idx[t * step]] += 1 for t < n (idx < cap, else chk[0]++)
+__global__ void k_check_count(uint64_t n, const uint32_t *__restrict__ idx, uint32_t step, uint64_t cap,
+                              uint32_t *__restrict__ cnt, unsigned long long *__restrict__ chk) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint32_t v = idx[t * step];
+  if (v < cap) atomicAdd(&cnt[v], 1u);
+  else atomicAdd(&chk[0], 1ull);
+}
+// BJX_CHECK: entries of cnt above `most` -> chk[1] (count), chk[2] (first)
+__global__ void k_check_most(uint64_t n, const uint32_t *__restrict__ cnt, uint32_t most, unsigned long long *__restrict__ chk) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n && cnt[t] > most && atomicAdd(&chk[1], 1ull) == 0) chk[2] = t;
 }
 
 __global__ void k_dbg_mask_hash(uint64_t n, uint64_t *__restrict__ h, uint64_t mask) {
@@ -3400,6 +3434,7 @@ struct bjx_engine {
   DevBuf<uint64_t> long_heads;
   DevBuf<uint64_t> lr_end, lr_len, lr_off, lr_win;
   DevBuf<unsigned long long> chk;
+  DevBuf<uint32_t> chk_w;  // BJX_CHECK: per-outcome write counts, event-index counts
   DevBuf<int64_t> lr_t0, lr_h0;
   DevBuf<uint32_t> lr_flags, lr_nwin;
   DevBuf<unsigned long long> long_count;
@@ -4761,12 +4796,18 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
   }
   const uint64_t n_chunks = (n_ev + kApplyChunk - 1) / kApplyChunk;
   const bool check = getenv("BJX_CHECK") != nullptr;
-  if (check) HIP_OK(hipMemsetAsync(e->ev_out_s.p, 0, n_ev, st));
+  uint32_t *wcnt = nullptr;
+  if (check) {
+    HIP_OK(hipMemsetAsync(e->ev_out_s.p, 0, n_ev, st));
+    e->chk_w.ensure(2 * n_ev);
+    wcnt = e->chk_w.p;
+    HIP_OK(hipMemsetAsync(wcnt, 0, 2 * n_ev * 4, st));
+  }
   e->long_heads.ensure(n_chunks + 1);
   e->long_count.ensure(1);
   HIP_OK(hipMemsetAsync(e->long_count.p, 0, 8, st));
   hipLaunchKernelGGL(k_apply, dim3((unsigned)n_chunks), dim3(kBlock), 0, st, n_ev, e->ev_st2.p, e->ev_rec2.p, B.rules, e->S.st,
-                     e->ev_out_s.p, e->long_heads.p, e->long_count.p);
+                     e->ev_out_s.p, e->long_heads.p, e->long_count.p, wcnt);
   HIP_OK(hipGetLastError());
   unsigned long long n_long = 0;
   HIP_OK(hipMemcpyAsync(&n_long, e->long_count.p, 8, hipMemcpyDeviceToHost, st));
@@ -4779,7 +4820,7 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
     e->lr_end.ensure(n_long); e->lr_len.ensure(n_long + 1); e->lr_off.ensure(n_long + 1); e->lr_t0.ensure(n_long);
     e->lr_h0.ensure(n_long); e->lr_flags.ensure(n_long); e->lr_nwin.ensure(n_long);
     R.head = e->long_heads.p; R.end = e->lr_end.p; R.off = e->lr_off.p; R.t0 = e->lr_t0.p; R.h0 = e->lr_h0.p;
-    R.flags = e->lr_flags.p; R.nwin = e->lr_nwin.p; R.n = n_long; R.win = nullptr;
+    R.flags = e->lr_flags.p; R.nwin = e->lr_nwin.p; R.n = n_long; R.win = nullptr; R.wcnt = wcnt;
     HIP_OK(hipMemsetAsync(e->lr_len.p + n_long, 0, 8, st));
     hipLaunchKernelGGL(k_long_ends, dim3((unsigned)n_long), dim3(kBlock), 0, st, n_ev, e->ev_st2.p, e->ev_rec2.p, e->S.st,
                        B.rules, R, e->lr_len.p);
@@ -4800,19 +4841,26 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
     HIP_OK(hipGetLastError());
   }
   if (check) {
-    e->chk.ensure(8);
-    HIP_OK(hipMemsetAsync(e->chk.p, 0, 64, st));
+    e->chk.ensure(16);
+    HIP_OK(hipMemsetAsync(e->chk.p, 0, 128, st));
+    uint32_t *pc = wcnt + n_ev;
+    hipLaunchKernelGGL(k_check_count, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev,
+                       reinterpret_cast<const uint32_t *>(e->ev_rec2.p) + 3, 4u, n_ev, pc, e->chk.p + 14);
     hipLaunchKernelGGL(k_check_rl, dim3(grid_for(std::max<uint64_t>(E.n, n_ev))), dim3(kBlock), 0, st, E, n_ev, ev_el, ev_rule,
-                       e->el_slot.p, e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_out_s.p, e->chk.p);
-    unsigned long long c[8];
-    HIP_OK(hipMemcpyAsync(c, e->chk.p, 64, hipMemcpyDeviceToHost, st));
+                       e->el_slot.p, e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_out_s.p, wcnt, pc, e->chk.p);
+    HIP_OK(hipGetLastError());
+    unsigned long long c[16];
+    HIP_OK(hipMemcpyAsync(c, e->chk.p, 128, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    if (c[0] || c[3] || c[6]) {
-      char msg[512];
+    if (c[0] || c[3] || c[6] || c[8] || c[10] || c[12] || c[14]) {
+      char msg[768];
       snprintf(msg, sizeof msg,
                "BJX_CHECK: %llu event lines with a wrong IP id (first line %llu id %llu), %llu events in a wrong state slot "
-               "(first %llu slot %llu), %llu unwritten outcomes (first %llu); epoch %u, %llu long runs, n_ev %llu",
-               c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], e->epoch, (unsigned long long)n_long, (unsigned long long)n_ev);
+               "(first %llu slot %llu), %llu unwritten outcomes (first %llu), %llu outcomes not written exactly once (first "
+               "%llu), %llu seenIp=false outcomes that are not FirstTime (first %llu), %llu sorted positions whose event "
+               "index is not a permutation (first %llu; %llu out of range); epoch %u, %llu long runs, n_ev %llu",
+               c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9], c[10], c[11], c[12], c[13], c[14], e->epoch,
+               (unsigned long long)n_long, (unsigned long long)n_ev);
       fprintf(stderr, "%s\n", msg);
       throw BjxError(BJX_ERR_DEVICE, msg);
     }
@@ -5283,7 +5331,10 @@ static void emit_bans(bjx_engine *e, uint64_t n, bool records_only) {
   e->ban_ipb.resize(0);
   if (n_ips) {
     HIP_OK(hipMemcpyAsync(e->ban_ips.data(), e->bn_sel.p, n_ips * sizeof(bjx_ip_decision), hipMemcpyDeviceToHost, st));
-    uint64_t *len = e->bn_len.p, *off = e->bn_off.p;  // the log offsets are on the host already
+    // scratch for the IP lengths / offsets (the log offsets are on the host
+    // already); sized here, since a records-only batch never sized them
+    e->bn_len.ensure(n_ips + 1); e->bn_off.ensure(n_ips + 1);
+    uint64_t *len = e->bn_len.p, *off = e->bn_off.p;
     hipLaunchKernelGGL(k_ban_iplen, dim3(grid_for(n_ips + 1)), dim3(kBlock), 0, st, A, (uint64_t)n_ips, e->bn_sel.p, len);
     cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, len, off, (int)(n_ips + 1), st); });
     HIP_OK(hipMemcpyAsync(e->ban_ipo.data(), off, (n_ips + 1) * 8, hipMemcpyDeviceToHost, st));
@@ -5362,6 +5413,25 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
         hipLaunchKernelGGL(k_unsort, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_rec2.p, e->ev_out_s.p, e->ev_out.p);
       hipLaunchKernelGGL(k_scatter_rl, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_res.p, e->ev_out.p, e->rl_out.p);
       HIP_OK(hipGetLastError());
+      if (getenv("BJX_CHECK")) {  // every event names its own RuleResult (ev_res injective)
+        e->chk_w.ensure(n_res + 1);
+        e->chk.ensure(16);
+        HIP_OK(hipMemsetAsync(e->chk_w.p, 0, (n_res + 1) * 4, st));
+        HIP_OK(hipMemsetAsync(e->chk.p, 0, 32, st));
+        hipLaunchKernelGGL(k_check_count, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_res.p, 1u, n_res, e->chk_w.p,
+                           e->chk.p);
+        hipLaunchKernelGGL(k_check_most, dim3(grid_for(n_res)), dim3(kBlock), 0, st, n_res, e->chk_w.p, 1u, e->chk.p);
+        HIP_OK(hipGetLastError());
+        unsigned long long c[3];
+        HIP_OK(hipMemcpyAsync(c, e->chk.p, 24, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        if (c[0] || c[1]) {
+          char msg[256];
+          snprintf(msg, sizeof msg, "BJX_CHECK: %llu event result indices out of range, %llu RuleResults named by more than "
+                   "one event (first %llu)", c[0], c[1], c[2]);
+          throw BjxError(BJX_ERR_DEVICE, msg);
+        }
+      }
     }
   }
   HIP_OK(hipEventRecord(e->ev1, st));

@@ -630,6 +630,7 @@ extern "C" int bjx_node_batch_bans(bjx_node *n, bjx_ban_batch *out) {
 extern "C" int bjx_node_state_get(bjx_node *n, const char *ip, size_t ip_len, const char *name, size_t name_len,
                                   int64_t *num_hits, int64_t *interval_start_ns) {
   if (!n) return BJX_ERR_ARG;
+  std::lock_guard<std::mutex> g(n->mu);  // not between one batch's shard phases
   for (auto &P : n->parts) {
     const int rc = bjx_state_get(P.e, ip, ip_len, name, name_len, num_hits, interval_start_ns);
     if (rc != 0) return rc;
@@ -639,6 +640,7 @@ extern "C" int bjx_node_state_get(bjx_node *n, const char *ip, size_t ip_len, co
 
 extern "C" int64_t bjx_node_state_len(bjx_node *n) {
   if (!n) return BJX_ERR_ARG;
+  std::lock_guard<std::mutex> g(n->mu);
   int64_t t = 0;
   for (auto &P : n->parts) {
     const int64_t v = bjx_state_len(P.e);
@@ -650,6 +652,7 @@ extern "C" int64_t bjx_node_state_len(bjx_node *n) {
 
 extern "C" size_t bjx_node_state_dump(bjx_node *n, char *out, size_t cap) {
   if (!n) return 0;
+  std::lock_guard<std::mutex> g(n->mu);
   size_t t = 0;
   for (auto &P : n->parts) {
     const size_t room = out && t < cap ? cap - t : 0;
@@ -660,6 +663,7 @@ extern "C" size_t bjx_node_state_dump(bjx_node *n, char *out, size_t cap) {
 
 extern "C" int bjx_node_state_stats_get(bjx_node *n, bjx_state_stats *out) {
   if (!n || !out) return BJX_ERR_ARG;
+  std::lock_guard<std::mutex> g(n->mu);
   memset(out, 0, sizeof *out);
   for (auto &P : n->parts) {
     bjx_state_stats s{};
@@ -674,6 +678,7 @@ extern "C" int bjx_node_state_stats_get(bjx_node *n, bjx_state_stats *out) {
 
 extern "C" int bjx_node_state_clear(bjx_node *n) {
   if (!n) return BJX_ERR_ARG;
+  std::lock_guard<std::mutex> g(n->mu);
   for (auto &P : n->parts) {
     const int rc = bjx_state_clear(P.e);
     if (rc != BJX_OK) return rc;

@@ -246,6 +246,11 @@ class DynamicDecisionLists:
                 return
             self.expiring[ip] = ExpiringDecision(decision, expires_ns, ip, from_baskerville, domain)
 
+    def clear(self):
+        """Clear (decision.go:540-546)."""
+        with self._mu:
+            self.expiring.clear()
+
     def check(self, ip: str, now_ns: int):
         """decision.go:474-500 (lazy delete on expiry)."""
         with self._mu:
@@ -377,14 +382,21 @@ class RegexRateLimiter:
     equivalent of RunLogTailer's loop body over a batch of lines."""
 
     def __init__(self, cfg: Config, engine: Optional[Engine] = None, banner: Optional[Banner] = None,
-                 device_bans: bool = False, tz_offset_s: int = 0, zone: Optional[Zone] = None):
+                 device_bans: bool = False, tz_offset_s: int = 0, zone: Optional[Zone] = None,
+                 device_ban_log: bool = True):
         """device_bans: the engine emits one decision update per tripped IP and
         the formatted ban-log lines (bjx_batch_bans) instead of
-        the per-trip Banner replay on the host.  zone: time.Local of the ban
-        log (default: the fixed offset tz_offset_s)."""
+        the per-trip Banner replay on the host.  device_ban_log=False: the
+        engine emits only the decision records (BJX_BAN_RECORDS_ONLY) and the
+        host writes the LogRegexBan lines.  zone: time.Local of the ban log
+        (default: the fixed offset tz_offset_s)."""
         self.engine = engine or Engine()
         self.banner = banner or MockBanner()
         self.device_bans = device_bans
+        self.device_ban_log = device_ban_log
+        # one batch at a time sees one (config, ruleset, decision lists, ban
+        # options): reload() publishes all of them under this lock
+        self._mu = threading.Lock()
         self.zone = zone if zone is not None else Zone.fixed(tz_offset_s)
         self.banner.zone = self.zone
         self._seen_names: Dict[str, None] = {}
@@ -398,13 +410,25 @@ class RegexRateLimiter:
         reference's atomic config pointer (config_holder.go:28,63): a batch
         takes one snapshot and uses it from process() to its Banner replay, so a
         reload on another thread takes effect at the next batch."""
-        rs = Ruleset(cfg)
-        for r in rs.rules:
-            self._seen_names.setdefault(r.rule, None)
-        self._snap = _Snapshot(cfg, rs)
-        self.engine.set_decision_lists(cfg.decision_entries)
-        self.engine.set_ban_options(cfg.expiring_decision_ttl_seconds,
-                                    [h for h, v in cfg.disable_logging.items() if v], zone=self.zone)
+        rs = Ruleset(cfg)  # compiled outside the lock: a bad config raises here, nothing changes
+        with self._mu:
+            for r in rs.rules:
+                self._seen_names.setdefault(r.rule, None)
+            # the engine's decision lists and ban options first, then the
+            # snapshot: no batch runs between them (it holds the same lock)
+            self.engine.set_decision_lists(cfg.decision_entries)
+            self.engine.set_ban_options(cfg.expiring_decision_ttl_seconds,
+                                        [h for h, v in cfg.disable_logging.items() if v], zone=self.zone)
+            self._snap = _Snapshot(cfg, rs)
+
+    def sighup(self, cfg: Config):
+        """The reference's SIGHUP handler (banjax.go:101-115): Reload; on
+        success the static lists follow the new config (pushed by reload) and
+        the dynamic decision lists are cleared.  A config that does not compile
+        raises and changes nothing, as `continue` does there."""
+        self.reload(cfg)
+        with self._mu:
+            self.banner.decision_lists.clear()
 
     @property
     def config(self) -> Config:
@@ -416,22 +440,29 @@ class RegexRateLimiter:
 
     def consume_lines(self, data: bytes, now_ns: int, want_results: bool = True):
         """consumeLine for every complete line; returns (results, batch output)."""
-        snap = self._snap
-        out = self.engine.process(snap.ruleset, data, now_ns, copy_results=want_results, emit_bans=self.device_bans)
-        return self._finish(snap, data, out, now_ns, want_results)
+        with self._mu:
+            snap = self._snap
+            out = self.engine.process(snap.ruleset, data, now_ns, copy_results=want_results, **self._ban_kw())
+            return self._finish(snap, data, out, now_ns, want_results)
+
+    def _ban_kw(self):
+        if not self.device_bans:
+            return {}
+        return {"emit_bans": True} if self.device_ban_log else {"emit_bans": True, "ban_log": False}
 
     def consume_device_batch(self, host_view, device_ptr: Optional[int], nbytes: int, now_ns: int,
                              want_results: bool = True):
         """consumeLine over a batch already in HBM (the tailer's copy); host_view
         holds the same bytes for the Banner's log lines.  device_ptr None: host."""
-        snap = self._snap
-        if device_ptr is None:
-            out = self.engine.process(snap.ruleset, bytes(host_view[:nbytes]), now_ns, copy_results=want_results,
-                                      emit_bans=self.device_bans)
-        else:
-            out = self.engine.process(snap.ruleset, None, now_ns, copy_results=want_results, device_ptr=device_ptr,
-                                      nbytes=nbytes, emit_bans=self.device_bans)
-        return self._finish(snap, host_view, out, now_ns, want_results)
+        with self._mu:
+            snap = self._snap
+            if device_ptr is None:
+                out = self.engine.process(snap.ruleset, bytes(host_view[:nbytes]), now_ns, copy_results=want_results,
+                                          **self._ban_kw())
+            else:
+                out = self.engine.process(snap.ruleset, None, now_ns, copy_results=want_results, device_ptr=device_ptr,
+                                          nbytes=nbytes, **self._ban_kw())
+            return self._finish(snap, host_view, out, now_ns, want_results)
 
     def _finish(self, snap, data, out, now_ns: int, want_results: bool):
         """Banner replay of the trips in reference order (regex_rate_limiter.go:254-266)
@@ -439,6 +470,13 @@ class RegexRateLimiter:
         rules = snap.ruleset.rules
         if self.device_bans:
             self.banner.apply_device_bans(snap.config, self.engine.bans(), out.trips, data)
+            if not self.device_ban_log:  # records only: LogRegexBan per trip on the host, in order
+                rules, config = snap.ruleset.rules, snap.config
+                for t in out.trips:
+                    line = bytes(data[t.line_offset:t.line_offset + t.line_len])
+                    rule = rules[t.rule_idx]
+                    self.banner.log_regex_ban(config, t.ts_ns, line[t.ip_off:t.ip_off + t.ip_len], rule.rule,
+                                              line[t.rest_off:], rule.decision)
         else:
             self._replay_trips(snap, data, out, now_ns)
         if not want_results:

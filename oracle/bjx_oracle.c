@@ -773,6 +773,9 @@ int orc_decision_get(orc_state *s, const char *ip, size_t il, int *decision, int
   return (int)e->dl + 1;  /* found: domain length + 1 (caller re-asks with a larger buffer) */
 }
 int64_t orc_decision_len(orc_state *s) { return (int64_t)s->decisions.n; }
+/* DynamicDecisionLists.Clear (internal/decision.go:540-546), which the SIGHUP
+   handler runs after a successful ConfigHolder.Reload (banjax.go:101-115) */
+void orc_decision_clear(orc_state *s) { map_free(&s->decisions, free_exp); }
 size_t orc_last_banned_ip(orc_state *s, char *out, size_t cap) {
   size_t k = s->banned_len < cap ? s->banned_len : cap;
   if (s->banned_ip && out) memcpy(out, s->banned_ip, k);

@@ -73,6 +73,7 @@ int64_t orc_state_len(orc_state *s);
 int orc_decision_get(orc_state *s, const char *ip, size_t ip_len, int *decision, int64_t *expires_ns,
                      char *domain, size_t domain_cap);
 int64_t orc_decision_len(orc_state *s);
+void orc_decision_clear(orc_state *s);
 /* MockBanner.bannedIp (regex_rate_limiter_test.go:27-35). */
 size_t orc_last_banned_ip(orc_state *s, char *out, size_t cap);
 /* Banning-log JSON lines produced by LogRegexBan (iptables.go:179-228), each

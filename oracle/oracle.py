@@ -70,6 +70,8 @@ def lib():
         L.orc_decision_get.argtypes = [vp, C.c_char_p, sz, C.POINTER(C.c_int), C.POINTER(i64), C.c_char_p, sz]
         L.orc_decision_len.restype = i64
         L.orc_decision_len.argtypes = [vp]
+        L.orc_decision_clear.restype = None
+        L.orc_decision_clear.argtypes = [vp]
         L.orc_last_banned_ip.restype = sz
         L.orc_last_banned_ip.argtypes = [vp, C.c_char_p, sz]
         L.orc_ban_log.restype = sz
@@ -210,6 +212,10 @@ class State:
 
     def decisions_len(self):
         return lib().orc_decision_len(self._h)
+
+    def decisions_clear(self):
+        """DynamicDecisionLists.Clear (decision.go:540-546), as banjax.go:101-115 after a reload."""
+        lib().orc_decision_clear(self._h)
 
     def banned_ip(self):
         n = lib().orc_last_banned_ip(self._h, None, 0)

@@ -15,7 +15,8 @@ TestRegexWithRate, the user-agent regexp known answers).  No Go toolchain
 exists in this image, so the reference binary cannot produce them directly
 (SURVEY.md §8c).
 
-usage: python tests/golden/make_golden.py      (rewrites tests/golden/*.json.gz)
+usage: python tests/golden/make_golden.py [NAME ...]
+       (rewrites tests/golden/NAME.json.gz, or every fixture without NAME)
 """
 from __future__ import annotations
 
@@ -106,23 +107,42 @@ def workload_batches(name, n_lines, batches, n_ips):
     return w.rules_yaml, out
 
 
+ONLY = set(sys.argv[1:])
+
+
 def run(name, cfg_yaml, batches, note):
+    """batches: (log bytes, now_ns) or (log bytes, now_ns, yaml): the third
+    form first runs the reference's SIGHUP handler with that config
+    (banjax.go:101-115: ConfigHolder.Reload, DynamicDecisionLists.Clear)."""
+    if ONLY and name not in ONLY:
+        return
     cfg = Config.from_yaml(cfg_yaml)
     oc = oracle_config(cfg)
     st = O.State()
     n_rules = len(cfg.all_rules())
     rule_names = [r.rule for r in cfg.all_rules()]  # ruleset index order: globals, then sites in YAML order
     recs, keys = [], {}
-    for data, now in batches:
+    for data, now, *reload in batches:
+        sighup = None
+        if reload:
+            sighup = reload[0]
+            cfg = Config.from_yaml(sighup)
+            oc = oracle_config(cfg)
+            n_rules = len(cfg.all_rules())
+            rule_names = [r.rule for r in cfg.all_rules()]
+            st.decisions_clear()
         flags, res, consumed = st.consume(oc, data, now, cap=(data.count(b"\n") + 1) * (n_rules + 1))
         lines = data[:consumed].split(b"\n")
         results = [[r.line_idx, r.rule_id, r.rule_pos, r.skip_host, r.seen_ip, r.match_type, r.exceeded] for r in res]
         for r in res:
             parts = lines[r.line_idx].split(b" ", 2)
             keys[(parts[1], rule_names[r.rule_id])] = None
-        recs.append({"log_b64": base64.b64encode(data).decode(), "now_ns": now, "consumed": consumed,
-                     "flags": flags, "results": results,
-                     "trips": [[r.line_idx, r.rule_id] for r in res if r.exceeded]})
+        rec = {"log_b64": base64.b64encode(data).decode(), "now_ns": now, "consumed": consumed,
+               "flags": flags, "results": results,
+               "trips": [[r.line_idx, r.rule_id] for r in res if r.exceeded]}
+        if sighup is not None:
+            rec["sighup_yaml"] = sighup
+        recs.append(rec)
     states = []
     for ip, nm in keys:
         g = st.get(ip, nm)
@@ -143,8 +163,36 @@ def run(name, cfg_yaml, batches, note):
         sum(len(r["trips"]) for r in recs)))
 
 
+def integration_challengeme(t):
+    """banjax_integration_test.go:293-325 TestRegexesWithRatesChallengeme: the
+    standalone-testing log lines (internal/http_server.go:150-167) of its
+    requests, then the reload that removes the rule."""
+    L = W.standalone_line
+    return [(L(t, "9.9.9.9", "/1?challengeme"), t * S),
+            (L(t + 2, "9.9.9.9", "/2?challengeme"), (t + 2) * S),
+            (L(t + 3, "9.9.9.9", "/3?challengeme") + L(t + 3, "9.9.9.9", "/4?challengeme"), (t + 3) * S,
+             W.RELOAD_RULES)]
+
+
+def integration_rates(t):
+    """banjax_integration_test.go:327-385 TestRegexesWithRates: hosts_to_skip
+    on `.*`, 46 GETs within 60 s (httpStress sends repeat + 1) -> nginx_block,
+    and the same burst from the global allow list."""
+    L = W.standalone_line
+    return [(L(t, "10.10.10.10", "/1"), t * S),
+            (L(t + 2, "10.10.10.10", "/2"), (t + 2) * S),
+            (L(t + 2, "11.11.11.11", "/45in60") * 46, (t + 2) * S),
+            (L(t + 4, "11.11.11.11", "/45in60"), (t + 4) * S),
+            (L(t + 4, "12.12.12.12", "/45in60-whitelist") * 46, (t + 4) * S),
+            (L(t + 6, "12.12.12.12", "/45in60-whitelist"), (t + 6) * S)]
+
+
 def main():
     t = 1700000000
+    run("integration_challengeme", W.FIXTURE_RULES, integration_challengeme(t),
+        "banjax_integration_test.go:293-325 + SIGHUP reload to fixtures/banjax-config-test-reload.yaml")
+    run("integration_rates", W.REGEX_BANNER_RULES, integration_rates(t),
+        "banjax_integration_test.go:327-385 with fixtures/banjax-config-test-regex-banner.yaml:63-92")
     run("consume_line_sequence", SEQ_CFG, seq_batches(),
         "regex_rate_limiter_test.go:77-260 TestConsumeLine, one batch per line")
     run("fixture_config", W.FIXTURE_RULES, [(fixture_lines(t), t * S), (fixture_lines(t + 1), (t + 1) * S)],

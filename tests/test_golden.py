@@ -24,7 +24,8 @@ def load(path):
 
 def test_golden_set_present():
     assert {"consume_line_sequence", "fixture_config", "edge_lines", "tile_geometry", "workload_cfg1",
-            "workload_cfg2", "workload_cfg3", "workload_cfg4", "workload_cfg5"} <= set(NAMES)
+            "workload_cfg2", "workload_cfg3", "workload_cfg4", "workload_cfg5", "integration_challengeme",
+            "integration_rates"} <= set(NAMES)
 
 
 @pytest.mark.parametrize("path", GOLDEN, ids=NAMES)
@@ -35,6 +36,11 @@ def test_oracle_reproduces_golden(path):
     st = O.State()
     n_rules = len(cfg.all_rules())
     for b in fx["batches"]:
+        if "sighup_yaml" in b:  # banjax.go:101-115: Reload, then DynamicDecisionLists.Clear
+            cfg = Config.from_yaml(b["sighup_yaml"])
+            oc = oracle_config(cfg)
+            n_rules = len(cfg.all_rules())
+            st.decisions_clear()
         data = base64.b64decode(b["log_b64"])
         flags, res, consumed = st.consume(oc, data, b["now_ns"], cap=(data.count(b"\n") + 1) * (n_rules + 1))
         assert consumed == b["consumed"]
@@ -67,6 +73,8 @@ def test_engine_reproduces_golden(engine, path, device_bans):
     engine.state_clear()
     lim = RegexRateLimiter(cfg, engine=engine, banner=MockBanner(), device_bans=device_bans)
     for b in fx["batches"]:
+        if "sighup_yaml" in b:
+            lim.sighup(Config.from_yaml(b["sighup_yaml"]))
         data = base64.b64decode(b["log_b64"])
         _, out = lim.consume_lines(data, b["now_ns"], want_results=True)
         assert out.consumed_bytes == b["consumed"]

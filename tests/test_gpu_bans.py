@@ -178,3 +178,21 @@ def test_device_bans_records_only(engine):
     assert full.ip_bytes == rec.ip_bytes and np.array_equal(full.ip_off, rec.ip_off)
     assert len(full.log) > 0 and rec.log == b""
     assert not rec.log_kind.any() and not rec.log_off.any()
+
+
+def test_device_bans_records_only_first():
+    """Records-only as the first emission of a fresh engine, then a larger
+    batch (the IP-length scratch was sized only by the full
+    emission): the records equal the oracle's Banner replay each time."""
+    from banjax_amd import Engine
+    e = Engine()
+    try:
+        w = W.scaled(W.CFG5, 60_000, n_ips=6_000)
+        pair = Pair(w.rules_yaml, e, device_bans=True)
+        pair.lim.device_ban_log = False
+        for lo, n in ((0, 10_000), (10_000, 50_000)):
+            out = pair.feed(w.host_lines(lo, n), w.now_ns(lo, n))
+            assert out.n_trips > 0 and e.bans().log == b""
+        pair.compare_state()  # decision lists and the host-written ban log vs the oracle replay
+    finally:
+        e.close()

@@ -148,3 +148,84 @@ def test_line_errors_and_old_lines():
         + line(t - 11, "1.2.3.4 GET h GET / x") + line(t - 9, "1.2.3.4 GET h GET / x") + b"1e400 1.2.3.4 GET h x\n"
     flags, res, _ = st.consume(cfg, buf, now)
     assert flags == [1, 1, 1, 1, 1, 2, 0, 1]
+
+
+# ---- banjax_integration_test.go:293-385: the reference's end-to-end rate-limit
+# cases, restated at the consumeLine boundary.  In -standalone-testing mode the
+# HTTP server writes one log line per request (internal/http_server.go:150-167,
+# workloads.standalone_line) and the tailer consumes it; the HTTP status the
+# test asserts comes from the dynamic decision list the trips leave behind
+# (Challenge -> 429, NginxBlock -> 403, none -> 200).
+
+def _kat_state(yaml_text):
+    from banjax_amd import Config
+    from tests.parity import oracle_config
+    cfg = Config.from_yaml(yaml_text)
+    return oracle_config(cfg), [r.rule for r in cfg.all_rules()]
+
+
+def _summary(res, names):
+    return [(r.line_idx, names[r.rule_id], r.skip_host, r.seen_ip, r.match_type, r.exceeded) for r in res]
+
+
+FT, OI, II = 0, 1, 2  # RateLimitMatchType: FirstTime, OutsideInterval, InsideInterval
+
+
+def test_regexes_with_rates_challengeme_and_reload():
+    """TestRegexesWithRatesChallengeme (:293-325) with
+    fixtures/banjax-config-test.yaml, then the SIGHUP reload to
+    fixtures/banjax-config-test-reload.yaml (banjax.go:101-115), which removes
+    the rule and clears the dynamic decision lists."""
+    import workloads as W
+    cfg, names = _kat_state(W.FIXTURE_RULES)
+    st = O.State()
+    t0 = 1700000000
+    # request 1 passes (its own trip lands after the response) ...
+    flags, res, _ = st.consume(cfg, W.standalone_line(t0, "9.9.9.9", "/1?challengeme"), t0 * S)
+    assert flags == [0]
+    assert _summary(res, names) == [(0, "instant challenge", 0, 0, FT, 1)]
+    assert st.decision("9.9.9.9") == (O.CHALLENGE, (t0 + 10) * S, "localhost:8081")
+    # ... request 2, two seconds later, meets the Challenge: 429
+    flags, res, _ = st.consume(cfg, W.standalone_line(t0 + 2, "9.9.9.9", "/2?challengeme"), (t0 + 2) * S)
+    assert _summary(res, names) == [(0, "instant challenge", 0, 1, OI, 1)]
+    assert st.decision("9.9.9.9")[0] == O.CHALLENGE
+    # SIGHUP: the rule is gone and the dynamic lists are cleared: 200, 200
+    cfg, names = _kat_state(W.RELOAD_RULES)
+    st.decisions_clear()
+    for k in (3, 4):
+        flags, res, _ = st.consume(cfg, W.standalone_line(t0 + 3, "9.9.9.9", "/%d?challengeme" % k), (t0 + 3) * S)
+        assert flags == [0] and res == []
+    assert st.decision("9.9.9.9") is None and st.decisions_len() == 0
+    # RegexRateLimitStates survives the reload (banjax.go:113-115 keeps regexStates)
+    assert st.get("9.9.9.9", "instant challenge") == (0, (t0 + 2) * S)
+
+
+def test_regexes_with_rates_skip_limit_and_allow_list():
+    """TestRegexesWithRates (:327-385) with
+    fixtures/banjax-config-test-regex-banner.yaml:63-92."""
+    import workloads as W
+    cfg, names = _kat_state(W.REGEX_BANNER_RULES)
+    st = O.State()
+    t0 = 1700000000
+    every, get45 = "Challenge all but skip localhost:8081", "All sites/GET: 45 req/60 sec"
+    # target 1: `.*` challenges every host but localhost:8081 -> SkipHost, no Apply: 200, 200
+    flags, res, _ = st.consume(cfg, W.standalone_line(t0, "10.10.10.10", "/1"), t0 * S)
+    assert _summary(res, names) == [(0, every, 1, 0, FT, 0), (0, get45, 0, 0, FT, 0)]
+    flags, res, _ = st.consume(cfg, W.standalone_line(t0 + 2, "10.10.10.10", "/2"), (t0 + 2) * S)
+    assert _summary(res, names) == [(0, every, 1, 0, FT, 0), (0, get45, 0, 1, II, 0)]
+    assert st.decision("10.10.10.10") is None and st.get("10.10.10.10", every) is None
+    # target 2: httpStress sends repeat + 1 = 46 requests; the 46th exceeds 45 in 60 s
+    buf = W.standalone_line(t0 + 2, "11.11.11.11", "/45in60") * 46
+    flags, res, _ = st.consume(cfg, buf, (t0 + 2) * S)
+    g = [x for x in _summary(res, names) if x[1] == get45]
+    assert len(g) == 46 and g[0][2:] == (0, 0, FT, 0)
+    assert all(x[2:] == (0, 1, II, 0) for x in g[1:45]) and g[45][2:] == (0, 1, II, 1)
+    assert st.decision("11.11.11.11") == (O.NGINX_BLOCK, (t0 + 12) * S, "localhost:8081")  # -> 403
+    flags, res, _ = st.consume(cfg, W.standalone_line(t0 + 4, "11.11.11.11", "/45in60"), (t0 + 4) * S)
+    assert [x for x in _summary(res, names) if x[1] == get45] == [(0, get45, 0, 1, II, 0)]
+    assert st.get("11.11.11.11", get45) == (1, (t0 + 2) * S)
+    # target 3: the same 46 requests from the global allow list: Exempted, no state, 200
+    buf = W.standalone_line(t0 + 4, "12.12.12.12", "/45in60-whitelist") * 46
+    flags, res, _ = st.consume(cfg, buf, (t0 + 4) * S)
+    assert flags == [O.LINE_EXEMPTED] * 46 and res == []
+    assert st.get("12.12.12.12", get45) is None and st.decision("12.12.12.12") is None

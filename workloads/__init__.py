@@ -293,6 +293,110 @@ regexes_with_rates:
 CFG1 = Workload("cfg1", "fixtures/banjax-config-test.yaml rules over 1M synthetic nginx lines, IPs Zipf(1.1) over 100k",
                 FIXTURE_RULES, seed=1, n_lines=1_000_000, n_ips=100_000, n_hosts=32, trigger_permille=10,
                 fixture_hosts=1, ip_mode=1)
+REGEX_BANNER_RULES = """\
+# fixtures/banjax-config-test-regex-banner.yaml (reference): the hot-path keys only
+global_decision_lists:
+  allow:
+    - 20.20.20.20
+    - 12.12.12.12
+  iptables_block:
+    - 30.40.50.60
+  nginx_block:
+    - 70.80.90.100
+  challenge:
+    - 8.8.8.8
+per_site_decision_lists:
+  example.com:
+    allow:
+      - 90.90.90.90
+    challenge:
+      - 91.91.91.91
+  "localhost:8081":
+    allow:
+      - 90.90.90.90
+    challenge:
+      - 91.91.91.91
+    nginx_block:
+      - 92.92.92.92
+per_site_regexes_with_rates: {}
+regexes_with_rates:
+  - decision: allow
+    hits_per_interval: 0
+    interval: 1
+    regex: .*allowme.*
+    rule: "unblock backdoor"
+  - decision: nginx_block
+    hits_per_interval: 0
+    interval: 1
+    regex: .*blockme.*
+    rule: "instant block"
+  - decision: challenge
+    hits_per_interval: 0
+    interval: 1
+    regex: .*challengeme.*
+    rule: "instant challenge"
+  - decision: challenge
+    hits_per_interval: 0
+    interval: 1
+    regex: .*
+    rule: "Challenge all but skip localhost:8081"
+    hosts_to_skip:
+      "localhost:8081": true
+  - decision: nginx_block
+    hits_per_interval: 45
+    interval: 60
+    regex: "GET .* /"
+    rule: "All sites/GET: 45 req/60 sec"
+expiring_decision_ttl_seconds: 10
+"""
+
+RELOAD_RULES = """\
+# fixtures/banjax-config-test-reload.yaml (reference): the hot-path keys only
+global_decision_lists:
+  allow: []
+  iptables_block:
+    - 30.40.50.60
+  nginx_block:
+    - 70.80.90.100
+  challenge:
+    - 20.20.20.20
+per_site_decision_lists:
+  example.com:
+    allow:
+      - 90.90.90.90
+    challenge:
+      - 91.91.91.91
+  "localhost:8081":
+    allow:
+      - 91.91.91.91
+    challenge: []
+    nginx_block:
+      - 92.92.92.92
+per_site_regexes_with_rates: {}
+regexes_with_rates:
+  - decision: allow
+    hits_per_interval: 0
+    interval: 1
+    regex: .*allowme.*
+    rule: "unblock backdoor"
+  - decision: nginx_block
+    hits_per_interval: 0
+    interval: 1
+    regex: .*blockme.*
+    rule: "instant block"
+expiring_decision_ttl_seconds: 10
+"""
+
+
+def standalone_line(t_s: int, ip: str, path: str, host: str = "localhost:8081", method: str = "GET",
+                    ua: str = "Go-http-client/1.1") -> bytes:
+    """The log line banjax's standalone-testing middleware writes for each
+    integration-test request (reference internal/http_server.go:150-167):
+    '%f %s %s %s %s %s HTTP/1.1 %s' of float64(Unix seconds), X-Client-IP,
+    method, Host, method, the `path` query value, User-Agent."""
+    return ("%f %s %s %s %s %s HTTP/1.1 %s\n" % (float(t_s), ip, method, host, method, path, ua)).encode()
+
+
 CFG2 = Workload("cfg2", "100 global rules (TestPerSiteRegexStress shape + banjax-config.yaml globals), 100M lines, 1M IPs",
                 stress_global_rules(100) + "expiring_decision_ttl_seconds: 10\n",
                 seed=2, n_lines=100_000_000, n_ips=1_000_000, n_hosts=100)
