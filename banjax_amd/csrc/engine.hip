@@ -389,6 +389,7 @@ __device__ bool rule_match(const Bind &B, uint32_t r, const uint8_t *t, uint32_t
   const DevRule R = B.rules[r];
   if (R.flags & kRuleAlways) return true;
   if (R.flags & kRuleNever) return false;
+  if (R.flags & kRuleNfaWide) return false;  // never asked: the per-line fallback lists wide rules for k_nfa_wide
   if (R.flags & kRuleNfa) return nfa_match_generic(B, R, t, n);
   const uint16_t *tr = B.trans + R.trans_off;
   const uint8_t *ac = B.ascii_cls + (size_t)r * 128;
@@ -421,9 +422,16 @@ __device__ bool rule_match(const Bind &B, uint32_t r, const uint8_t *t, uint32_t
 
 // --------------------------------------------------------------- per line
 
+// Wide-NFA jobs of the per-line fallback (k_nfa_wide runs them after it)
+struct WideList {
+  uint32_t *line, *rule, *pos;
+  unsigned long long *count;
+  uint64_t cap;
+};
+
 template <bool SLOW>
 __device__ void parse_and_match(const Bind &B, const uint8_t *__restrict__ p, uint32_t n, uint64_t j, int64_t now_ns,
-                                const Lines &L, uint32_t *slow_list, unsigned long long *slow_count) {
+                                const Lines &L, uint32_t *slow_list, unsigned long long *slow_count, const WideList &WL) {
   uint8_t fl = 0;
   L.counts[j] = 0;
   const uint32_t sp1 = find_space(p, 0, n);
@@ -476,7 +484,10 @@ __device__ void parse_and_match(const Bind &B, const uint8_t *__restrict__ p, ui
   const uint32_t napp = (s_end - s_begin) + B.n_global;
   for (uint32_t k = 0; k < napp; ++k) {
     const uint32_t r = k < s_end - s_begin ? B.site_rules[s_begin + k] : B.global_rules[k - (s_end - s_begin)];
-    if (rule_match(B, r, rest, rest_len)) {
+    if (B.any_wide && (B.rules[r].flags & kRuleNfaWide)) {
+      const unsigned long long q = atomicAdd(WL.count, 1ull);
+      if (q < WL.cap) { WL.line[q] = (uint32_t)j; WL.rule[q] = r; WL.pos[q] = pos; }
+    } else if (rule_match(B, r, rest, rest_len)) {
       word |= 1ull << (pos & 63);
       ++nres;
       nev += is_skip(B, r, hid) ? 0u : 1u;
@@ -492,13 +503,13 @@ template <bool SLOW>
 __global__ __launch_bounds__(kBlock) void k_parse_match(Bind B, const uint8_t *__restrict__ buf,
                                                         const uint64_t *__restrict__ nl, uint64_t n_lines,
                                                         const uint32_t *__restrict__ list, int64_t now_ns, Lines L,
-                                                        uint32_t *slow_list, unsigned long long *slow_count) {
+                                                        uint32_t *slow_list, unsigned long long *slow_count, WideList WL) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_lines) return;
   const uint64_t j = SLOW ? list[t] : t;
   const uint64_t s = j ? nl[j - 1] + 1 : 0;
   const uint32_t n = (uint32_t)(nl[j] - s);
-  parse_and_match<SLOW>(B, buf + s, n, j, now_ns, L, slow_list, slow_count);
+  parse_and_match<SLOW>(B, buf + s, n, j, now_ns, L, slow_list, slow_count, WL);
 }
 
 // =====================================================================
@@ -2026,6 +2037,133 @@ __global__ __launch_bounds__(kBlock) void k_nfa(Bind B, uint32_t rule, const uin
   atomicAdd(reinterpret_cast<unsigned long long *>(L.counts + j), (1ull << 32) | (skp ? 0ull : 1ull));
 }
 
+// Jobs of kRuleNfaWide rules (regex_compiler.h NfaWideLayout: past the
+// per-lane NFA's 1024 positions, e.g. `(?s).*x.{600}y.{600}z`): one block per
+// job, the W-word state in LDS (GLB = false) or in a per-block HBM scratch
+// (patterns whose state does not fit).  Each thread owns a run of kw words;
+// per rune (every thread decodes the same rune): assertion closures of the
+// context into A (sparse target lists), the match check, Y = A & CM[c] with
+// the groups of Y's positions marked, A = shift(Y & SH) | S0 (the carry from
+// the previous thread's last word), then the marked groups' targets into A.
+// Same steps as nfa_rune / nfa_wide_match_host.  jpos: RuleResult positions
+// of the per-line fallback's jobs (null: position = key >> 24).
+template <bool GLB>
+__device__ __forceinline__ void wide_sync() {
+  if (GLB) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (GLB) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+template <bool GLB>
+__global__ __launch_bounds__(kBlock) void k_nfa_wide(Bind B, const uint8_t *__restrict__ buf, uint64_t n_buf,
+                                                     const uint64_t *__restrict__ nl, const uint32_t *__restrict__ jkey,
+                                                     const uint32_t *__restrict__ jline, const uint32_t *__restrict__ jpos,
+                                                     uint64_t j0, uint64_t j1, Lines L, uint64_t *scratch,
+                                                     uint64_t scratch_words) {
+  __shared__ uint32_t s_flag;
+  const uint32_t tid = threadIdx.x;
+  for (uint64_t t = j0 + blockIdx.x; t < j1; t += gridDim.x) {
+    const uint32_t key = jkey[t], r = key & 0xFFFFFFu;
+    const uint32_t pos = jpos ? jpos[t] : key >> 24;
+    const uint64_t j = jline[t];
+    const DevRule R = B.rules[r];
+    const uint64_t *b = B.nfa + R.nfa_off;
+    const NfaWideLayout Ly = nfa_wide_layout_of(reinterpret_cast<const uint32_t *>(b));
+    const uint32_t W = Ly.W, kw = (W + kBlock - 1) / kBlock, w0 = min(W, tid * kw), w1 = min(W, w0 + kw);
+    const uint32_t gw = (Ly.ngroups + 31) / 32;
+    uint64_t *A = GLB ? scratch + blockIdx.x * scratch_words : reinterpret_cast<uint64_t *>(s_dyn);
+    uint64_t *Yb = A + W;
+    uint32_t *gmark = reinterpret_cast<uint32_t *>(Yb + W);
+    const uint64_t *s0 = b + Ly.o_s0, *sh = b + Ly.o_sh, *gall = b + Ly.o_gall, *am = b + Ly.o_am;
+    const uint16_t *a16 = reinterpret_cast<const uint16_t *>(b + Ly.o_ascii);
+    const uint8_t *cat = reinterpret_cast<const uint8_t *>(b + Ly.o_cat);
+    const uint32_t *aux = reinterpret_cast<const uint32_t *>(b + Ly.o_aux);
+    const uint32_t *goff = reinterpret_cast<const uint32_t *>(b + Ly.o_goff), *gtgt = reinterpret_cast<const uint32_t *>(b + Ly.o_gtgt);
+    const uint32_t *aoff = reinterpret_cast<const uint32_t *>(b + Ly.o_aoff), *atgt = reinterpret_cast<const uint32_t *>(b + Ly.o_atgt);
+    const uint32_t mw = Ly.match >> 6;
+    const uint64_t mbit = 1ull << (Ly.match & 63);
+    const bool owner = Ly.match != 0xFFFFFFFFu && mw >= w0 && mw < w1;
+    for (uint32_t w = w0; w < w1; ++w) A[w] = s0[w];
+    for (uint32_t i = tid; i < gw; i += kBlock) gmark[i] = 0;
+    if (tid == 0) s_flag = 0;
+    wide_sync<GLB>();
+    auto cross = [&](uint32_t k) {  // A |= closures (context k) of the assertions in A
+      for (uint32_t w = w0; w < w1; ++w)
+        for (uint64_t m = A[w] & am[w]; m; m &= m - 1) {
+          const uint32_t a = aux[w * 64u + (uint32_t)__builtin_ctzll(m)];
+          for (uint32_t i = aoff[a * 16 + k]; i < aoff[a * 16 + k + 1]; ++i)
+            atomicOr(reinterpret_cast<unsigned long long *>(&A[atgt[i] >> 6]), 1ull << (atgt[i] & 63));
+        }
+    };
+    const uint64_t s = j ? nl[j - 1] + 1 : 0;
+    const uint64_t end = nl[j];
+    uint64_t i = s + L.rest_off[j];
+    uint32_t ctx = 3;
+    bool m = false;
+    while (i < end) {
+      uint32_t c;
+      const uint8_t by = buf[i];
+      if (by < 0x80) { c = a16[by]; ++i; }
+      else {
+        int wd;
+        const int32_t rune = decode_rune_hd(buf + i, (uint32_t)(end - i), &wd);
+        c = nonascii_class(B, R, rune);
+        i += (uint32_t)wd;
+      }
+      const uint32_t cc = (Ly.flags & kNfaAsserts) ? cat[c] : 0u;
+      if (Ly.flags & kNfaAsserts) {
+        cross(ctx * 4 + cc);
+        wide_sync<GLB>();
+        // matched before c (without assertions A is the D checked after the
+        // previous rune); every read of s_flag came before the barrier above
+        if (owner && (A[mw] & mbit)) s_flag = 1;
+      }
+      ctx = cc == 1 ? 1u : (cc == 2 ? 2u : 0u);
+      const uint64_t *cm = b + Ly.o_cm + (uint64_t)c * W;
+      for (uint32_t w = w0; w < w1; ++w) {
+        const uint64_t y = A[w] & cm[w];
+        Yb[w] = y;
+        for (uint64_t g = y & gall[w]; g; g &= g - 1) {
+          const uint32_t gid = aux[w * 64u + (uint32_t)__builtin_ctzll(g)];
+          atomicOr(&gmark[gid >> 5], 1u << (gid & 31));
+        }
+      }
+      wide_sync<GLB>();
+      if (s_flag) { m = true; break; }
+      for (uint32_t w = w0; w < w1; ++w)
+        A[w] = ((Yb[w] & sh[w]) << 1) | (w ? (Yb[w - 1] & sh[w - 1]) >> 63 : 0ull) | s0[w];
+      wide_sync<GLB>();
+      for (uint32_t gi = tid; gi < gw; gi += kBlock) {
+        uint32_t mm = gmark[gi];
+        if (!mm) continue;
+        gmark[gi] = 0;
+        for (; mm; mm &= mm - 1) {
+          const uint32_t g = gi * 32 + (uint32_t)__ffs(mm) - 1;
+          for (uint32_t q = goff[g]; q < goff[g + 1]; ++q)
+            atomicOr(reinterpret_cast<unsigned long long *>(&A[gtgt[q] >> 6]), 1ull << (gtgt[q] & 63));
+        }
+      }
+      wide_sync<GLB>();
+      if (owner && (A[mw] & mbit)) s_flag = 1;  // matched after c
+      wide_sync<GLB>();
+      if (s_flag) { m = true; break; }
+    }
+    if (!m) {  // end of text: the assertions once more with next category "end"
+      if (Ly.flags & kNfaAsserts) cross(ctx * 4 + 3);
+      wide_sync<GLB>();  // also: every read of s_flag in the loop came before this
+      if (owner && (A[mw] & mbit)) s_flag = 1;
+      wide_sync<GLB>();
+      m = s_flag != 0;
+    }
+    if (m && tid == 0) {
+      const int32_t hid = L.host_id[j];
+      atomicOr(reinterpret_cast<unsigned long long *>(L.masks + j * B.mask_words + (pos >> 6)), 1ull << (pos & 63));
+      atomicAdd(reinterpret_cast<unsigned long long *>(L.counts + j), (1ull << 32) | (is_skip(B, r, hid) ? 0ull : 1ull));
+    }
+    wide_sync<GLB>();  // the next job reuses A / Yb / gmark / s_flag
+  }
+}
+
 // first / one-past-last sorted job of every rule that has jobs
 __global__ void k_rule_bounds(uint64_t n, const uint32_t *__restrict__ jkey, uint32_t *__restrict__ first,
                               uint32_t *__restrict__ last) {
@@ -3434,6 +3572,9 @@ struct bjx_engine {
   DevBuf<uint64_t> long_heads;
   DevBuf<uint64_t> lr_end, lr_len, lr_off, lr_win;
   DevBuf<unsigned long long> chk;
+  DevBuf<uint64_t> wide_scratch;             // k_nfa_wide<true>: per-block state sets
+  DevBuf<uint32_t> wl_line, wl_rule, wl_pos;  // the per-line fallback's wide-NFA jobs
+  uint32_t wide_max_w = 0, wide_max_g = 0, n_wide = 0;
   DevBuf<uint32_t> chk_w;  // BJX_CHECK: per-outcome write counts, event-index counts
   DevBuf<int64_t> lr_t0, lr_h0;
   DevBuf<uint32_t> lr_flags, lr_nwin;
@@ -4448,11 +4589,24 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.n_pref_glob = (uint32_t)pref_glob.size();
   B.nfa = reinterpret_cast<const uint64_t *>(base + o_nfa);
   B.any_nfa = nfa_blob.empty() ? 0 : 1;
+  B.any_wide = 0;
+  for (const auto &rr : rs->rules) B.any_wide |= (rr.rx.flags & kRuleNfaWide) ? 1u : 0u;
   // DFA jobs name the first rule of each pattern (canon): those of the NFA rules
   e->nfa_rules.clear();
+  e->wide_max_w = e->wide_max_g = e->n_wide = 0;
   for (uint32_t r = 0; r < (uint32_t)rs->rules.size(); ++r)
-    if (canon[r] == r && (rs->rules[r].rx.flags & kRuleNfa) && !(rs->rules[r].rx.flags & (kRuleAlways | kRuleNever)))
-      e->nfa_rules.push_back(make_uint4(r, rs->rules[r].rx.nfa_words, (uint32_t)rs->rules[r].rx.nfa.size(), 0));
+    if (canon[r] == r && (rs->rules[r].rx.flags & kRuleNfa) && !(rs->rules[r].rx.flags & (kRuleAlways | kRuleNever))) {
+      const CompiledRegex &rx = rs->rules[r].rx;
+      if (rx.flags & kRuleNfaWide) {
+        const uint32_t ng = reinterpret_cast<const uint32_t *>(rx.nfa.data())[3];
+        e->nfa_rules.push_back(make_uint4(r, rx.nfa_words, ng, 1));
+        e->wide_max_w = std::max(e->wide_max_w, rx.nfa_words);
+        e->wide_max_g = std::max(e->wide_max_g, ng);
+        ++e->n_wide;
+      } else {
+        e->nfa_rules.push_back(make_uint4(r, rx.nfa_words, (uint32_t)rx.nfa.size(), 0));
+      }
+    }
   e->host_rules = drules;
   {
     // the state-slot cache follows the first global rule that matches every line
@@ -4867,6 +5021,27 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
   }
 }
 
+// k_nfa_wide over jobs [j0, j1): the state in LDS when it fits 64 KB, else
+// in a per-block HBM scratch (grid-stride over the jobs either way)
+static void launch_wide(bjx_engine *e, const Bind &B, const uint8_t *buf, uint64_t n, const uint32_t *jkey,
+                        const uint32_t *jline, const uint32_t *jpos, uint64_t j0, uint64_t j1, const Lines &L, uint32_t W,
+                        uint32_t ng) {
+  hipStream_t st = e->stream;
+  const uint64_t words = 2ull * W + (ng + 63) / 64 + 1;
+  static const bool force_glb = getenv("BJX_WIDE_GLB") != nullptr;  // test hook: the HBM-scratch variant
+  if (words * 8 <= 64 * 1024 && !force_glb) {
+    const unsigned grid = (unsigned)std::min<uint64_t>(j1 - j0, 8192);
+    hipLaunchKernelGGL(k_nfa_wide<false>, dim3(grid), dim3(kBlock), (uint32_t)(words * 8), st, B, buf, n, e->nl.p, jkey,
+                       jline, jpos, j0, j1, L, nullptr, (uint64_t)0);
+  } else {
+    const unsigned grid = (unsigned)std::min<uint64_t>(j1 - j0, 512);
+    e->wide_scratch.ensure(grid * words);
+    hipLaunchKernelGGL(k_nfa_wide<true>, dim3(grid), dim3(kBlock), 0, st, B, buf, n, e->nl.p, jkey, jline, jpos, j0, j1, L,
+                       e->wide_scratch.p, words);
+  }
+  HIP_OK(hipGetLastError());
+}
+
 // The sorted DFA jobs of the bit-parallel NFA rules: each rule's job range
 // (k_rule_bounds), then one k_nfa launch per rule with its state width.
 static void run_nfa_jobs(bjx_engine *e, const Bind &B, const uint8_t *buf, uint64_t n, uint64_t n_jobs, const Lines &L) {
@@ -4883,6 +5058,10 @@ static void run_nfa_jobs(bjx_engine *e, const Bind &B, const uint8_t *buf, uint6
   for (const uint4 &nr : e->nfa_rules) {
     const uint64_t j0 = e->h_first[nr.x], j1 = e->h_last[nr.x];
     if (j1 <= j0) continue;
+    if (nr.w) {  // kRuleNfaWide: nr.y = state words, nr.z = groups
+      launch_wide(e, B, buf, n, e->jkey2.p, e->jline2.p, nullptr, j0, j1, L, nr.y, nr.z);
+      continue;
+    }
     const unsigned grid = grid_for(j1 - j0);
     const uint32_t lds = nr.z * 8;
     switch (nr.y) {
@@ -5146,9 +5325,23 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     if (B.any_nfa && !e->nfa_rules.empty()) run_nfa_jobs(e, B, buf, n, n_jobs, L);
   }
   if (n_slow) {
+    WideList WL{nullptr, nullptr, nullptr, e->scalars.p + 13, 0};
+    if (B.any_wide) {
+      const uint64_t cap = n_slow * (uint64_t)e->n_wide + 1;
+      e->wl_line.ensure(cap); e->wl_rule.ensure(cap); e->wl_pos.ensure(cap);
+      WL.line = e->wl_line.p; WL.rule = e->wl_rule.p; WL.pos = e->wl_pos.p; WL.cap = cap;
+      HIP_OK(hipMemsetAsync(e->scalars.p + 13, 0, 8, st));
+    }
     hipLaunchKernelGGL(k_parse_match<true>, dim3(grid_for(n_slow)), dim3(kBlock), 0, st, B, buf, e->nl.p, (uint64_t)n_slow,
-                       e->slow_list.p, now_ns, L, e->slow_list.p, e->scalars.p);
+                       e->slow_list.p, now_ns, L, e->slow_list.p, e->scalars.p, WL);
     HIP_OK(hipGetLastError());
+    if (B.any_wide) {
+      unsigned long long n_wl = 0;
+      HIP_OK(hipMemcpyAsync(&n_wl, e->scalars.p + 13, 8, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      if (n_wl > WL.cap) throw BjxError(BJX_ERR_DEVICE, "internal: wide-NFA job list overflow");
+      if (n_wl) launch_wide(e, B, buf, n, e->wl_rule.p, e->wl_line.p, e->wl_pos.p, 0, n_wl, L, e->wide_max_w, e->wide_max_g);
+    }
   }
   e->last_slow = n_slow;
   if (e->dbg_hash_mask)
@@ -5898,6 +6091,12 @@ extern "C" int bjx_debug_set_dfa_state_cap(uint32_t cap) {
   set_dfa_state_cap(cap);
   std::lock_guard<std::mutex> g(g_rx_mu);
   g_rx_cache.clear();  // compiled patterns depend on the cap
+  return BJX_OK;
+}
+extern "C" int bjx_debug_force_wide_nfa(int on) {
+  set_force_wide_nfa(on != 0);
+  std::lock_guard<std::mutex> g(g_rx_mu);
+  g_rx_cache.clear();  // compiled patterns depend on it
   return BJX_OK;
 }
 extern "C" int bjx_debug_set_ip_hash_mask(bjx_engine *e, uint64_t mask) {

@@ -168,6 +168,7 @@ struct Bind {
   // bit-parallel NFA tables of the kRuleNfa rules (DevRule::nfa_off)
   const uint64_t *nfa;
   uint32_t any_nfa;
+  uint32_t any_wide;  // some rule is kRuleNfaWide (the per-line fallback lists those for k_nfa_wide)
   // rule plans (decide_plan): per rule of a scope that is neither ALWAYS nor
   // NEVER, one 32 B entry {a, b} holding everything its decision needs (kind,
   // position, literal ids, host-split full literal, inline anchor test), so a

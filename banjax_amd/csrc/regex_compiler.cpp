@@ -731,7 +731,7 @@ struct Nfa {
   std::map<Ranges, int32_t> set_ids;
   int32_t start = -1;
   uint8_t conds = 0;  // union of assertion kinds present
-  size_t limit = 2000000;
+  size_t limit = 8000000;  // past Go's program limit (regexp/syntax maxSize, 3355443 instructions)
 
   int32_t node(NK k) {
     if (nodes.size() >= limit) throw ParseError{"", ""};
@@ -1534,24 +1534,32 @@ class BitNfaBuilder {
  public:
   BitNfaBuilder(const Nfa &nfa, const ClassPart &P) : n_(nfa), P_(P) {}
 
-  int build(CompiledRegex *out) {
+  // DFS preorder numbering over the position graph (false past `limit`)
+  bool number(std::vector<int32_t> &s0, uint32_t limit) {
     mark_.assign(n_.nodes.size(), 0);
     pos_.assign(n_.nodes.size(), -1);
-    std::vector<int32_t> s0;
+    order_.clear();
+    kids_.clear();
+    s0.clear();
     closure(n_.start, 0, false, s0);
-    // DFS preorder numbering over the position graph
     std::vector<int32_t> st(s0.rbegin(), s0.rend());
     while (!st.empty()) {
       const int32_t i = st.back();
       st.pop_back();
       if (pos_[i] >= 0) continue;
-      if (order_.size() >= kNfaMaxPos) return BJX_ERR_TOO_COMPLEX;
+      if (order_.size() >= limit) return false;
       pos_[i] = static_cast<int32_t>(order_.size());
       order_.push_back(i);
       const std::vector<int32_t> &ch = children(i);
       for (auto it = ch.rbegin(); it != ch.rend(); ++it)
         if (pos_[*it] < 0) st.push_back(*it);
     }
+    return true;
+  }
+
+  int build(CompiledRegex *out) {
+    std::vector<int32_t> s0;
+    if (!number(s0, kNfaMaxPos)) return BJX_ERR_TOO_COMPLEX;
     const uint32_t npos = static_cast<uint32_t>(order_.size());
     uint32_t W = 1;
     while (64 * W < npos) W *= 2;
@@ -1641,6 +1649,108 @@ class BitNfaBuilder {
     return 0;
   }
 
+  // The wide NFA (kRuleNfaWide, regex_compiler.h NfaWideLayout): the same
+  // positions, S0 / SH / CM as build(); each group's follow targets and each
+  // (assertion, context) closure as a sorted target list instead of a W-word
+  // mask, so the tables grow with the pattern, not with groups x positions.
+  int build_wide(CompiledRegex *out) {
+    std::vector<int32_t> s0;
+    if (!number(s0, kNfaWideMaxPos)) return BJX_ERR_TOO_COMPLEX;
+    const uint32_t npos = static_cast<uint32_t>(order_.size());
+    const uint32_t W = (npos + 63) / 64;
+    std::vector<uint64_t> s0m(W, 0), sh(W, 0), gall(W, 0), am(W, 0);
+    auto set = [](std::vector<uint64_t> &v, uint32_t p) { v[p / 64] |= 1ull << (p % 64); };
+    for (int32_t i : s0) set(s0m, static_cast<uint32_t>(pos_[i]));
+    std::vector<uint32_t> aux(npos, 0);
+    std::map<std::vector<int32_t>, uint32_t> group_of;
+    std::vector<std::vector<int32_t>> gtarget;
+    std::vector<uint32_t> asserts;
+    uint32_t match = 0xFFFFFFFFu;
+    for (uint32_t p = 0; p < npos; ++p) {
+      const int32_t node = order_[p];
+      const NNode &nd = n_.nodes[node];
+      if (nd.k == NK_MATCH) match = p;
+      if (nd.k == NK_ASSERT) {
+        aux[p] = static_cast<uint32_t>(asserts.size());
+        asserts.push_back(p);
+        set(am, p);
+        continue;
+      }
+      if (nd.k != NK_CHAR) continue;
+      std::vector<int32_t> rest;
+      for (int32_t f : children(node)) {
+        if (static_cast<uint32_t>(pos_[f]) == p + 1) set(sh, p);
+        else rest.push_back(pos_[f]);
+      }
+      if (rest.empty()) continue;
+      std::sort(rest.begin(), rest.end());
+      auto it = group_of.find(rest);
+      if (it == group_of.end()) {
+        it = group_of.emplace(rest, static_cast<uint32_t>(gtarget.size())).first;
+        gtarget.push_back(rest);
+      }
+      aux[p] = it->second;
+      set(gall, p);
+    }
+    const uint32_t ncls = P_.ncls, ng = static_cast<uint32_t>(gtarget.size()), na = static_cast<uint32_t>(asserts.size());
+    std::vector<uint32_t> goff{0}, gtgt, aoff{0}, atgt;
+    for (auto &t : gtarget) {
+      for (int32_t q : t) gtgt.push_back(static_cast<uint32_t>(q));
+      goff.push_back(static_cast<uint32_t>(gtgt.size()));
+    }
+    for (uint32_t a = 0; a < na; ++a) {
+      const NNode &nd = n_.nodes[order_[asserts[a]]];
+      for (uint32_t k = 0; k < 16; ++k) {
+        const uint8_t f = empty_flags(static_cast<uint8_t>(k / 4), static_cast<int>(k % 4));
+        if ((nd.cond & ~f) == 0) {
+          std::vector<int32_t> t;
+          closure(nd.out, f, true, t);
+          std::vector<uint32_t> q;
+          for (int32_t i : t) q.push_back(static_cast<uint32_t>(pos_[i]));
+          std::sort(q.begin(), q.end());
+          atgt.insert(atgt.end(), q.begin(), q.end());
+        }
+        aoff.push_back(static_cast<uint32_t>(atgt.size()));
+      }
+    }
+    const NfaWideLayout L = nfa_wide_layout(W, npos, ncls, ng, na, static_cast<uint32_t>(gtgt.size()),
+                                            static_cast<uint32_t>(atgt.size()));
+    if (L.total > (1ull << 31)) return BJX_ERR_TOO_COMPLEX;
+    std::vector<uint64_t> b(L.total, 0);
+    const uint32_t hdr[16] = {W, npos, ncls, ng, na, match, na ? (uint32_t)kNfaAsserts : 0u, static_cast<uint32_t>(L.total),
+                              L.n_gtgt, L.n_atgt, 0, 0, 0, 0, 0, 0};
+    memcpy(b.data(), hdr, sizeof hdr);
+    uint16_t a16[128] = {};
+    class_tables(P_, a16, &out->nonascii);
+    memcpy(&b[L.o_ascii], a16, sizeof a16);
+    uint8_t *cat = reinterpret_cast<uint8_t *>(&b[L.o_cat]);
+    for (uint32_t c = 0; c < ncls; ++c) cat[c] = static_cast<uint8_t>(P_.cat[c]);
+    for (uint32_t w = 0; w < W; ++w) {
+      b[L.o_s0 + w] = s0m[w]; b[L.o_sh + w] = sh[w]; b[L.o_gall + w] = gall[w]; b[L.o_am + w] = am[w];
+    }
+    for (uint32_t p = 0; p < npos; ++p) {
+      const NNode &nd = n_.nodes[order_[p]];
+      if (nd.k != NK_CHAR) continue;
+      for (uint32_t c = 0; c < ncls; ++c)
+        if (P_.member[nd.set][c]) b[L.o_cm + (uint64_t)c * W + p / 64] |= 1ull << (p % 64);
+    }
+    memcpy(&b[L.o_aux], aux.data(), aux.size() * 4);
+    memcpy(&b[L.o_goff], goff.data(), goff.size() * 4);
+    if (!gtgt.empty()) memcpy(&b[L.o_gtgt], gtgt.data(), gtgt.size() * 4);
+    memcpy(&b[L.o_aoff], aoff.data(), aoff.size() * 4);
+    if (!atgt.empty()) memcpy(&b[L.o_atgt], atgt.data(), atgt.size() * 4);
+    out->nfa.swap(b);
+    out->nfa_words = W;
+    out->nstates = npos;
+    out->ncls = ncls;
+    out->start = 0;
+    for (int r = 0; r < 128; ++r) out->ascii_cls[r] = static_cast<uint8_t>(a16[r]);
+    out->flags = kRuleNfa | kRuleNfaWide;
+    if (match != 0xFFFFFFFFu && ((s0m[match / 64] >> (match % 64)) & 1)) out->flags |= kRuleAlways;
+    if (match == 0xFFFFFFFFu) out->flags |= kRuleNever;
+    return 0;
+  }
+
  private:
   const Nfa &n_;
   const ClassPart &P_;
@@ -1700,6 +1810,8 @@ std::atomic<uint32_t> g_dfa_state_cap{kDfaStateCap};
 
 }  // namespace
 
+std::atomic<bool> g_force_wide{false};
+void set_force_wide_nfa(bool on) { g_force_wide = on; }
 void set_dfa_state_cap(uint32_t cap) { g_dfa_state_cap = cap ? cap : kDfaStateCap; }
 uint32_t dfa_state_cap() { return g_dfa_state_cap; }
 
@@ -1729,8 +1841,9 @@ int compile_regex(const std::string &pattern, CompiledRegex *out, std::string *e
   const ClassPart part = make_classes(nfa);
   *out = CompiledRegex();
   const uint32_t cap = std::min<uint32_t>(max_dfa_states, dfa_state_cap());
-  int rc = DfaBuilder(nfa, part, std::max<uint32_t>(cap, 3)).build(out);
-  if (rc != 0) {
+  int rc = g_force_wide ? BJX_ERR_TOO_COMPLEX : DfaBuilder(nfa, part, std::max<uint32_t>(cap, 3)).build(out);
+  if (g_force_wide) max_dfa_states = cap;  // test hook: no DFA / per-lane NFA on the way
+  if (rc != 0 && !g_force_wide) {
     *out = CompiledRegex();
     rc = BitNfaBuilder(nfa, part).build(out);
   }
@@ -1738,9 +1851,13 @@ int compile_regex(const std::string &pattern, CompiledRegex *out, std::string *e
     *out = CompiledRegex();
     rc = DfaBuilder(nfa, part, std::min<uint32_t>(max_dfa_states, 65000)).build(out);
   }
+  if (rc != 0) {  // past both: the block-cooperative wide NFA, no position limit short of Go's own
+    *out = CompiledRegex();
+    rc = BitNfaBuilder(nfa, part).build_wide(out);
+  }
   if (rc != 0) {
-    if (err) *err = "rule too complex for the automaton engines (more than " + std::to_string(kNfaMaxPos) +
-                    " NFA positions and more than " + std::to_string(max_dfa_states) + " DFA states)";
+    if (err) *err = "rule too complex for the automaton engines (more than " + std::to_string(kNfaWideMaxPos) +
+                    " NFA positions)";
     return rc;
   }
   if (out->flags & kRuleAlways) out->mode = kModeAlways;
@@ -1828,7 +1945,61 @@ static bool nfa_match_host(const CompiledRegex &rx, const uint8_t *text, size_t 
   return has(X, match);
 }
 
+// the wide NFA (build_wide), stepped as k_nfa_wide does: the host copy of
+// the device algorithm (compiler self-test and CPU tests)
+static bool nfa_wide_match_host(const CompiledRegex &rx, const uint8_t *text, size_t n) {
+  const uint64_t *b = rx.nfa.data();
+  const NfaWideLayout L = nfa_wide_layout_of(reinterpret_cast<const uint32_t *>(b));
+  const uint32_t W = L.W, match = L.match;
+  const uint16_t *a16 = reinterpret_cast<const uint16_t *>(b + L.o_ascii);
+  const uint8_t *cat = reinterpret_cast<const uint8_t *>(b + L.o_cat);
+  const uint32_t *aux = reinterpret_cast<const uint32_t *>(b + L.o_aux);
+  const uint32_t *goff = reinterpret_cast<const uint32_t *>(b + L.o_goff), *gtgt = reinterpret_cast<const uint32_t *>(b + L.o_gtgt);
+  const uint32_t *aoff = reinterpret_cast<const uint32_t *>(b + L.o_aoff), *atgt = reinterpret_cast<const uint32_t *>(b + L.o_atgt);
+  auto has = [&](const std::vector<uint64_t> &v, uint32_t p) { return p != 0xFFFFFFFFu && ((v[p / 64] >> (p % 64)) & 1); };
+  std::vector<uint64_t> A(b + L.o_s0, b + L.o_s0 + W), Y(W);
+  auto cross = [&](uint32_t k) {  // A |= closures of the assertions A holds (targets hold no assertions)
+    for (uint32_t w = 0; w < W; ++w)
+      for (uint64_t m = A[w] & b[L.o_am + w]; m; m &= m - 1) {
+        const uint32_t a = aux[w * 64 + __builtin_ctzll(m)];
+        for (uint32_t i = aoff[a * 16 + k]; i < aoff[a * 16 + k + 1]; ++i) A[atgt[i] / 64] |= 1ull << (atgt[i] % 64);
+      }
+  };
+  std::vector<uint8_t> gmark(L.ngroups, 0);
+  uint32_t ctx = 3;
+  size_t p = 0;
+  while (p < n) {
+    int w;
+    const int32_t r = decode_rune(text + p, n - p, &w);
+    uint32_t c;
+    if (r < 0x80) c = a16[r];
+    else {
+      auto it = std::upper_bound(rx.nonascii.begin(), rx.nonascii.end(), std::make_pair(static_cast<uint32_t>(r), 0xFFFFFFFFu));
+      c = std::prev(it)->second;
+    }
+    cross(ctx * 4 + cat[c]);
+    if (has(A, match)) return true;
+    for (uint32_t k = 0; k < W; ++k) {
+      Y[k] = A[k] & b[L.o_cm + (uint64_t)c * W + k];
+      for (uint64_t m = Y[k] & b[L.o_gall + k]; m; m &= m - 1) gmark[aux[k * 64 + __builtin_ctzll(m)]] = 1;
+    }
+    for (uint32_t k = 0; k < W; ++k)
+      A[k] = ((Y[k] & b[L.o_sh + k]) << 1) | (k ? (Y[k - 1] & b[L.o_sh + k - 1]) >> 63 : 0) | b[L.o_s0 + k];
+    for (uint32_t g = 0; g < L.ngroups; ++g) {
+      if (!gmark[g]) continue;
+      gmark[g] = 0;
+      for (uint32_t i = goff[g]; i < goff[g + 1]; ++i) A[gtgt[i] / 64] |= 1ull << (gtgt[i] % 64);
+    }
+    if (has(A, match)) return true;
+    ctx = cat[c] == 1 ? 1 : (cat[c] == 2 ? 2 : 0);
+    p += static_cast<size_t>(w);
+  }
+  cross(ctx * 4 + 3);
+  return has(A, match);
+}
+
 bool dfa_match_host(const CompiledRegex &rx, const uint8_t *text, size_t n) {
+  if (rx.flags & kRuleNfaWide) return nfa_wide_match_host(rx, text, n);
   if (rx.flags & kRuleNfa) return nfa_match_host(rx, text, n);
   uint32_t st = rx.start;
   size_t p = 0;

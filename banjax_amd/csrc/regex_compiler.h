@@ -24,6 +24,7 @@ enum RuleFlags : uint32_t {
   kRuleAlways = 1,  // matches every input (e.g. ".*", "^"): no scan needed
   kRuleNever = 2,   // matches nothing
   kRuleNfa = 4,     // matched by the bit-parallel NFA (CompiledRegex::nfa), not a DFA
+  kRuleNfaWide = 8, // with kRuleNfa: the block-cooperative NFA (no position limit; layout NfaWideLayout)
 };
 
 // DFA states before a rule switches to the bit-parallel NFA; NFA limits
@@ -61,10 +62,50 @@ BJX_RX_HD inline NfaLayout nfa_layout_of(const uint32_t *h) {
   return L;
 }
 
+// The wide NFA (kRuleNfaWide): the same position automaton as the
+// bit-parallel NFA, for rules past kNfaMaxPos positions (e.g. `.*x.{600}y`).
+// A whole block steps one text: shift edges bit-parallel over the W-word
+// state (each thread owns a run of words), the other follow edges as sparse
+// target lists of the position groups, assertion closures as sparse target
+// lists per (assert position, context).  Limit: Go's own program size
+// (regexp/syntax maxSize, 128 MB / 40 B per instruction = 3355443).
+constexpr uint32_t kNfaWideMaxPos = 3355443;
+struct NfaWideLayout {
+  uint32_t W, npos, ncls, ngroups, nassert, match, flags, n_gtgt, n_atgt;
+  uint64_t o_ascii, o_cat, o_s0, o_sh, o_gall, o_am, o_cm, o_aux, o_goff, o_gtgt, o_aoff, o_atgt, total;
+};
+BJX_RX_HD inline NfaWideLayout nfa_wide_layout(uint32_t W, uint32_t npos, uint32_t ncls, uint32_t ng, uint32_t na,
+                                               uint32_t n_gtgt, uint32_t n_atgt) {
+  NfaWideLayout L{};
+  L.W = W; L.npos = npos; L.ncls = ncls; L.ngroups = ng; L.nassert = na; L.n_gtgt = n_gtgt; L.n_atgt = n_atgt;
+  L.o_ascii = 8;                                   // header: 16 u32
+  L.o_cat = L.o_ascii + 32;                        // u16[128] ascii classes
+  L.o_s0 = L.o_cat + (ncls + 7) / 8;               // u8[ncls] class categories
+  L.o_sh = L.o_s0 + W;
+  L.o_gall = L.o_sh + W;                           // positions with a group
+  L.o_am = L.o_gall + W;                           // assert positions
+  L.o_cm = L.o_am + W;                             // [ncls][W]
+  L.o_aux = L.o_cm + (uint64_t)ncls * W;           // u32[npos]: group id (CHAR) / assert index (ASSERT)
+  L.o_goff = L.o_aux + (npos + 1) / 2;             // u32[ng + 1]
+  L.o_gtgt = L.o_goff + (ng + 2) / 2;              // u32[n_gtgt]
+  L.o_aoff = L.o_gtgt + (n_gtgt + 1) / 2;          // u32[na * 16 + 1]
+  L.o_atgt = L.o_aoff + (na * 16 + 2) / 2;         // u32[n_atgt]
+  L.total = L.o_atgt + (n_atgt + 1) / 2;
+  return L;
+}
+BJX_RX_HD inline NfaWideLayout nfa_wide_layout_of(const uint32_t *h) {
+  NfaWideLayout L = nfa_wide_layout(h[0], h[1], h[2], h[3], h[4], h[8], h[9]);
+  L.match = h[5];
+  L.flags = h[6];
+  return L;
+}
+
 // rules compiled after this call switch to the bit-parallel NFA past `cap` DFA
 // states (test hook: 1 sends every rule that fits the NFA limits to it)
 void set_dfa_state_cap(uint32_t cap);
 uint32_t dfa_state_cap();
+// test hook: rules compiled after this call go straight to the wide NFA
+void set_force_wide_nfa(bool on);
 
 // How the device decides a rule on a line.
 enum RuleMode : uint8_t {

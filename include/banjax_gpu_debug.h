@@ -38,6 +38,10 @@ int bjx_debug_set_claim_budget(bjx_engine *e, uint64_t max_new);
    passes `cap` states (0 = default 4096; 1 = every rule that fits the NFA),
    process-wide; clears the compiled-pattern cache. */
 int bjx_debug_set_dfa_state_cap(uint32_t cap);
+/* Test hook: rules compiled afterwards (on != 0) go straight to the wide
+   block-cooperative NFA (kRuleNfaWide), process-wide; clears the
+   compiled-pattern cache. */
+int bjx_debug_force_wide_nfa(int on);
 #ifdef __cplusplus
 }
 #endif

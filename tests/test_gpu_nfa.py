@@ -112,3 +112,77 @@ def test_forced_nfa_regex_corpus(engine, forced_nfa):
         body = b"".join(rnd.choice(alpha) for _ in range(rnd.randrange(0, 14)))
         lines.append(b"1700000000 9.9.9.%d GET h%d.com " % (j % 250, j % 7) + body)
     pair.feed(b"\n".join(lines) + b"\n", 1700000000 * S)
+
+
+# ---- the wide NFA (k_nfa_wide, kRuleNfaWide): rules past the per-lane NFA's
+# 1024 positions (VERDICT r02 "missing" #1), on the device, against the oracle
+
+WIDE_RULES = [r"(?s).*x.{600}y.{600}z", r"a.{750}.{750}b", r"\bk.{550}.{550}\b"]
+
+
+@pytest.fixture
+def forced_wide():
+    L = _lib.lib()
+    assert L.bjx_debug_force_wide_nfa(1) == 0
+    yield
+    L.bjx_debug_force_wide_nfa(0)
+
+
+def _wide_lines(rnd, n, exotic_every=0):
+    out = []
+    for j in range(n):
+        parts = []
+        for _ in range(rnd.randrange(1, 4)):
+            k = rnd.choice([599, 600, 601, 1099, 1100, 1101, 1499, 1500, 1501, 5])
+            parts.append(rnd.choice([b"x", b"y", b"z", b"a", b"b", b"k", b" k", b"\xc3\xa9"]))
+            parts.append(bytes(rnd.choice(b"xyzab012 .-") for _ in range(k)))
+        if j % 5 == 0:
+            parts = [b"x", b"." * 600, b"y", b"-" * 600, b"z"]
+        if j % 9 == 0:
+            parts = [b"a", b"." * 1500, b"b"]
+        ts = b"1700000000.%03d" % (j % 1000)
+        if exotic_every and j % exotic_every == 0:
+            ts = b"17.00000000%03de8" % (j % 1000)  # general ParseFloat: the per-line fallback (wide job list)
+        out.append(ts + b" 10.0.%d.%d GET h%d.com GET /" % (j % 7, j % 50, j % 3) + b"".join(parts))
+    return b"\n".join(out) + b"\n"
+
+
+def test_wide_rules_match_oracle(engine):
+    pair = Pair(_rules_yaml(WIDE_RULES + [r"GET", r"\d{3}"], 2), engine)
+    n_wide = sum(1 for i in range(len(pair.lim.ruleset)) if pair.lim.ruleset.rule_info(i)[2] & 8)
+    assert n_wide == 3
+    rnd = random.Random(9)
+    pair.feed(_wide_lines(rnd, 600), 1700000000 * S)
+    pair.feed(_wide_lines(rnd, 600, exotic_every=4), 1700000001 * S)
+    pair.compare_state(["10.0.1.1", "10.0.3.7"])
+
+
+def test_forced_wide_edge_lines_and_corpus(engine, forced_wide):
+    """Every edge-case rule (\\b, ^ / $, (?i) folds, negated classes, Unicode
+    groups) through k_nfa_wide: its sparse group and assertion target lists."""
+    t = 1700000000
+    pair = Pair(EDGE_CFG, engine)
+    data = edge_lines(t)
+    pair.feed(data, t * S)
+    pair.feed(data, (t + 1) * S)
+    pair.compare_state(["1.2.3.4", "3.3.3.3", "4.4.4.4", "8.8.8.8"])
+    pair = Pair(_rules_yaml(NFA_RULES), engine)
+    rnd = random.Random(10)
+    pair.feed(_lines(rnd, 1500), 1700000000 * S)
+
+
+def test_wide_rules_hbm_scratch_variant():
+    """k_nfa_wide<true> (state sets in a per-block HBM scratch, for patterns
+    whose state does not fit 64 KB of LDS), forced by BJX_WIDE_GLB in a child
+    process (the hook is read once per process)."""
+    import os
+    import subprocess
+    import sys
+    code = ("import random; from banjax_amd import Engine; from tests.test_gpu_nfa import _rules_yaml, _wide_lines, "
+            "WIDE_RULES, S; from tests.parity import Pair; e = Engine(); p = Pair(_rules_yaml(WIDE_RULES, 2), e); "
+            "r = random.Random(11); p.feed(_wide_lines(r, 300, exotic_every=3), 1700000000 * S); "
+            "p.compare_state(['10.0.1.1']); print('WIDE_GLB_OK')")
+    env = dict(os.environ, BJX_WIDE_GLB="1")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert "WIDE_GLB_OK" in out.stdout, out.stdout[-2000:] + out.stderr[-3000:]

@@ -150,3 +150,75 @@ def test_unicode14_simple_fold_pairs(a, b):
         assert O.Regex(pat).match(t), (hex(x), hex(y))
         assert _host_match(_rs(pat), t) == 1
     assert not O.Regex(r"\x{%X}" % a).match(chr(b).encode())
+
+
+# ---- the wide NFA (kRuleNfaWide): rules past the per-lane NFA's 1024
+# positions compile (Go's regexp.Compile accepts them, internal/config.go:110)
+# and match as the oracle's Pike VM does
+
+INFO_WIDE = 8  # kRuleNfaWide
+
+WIDE_PATTERNS = [r"(?s).*x.{600}y.{600}z", r"a.{750}.{750}b", r"(ab|cd).*[0-9]{1000}[0-9]{100}(ef|gh)",
+                 r"\bk.{550}.{550}\b", r"^GET .{0,600}.{0,600}wp-admin", r"(?i)(x[a-c][a-c][a-c][a-c]){240}"]
+
+
+def _wide_texts(rnd, pat):
+    """Texts around each pattern's shape: the right gaps, off-by-one gaps,
+    other runes, word boundaries."""
+    out = [b"", b"x", b"xyz"]
+    for _ in range(40):
+        parts = []
+        for _ in range(rnd.randrange(1, 5)):
+            k = rnd.choice([599, 600, 601, 1099, 1100, 1101, 1199, 1200, 1201, 1499, 1500, 1501, 3, 0])
+            parts.append(rnd.choice([b"x", b"y", b"z", b"a", b"b", b"ab", b"cd", b"ef", b"gh", b"k", b" k", b"GET ", b"xAbCa" * 240,
+                                     b"wp-admin", b"XAbC", b"xabc" * 400]))
+            parts.append(bytes(rnd.choice(b"xyzab01289 .\xc3\xa9-") for _ in range(k)))
+        out.append(b"".join(parts))
+    out.append(b"x" + b"." * 600 + b"y" + b"." * 600 + b"z")
+    out.append(b"a" + b"-" * 1500 + b"b")
+    out.append(b"ab-" + b"7" * 1100 + b"gh")
+    out.append(b"GET " + b"/" * 1200 + b"wp-admin")
+    out.append(b"xabc" * 400)
+    return out
+
+
+def test_wide_patterns_compile_and_match_oracle():
+    """VERDICT r02 'missing' #1: no size cap short of Go's own."""
+    rnd = random.Random(5)
+    n_wide = 0
+    for pat in WIDE_PATTERNS:
+        assert O.compile_error(pat) is None, pat
+        rs = _rs(pat)
+        npos, _, fl = _flags(rs)
+        n_wide += bool(fl & INFO_WIDE and npos > 1024)
+        ore = O.Regex(pat)
+        for t in _wide_texts(rnd, pat):
+            assert _host_match(rs, t) == int(ore.match(t)), (pat, t[:80], len(t))
+    assert n_wide >= 3
+
+
+def test_forced_wide_nfa_matches_oracle_on_corpus():
+    """Every rule of the CPU corpus through the wide NFA (its sparse group /
+    assertion target lists against the oracle's Pike VM)."""
+    from tests.test_cpu_boundary import PATTERNS
+    L = _lib.lib()
+    rnd = random.Random(22)
+    alpha = [b"a", b"b", b"c", b"d", b"A", b"K", b"k", b"x", b"y", b"z", b"1", b" ", b"\n", b"_", b".", b"?", b"=",
+             b"/", b"\xc3\xa9", b"\xc3\x9f", b"\xff", b"\xe2\x84\xaa", b"\xc3", b"-", b"]", b"GET ", b"blockme"]
+    extra = [r"\b\w+\b.{3}\B", r"(?m)^a.{5}$", r"^x.{6}y$", r"\A(ab|c){2,}\z", r"(?i)\p{Lu}.{4}x", r"[^\pL\pN]{3}",
+             r".*a.{20}", r"(a|b)*a(a|b){16}"]
+    assert L.bjx_debug_force_wide_nfa(1) == 0
+    try:
+        n_wide = 0
+        for pat in PATTERNS + extra:
+            if O.compile_error(pat):
+                continue
+            rs = _rs(pat)
+            n_wide += bool(_flags(rs)[2] & INFO_WIDE)
+            ore = O.Regex(pat)
+            for _ in range(200):
+                t = b"".join(rnd.choice(alpha) for _ in range(rnd.randrange(0, 24)))
+                assert _host_match(rs, t) == int(ore.match(t)), (pat, t)
+        assert n_wide >= 30
+    finally:
+        L.bjx_debug_force_wide_nfa(0)
