@@ -107,7 +107,7 @@ EXPORTS = [
     "bjx_node_create", "bjx_node_destroy", "bjx_node_size", "bjx_node_engine", "bjx_node_last_error", "bjx_node_set_decision_lists",
     "bjx_node_set_ban_options", "bjx_node_process_batch", "bjx_node_process_chunks", "bjx_node_batch_bans",
     "bjx_node_state_get", "bjx_node_state_len", "bjx_node_state_dump", "bjx_node_state_stats_get",
-    "bjx_node_state_clear",
+    "bjx_node_state_clear", "bjx_node_exchange_kind",
 ]
 
 
@@ -182,6 +182,8 @@ def lib():
     L.bjx_debug_rule_literal.argtypes = [vp, sz, C.c_char_p, sz]
     L.bjx_debug_phase_ms.restype = sz
     L.bjx_debug_phase_ms.argtypes = [vp, C.POINTER(C.c_double), sz]
+    L.bjx_debug_kernel_ms.restype = sz
+    L.bjx_debug_kernel_ms.argtypes = [vp, C.POINTER(C.c_double), sz]
     L.bjx_debug_scan_stats.restype = sz
     L.bjx_debug_scan_stats.argtypes = [vp, C.POINTER(C.c_uint64), sz]
     L.bjx_debug_set_claim_budget.restype = C.c_int
@@ -215,6 +217,8 @@ def lib():
     L.bjx_node_engine.restype = vp
     L.bjx_node_engine.argtypes = [vp, sz]
     L.bjx_node_last_error.restype = C.c_char_p
+    L.bjx_node_exchange_kind.restype = C.c_int
+    L.bjx_node_exchange_kind.argtypes = [vp]
     L.bjx_node_last_error.argtypes = [vp]
     L.bjx_node_set_decision_lists.restype = C.c_int
     L.bjx_node_set_decision_lists.argtypes = [vp, C.POINTER(DecisionEntry), sz]

@@ -54,7 +54,7 @@ def build(force: bool = False, verbose: bool = False):
             if pr.wait() != 0:
                 raise subprocess.CalledProcessError(pr.returncode, cmd)
         if force or procs or _stale(dst, objs):
-            cmd = ["hipcc"] + COMMON + ["-o", dst] + objs
+            cmd = ["hipcc"] + COMMON + ["-o", dst] + objs + ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
             if verbose:
                 print(" ".join(cmd), flush=True)
             subprocess.run(cmd, check=True)

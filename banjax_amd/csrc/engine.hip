@@ -774,6 +774,7 @@ struct JobSink {
   unsigned long long *count;
   uint64_t cap;
 };
+constexpr uint32_t kWaveJobBytes = kWaveJobs * 8 + 16;  // per wave: staged jobs + their counter
 __device__ __forceinline__ void emit_job(const JobSink &S, uint64_t j, uint32_t r, uint32_t pos) {
   const uint2 v = make_uint2((uint32_t)j, r | (pos << 24));
   const uint32_t c = atomicAdd(S.cnt, 1u);
@@ -946,10 +947,17 @@ constexpr uint32_t kPlanLitAny = 1;  // prefilter rule the entry cannot spell ou
 constexpr uint32_t kPlanAnchor = 2;  // anchored rule: inline window test, anchor literal, DFA
 constexpr uint32_t kPlanScan = 3;    // no literal: a DFA job on every line
 
+// Hits past the line's slots (ovf): which literals occurred (bit = id & 63,
+// CandMeta::bits plus the slots' hits)
+struct OvfInfo {
+  uint64_t bits;
+};
+
 template <bool EMIT>
 __device__ __forceinline__ void plan_rule(const Bind &B, const Tabs &T, const uint4 a, const uint4 b, uint32_t pos_base,
                                           const uint8_t *rest, uint32_t rest_len, uint64_t lits, uint64_t lpos, uint32_t nlit,
-                                          bool ovf, uint64_t &m0, uint64_t &m1, uint64_t j, const JobSink &S) {
+                                          bool ovf, const OvfInfo &ov, uint64_t &m0, uint64_t &m1, uint64_t j,
+                                          const JobSink &S) {
   const uint32_t r = a.x & 0xFFFFFu, pos = pos_base + ((a.x >> 20) & 0x7Fu), kind = (a.x >> 27) & 7u;
   const bool eq = ((a.x >> 30) & 1u) != 0;
   if (kind == kPlanScan) {
@@ -970,7 +978,17 @@ __device__ __forceinline__ void plan_rule(const Bind &B, const Tabs &T, const ui
     dfa_rule<EMIT>(B, T, r, pos, true, rest, rest_len, m0, m1, j, S);
     return;
   }
-  if (ovf) {  // more hits than slots: every literal rule by its automaton
+  if (ovf) {
+    // more hits than slots: a rule none of whose literals occurred cannot
+    // match; the others go to their automaton, from the first hit on
+    if (kind == kPlanLit) {
+      uint64_t need = 0;
+      for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t id = ((k < 2 ? a.y : a.z) >> (16 * (k & 1))) & 0xFFFFu;
+        if (id != 0xFFFFu) need |= 1ull << (id & 63);
+      }
+      if (!(ov.bits & need)) return;
+    }
     dfa_rule<EMIT>(B, T, r, pos, false, rest, rest_len, m0, m1, j, S);
     return;
   }
@@ -1004,8 +1022,8 @@ __device__ __forceinline__ void plan_rule(const Bind &B, const Tabs &T, const ui
 // time, side by side
 template <bool EMIT>
 __device__ __forceinline__ void decide_plan(const Bind &B, const Tabs &T, const uint8_t *rest, uint32_t rest_len, int32_t hid,
-                                            const HostRules &H, uint64_t lits, uint64_t lpos, uint32_t nlit, bool ovf, uint64_t j,
-                                            const Lines &L, const JobSink &S, uint32_t dbg = 0) {
+                                            const HostRules &H, uint64_t lits, uint64_t lpos, uint32_t nlit, bool ovf,
+                                            const OvfInfo &ov, uint64_t j, const Lines &L, const JobSink &S, uint32_t dbg = 0) {
   const uint32_t nsite = H.s_end - H.s_begin;
   uint64_t m0 = H.a0, m1 = H.a1;
   if (dbg & 32) nlit = 0;  // timing experiments only (BJX_DEBUG_LINES): 16 no site entries, 32 no literal hits
@@ -1021,12 +1039,12 @@ __device__ __forceinline__ void decide_plan(const Bind &B, const Tabs &T, const 
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if (i + k < pe) plan_rule<EMIT>(B, T, a[k], b[k], 0, rest, rest_len, lits, lpos, nlit, ovf, m0, m1, j, S);
+        if (i + k < pe) plan_rule<EMIT>(B, T, a[k], b[k], 0, rest, rest_len, lits, lpos, nlit, ovf, ov, m0, m1, j, S);
     }
   }
   for (uint32_t i = 0; i < B.n_plan_glob; ++i)
-    plan_rule<EMIT>(B, T, B.plan_glob[2 * i], B.plan_glob[2 * i + 1], nsite, rest, rest_len, lits, lpos, nlit, ovf, m0, m1, j,
-                    S);
+    plan_rule<EMIT>(B, T, B.plan_glob[2 * i], B.plan_glob[2 * i + 1], nsite, rest, rest_len, lits, lpos, nlit, ovf, ov, m0, m1,
+                    j, S);
   uint64_t *mask = L.masks + j * B.mask_words;
   mask[0] = m0;
   if (B.mask_words > 1) mask[1] = m1;
@@ -1090,7 +1108,7 @@ template <bool EMIT>
 __device__ __forceinline__ void plan_rule_lds(const Bind &B, const Tabs &T, const LdsTabs &LT, uint4 a, const uint4 b,
                                               uint32_t first_rule, const uint8_t *rest, uint32_t rest_len, uint32_t host_rel,
                                               uint32_t host_len, uint64_t lits, uint64_t lpos, uint32_t nlit, bool ovf,
-                                              uint64_t &m0, uint64_t &m1, uint64_t j, const JobSink &S) {
+                                              const OvfInfo &ov, uint64_t &m0, uint64_t &m1, uint64_t j, const JobSink &S) {
   const uint32_t pos = (a.x >> 20) & 0x7Fu, kind = (a.x >> 27) & 7u;
   if (a.x & kPlanOwn) a.x = (a.x & 0x7FF00000u) | ((first_rule + pos) & 0xFFFFFu);
   const uint32_t r = a.x & 0xFFFFFu;
@@ -1102,12 +1120,18 @@ __device__ __forceinline__ void plan_rule_lds(const Bind &B, const Tabs &T, cons
     return;
   }
   if (kind != kPlanLitT) {
-    plan_rule<EMIT>(B, T, a, b, 0, rest, rest_len, lits, lpos, nlit, ovf, m0, m1, j, S);
+    plan_rule<EMIT>(B, T, a, b, 0, rest, rest_len, lits, lpos, nlit, ovf, ov, m0, m1, j, S);
     return;
   }
   // the rule requires F = A + host + C; its prefilter literal is the piece A
   // (side 0: F starts at the hit) or C (side 1: the host ends at the hit)
   if (ovf) {
+    uint64_t need = 0;
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint32_t id = ((k < 2 ? a.y : a.z) >> (16 * (k & 1))) & 0xFFFFu;
+      if (id != 0xFFFFu) need |= 1ull << (id & 63);
+    }
+    if (!(ov.bits & need)) return;  // the piece never occurred
     dfa_rule<EMIT>(B, T, r, pos, false, rest, rest_len, m0, m1, j, S);
     return;
   }
@@ -1135,7 +1159,7 @@ template <bool EMIT>
 __device__ __forceinline__ void decide_plan_lds(const Bind &B, const Tabs &T, const LdsTabs &LT, const uint8_t *rest,
                                                 uint32_t rest_len, uint32_t host_rel, uint32_t host_len, int32_t hid,
                                                 const HostRules &H, uint64_t lits, uint64_t lpos, uint32_t nlit, bool ovf,
-                                                uint64_t j, const Lines &L, const JobSink &S) {
+                                                const OvfInfo &ov, uint64_t j, const Lines &L, const JobSink &S) {
   const uint32_t nsite = H.s_end - H.s_begin;
   uint64_t m0 = H.a0, m1 = H.a1;
   if (hid >= 0) {
@@ -1143,11 +1167,11 @@ __device__ __forceinline__ void decide_plan_lds(const Bind &B, const Tabs &T, co
     const uint32_t cb = hi.x & 0xFFFFu, ce = cb + (hi.x >> 16);
     for (uint32_t i = cb; i < ce; ++i)
       plan_rule_lds<EMIT>(B, T, LT, LT.cls[2 * i], LT.cls[2 * i + 1], hi.y, rest, rest_len, host_rel, host_len, lits, lpos,
-                          nlit, ovf, m0, m1, j, S);
+                          nlit, ovf, ov, m0, m1, j, S);
   }
   for (uint32_t i = 0; i < B.n_plan_glob; ++i)
-    plan_rule<EMIT>(B, T, B.plan_glob[2 * i], B.plan_glob[2 * i + 1], nsite, rest, rest_len, lits, lpos, nlit, ovf, m0, m1, j,
-                    S);
+    plan_rule<EMIT>(B, T, B.plan_glob[2 * i], B.plan_glob[2 * i + 1], nsite, rest, rest_len, lits, lpos, nlit, ovf, ov, m0, m1,
+                    j, S);
   uint64_t *mask = L.masks + j * B.mask_words;
   mask[0] = m0;
   if (B.mask_words > 1) mask[1] = m1;
@@ -1360,6 +1384,8 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
       }
     }
     if (!B.any_prefilter || (A.debug_skip & 1)) continue;
+    // bytes of the batch held by the tile + halo in LDS
+    const uint64_t win_end = A.n - ts0 < (uint64_t)(kWT + kHalo) ? A.n - ts0 : (uint64_t)(kWT + kHalo);
     // the line open at the tile start is long iff it started before the previous
     // tile (that tile has no '\n') or runs past the previous tile's halo
     const bool open_long = !head && (p0 == kNone || p0 >= kHalo || tb == A.tile_base[t - 1]);
@@ -1457,15 +1483,29 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
             const uint32_t lit = en >> 8, goff = en & 0xFF;
             const int64_t q0 = (int64_t)(ts0 + p) - (int64_t)goff;
             if (q0 < 0) continue;
+            const int32_t s0 = (int32_t)p - (int32_t)goff;
+            uint32_t cc;
+            uint64_t ver = 0;
             if (in_window) {
-              const int32_t s0 = (int32_t)p - (int32_t)goff;
               if (s0 < (int32_t)ls[lk] || (uint32_t)s0 + lit_len_of(TB, lit) > le[lk]) continue;
               if (!literal_at(TB, lit, T + s0)) continue;
-              const uint32_t cc = atomicAdd(&lcnt[lk], 1u);
-              if (cc < (uint32_t)kCandSlots) L.cand[gline * kCandSlots + cc] = ((uint64_t)q0 << 24) | kCandVerified | lit;
+              cc = atomicAdd(&lcnt[lk], 1u);
+              ver = kCandVerified;
             } else {
-              const uint32_t cc = atomicAdd(&L.cand_cnt[gline], 1u);
-              if (cc < (uint32_t)kCandSlots) L.cand[gline * kCandSlots + cc] = ((uint64_t)q0 << 24) | lit;
+              // the line does not fit the window, the literal usually does:
+              // checked here when all its bytes are in the tile + halo (literals
+              // hold no '\n', so a match cannot cross into another line)
+              if (s0 >= 0 && !B.lit_nl && (uint64_t)s0 + lit_len_of(TB, lit) <= win_end) {
+                if (!literal_at(TB, lit, T + s0)) continue;
+                ver = kCandVerified;
+              }
+              cc = atomicAdd(&L.cand_meta[gline].cnt, 1u);
+            }
+            if (cc < (uint32_t)kCandSlots) {
+              L.cand[gline * kCandSlots + cc] = ((uint64_t)q0 << 24) | ver | lit;
+            } else {  // past the slots: the line's summary only (CandMeta)
+              atomicOr(reinterpret_cast<unsigned long long *>(&L.cand_meta[gline].bits), 1ull << (lit & 63));
+              atomicMax(&L.cand_meta[gline].first_inv, ~(uint32_t)((uint64_t)q0 >> 3));
             }
             ++n_hit;
           }
@@ -1475,7 +1515,7 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
       // hit counts of the lines decided in this window
       const uint32_t n_win = min(n_st, kLineCap) - ((last_long && n_st <= kLineCap) ? 1u : 0u);
       for (uint32_t i = lane; i < n_win; i += 64)
-        if (tb + nh + i < A.n_lines) L.cand_cnt[tb + nh + i] = lcnt[i];
+        if (tb + nh + i < A.n_lines) L.cand_meta[tb + nh + i].cnt = lcnt[i];
       wave_sync();
     }
   }
@@ -1534,8 +1574,9 @@ struct LinesProf {
 template <bool STAGED, bool PROF = false, bool HOST_LDS = false>
 __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const LinesArgs &A, const uint8_t *base,
                                           uint64_t origin, uint64_t s, uint32_t n, uint64_t j, const JobSink &S,
-                                          uint32_t cc, const uint64_t (&cv)[kCandSlots], LinesProf &P,
+                                          const CandMeta &cm, const uint64_t (&cv)[kCandSlots], LinesProf &P,
                                           const uint32_t *hl) {
+  const uint32_t cc = cm.cnt;
   const Lines &L = A.L;
   const uint8_t *p = base + (s - origin);
   uint32_t sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
@@ -1582,6 +1623,7 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
       uint64_t lits = 0, lpos = 0;
       uint32_t nlit = 0;
       const uint64_t rs = s + rest_off;
+      OvfInfo ov{0};
 #pragma unroll
       for (uint32_t c = 0; c < (uint32_t)kCandSlots; ++c) {
         if (c >= cc) break;
@@ -1594,7 +1636,9 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
           continue;
         lpos |= (uint64_t)(q - rs < 0xFFFF ? (uint32_t)(q - rs) : 0xFFFFu) << (16 * nlit);
         lits |= (uint64_t)lit << (16 * nlit++);
+        ov.bits |= 1ull << (lit & 63);
       }
+      if (cc > (uint32_t)kCandSlots) ov.bits |= cm.bits;  // the hits past the slots
       if (HOST_LDS && B.lt_cls && !(A.dbg & 15)) {
         LdsTabs LT;
         LT.hinfo = reinterpret_cast<const uint2 *>(hl + B.lt_hinfo);
@@ -1602,9 +1646,9 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
         LT.trec = reinterpret_cast<const uint4 *>(hl + B.lt_trec);
         LT.pool = reinterpret_cast<const uint8_t *>(hl + B.lt_pool);
         decide_plan_lds<true>(B, TB, LT, p + rest_off, n - rest_off, host_off - rest_off, host_len, hid, H, lits, lpos, nlit,
-                              cc > (uint32_t)kCandSlots, j, L, S);
+                              cc > (uint32_t)kCandSlots, ov, j, L, S);
       } else if (B.use_plan && !(A.dbg & 15))
-        decide_plan<true>(B, TB, p + rest_off, n - rest_off, hid, H, lits, lpos, nlit, cc > (uint32_t)kCandSlots, j, L, S,
+        decide_plan<true>(B, TB, p + rest_off, n - rest_off, hid, H, lits, lpos, nlit, cc > (uint32_t)kCandSlots, ov, j, L, S,
                           A.dbg);
       else
         decide_rules<true>(B, TB, p + rest_off, n - rest_off, hid, H, lits, lpos, (A.dbg & 2) ? 0u : nlit,
@@ -1645,7 +1689,7 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
     __syncthreads();
   }
   JobSink S;
-  S.lds = reinterpret_cast<uint2 *>(s_dyn + img_al + hl_al + wave * (kWaveJobs * 8 + 16));
+  S.lds = reinterpret_cast<uint2 *>(s_dyn + img_al + hl_al + wave * kWaveJobBytes);
   S.cnt = reinterpret_cast<uint32_t *>(S.lds + kWaveJobs);
   S.jline = A.jline;
   S.jkey = A.jkey;
@@ -1656,7 +1700,7 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
   const Lines &L = A.L;
   // this wave's 64 lines, staged whole in LDS with coalesced 16 B loads when
   // they span at most kSpanBytes (otherwise read from HBM per lane)
-  uint8_t *span = s_dyn + img_al + hl_al + (kBlock / 64) * (kWaveJobs * 8 + 16) + wave * (A.span_bytes + 32);
+  uint8_t *span = s_dyn + img_al + hl_al + (kBlock / 64) * kWaveJobBytes + wave * (A.span_bytes + 32);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t n_work = A.list ? A.n_list : A.n_lines;
   // span bounds of the wave's next 64 lines, loaded one iteration ahead
@@ -1676,12 +1720,13 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
     const bool staged = !A.list && s1 + 16 - b16 <= A.span_bytes && !(A.dbg & 4);  // 16 B of slack for word-wise over-reads
     // per-line loads that do not depend on the staged bytes go out first
     uint64_t s = 0, cv[kCandSlots];
-    uint32_t n = 0, cc = 0;
+    uint32_t n = 0;
+    CandMeta cm{0, 0, 0};
     if (j < A.n_lines) {
       s = j ? A.nl[j - 1] + 1 : 0;
       n = (uint32_t)(A.nl[j] - s);
       if (B.any_prefilter) {
-        cc = L.cand_cnt[j];
+        cm = L.cand_meta[j];
         const ulonglong2 *cp = reinterpret_cast<const ulonglong2 *>(L.cand + j * kCandSlots);
 #pragma unroll
         for (int k = 0; k < kCandSlots / 2; ++k) {
@@ -1727,8 +1772,8 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
     if (PROF) { __builtin_amdgcn_s_waitcnt(0); P.mark(0); }
     if (j < A.n_lines) {
       // two inlined copies: LDS addressing for staged waves, global otherwise
-      if (staged) line_body<true, PROF, HOST_LDS>(B, TB, A, span, b16, s, n, j, S, cc, cv, P, s_hl);
-      else line_body<false, PROF, HOST_LDS>(B, TB, A, A.buf, 0, s, n, j, S, cc, cv, P, s_hl);
+      if (staged) line_body<true, PROF, HOST_LDS>(B, TB, A, span, b16, s, n, j, S, cm, cv, P, s_hl);
+      else line_body<false, PROF, HOST_LDS>(B, TB, A, A.buf, 0, s, n, j, S, cm, cv, P, s_hl);
     }
     if (PROF) P.t = __builtin_amdgcn_s_memtime();
     // ---- append this wave's DFA jobs (one global atomic per 64 lines)
@@ -1778,7 +1823,7 @@ __global__ __launch_bounds__(kBlock) void k_rules(Bind B, RulesArgs A) {
   const Tabs TB = make_tabs(IMG_LDS ? s_img : B.img, B.il);
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   JobSink S;
-  S.lds = reinterpret_cast<uint2 *>(s_dyn + ((IMG_LDS ? B.img_bytes : 0) + 15u & ~15u) + wave * (kWaveJobs * 8 + 16));
+  S.lds = reinterpret_cast<uint2 *>(s_dyn + ((IMG_LDS ? B.img_bytes : 0) + 15u & ~15u) + wave * kWaveJobBytes);
   S.cnt = reinterpret_cast<uint32_t *>(S.lds + kWaveJobs);
   S.jline = A.jline;
   S.jkey = A.jkey;
@@ -1807,7 +1852,7 @@ __global__ __launch_bounds__(kBlock) void k_rules(Bind B, RulesArgs A) {
           uint64_t lits = 0, lpos = 0;
           uint32_t nlit = 0, cc = 0;
           if (B.any_prefilter) {
-            cc = L.cand_cnt[j];
+            cc = L.cand_meta[j].cnt;
             const uint64_t rs = s + ro;
 #pragma unroll
             for (uint32_t c = 0; c < (uint32_t)kCandSlots; ++c) {
@@ -1847,6 +1892,42 @@ __global__ __launch_bounds__(kBlock) void k_rules(Bind B, RulesArgs A) {
 // at a time and steps the DFA over the ASCII bytes from registers (a non-ASCII
 // byte hands the rest of the text to the rune-decoding loop).  A match sets
 // the rule's bit and adds to the line's result / event counts.
+// Offset in rest where a DFA job of a lead rule may start (DevRule::lead: the
+// pattern's every match begins with one of its literals, and this copy's
+// literals are not host-split pieces).  Every occurrence of a literal is one
+// of the line's scan candidates (the gram filter misses none): without
+// overflow the lowest candidate of the rule's own literals at or past rest
+// bounds the first match start (none: no match, start at the end); with
+// overflow the lowest candidate of any literal does (CandMeta::first_inv),
+// unless one lies before rest.  0 for every other job.
+__device__ __forceinline__ uint32_t lead_start(const Bind &B, const Lines &L, uint64_t j, uint32_t pos, uint64_t rs,
+                                               uint32_t rl) {
+  const int32_t hid = L.host_id[j];
+  uint32_t sb = 0, nsite = 0;
+  if (hid >= 0) { sb = B.site_off[hid]; nsite = B.site_off[hid + 1] - sb; }
+  const uint32_t r = pos < nsite ? B.site_rules[sb + pos] : B.global_rules[pos - nsite];  // the line's own rule
+  const uint32_t lead = B.rules[r].lead, lo = B.rules[r].lits_off, ln = B.rules[r].lits_len;
+  if ((lead & 3u) != 3u) return 0;
+  const CandMeta cm = L.cand_meta[j];
+  const bool ovf = cm.cnt > (uint32_t)kCandSlots;
+  uint64_t f = ~0ull;
+  const uint32_t ns = min(cm.cnt, (uint32_t)kCandSlots);
+  for (uint32_t c = 0; c < ns; ++c) {
+    const uint64_t v = L.cand[j * kCandSlots + c];
+    const uint64_t q = v >> 24;
+    if (q < rs || q >= f) continue;
+    bool mine = ovf;
+    for (uint32_t k = 0; k < ln && !mine; ++k) mine = B.rule_lits[lo + k] == (uint32_t)(v & 0x7FFFFF);
+    if (mine) f = q;
+  }
+  if (ovf) {
+    const uint64_t mf = cm.first_inv ? (uint64_t)(~cm.first_inv) << 3 : ~0ull;
+    if (mf < rs) return 0;
+    f = mf < f ? mf : f;
+  }
+  return f == ~0ull ? rl : (uint32_t)min<uint64_t>(f - rs, rl);
+}
+
 constexpr uint32_t kDfaLdsEntries = 8192;  // u16 transitions staged per block (16 KB)
 
 // STAGED: tr / ac point into LDS (a distinct instantiation keeps the call
@@ -1943,15 +2024,22 @@ __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restric
   const uint32_t rl = (uint32_t)(nl[j] - rs);
   bool m;
   if (staged) {
-    // anchored prefix literal already matched by k_lines: step in past it
+    // anchored prefix literal already matched by k_lines: step in past it;
+    // a lead rule's job starts at the first hit of its literals (every match
+    // begins at one, regex_compiler.h pref_lead)
     const uint32_t sk = R0.skip_len && R0.skip_len <= rl ? R0.skip_len : 0u;
-    m = dfa_text<true>(B, R0, s_tr, s_ac, buf, n_buf, rs + sk, rl - sk, sk ? R0.skip_state : R0.start);
+    const uint32_t st0 = (R0.lead & 1u) ? lead_start(B, L, j, pos, rs, rl) : 0u;
+    m = st0 ? dfa_text<true>(B, R0, s_tr, s_ac, buf, n_buf, rs + st0, rl - st0, R0.start)
+            : dfa_text<true>(B, R0, s_tr, s_ac, buf, n_buf, rs + sk, rl - sk, sk ? R0.skip_state : R0.start);
   } else {
     const DevRule R = B.rules[r];
     if (R.flags & kRuleNfa) return;  // k_nfa's
     const uint32_t sk = R.skip_len && R.skip_len <= rl ? R.skip_len : 0u;
-    m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, buf, n_buf, rs + sk, rl - sk,
-                        sk ? R.skip_state : R.start);
+    const uint32_t st0 = (R.lead & 1u) ? lead_start(B, L, j, pos, rs, rl) : 0u;
+    if (st0) m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, buf, n_buf, rs + st0, rl - st0,
+                                 R.start);
+    else m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, buf, n_buf, rs + sk, rl - sk,
+                             sk ? R.skip_state : R.start);
   }
   if (!m) return;
   const int32_t hid = L.host_id[j];
@@ -1982,7 +2070,9 @@ __global__ __launch_bounds__(kBlock) void k_nfa(Bind B, uint32_t rule, const uin
   const uint32_t key = jkey[t], pos = key >> 24;
   const uint64_t j = jline[t];
   const uint64_t s = j ? nl[j - 1] + 1 : 0;
-  const uint64_t t0 = s + L.rest_off[j], end = nl[j];
+  const uint64_t end = nl[j];
+  uint64_t t0 = s + L.rest_off[j];
+  if (R.lead & 1u) t0 += lead_start(B, L, j, pos, t0, (uint32_t)(end - t0));  // from the first hit of its literals
   uint64_t D[WT];
 #pragma unroll
   for (int w = 0; w < WT; ++w) D[w] = s_b[Ly.o_s0 + w];
@@ -2098,6 +2188,7 @@ __global__ __launch_bounds__(kBlock) void k_nfa_wide(Bind B, const uint8_t *__re
     const uint64_t s = j ? nl[j - 1] + 1 : 0;
     const uint64_t end = nl[j];
     uint64_t i = s + L.rest_off[j];
+    if ((R.lead & 1u) && !jpos) i += lead_start(B, L, j, pos, i, (uint32_t)(end - i));  // from the first hit of its literals
     uint32_t ctx = 3;
     bool m = false;
     while (i < end) {
@@ -3502,7 +3593,9 @@ extern "C" int bjx_ruleset_rule_info(const bjx_ruleset *rs, size_t i, uint32_t *
   const auto &rx = rs->rules[i].rx;
   if (states) *states = rx.nstates;
   if (classes) *classes = rx.ncls;
-  if (flags) *flags = rx.flags | ((uint32_t)rx.mode << 8) | (rx.pref_equivalent ? 0x10000u : 0u) | ((uint32_t)rx.pref.size() << 20);
+  if (flags)
+    *flags = rx.flags | ((uint32_t)rx.mode << 8) | (rx.pref_equivalent ? 0x10000u : 0u) | (rx.pref_lead ? 0x20000u : 0u) |
+             ((uint32_t)rx.pref.size() << 20);
   return BJX_OK;
 }
 
@@ -3524,6 +3617,8 @@ struct bjx_engine {
   std::string last_error;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evm0 = nullptr, evm1 = nullptr;
+  hipEvent_t evk[4] = {};      // k_lines launch, DFA-job sort + k_dfa / k_nfa (bench: per-kernel roofline)
+  double kernel_ms[3] = {};   // last batch: k_scan, k_lines, DFA jobs
   static constexpr int kPhases = 8;
   hipEvent_t ph[kPhases + 1] = {};
   double phase_ms[kPhases] = {};
@@ -3581,7 +3676,7 @@ struct bjx_engine {
   DevBuf<unsigned long long> long_count;
   uint32_t scan_lds[2] = {0, 0};
   bool lines_attr = false;
-  DevBuf<uint32_t> l_ccnt;
+  DevBuf<CandMeta> l_ccnt;
   unsigned long long scan_stats[6] = {0, 0, 0, 0, 0, 0};
   uint64_t last_slow = 0;
   DevBuf<uint8_t> l_flags;
@@ -3981,6 +4076,15 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
       for (auto &pl : r.rx.anchor) { rule_lits.push_back(intern_lit(pl, false)); rule_full.push_back(kNone); }
     d.anc_len = (uint16_t)(rule_lits.size() - d.anc_off);
     d.anc_equiv = r.rx.anchor_equivalent ? 1 : 0;
+    // bit 0: every match of the pattern begins with a literal of pref; bit 1:
+    // this copy's literals are those (not host-split pieces): lead_start
+    if (r.rx.mode == kModePrefilter && r.rx.pref_lead) {
+      bool split = false;
+      for (uint32_t k = d.lits_off; k < d.lits_off + d.lits_len; ++k) split = split || rule_full[k] != kNone;
+      d.lead = split ? 1 : 3;
+    } else {
+      d.lead = 0;
+    }
     any_anchored = any_anchored || r.rx.mode == kModeAnchored;
     d.interval_ns = r.interval_ns;
     d.hits = r.hits;
@@ -4553,6 +4657,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.n_lits = n_lit;
   B.any_anchored = any_anchored ? 1 : 0;
   B.any_prefilter = use_pref ? 1 : 0;
+  B.lit_nl = std::find(lit_bytes.begin(), lit_bytes.end(), (uint8_t)'\n') != lit_bytes.end() ? 1u : 0u;
   B.img = base + o_img;
   B.img_bytes = (uint32_t)img.size();
   B.il = il;
@@ -4764,6 +4869,7 @@ extern "C" int bjx_engine_create(int device, const bjx_engine_options *opts, bjx
     HIP_OK(hipEventCreate(&e->ev1));
     HIP_OK(hipEventCreate(&e->evm0));
     HIP_OK(hipEventCreate(&e->evm1));
+    for (auto &x : e->evk) HIP_OK(hipEventCreate(&x));
     for (auto &x : e->ph) HIP_OK(hipEventCreate(&x));
     // >= 4M slots: a quarter of the table stays free for the claims in flight
     // when a launch spends its budget (see k_ip_claim)
@@ -4815,6 +4921,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   e->ban_ipo.release();
   e->long_list.release(); e->l_ip16.release(); e->jline.release(); e->jkey.release(); e->jline2.release(); e->jkey2.release(); e->l_cand.release(); e->l_ccnt.release();
   (void)hipEventDestroy(e->ev0); (void)hipEventDestroy(e->ev1); (void)hipEventDestroy(e->evm0); (void)hipEventDestroy(e->evm1);
+  for (auto &x : e->evk) (void)hipEventDestroy(x);
   for (auto &x : e->ph) (void)hipEventDestroy(x);
   (void)hipStreamDestroy(e->stream);
   delete e;
@@ -5148,11 +5255,11 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   L.ts = e->l_ts.p; L.ip_hash = e->l_iph.p; L.ip_off = e->l_ipoff.p; L.ip_len = e->l_iplen.p; L.host_off = e->l_hoff.p;
   L.host_len = e->l_hlen.p; L.rest_off = e->l_roff.p; L.host_id = e->l_hid.p; L.flags = e->l_flags.p;
   L.counts = e->l_counts.p; L.masks = e->l_masks.p;
-  L.cand_cnt = e->l_ccnt.p; L.cand = e->l_cand.p; L.ip16 = e->l_ip16.p;
+  L.cand_meta = e->l_ccnt.p; L.cand = e->l_cand.p; L.ip16 = e->l_ip16.p;
   e->jline.ensure(std::max<uint64_t>(e->jline.n, n_lines + (1u << 20)));
   e->jkey.ensure(e->jline.n);
   HIP_OK(hipMemsetAsync(e->scalars.p, 0, 16 * sizeof(unsigned long long), st));
-  if (B.any_prefilter) HIP_OK(hipMemsetAsync(e->l_ccnt.p, 0, n_lines * 4, st));
+  if (B.any_prefilter) HIP_OK(hipMemsetAsync(e->l_ccnt.p, 0, n_lines * sizeof(CandMeta), st));
   // BJX_SCAN_HEADER=1: the scan pass parses the header of every line that fits
   // its window and k_rules decides their rules (the others keep kLineTodo for
   // k_lines).  Off by default: measured slower at cfg3 (profiles/r02_v2: scan
@@ -5232,7 +5339,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       R.buf = buf; R.nl = e->nl.p; R.n_lines = n_lines; R.L = L; R.todo = e->long_list.p; R.todo_count = e->scalars.p + 12;
       R.jline = A.jline; R.jkey = A.jkey; R.job_count = A.job_count; R.job_cap = A.job_cap;
       const bool img_lds = B.img_bytes <= kRulesImgMax;
-      const uint32_t lds = ((img_lds ? B.img_bytes : 0) + 15u & ~15u) + (kBlock / 64) * (kWaveJobs * 8 + 16);
+      const uint32_t lds = ((img_lds ? B.img_bytes : 0) + 15u & ~15u) + (kBlock / 64) * kWaveJobBytes;
       const void *fn = img_lds ? reinterpret_cast<const void *>(&k_rules<true>) : reinterpret_cast<const void *>(&k_rules<false>);
       const unsigned grid = resident_grid(fn, lds, n_lines);
       if (img_lds) hipLaunchKernelGGL(k_rules<true>, dim3(grid), dim3(kBlock), lds, st, B, R);
@@ -5244,11 +5351,12 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       A.n_list = n_todo;
       A.span_bytes = 0;
     }
+    HIP_OK(hipEventRecord(e->evk[0], st));
     if (!scan_hdr || n_todo) {
       const bool img_lds = B.img_bytes <= kLinesImgMax;
       const bool host_lds = B.hl_bytes != 0;
       const uint32_t fixed = ((img_lds ? B.img_bytes : 0) + 15u & ~15u) + (host_lds ? B.hl_bytes + 15u & ~15u : 0u) +
-                             (kBlock / 64) * (kWaveJobs * 8 + 16);
+                             (kBlock / 64) * kWaveJobBytes;
       if (A.span_bytes && !getenv("BJX_SPAN_BYTES")) {
         // spans take what kLinesBlocksPerCu blocks leave of the CU's LDS
         // (LDS goes to blocks in granules: 53 KB blocks fit only twice per CU,
@@ -5291,6 +5399,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       else hipLaunchKernelGGL(k_lines<false>, dim3(grid), dim3(kBlock), lds, st, B, A);
       HIP_OK(hipGetLastError());
     }
+    HIP_OK(hipEventRecord(e->evk[1], st));
     e->last_todo = n_todo;
     HIP_OK(hipMemcpyAsync(&last_nl, e->nl.p + (n_lines - 1), 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(sc4, e->scalars.p + 8, 32, hipMemcpyDeviceToHost, st));
@@ -5309,6 +5418,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   e->last_jobs = n_jobs;
   e->scan_stats[0] = sc4[0]; e->scan_stats[1] = sc4[1]; e->scan_stats[2] = n_slow; e->scan_stats[3] = B.img_bytes;
   e->scan_stats[4] = n_jobs; e->scan_stats[5] = sc4[2];
+  HIP_OK(hipEventRecord(e->evk[2], st));
   if (n_jobs) {
     // group the jobs by rule (stable: line order inside a rule), then one lane per job
     e->jline2.ensure(n_jobs); e->jkey2.ensure(n_jobs);
@@ -5324,6 +5434,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     HIP_OK(hipGetLastError());
     if (B.any_nfa && !e->nfa_rules.empty()) run_nfa_jobs(e, B, buf, n, n_jobs, L);
   }
+  HIP_OK(hipEventRecord(e->evk[3], st));
   if (n_slow) {
     WideList WL{nullptr, nullptr, nullptr, e->scalars.p + 13, 0};
     if (B.any_wide) {
@@ -5645,6 +5756,12 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
   float ms = 0, mms = 0;
   HIP_OK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
   HIP_OK(hipEventElapsedTime(&mms, e->evm0, e->evm1));
+  {
+    float kl = 0, kd = 0;
+    HIP_OK(hipEventElapsedTime(&kl, e->evk[0], e->evk[1]));
+    HIP_OK(hipEventElapsedTime(&kd, e->evk[2], e->evk[3]));
+    e->kernel_ms[0] = mms; e->kernel_ms[1] = kl; e->kernel_ms[2] = kd;
+  }
   out->device_ms = ms;
   out->match_kernel_ms = mms;
   for (int k = 0; k < bjx_engine::kPhases; ++k) {
@@ -6115,6 +6232,11 @@ extern "C" size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap) {
   if (!e) return 0;
   for (size_t k = 0; k < cap && k < (size_t)bjx_engine::kPhases; ++k) out[k] = e->phase_ms[k];
   return bjx_engine::kPhases;
+}
+extern "C" size_t bjx_debug_kernel_ms(bjx_engine *e, double *out, size_t cap) {
+  if (!e) return 0;
+  for (size_t k = 0; k < cap && k < 3; ++k) out[k] = e->kernel_ms[k];
+  return 3;
 }
 extern "C" size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap) {
   if (!e) return 0;

@@ -22,7 +22,7 @@ struct DevRule {
   uint32_t anc_off;      // anchored rules: prefix literal ids rule_lits[anc_off .. + anc_len)
   uint16_t anc_len;
   uint8_t anc_equiv;     // match <=> rest starts with one of them
-  uint8_t _pad;
+  uint8_t lead;          // every match begins with a prefilter literal: a DFA job may start at its first hit
   uint32_t n_states;     // DFA states (rows of trans); NFA positions for kRuleNfa
   int64_t interval_ns;
   int64_t hits;
@@ -124,6 +124,7 @@ struct Bind {
   uint32_t n_lits;
   uint32_t any_anchored;
   uint32_t any_prefilter;
+  uint32_t lit_nl;  // some literal holds '\n' (k_scan then verifies only lines inside its window)
   ImgLayout il;
   // Lookup image for the scan pass (one blob, copied whole to LDS when it
   // fits; ImgLayout gives the offsets):
@@ -192,6 +193,16 @@ struct Bind {
 };
 
 // Per-line SoA arrays (batch workspace).
+// Per line, the scan pass's literal-hit summary: the first kCandSlots hits go
+// to Lines::cand; past them (overflow) only which literals (bit = id & 63)
+// and the lowest hit position are kept, which still rules out the literal
+// rules whose literals are absent and starts the other DFA jobs at the first hit.
+struct CandMeta {
+  uint32_t cnt;        // hits recorded (slots hold the first kCandSlots)
+  uint32_t first_inv;  // ~(lowest position >> 3) of the hits past the slots (0: none)
+  uint64_t bits;       // bit (literal id & 63) of every hit past the slots
+};
+
 struct Lines {
   int64_t *ts;
   uint64_t *ip_hash;
@@ -201,8 +212,8 @@ struct Lines {
   uint64_t *counts;    // (n_results << 32) | n_events per line, then scanned in place
   uint64_t *masks;     // mask_words per line
   uint4 *ip16;         // key16 of the line's IP (see IpSlot)
-  uint32_t *cand_cnt;  // literal hits recorded by the scan pass
-  uint64_t *cand;      // kCandSlots per line: (literal start << 24) | verified | literal id
+  CandMeta *cand_meta;  // literal hits recorded by the scan pass (zeroed before it)
+  uint64_t *cand;       // kCandSlots per line: (literal start << 24) | verified | literal id
 };
 
 // Persistent rate-limit state (RegexRateLimitStates, rate_limit.go:17-21),

@@ -8,9 +8,13 @@
 //      (bjx_match_batch);
 //   2. each engine sorts its event lines by owner, (ip_hash >> 32) % n, and
 //      packs them owner-major (bjx_events_partition / bjx_events_pack);
-//   3. the node copies every (source, owner) segment into the owner's receive
-//      buffers, concatenated in source order (hipMemcpyPeerAsync over xGMI;
-//      one copy stream per GPU);
+//   3. the node moves every (source, owner) segment into the owner's receive
+//      buffers, concatenated in source order: one RCCL group of
+//      ncclSend / ncclRecv pairs over xGMI when the engines sit on distinct
+//      GPUs (an all-to-all of variable-size segments, one communicator clique
+//      made by ncclCommInitAll), else copies on one stream per GPU
+//      (hipMemcpyPeerAsync / hipMemcpyAsync: several engines sharing a GPU,
+//      the one-GPU rehearsal; BJX_NODE_EXCHANGE=peer selects it always);
 //   4. each owner applies its events (bjx_apply_events): chunks are in stream
 //      order, so every (ip, rule name) state sees its events in the
 //      reference's order;
@@ -21,7 +25,9 @@
 // Phases 1, 2, 4 and 5 run on one host thread per engine, so the GPUs work
 // concurrently; 3 and 5's copies are issued from the calling thread.
 #include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
 
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -89,6 +95,8 @@ struct Part {
 
 struct bjx_node {
   std::vector<Part> parts;
+  std::vector<ncclComm_t> comms;  // RCCL clique over the engines' GPUs (empty: peer copies)
+  bool force_exchange = false;    // test hook (BJX_NODE_FORCE_EXCHANGE=1): exchange even for one engine
   std::mutex mu;
   std::string last_error;
   // merged results of the last batch
@@ -150,6 +158,46 @@ int guarded(bjx_node *n, F f) {
     n->last_error = "host out of memory";
     return BJX_ERR_NOMEM;
   }
+}
+
+void peer_copy(void *dst, const Part &D, const void *src, const Part &S, size_t bytes);
+
+void nccl_ok(ncclResult_t r, const char *what) {
+  if (r != ncclSuccess) fail(BJX_ERR_DEVICE, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+// One all-to-all of variable-size segments: seg(dst_part, src_part) gives the
+// destination pointer, source pointer and bytes.  RCCL: a single group of
+// ncclSend / ncclRecv over every pair (self pairs included), each GPU's side
+// on its copy stream; otherwise a copy per pair on the destination's copy
+// stream.  Zero-byte segments move nothing on either side (both sides know
+// every size).
+template <typename Seg>
+void exchange(bjx_node *n, Seg seg) {
+  const size_t N = n->parts.size();
+  if (n->comms.empty()) {
+    for (size_t p = 0; p < N; ++p)
+      for (size_t k = 0; k < N; ++k) {
+        void *d;
+        const void *s;
+        size_t b;
+        seg(p, k, &d, &s, &b);
+        peer_copy(d, n->parts[p], s, n->parts[k], b);
+      }
+    return;
+  }
+  nccl_ok(ncclGroupStart(), "ncclGroupStart");
+  for (size_t p = 0; p < N; ++p)
+    for (size_t k = 0; k < N; ++k) {
+      void *d;
+      const void *s;
+      size_t b;
+      seg(p, k, &d, &s, &b);
+      if (!b) continue;
+      nccl_ok(ncclSend(s, b, ncclUint8, (int)p, n->comms[k], n->parts[k].copy), "ncclSend");
+      nccl_ok(ncclRecv(d, b, ncclUint8, (int)k, n->comms[p], n->parts[p].copy), "ncclRecv");
+    }
+  nccl_ok(ncclGroupEnd(), "ncclGroupEnd");
 }
 
 void sync_copies(bjx_node *n) {
@@ -359,7 +407,7 @@ void run_batch(bjx_node *n, const bjx_ruleset *rs, const uint8_t *const *chunks,
   const size_t N = n->parts.size();
   const uint32_t match_flags = flags & ~(uint32_t)BJX_EMIT_BANS;
   n->bans = false;
-  if (N == 1) {  // nothing to exchange: the engine's own rate-limit stage
+  if (N == 1 && !n->force_exchange) {  // nothing to exchange: the engine's own rate-limit stage
     Part &P = n->parts[0];
     const int rc = bjx_process_batch(P.e, rs, chunks[0], lens[0], now_ns, flags, out);
     if (rc != BJX_OK) fail(rc, std::string("engine 0: ") + bjx_engine_last_error(P.e));
@@ -404,17 +452,14 @@ void run_batch(bjx_node *n, const bjx_ruleset *rs, const uint8_t *const *chunks,
                            P.s_bytes.p);
   });
   static const size_t unit[3] = {kLineRec, 4, 1};
-  for (size_t p = 0; p < N; ++p) {
-    Part &D = n->parts[p];
-    DevMem *dst[3] = {&D.r_lines, &D.r_ev, &D.r_bytes};
-    for (size_t k = 0; k < N; ++k) {
-      const Part &S = n->parts[k];
-      const DevMem *src[3] = {&S.s_lines, &S.s_ev, &S.s_bytes};
-      for (int c = 0; c < 3; ++c)
-        peer_copy(dst[c]->p + r_off[(p * N + k) * 3 + c] * unit[c], D, src[c]->p + s_off[(k * N + p) * 3 + c] * unit[c], S,
-                  recv_counts[(p * N + k) * 3 + c] * unit[c]);
-    }
-  }
+  for (int c = 0; c < 3; ++c)
+    exchange(n, [&](size_t p, size_t k, void **d, const void **s, size_t *b) {
+      DevMem *dst[3] = {&n->parts[p].r_lines, &n->parts[p].r_ev, &n->parts[p].r_bytes};
+      const DevMem *src[3] = {&n->parts[k].s_lines, &n->parts[k].s_ev, &n->parts[k].s_bytes};
+      *d = dst[c]->p + r_off[(p * N + k) * 3 + c] * unit[c];
+      *s = src[c]->p + s_off[(k * N + p) * 3 + c] * unit[c];
+      *b = recv_counts[(p * N + k) * 3 + c] * unit[c];
+    });
   sync_copies(n);
   // 4. owners apply their events in source order
   each(n, [&](size_t p) {
@@ -424,14 +469,11 @@ void run_batch(bjx_node *n, const bjx_ruleset *rs, const uint8_t *const *chunks,
                             P.r_out.p);
   });
   // 5. outcomes back to the sources (owner-major, the pack order)
-  for (size_t k = 0; k < N; ++k) {
-    Part &D = n->parts[k];
-    for (size_t p = 0; p < N; ++p) {
-      const Part &S = n->parts[p];
-      peer_copy(D.s_out.p + s_off[(k * N + p) * 3 + 1], D, S.r_out.p + r_off[(p * N + k) * 3 + 1], S,
-                recv_counts[(p * N + k) * 3 + 1]);
-    }
-  }
+  exchange(n, [&](size_t k, size_t p, void **d, const void **s, size_t *b) {
+    *d = n->parts[k].s_out.p + s_off[(k * N + p) * 3 + 1];
+    *s = n->parts[p].r_out.p + r_off[(p * N + k) * 3 + 1];
+    *b = recv_counts[(p * N + k) * 3 + 1];
+  });
   sync_copies(n);
   each(n, [&](size_t k) { return bjx_finish_batch(n->parts[k].e, n->parts[k].s_out.p, flags, &n->parts[k].res); });
   // 6. merge in chunk (= stream) order
@@ -522,6 +564,32 @@ extern "C" int bjx_node_create(const int *devices, size_t n_devices, const bjx_e
         }
       }
   }
+  if (rc == BJX_OK) {
+    // the RCCL clique when every engine has a GPU of its own (an RCCL
+    // communicator holds one rank per GPU); peer copies otherwise, on request
+    // (BJX_NODE_EXCHANGE=peer), or when RCCL cannot be set up here
+    const char *mode = getenv("BJX_NODE_EXCHANGE");
+    const char *force = getenv("BJX_NODE_FORCE_EXCHANGE");
+    n->force_exchange = force && atoi(force) == 1;
+    bool distinct = true;
+    for (size_t a = 0; a < n_devices; ++a)
+      for (size_t b = a + 1; b < n_devices; ++b) distinct = distinct && devices[a] != devices[b];
+    if (distinct && !(mode && strcmp(mode, "peer") == 0) && (n_devices > 1 || n->force_exchange)) {
+      n->comms.assign(n_devices, nullptr);
+      std::vector<int> dl(devices, devices + n_devices);
+      const ncclResult_t r = ncclCommInitAll(n->comms.data(), (int)n_devices, dl.data());
+      if (r != ncclSuccess) {
+        n->comms.clear();
+        if (mode && strcmp(mode, "rccl") == 0) {
+          say(std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+          rc = BJX_ERR_DEVICE;
+        }
+      }
+    } else if (mode && strcmp(mode, "rccl") == 0) {
+      say("BJX_NODE_EXCHANGE=rccl needs one engine per GPU");
+      rc = BJX_ERR_ARG;
+    }
+  }
   if (rc != BJX_OK) {
     bjx_node_destroy(n);
     return rc;
@@ -530,8 +598,12 @@ extern "C" int bjx_node_create(const int *devices, size_t n_devices, const bjx_e
   return BJX_OK;
 }
 
+extern "C" int bjx_node_exchange_kind(const bjx_node *n) { return !n ? -1 : n->comms.empty() ? 0 : 1; }
+
 extern "C" void bjx_node_destroy(bjx_node *n) {
   if (!n) return;
+  for (ncclComm_t c : n->comms)
+    if (c) (void)ncclCommDestroy(c);
   for (auto &P : n->parts) {
     for (DevMem *m : {&P.s_lines, &P.s_ev, &P.s_bytes, &P.s_out, &P.r_lines, &P.r_ev, &P.r_bytes, &P.r_out}) m->release();
     if (P.copy) {

@@ -1172,6 +1172,44 @@ bool prefilter_equivalent(const Re *r, const LSet &chosen) {
   return key(x) == key(chosen);
 }
 
+// The strings every match begins with, when the pattern is (.*)* X ... and
+// X's leading pieces are exact and assertion-free (text has no '\n', so the
+// leading .* never constrains an unanchored match): their cross product.
+bool leading_literals(const Re *r, LSet *out) {
+  while (r->op == kCap) r = r->sub[0].get();
+  LSet run{LStr{}};
+  if (r->op != kConcat) {
+    LInfo li = analyze(r);
+    if (!li.exact || !li.pure) return false;
+    run = li.ex;
+  } else {
+    size_t i = 0;
+    const size_t n = r->sub.size();
+    while (i < n && is_dotstar(r->sub[i].get())) ++i;
+    for (size_t k = i; k < n; ++k) {
+      LInfo li = analyze(r->sub[k].get());
+      LSet nr;
+      if (!li.exact || !li.pure || !cross(run, li.ex, &nr)) break;
+      run = std::move(nr);
+    }
+  }
+  if (!nonempty_all(run)) return false;
+  *out = std::move(run);
+  return true;
+}
+
+constexpr int kLeadScoreMargin = 32;  // window-score units (byte_weight) a leading set may trail the best by
+
+bool same_set(const LSet &a, const LSet &b) {
+  auto key = [](const LSet &s) {
+    std::vector<std::string> v;
+    for (auto &e : s) v.push_back(e.s + '\0' + e.ci);
+    std::sort(v.begin(), v.end());
+    return v;
+  };
+  return key(a) == key(b);
+}
+
 // ------------------------------------------------------------------ DFA
 
 enum Ctx : uint8_t { X_OTHER = 0, X_WORD = 1, X_NL = 2, X_START = 3 };
@@ -1877,6 +1915,14 @@ int compile_regex(const std::string &pattern, CompiledRegex *out, std::string *e
     bool have = false;
     if (li.exact && nonempty_all(li.ex)) { best = li.ex; have = true; }
     if (li.has_req && (!have || set_score(li.req) < set_score(best))) { best = li.req; have = true; }
+    // the strings every match begins with, when nearly as rare as the best
+    // required set: a DFA job then starts at their first hit, not at rest[0]
+    LSet lead;
+    if (leading_literals(root.get(), &lead) && set_score(lead) < 1000 &&
+        (!have || set_score(lead) <= set_score(best) + kLeadScoreMargin)) {
+      best = lead;
+      have = true;
+    }
     if (have && set_score(best) < (1 << 20)) {
       out->mode = kModePrefilter;
       for (auto &x : best) {
@@ -1889,6 +1935,8 @@ int compile_regex(const std::string &pattern, CompiledRegex *out, std::string *e
         out->pref.push_back(pl);
       }
       out->pref_equivalent = prefilter_equivalent(root.get(), best);
+      LSet lead;
+      out->pref_lead = leading_literals(root.get(), &lead) && same_set(lead, best);
       out->required_literal = best[0].s;
     } else {
       out->mode = kModeScan;

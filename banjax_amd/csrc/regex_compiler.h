@@ -139,6 +139,10 @@ struct CompiledRegex {
   // every match contains at least one of these (kModePrefilter); each >= 4 bytes
   std::vector<PrefLit> pref;
   bool pref_equivalent = false;  // match <=> text contains one of `pref`
+  // every match begins with one of `pref` (the pattern is (.*)* X ... with X's
+  // leading assertion-free exact strings = pref): a DFA job may start at the
+  // first occurrence of a pref literal instead of rest[0]
+  bool pref_lead = false;
   // kModeAnchored: every match starts with one of these (exact, ASCII-ci as above)
   std::vector<PrefLit> anchor;
   bool anchor_equivalent = false;  // match <=> text starts with one of `anchor`

@@ -225,6 +225,12 @@ class Engine:
         _lib.lib().bjx_debug_phase_ms(self._h, out, 8)
         return {k: round(out[i], 3) for i, k in enumerate(self.PHASES)}
 
+    def kernel_ms(self):
+        """Device ms of the last batch's k_scan, k_lines and DFA-job resolve (HIP events)."""
+        out = (C.c_double * 3)()
+        _lib.lib().bjx_debug_kernel_ms(self._h, out, 3)
+        return {"k_scan": out[0], "k_lines": out[1], "dfa_jobs": out[2]}
+
     def state_get(self, ip, name):
         hits, start = C.c_int64(), C.c_int64()
         ipb, nb = _lib.b(ip), _lib.b(name)
@@ -289,6 +295,11 @@ class Node:
 
     def __len__(self):
         return len(self.devices)
+
+    @property
+    def exchange(self) -> str:
+        """How the library moves the event records: "rccl" or "copies"."""
+        return "rccl" if _lib.lib().bjx_node_exchange_kind(self._h) == 1 else "copies"
 
     def engine(self, k: int) -> "Engine":
         """Engine k (stats and debug hooks); owned by the node."""

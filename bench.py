@@ -48,17 +48,29 @@ def cpu_baseline(w, sample_lines):
     return out
 
 
+def cgroup_cpus():
+    """CPUs of quota this process's cgroup grants (cgroup v2 cpu.max), or None."""
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if quota == "max" else max(1, int(int(quota) // int(period)))
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline_sharded(w, sample_lines):
-    """N worker processes (N = the CPUs this process may use, at most 16), each
-    running the oracle over its IP-hash shard of N x sample_lines / 4 lines;
-    throughput = lines / slowest worker."""
+    """N worker processes, each running the oracle over its IP-hash shard of
+    N x sample_lines / 4 lines; throughput = lines / slowest worker.  N = every
+    CPU this process may run on, capped by its cgroup's CPU quota (the GPU box
+    shows 256 CPUs but grants 16 of quota: more workers than that only
+    time-slice the same 16)."""
     import subprocess
     import tempfile
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    n = max(1, min(16, avail))
+    quota = cgroup_cpus()
+    n = max(1, min(avail, quota) if quota else avail)
     total = sample_lines * n // 4
     data = w.host_lines(0, total)
     with tempfile.TemporaryDirectory() as d:
@@ -72,37 +84,55 @@ def cpu_baseline_sharded(w, sample_lines):
         res = [json.loads(p.communicate()[0].decode().strip().splitlines()[-1]) for p in procs]
     slowest = max(r["seconds"] for r in res)
     return {"value": round(sum(r["lines"] for r in res) / slowest, 1), "unit": "lines/s", "cores": n,
-            "host_cpus": os.cpu_count(), "kind": "port",
+            "host_cpus": os.cpu_count(), "affinity_cpus": avail, "cgroup_cpu_quota": quota, "kind": "port",
             "sample": "first %d lines of %s, IP-hash sharded over %d oracle processes (per-IP order kept), "
                       "slowest shard %.1f s" % (total, w.name, n, slowest)}
 
 
-def pmc_traffic(nbytes):
-    """HBM bytes per k_scan launch from the committed rocprofv3 PMC passes over
-    this same command (profiles/pmc_traffic.json, written from the pass CSVs
-    under profiles/<round>/ by tools/pmc_session.sh): FETCH_SIZE x 2 (gfx950
-    reports half of a wide streaming read, MI355X_MICROARCH.md "HBM") +
-    WRITE_SIZE, both in KB."""
+def pmc_traffic(kernel):
+    """HBM GB per launch of `kernel` from the committed rocprofv3 PMC passes
+    over this same command (profiles/pmc_traffic.json, written from the pass
+    CSVs under profiles/<round>/ by tools/pmc_traffic.py): FETCH_SIZE x 2
+    (gfx950 reports half of a wide streaming read, MI355X_MICROARCH.md "HBM")
+    + WRITE_SIZE, both in KB."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None, None
     d = json.load(open(path))
-    return d["hbm_gb_per_launch"], d["source"]
+    k = d.get("kernels", {}).get(kernel)
+    return (k["hbm_gb_per_launch"], d["source"]) if k else (None, None)
 
 
-def roofline(achieved, match_ms, nbytes, args):
+KERNELS = {
+    "k_scan": "k_scan (framing + line index + literal prefilter over every byte of the batch)",
+    "k_lines": "k_lines (one lane per line: header, host, CheckIsAllowed, rule decisions from the hits; "
+               "the batch's line bytes staged in LDS)",
+    "dfa_jobs": "DFA-job sort + k_dfa / k_nfa (the (line, rule) pairs the literals cannot decide)",
+}
+
+
+def roofline(kms, nbytes, args):
+    """The dominant kernel of the timed steps (HIP events on the engine stream,
+    averaged over the timed steps): algorithmic bytes = the batch's log bytes
+    (every line read once) / its average time."""
     default = args.config == "cfg3" and not args.lines
-    traffic, src = pmc_traffic(nbytes) if default else (None, None)
+    dom = max(kms, key=kms.get)
+    ms = kms[dom]
+    achieved = nbytes / (ms / 1000.0) / 1e9
+    traffic, src = pmc_traffic(dom) if default else (None, None)
     r = {
         "bound": "hbm",
-        "kernel": "k_scan (HBM-streaming match pass: framing + literal prefilter over every byte)",
+        "kernel": KERNELS[dom],
         "achieved": round(achieved, 1),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
         "algorithmic_GB_per_launch": round(nbytes / 1e9, 3),
-        "kernel_ms": round(match_ms, 3),
+        "kernel_ms": round(ms, 3),
+        "kernels_ms": {k: round(v, 3) for k, v in kms.items()},
+        "k_scan": {"ms": round(kms["k_scan"], 3), "achieved": round(nbytes / (kms["k_scan"] / 1000.0) / 1e9, 1),
+                   "frac": round(nbytes / (kms["k_scan"] / 1000.0) / 1e9 / HBM_PEAK_GBS, 4)},
     }
     if src:
         r["traffic_source"] = src + ": rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, same command, GB per launch"
@@ -213,8 +243,14 @@ def main():
     if dist:
         dist.barrier()
     sync_all()
+    kacc = {"k_scan": 0.0, "k_lines": 0.0, "dfa_jobs": 0.0}
     t0 = time.perf_counter()
-    outs = [step() for _ in range(args.steps)]
+    outs = []
+    for _ in range(args.steps):
+        outs.append(step())
+        if drives:  # HIP-event times of the step's kernels (host reads only, no sync)
+            for k, v in eng.kernel_ms().items():
+                kacc[k] += v
     sync_all()
     if dist:
         dist.barrier()
@@ -279,7 +315,7 @@ def main():
                        "to pinned host memory, without the LogRegexBan lines (BJX_EMIT_BANS | BJX_BAN_RECORDS_ONLY)"}
     total_lines = n_lines * n_parts
     value = total_lines / (elapsed / args.steps)
-    achieved = nbytes / (match_ms / 1000.0) / 1e9
+    kms = {k: v / args.steps for k, v in kacc.items()}
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -318,7 +354,7 @@ def main():
                     "hipMemcpyPeerAsync" % n_parts if node_mode else "RCCL all-to-all of the event records"))
                 if n_parts > 1 else "dp1",
             },
-            "roofline": roofline(achieved, match_ms, nbytes, args),
+            "roofline": roofline(kms, nbytes, args),
         }
         mp_ms = phases["count"] + phases["scan"] + phases["resolve"]
         line["roofline"]["match_pass"] = {

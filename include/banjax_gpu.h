@@ -347,9 +347,12 @@ int bjx_batch_bans(bjx_engine *e, bjx_ban_batch *out);
    a node keeps that shape over n_devices engines.  Engine k matches the k-th
    contiguous chunk of the batch, the rate-limit state is sharded by IP (owner
    (ip_hash >> 32) % n_devices), and the library moves the event records to
-   their owners and the outcome bytes back itself (device-to-device copies over
-   xGMI, no caller collective).  Results come back in the reference's global
-   order, exactly as one engine over the whole batch returns them. */
+   their owners and the outcome bytes back itself (an RCCL all-to-all of
+   ncclSend / ncclRecv pairs over xGMI when every engine has a GPU of its own,
+   device-to-device copies when engines share a GPU; no caller collective).
+   Results come back in the reference's global order, exactly as one engine
+   over the whole batch returns them.  Env: BJX_NODE_EXCHANGE=peer|rccl forces
+   the copies / RCCL (rccl: creation fails when it cannot be had). */
 typedef struct bjx_node bjx_node;
 /* devices: HIP device index of each engine (repeats allowed: engines sharing a GPU). */
 int bjx_node_create(const int *devices, size_t n_devices, const bjx_engine_options *opts, bjx_node **out, char *err,
@@ -358,6 +361,8 @@ void bjx_node_destroy(bjx_node *n);
 size_t bjx_node_size(const bjx_node *n);
 /* Engine k of the node (its own stats and debug hooks); owned by the node. */
 bjx_engine *bjx_node_engine(bjx_node *n, size_t k);
+/* How the node moves its records: 1 RCCL, 0 device copies, -1 no node. */
+int bjx_node_exchange_kind(const bjx_node *n);
 const char *bjx_node_last_error(bjx_node *n);
 /* bjx_engine_set_decision_lists / bjx_engine_set_ban_options on every engine. */
 int bjx_node_set_decision_lists(bjx_node *n, const bjx_decision_entry *entries, size_t count);

@@ -22,6 +22,10 @@ size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t rule_idx, char *out,
    emit, capacity check, IP/state slot claim, sort + automaton, trips
    (returns the phase count) */
 size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap);
+/* device ms of the last batch's dominant kernels, from HIP events on the
+   engine stream: k_scan, k_lines (0 when the scan-header path left it no
+   lines), DFA-job sort + k_dfa / k_nfa (returns the count, 3) */
+size_t bjx_debug_kernel_ms(bjx_engine *e, double *out, size_t cap);
 /* last batch: gram bitset hits, recorded literal hits, lines sent to the per-line
    fallback, lines decided by the long-line pass, DFA jobs; then the state
    tables: IP slots, IPs, state slots, states; then gram table hits, lines

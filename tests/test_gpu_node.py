@@ -1,7 +1,8 @@
 """bjx_node_*: several engines behind one handle, the exchange inside the library.
 
 The engines share GPU 0 here (the box has one GPU; the library takes the
-same-device copy path instead of hipMemcpyPeerAsync).  Every batch is checked
+same-device copy path instead of its RCCL clique, which needs one GPU per
+engine); the RCCL path itself runs with one engine forced through the exchange.  Every batch is checked
 bit-exact against one oracle over the whole stream: per-line flags, the
 RuleResults and trips in reference order, the merged decision records and
 ban-log lines, and the RegexRateLimitStates spread over the shards.
@@ -45,13 +46,19 @@ def _check_batch(cfg, st, oc, data, now_ns, out, bans, dl, blog):
     return len(trips)
 
 
-@pytest.mark.parametrize("wl,n_engines,device_input", [
-    (("cfg3", 2000), 2, False),
-    (("cfg5", 3000), 3, True),
-    (("cfg1", 500), 4, False),
-    (("cfg3", 2000), 1, True),
+@pytest.mark.parametrize("wl,n_engines,device_input,rccl", [
+    (("cfg3", 2000), 2, False, False),
+    (("cfg5", 3000), 3, True, False),
+    (("cfg1", 500), 4, False, False),
+    (("cfg3", 2000), 1, True, False),
+    (("cfg5", 3000), 1, True, True),
+    (("cfg3", 2000), 1, False, True),
 ])
-def test_node_matches_one_oracle(wl, n_engines, device_input):
+def test_node_matches_one_oracle(wl, n_engines, device_input, rccl, monkeypatch):
+    """rccl: one engine whose batches still go through the library's exchange
+    (BJX_NODE_FORCE_EXCHANGE), moved by the RCCL path (a one-GPU clique from
+    ncclCommInitAll, ncclSend / ncclRecv to itself) that a node of distinct
+    GPUs uses between all of them."""
     import torch
 
     steps, per = 3, 12_000
@@ -59,8 +66,12 @@ def test_node_matches_one_oracle(wl, n_engines, device_input):
     cfg = Config.from_yaml(w.rules_yaml)
     from banjax_amd import Ruleset
     rs = Ruleset(cfg)
+    if rccl:
+        monkeypatch.setenv("BJX_NODE_FORCE_EXCHANGE", "1")
+        monkeypatch.setenv("BJX_NODE_EXCHANGE", "rccl")
     node = Node([0] * n_engines)
     assert len(node) == n_engines
+    assert node.exchange == ("rccl" if rccl else "copies")
     node.set_decision_lists(cfg.decision_entries)
     node.set_ban_options(cfg.expiring_decision_ttl_seconds)
     oc = oracle_config(cfg)
