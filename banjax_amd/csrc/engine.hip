@@ -985,7 +985,7 @@ __device__ __forceinline__ void plan_rule(const Bind &B, const Tabs &T, const ui
       uint64_t need = 0;
       for (uint32_t k = 0; k < 4; ++k) {
         const uint32_t id = ((k < 2 ? a.y : a.z) >> (16 * (k & 1))) & 0xFFFFu;
-        if (id != 0xFFFFu) need |= 1ull << (id & 63);
+        if (id != 0xFFFFu) need |= 1ull << (id & 31);
       }
       if (!(ov.bits & need)) return;
     }
@@ -1129,7 +1129,7 @@ __device__ __forceinline__ void plan_rule_lds(const Bind &B, const Tabs &T, cons
     uint64_t need = 0;
     for (uint32_t k = 0; k < 4; ++k) {
       const uint32_t id = ((k < 2 ? a.y : a.z) >> (16 * (k & 1))) & 0xFFFFu;
-      if (id != 0xFFFFu) need |= 1ull << (id & 63);
+      if (id != 0xFFFFu) need |= 1ull << (id & 31);
     }
     if (!(ov.bits & need)) return;  // the piece never occurred
     dfa_rule<EMIT>(B, T, r, pos, false, rest, rest_len, m0, m1, j, S);
@@ -1504,7 +1504,11 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
             if (cc < (uint32_t)kCandSlots) {
               L.cand[gline * kCandSlots + cc] = ((uint64_t)q0 << 24) | ver | lit;
             } else {  // past the slots: the line's summary only (CandMeta)
-              atomicOr(reinterpret_cast<unsigned long long *>(&L.cand_meta[gline].bits), 1ull << (lit & 63));
+              // a verified hit kCertainGap bytes past the line start lies in
+              // rest whenever the header is shorter (k_dfa checks rest_off)
+              const bool far = lk >= 0 ? s0 - (int32_t)ls[lk] >= (int32_t)kCertainGap : s0 >= (int32_t)kCertainGap;
+              const uint64_t bit = 1ull << (lit & 31);
+              atomicOr(reinterpret_cast<unsigned long long *>(&L.cand_meta[gline].bits), ver && far ? bit | (bit << 32) : bit);
               atomicMax(&L.cand_meta[gline].first_inv, ~(uint32_t)((uint64_t)q0 >> 3));
             }
             ++n_hit;
@@ -1636,9 +1640,9 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
           continue;
         lpos |= (uint64_t)(q - rs < 0xFFFF ? (uint32_t)(q - rs) : 0xFFFFu) << (16 * nlit);
         lits |= (uint64_t)lit << (16 * nlit++);
-        ov.bits |= 1ull << (lit & 63);
+        ov.bits |= 1ull << (lit & 31);
       }
-      if (cc > (uint32_t)kCandSlots) ov.bits |= cm.bits;  // the hits past the slots
+      if (cc > (uint32_t)kCandSlots) ov.bits |= cm.bits & 0xFFFFFFFFull;  // the hits past the slots
       if (HOST_LDS && B.lt_cls && !(A.dbg & 15)) {
         LdsTabs LT;
         LT.hinfo = reinterpret_cast<const uint2 *>(hl + B.lt_hinfo);
@@ -1928,6 +1932,32 @@ __device__ __forceinline__ uint32_t lead_start(const Bind &B, const Lines &L, ui
   return f == ~0ull ? rl : (uint32_t)min<uint64_t>(f - rs, rl);
 }
 
+// A job of an equivalent literal rule (match <=> one of its literals occurs
+// in rest) decided without its automaton when the scan saw one for certain:
+// a verified slot hit of the line's own rule's literal at or past rest, or,
+// past the slots, a verified hit of it kCertainGap bytes into the line with
+// the header shorter than that (CandMeta::bits, exact while the ruleset has
+// at most 32 literals).
+__device__ __forceinline__ bool eq_certain(const Bind &B, const Lines &L, uint64_t j, uint32_t pos, uint64_t rs) {
+  const int32_t hid = L.host_id[j];
+  uint32_t sb = 0, nsite = 0;
+  if (hid >= 0) { sb = B.site_off[hid]; nsite = B.site_off[hid + 1] - sb; }
+  const uint32_t r = pos < nsite ? B.site_rules[sb + pos] : B.global_rules[pos - nsite];
+  const DevRule &R = B.rules[r];
+  if (!R.equiv || !(R.lead & 2u)) return false;  // equivalent, literals not host-split
+  const CandMeta cm = L.cand_meta[j];
+  const uint32_t ns = min(cm.cnt, (uint32_t)kCandSlots);
+  uint64_t need = 0;
+  for (uint32_t k = 0; k < R.lits_len; ++k) need |= 1ull << (B.rule_lits[R.lits_off + k] & 31);
+  for (uint32_t c = 0; c < ns; ++c) {
+    const uint64_t v = L.cand[j * kCandSlots + c];
+    if (!(v & kCandVerified) || (v >> 24) < rs) continue;
+    for (uint32_t k = 0; k < R.lits_len; ++k)
+      if (B.rule_lits[R.lits_off + k] == (uint32_t)(v & 0x7FFFFF)) return true;
+  }
+  return cm.cnt > (uint32_t)kCandSlots && B.lits_small && L.rest_off[j] <= kCertainGap && ((cm.bits >> 32) & need) != 0;
+}
+
 constexpr uint32_t kDfaLdsEntries = 8192;  // u16 transitions staged per block (16 KB)
 
 // STAGED: tr / ac point into LDS (a distinct instantiation keeps the call
@@ -2023,7 +2053,10 @@ __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restric
   const uint64_t rs = s + L.rest_off[j];
   const uint32_t rl = (uint32_t)(nl[j] - rs);
   bool m;
-  if (staged) {
+  if (!staged && (B.rules[r].flags & kRuleNfa)) return;  // k_nfa's (a mixed block)
+  if ((staged ? R0.equiv : B.rules[r].equiv) && eq_certain(B, L, j, pos, rs)) {
+    m = true;
+  } else if (staged) {
     // anchored prefix literal already matched by k_lines: step in past it;
     // a lead rule's job starts at the first hit of its literals (every match
     // begins at one, regex_compiler.h pref_lead)
@@ -2947,6 +2980,18 @@ __global__ void k_check_rl(EvSrc E, uint64_t n_ev, const uint32_t *__restrict__ 
       if (atomicAdd(&chk[12], 1ull) == 0) chk[13] = t;
     }
   }
+}
+
+// BJX_CHECK: each line's RuleResult count (counts >> 32) equals its match
+// mask's population (a (line, rule) decided twice shows here)
+__global__ void k_check_masks(uint64_t n_lines, Lines L, uint32_t mask_words, unsigned long long *__restrict__ chk) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_lines || mask_words > 2) return;  // past 128 positions the fast path leaves the words it never uses
+  uint32_t pc = 0;
+  const uint8_t f = L.flags[j];
+  if (!(f & (kLineError | kLineOld | kLineExempt)))
+    for (uint32_t w = 0; w < mask_words; ++w) pc += __popcll(L.masks[j * mask_words + w]);
+  if ((uint32_t)(L.counts[j] >> 32) != pc && atomicAdd(&chk[0], 1ull) == 0) chk[1] = j;
 }
 
 // BJX_CHECK: cnt[idx[t * step]] += 1 for t < n (idx < cap, else chk[0]++)
@@ -4077,13 +4122,13 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     d.anc_len = (uint16_t)(rule_lits.size() - d.anc_off);
     d.anc_equiv = r.rx.anchor_equivalent ? 1 : 0;
     // bit 0: every match of the pattern begins with a literal of pref; bit 1:
-    // this copy's literals are those (not host-split pieces): lead_start
-    if (r.rx.mode == kModePrefilter && r.rx.pref_lead) {
+    // this copy's literals are those (not host-split pieces): lead_start,
+    // eq_certain
+    d.lead = 0;
+    if (r.rx.mode == kModePrefilter) {
       bool split = false;
       for (uint32_t k = d.lits_off; k < d.lits_off + d.lits_len; ++k) split = split || rule_full[k] != kNone;
-      d.lead = split ? 1 : 3;
-    } else {
-      d.lead = 0;
+      d.lead = (r.rx.pref_lead ? 1 : 0) | (split ? 0 : 2);
     }
     any_anchored = any_anchored || r.rx.mode == kModeAnchored;
     d.interval_ns = r.interval_ns;
@@ -4658,6 +4703,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.any_anchored = any_anchored ? 1 : 0;
   B.any_prefilter = use_pref ? 1 : 0;
   B.lit_nl = std::find(lit_bytes.begin(), lit_bytes.end(), (uint8_t)'\n') != lit_bytes.end() ? 1u : 0u;
+  B.lits_small = lit_off.size() <= 32 ? 1u : 0u;
   B.img = base + o_img;
   B.img_bytes = (uint32_t)img.size();
   B.il = il;
@@ -5455,6 +5501,21 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     }
   }
   e->last_slow = n_slow;
+  if (getenv("BJX_CHECK")) {
+    e->chk.ensure(16);
+    HIP_OK(hipMemsetAsync(e->chk.p, 0, 16, st));
+    hipLaunchKernelGGL(k_check_masks, dim3(grid_for(n_lines)), dim3(kBlock), 0, st, n_lines, L, B.mask_words, e->chk.p);
+    HIP_OK(hipGetLastError());
+    unsigned long long c[2];
+    HIP_OK(hipMemcpyAsync(c, e->chk.p, 16, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (c[0]) {
+      char msg[160];
+      snprintf(msg, sizeof msg, "BJX_CHECK: %llu lines whose RuleResult count differs from their match mask (first %llu)", c[0],
+               c[1]);
+      throw BjxError(BJX_ERR_DEVICE, msg);
+    }
+  }
   if (e->dbg_hash_mask)
     hipLaunchKernelGGL(k_dbg_mask_hash, dim3(grid_for(n_lines)), dim3(kBlock), 0, st, n_lines, L.ip_hash, e->dbg_hash_mask);
   mark(e, 3);

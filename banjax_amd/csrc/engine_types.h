@@ -124,6 +124,7 @@ struct Bind {
   uint32_t n_lits;
   uint32_t any_anchored;
   uint32_t any_prefilter;
+  uint32_t lits_small;  // at most 32 interned literals: CandMeta bit id & 31 names one literal
   uint32_t lit_nl;  // some literal holds '\n' (k_scan then verifies only lines inside its window)
   ImgLayout il;
   // Lookup image for the scan pass (one blob, copied whole to LDS when it
@@ -200,8 +201,10 @@ struct Bind {
 struct CandMeta {
   uint32_t cnt;        // hits recorded (slots hold the first kCandSlots)
   uint32_t first_inv;  // ~(lowest position >> 3) of the hits past the slots (0: none)
-  uint64_t bits;       // bit (literal id & 63) of every hit past the slots
+  uint64_t bits;       // past the slots: bit (literal id & 31) of every hit; bit 32 + (id & 31) of the
+                       // verified ones at least kCertainGap bytes into the line
 };
+constexpr uint32_t kCertainGap = 256;
 
 struct Lines {
   int64_t *ts;
