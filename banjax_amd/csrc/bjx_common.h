@@ -164,10 +164,17 @@ BJX_HD int parse_float_fast(const uint8_t *s, uint32_t n, double *out) {
   if (frac < 0) frac = 0;
   if (s[0] == '.' || (n == 1 && s[0] == '.')) return 1;
   if (m >= (1ULL << 53) || frac > 22) return 1;
-  const double p10[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
-                          1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  // 10^frac as a product of exact powers of ten: every partial product is a
+  // power of ten <= 1e22, exactly representable, so each multiply is exact
+  // (no table: an indexed local array would live in scratch on the device)
+  double p = 1.0;
+  if (frac & 1) p *= 1e1;
+  if (frac & 2) p *= 1e2;
+  if (frac & 4) p *= 1e4;
+  if (frac & 8) p *= 1e8;
+  if (frac & 16) p *= 1e16;
   double f = (double)m;
-  *out = frac ? f / p10[frac] : f;
+  *out = frac ? f / p : f;
   return 0;
 }
 
