@@ -15,6 +15,8 @@ LIBDIR = os.path.join(HERE, "lib")
 ARCH = os.environ.get("BJX_OFFLOAD_ARCH", "gfx950")
 # BJX_PROF=1: also compile the k_lines segment-clock variants (BJX_PROF_LINES)
 PROF = ["-DBJX_PROF"] if os.environ.get("BJX_PROF") == "1" else []
+# BJX_EXTRA_FLAGS: extra compiler flags (timing experiments only)
+PROF += os.environ.get("BJX_EXTRA_FLAGS", "").split()
 COMMON = PROF + ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "--offload-arch=%s" % ARCH,
           "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result"]
 

@@ -1053,6 +1053,22 @@ __device__ __forceinline__ void decide_plan(const Bind &B, const Tabs &T, const 
   L.counts[j] = ((uint64_t)nres << 32) | nev;
 }
 
+// k_lines<.., PROF = true>: wave clock (s_memtime) per loop segment, summed
+// over waves: 0 loads + staging, 1 header + timestamp, 2 host lookup, 3 host
+// rule words, 4 rule decisions (with decide_plan_lds: the mask stores), 5
+// per-line stores, 6 DFA-job flush; in decide_plan_lds 7 hit decoding, 8 site
+// class walk, 9 global walk
+struct LinesProf {
+  uint64_t t = 0;
+  uint64_t acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  __device__ __forceinline__ void start() { t = __builtin_amdgcn_s_memtime(); }
+  __device__ __forceinline__ void mark(int k) {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    acc[k] += now - t;
+    t = now;
+  }
+};
+
 // ---- plan classes in LDS (k_lines<.., HOST_LDS>, Bind::lt_*).  Hosts whose
 // site plans are equal once (a) a host-specific literal F = A + host + C
 // becomes a template (A, C) checked around the line's own host field and (b)
@@ -1159,9 +1175,11 @@ template <bool EMIT>
 __device__ __forceinline__ void decide_plan_lds(const Bind &B, const Tabs &T, const LdsTabs &LT, const uint8_t *rest,
                                                 uint32_t rest_len, uint32_t host_rel, uint32_t host_len, int32_t hid,
                                                 const HostRules &H, uint64_t lits, uint64_t lpos, uint32_t nlit, bool ovf,
-                                                const OvfInfo &ov, uint64_t j, const Lines &L, const JobSink &S) {
+                                                const OvfInfo &ov, uint64_t j, const Lines &L, const JobSink &S,
+                                                LinesProf *P = nullptr) {
   const uint32_t nsite = H.s_end - H.s_begin;
   uint64_t m0 = H.a0, m1 = H.a1;
+  if (P) { __builtin_amdgcn_s_waitcnt(0); P->mark(7); }
   if (hid >= 0) {
     const uint2 hi = LT.hinfo[hid];
     const uint32_t cb = hi.x & 0xFFFFu, ce = cb + (hi.x >> 16);
@@ -1169,9 +1187,11 @@ __device__ __forceinline__ void decide_plan_lds(const Bind &B, const Tabs &T, co
       plan_rule_lds<EMIT>(B, T, LT, LT.cls[2 * i], LT.cls[2 * i + 1], hi.y, rest, rest_len, host_rel, host_len, lits, lpos,
                           nlit, ovf, ov, m0, m1, j, S);
   }
+  if (P) { __builtin_amdgcn_s_waitcnt(0); P->mark(8); }
   for (uint32_t i = 0; i < B.n_plan_glob; ++i)
     plan_rule<EMIT>(B, T, B.plan_glob[2 * i], B.plan_glob[2 * i + 1], nsite, rest, rest_len, lits, lpos, nlit, ovf, ov, m0, m1,
                     j, S);
+  if (P) { __builtin_amdgcn_s_waitcnt(0); P->mark(9); }
   uint64_t *mask = L.masks + j * B.mask_words;
   mask[0] = m0;
   if (B.mask_words > 1) mask[1] = m1;
@@ -1554,20 +1574,6 @@ struct LinesArgs {
   unsigned long long *prof;  // BJX_PROF_LINES: shader clocks per k_lines segment (k_lines<.., true>)
 };
 
-// k_lines<.., PROF = true>: wave clock (s_memtime) per loop segment, summed
-// over waves: 0 loads + staging, 1 header + timestamp, 2 host lookup, 3 host
-// rule words, 4 rule decisions, 5 per-line stores, 6 DFA-job flush
-struct LinesProf {
-  uint64_t t = 0;
-  uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
-  __device__ __forceinline__ void start() { t = __builtin_amdgcn_s_memtime(); }
-  __device__ __forceinline__ void mark(int k) {
-    const uint64_t now = __builtin_amdgcn_s_memtime();
-    acc[k] += now - t;
-    t = now;
-  }
-};
-
 // consumeLine up to the rule loop for line j (bytes at base + (s - origin)):
 // SplitN header, parseTimestamp fast path, host lookup, CheckIsAllowed,
 // OldLine, then the rule decisions from the scan pass's literal hits.
@@ -1650,7 +1656,7 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
         LT.trec = reinterpret_cast<const uint4 *>(hl + B.lt_trec);
         LT.pool = reinterpret_cast<const uint8_t *>(hl + B.lt_pool);
         decide_plan_lds<true>(B, TB, LT, p + rest_off, n - rest_off, host_off - rest_off, host_len, hid, H, lits, lpos, nlit,
-                              cc > (uint32_t)kCandSlots, ov, j, L, S);
+                              cc > (uint32_t)kCandSlots, ov, j, L, S, PROF ? &P : nullptr);
       } else if (B.use_plan && !(A.dbg & 15))
         decide_plan<true>(B, TB, p + rest_off, n - rest_off, hid, H, lits, lpos, nlit, cc > (uint32_t)kCandSlots, ov, j, L, S,
                           A.dbg);
@@ -1796,7 +1802,7 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
     if (PROF) { __builtin_amdgcn_s_waitcnt(0); P.mark(6); }
   }
   if (PROF && lane == 0)
-    for (int k = 0; k < 7; ++k) atomicAdd(&A.prof[k], (unsigned long long)P.acc[k]);
+    for (int k = 0; k < 10; ++k) atomicAdd(&A.prof[k], (unsigned long long)P.acc[k]);
 }
 
 // Rule decisions of the lines whose header the scan pass parsed (one lane per
@@ -1912,6 +1918,9 @@ __device__ __forceinline__ uint32_t lead_start(const Bind &B, const Lines &L, ui
   const uint32_t r = pos < nsite ? B.site_rules[sb + pos] : B.global_rules[pos - nsite];  // the line's own rule
   const uint32_t lead = B.rules[r].lead, lo = B.rules[r].lits_off, ln = B.rules[r].lits_len;
   if ((lead & 3u) != 3u) return 0;
+  // a bounded piece may precede the literal (lead_dist; + 3 so a rune cut by
+  // the start decodes to errors that end before the match)
+  const uint32_t back = B.rules[r].lead_dist ? B.rules[r].lead_dist + 3u : 0u;
   const CandMeta cm = L.cand_meta[j];
   const bool ovf = cm.cnt > (uint32_t)kCandSlots;
   uint64_t f = ~0ull;
@@ -1929,7 +1938,73 @@ __device__ __forceinline__ uint32_t lead_start(const Bind &B, const Lines &L, ui
     if (mf < rs) return 0;
     f = mf < f ? mf : f;
   }
-  return f == ~0ull ? rl : (uint32_t)min<uint64_t>(f - rs, rl);
+  if (f == ~0ull) return rl;
+  const uint32_t o = (uint32_t)min<uint64_t>(f - rs, rl);
+  return o > back ? o - back : 0u;
+}
+
+// First occurrence at or after p (before end) of one of lead rule R's
+// literals, or end: the job of a line whose hits overflowed its slots starts
+// from the first hit of ANY literal (lead_start), so it skips forward here 16 B
+// at a time (first-byte SWAR compare, then the literal's bytes) instead of
+// stepping the DFA byte by byte.  Rules with more than 4 literals: p.
+constexpr uint32_t kSeekLits = 4;
+__device__ __forceinline__ uint64_t lead_seek(const Bind &B, const DevRule &R, const uint8_t *__restrict__ buf, uint64_t n_buf,
+                                           uint64_t p, uint64_t end) {
+  if (R.lits_len == 0 || R.lits_len > kSeekLits || p >= end) return p;
+  const Tabs T = make_tabs(B.img, B.il);
+  uint32_t lit[kSeekLits], rep[kSeekLits], cim[kSeekLits];
+  const uint32_t nk = R.lits_len;
+#pragma unroll
+  for (uint32_t k = 0; k < kSeekLits; ++k) {
+    lit[k] = k < nk ? B.rule_lits[R.lits_off + k] : 0u;
+    const uint32_t off = T.lrec[lit[k]] >> 8;
+    rep[k] = k < nk ? (uint32_t)T.lbytes[off] * 0x01010101u : 0u;       // first byte (lower case where ci)
+    cim[k] = k < nk ? (uint32_t)T.lcim[off] * 0x01010101u : 0u;         // its case mask
+  }
+  uint64_t a = p & ~15ull;
+  uint32_t skip = (uint32_t)(p - a);
+  while (a < end) {
+    uint4 v;
+    if (a + 16 <= n_buf) v = *reinterpret_cast<const uint4 *>(buf + a);
+    else {
+      uint32_t w[4];
+      for (int k = 0; k < 4; ++k) {
+        uint32_t x = 0;
+        for (int b = 0; b < 4; ++b) x |= (a + 4 * k + b < n_buf ? (uint32_t)buf[a + 4 * k + b] : 0u) << (8 * b);
+        w[k] = x;
+      }
+      v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+    uint32_t cand = 0;  // bit i: byte a + i equals some literal's first byte
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (uint32_t k = 0; k < kSeekLits; ++k) {
+        if (k >= nk) break;
+        const uint32_t y = (wv[q] | cim[k]) ^ rep[k];
+        const uint32_t hb = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;  // exact zero-byte mask
+        cand |= (((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u)) << (4 * q);
+      }
+    }
+    cand &= ~((1u << skip) - 1u);
+    while (cand) {
+      const uint32_t i = (uint32_t)__ffs(cand) - 1;
+      cand &= cand - 1;
+      const uint64_t q = a + i;
+      if (q >= end) return end;
+#pragma unroll
+      for (uint32_t k = 0; k < kSeekLits; ++k) {
+        if (k >= nk) break;
+        const uint32_t len = T.lrec[lit[k]] & 0xFF;
+        if (q + len <= end && literal_at(T, lit[k], buf + q)) return q;
+      }
+    }
+    skip = 0;
+    a += 16;
+  }
+  return end;
 }
 
 // A job of an equivalent literal rule (match <=> one of its literals occurs
@@ -1956,6 +2031,18 @@ __device__ __forceinline__ bool eq_certain(const Bind &B, const Lines &L, uint64
       if (B.rule_lits[R.lits_off + k] == (uint32_t)(v & 0x7FFFFF)) return true;
   }
   return cm.cnt > (uint32_t)kCandSlots && B.lits_small && L.rest_off[j] <= kCertainGap && ((cm.bits >> 32) & need) != 0;
+}
+
+// lead_start, then, for a line whose hits overflowed its slots (the start is
+// then the first hit of any literal), lead_seek to the rule's own literal
+__device__ __forceinline__ uint32_t lead_start_seek(const Bind &B, const DevRule &R, const Lines &L, const uint8_t *buf,
+                                                    uint64_t n_buf, uint64_t j, uint32_t pos, uint64_t rs, uint32_t rl) {
+  const uint32_t st0 = lead_start(B, L, j, pos, rs, rl);
+  if ((R.lead & 3u) != 3u || st0 >= rl || L.cand_meta[j].cnt <= (uint32_t)kCandSlots) return st0;
+  const uint32_t back = R.lead_dist ? R.lead_dist + 3u : 0u;
+  const uint64_t q = lead_seek(B, R, buf, n_buf, rs + st0 + (st0 ? back : 0u), rs + rl);
+  const uint32_t o = (uint32_t)(q - rs);
+  return o >= rl ? rl : (o > back && o - back > st0 ? o - back : st0);
 }
 
 constexpr uint32_t kDfaLdsEntries = 8192;  // u16 transitions staged per block (16 KB)
@@ -2061,14 +2148,14 @@ __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restric
     // a lead rule's job starts at the first hit of its literals (every match
     // begins at one, regex_compiler.h pref_lead)
     const uint32_t sk = R0.skip_len && R0.skip_len <= rl ? R0.skip_len : 0u;
-    const uint32_t st0 = (R0.lead & 1u) ? lead_start(B, L, j, pos, rs, rl) : 0u;
+    const uint32_t st0 = (R0.lead & 1u) ? lead_start_seek(B, R0, L, buf, n_buf, j, pos, rs, rl) : 0u;
     m = st0 ? dfa_text<true>(B, R0, s_tr, s_ac, buf, n_buf, rs + st0, rl - st0, R0.start)
             : dfa_text<true>(B, R0, s_tr, s_ac, buf, n_buf, rs + sk, rl - sk, sk ? R0.skip_state : R0.start);
   } else {
     const DevRule R = B.rules[r];
     if (R.flags & kRuleNfa) return;  // k_nfa's
     const uint32_t sk = R.skip_len && R.skip_len <= rl ? R.skip_len : 0u;
-    const uint32_t st0 = (R.lead & 1u) ? lead_start(B, L, j, pos, rs, rl) : 0u;
+    const uint32_t st0 = (R.lead & 1u) ? lead_start_seek(B, R, L, buf, n_buf, j, pos, rs, rl) : 0u;
     if (st0) m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, buf, n_buf, rs + st0, rl - st0,
                                  R.start);
     else m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, buf, n_buf, rs + sk, rl - sk,
@@ -4130,6 +4217,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
       for (uint32_t k = d.lits_off; k < d.lits_off + d.lits_len; ++k) split = split || rule_full[k] != kNone;
       d.lead = (r.rx.pref_lead ? 1 : 0) | (split ? 0 : 2);
     }
+    d.lead_dist = r.rx.pref_lead ? r.rx.lead_dist : 0;
     any_anchored = any_anchored || r.rx.mode == kModeAnchored;
     d.interval_ns = r.interval_ns;
     d.hits = r.hits;
@@ -5423,20 +5511,21 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
 #ifndef BJX_PROF
         throw BjxError(BJX_ERR_ARG, "BJX_PROF_LINES needs a library built with BJX_PROF=1");
 #else
-        e->chk.ensure(8);
-        HIP_OK(hipMemsetAsync(e->chk.p, 0, 64, st));
+        e->chk.ensure(16);
+        HIP_OK(hipMemsetAsync(e->chk.p, 0, 128, st));
         A.prof = e->chk.p;
         if (img_lds && host_lds) hipLaunchKernelGGL((k_lines<true, true, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
         else if (img_lds) hipLaunchKernelGGL((k_lines<true, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
         else if (host_lds) hipLaunchKernelGGL((k_lines<false, true, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
         else hipLaunchKernelGGL((k_lines<false, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
-        unsigned long long c[8];
-        HIP_OK(hipMemcpyAsync(c, e->chk.p, 64, hipMemcpyDeviceToHost, st));
+        unsigned long long c[10];
+        HIP_OK(hipMemcpyAsync(c, e->chk.p, 80, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
         double tot = 0;
-        for (int k = 0; k < 7; ++k) tot += (double)c[k];
+        for (int k = 0; k < 10; ++k) tot += (double)c[k];
         fprintf(stderr, "[bjx] k_lines segments (%% of wave clocks): loads+staging %.1f header %.1f host %.1f host-rules %.1f "
-                "decide %.1f stores %.1f jobs %.1f\n", 100 * c[0] / tot, 100 * c[1] / tot, 100 * c[2] / tot, 100 * c[3] / tot,
+                "hit-decode %.1f site-walk %.1f global-walk %.1f mask-stores %.1f stores %.1f jobs %.1f\n", 100 * c[0] / tot,
+                100 * c[1] / tot, 100 * c[2] / tot, 100 * c[3] / tot, 100 * c[7] / tot, 100 * c[8] / tot, 100 * c[9] / tot,
                 100 * c[4] / tot, 100 * c[5] / tot, 100 * c[6] / tot);
 #endif
       } else if (img_lds && host_lds) hipLaunchKernelGGL((k_lines<true, false, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
@@ -6309,6 +6398,12 @@ extern "C" size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap)
   for (size_t k = 0; k < 12 && k < cap; ++k) out[k] = v[k];
   return 12;
 }
+extern "C" int bjx_debug_rule_lead(const bjx_ruleset *rs, size_t i) {
+  if (!rs || i >= rs->rules.size()) return BJX_ERR_ARG;
+  const auto &rx = rs->rules[i].rx;
+  return rx.mode == kModePrefilter && rx.pref_lead ? (int)rx.lead_dist : -1;
+}
+
 extern "C" size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t i, char *out, size_t cap) {
   if (!rs || i >= rs->rules.size()) return 0;
   // "<mode> <equiv>" then per literal "\n<gram_off> <ci mask as 0/1> <bytes>"

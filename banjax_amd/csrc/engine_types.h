@@ -32,6 +32,9 @@ struct DevRule {
   // a DFA job is made: k_dfa starts skip_len bytes in, in state skip_state
   uint16_t skip_len;
   uint16_t skip_state;
+  // lead rules (CompiledRegex::lead_dist): a job starts this many bytes (plus
+  // a rune's worth) before the first hit of the rule's literals
+  uint16_t lead_dist;
 };
 
 // Prefilter gram bitset: one bit per hash of a 4-byte window (LDS resident).

@@ -1198,6 +1198,111 @@ bool leading_literals(const Re *r, LSet *out) {
   return true;
 }
 
+// Most bytes (UTF-8) a pure node can match; -1 when unbounded or when the node
+// holds an empty-width assertion.
+int max_match_bytes(const Re *r) {
+  auto utf8_len = [](int32_t c) { return c < 0x80 ? 1 : c < 0x800 ? 2 : c < 0x10000 ? 3 : 4; };
+  switch (r->op) {
+    case kEmpty: case kNoMatch: return 0;
+    case kLit: return (r->flags & kFold) ? 4 : utf8_len(r->rune);  // a fold orbit may leave ASCII
+    case kClass: {
+      int m = 0;
+      for (auto &rg : r->cls) m = std::max(m, utf8_len(rg.second));
+      return m;
+    }
+    case kAnyNotNL: case kAnyChar: return 4;
+    case kCap: case kQuest: return max_match_bytes(r->sub[0].get());
+    case kRepeat: {
+      if (r->max < 0) return -1;
+      const int s = max_match_bytes(r->sub[0].get());
+      return s < 0 ? -1 : (r->max * s > 4096 ? -1 : r->max * s);
+    }
+    case kConcat: {
+      int t = 0;
+      for (auto &s : r->sub) {
+        const int m = max_match_bytes(s.get());
+        if (m < 0 || t + m > 4096) return -1;
+        t += m;
+      }
+      return t;
+    }
+    case kAlt: {
+      int t = 0;
+      for (auto &s : r->sub) {
+        const int m = max_match_bytes(s.get());
+        if (m < 0) return -1;
+        t = std::max(t, m);
+      }
+      return t;
+    }
+    default: return -1;  // star, plus, assertions
+  }
+}
+
+// The strings S every match contains at most *dist bytes after its start,
+// when (per branch of a top-level alternation) the pattern is (.*)* P X ...
+// with P pure and at most *dist bytes long and X's leading exact,
+// assertion-free pieces spelling S (each >= 4 bytes): a DFA job may start
+// *dist bytes (plus a rune's worth) before the first hit of S.  dist 0 is
+// leading_literals' case.  P being assertion-free keeps the start context of a
+// job started inside the text irrelevant.
+bool bounded_leading_literals(const Re *r, LSet *out, int *dist) {
+  while (r->op == kCap) r = r->sub[0].get();
+  if (r->op == kAlt) {
+    LSet all;
+    int d = 0;
+    for (auto &b : r->sub) {
+      LSet s;
+      int bd = 0;
+      if (!bounded_leading_literals(b.get(), &s, &bd)) return false;
+      all.insert(all.end(), s.begin(), s.end());
+      d = std::max(d, bd);
+    }
+    if (all.size() > kMaxSet) return false;
+    *out = std::move(all);
+    *dist = d;
+    return true;
+  }
+  auto long_enough = [](const LSet &s) {
+    if (!nonempty_all(s)) return false;
+    for (auto &x : s)
+      if (x.s.size() < 4) return false;
+    return true;
+  };
+  if (r->op != kConcat) {
+    LInfo li = analyze(r);
+    if (!li.exact || !li.pure || !long_enough(li.ex)) return false;
+    *out = li.ex;
+    *dist = 0;
+    return true;
+  }
+  const size_t n = r->sub.size();
+  size_t i = 0;
+  while (i < n && is_dotstar(r->sub[i].get())) ++i;
+  int pre = 0;
+  for (size_t k = i; k < n; ++k) {
+    LInfo li = analyze(r->sub[k].get());
+    if (li.exact && li.pure && nonempty_all(li.ex)) {
+      LSet run = li.ex;
+      for (size_t q = k + 1; q < n; ++q) {
+        LInfo l2 = analyze(r->sub[q].get());
+        LSet nr;
+        if (!l2.exact || !l2.pure || !cross(run, l2.ex, &nr)) break;
+        run = std::move(nr);
+      }
+      if (long_enough(run)) {
+        *out = std::move(run);
+        *dist = pre;
+        return true;
+      }
+    }
+    const int m = max_match_bytes(r->sub[k].get());
+    if (m < 0 || pre + m > 255) return false;
+    pre += m;
+  }
+  return false;
+}
+
 constexpr int kLeadScoreMargin = 32;  // window-score units (byte_weight) a leading set may trail the best by
 
 bool same_set(const LSet &a, const LSet &b) {
@@ -1918,8 +2023,9 @@ int compile_regex(const std::string &pattern, CompiledRegex *out, std::string *e
     // the strings every match begins with, when nearly as rare as the best
     // required set: a DFA job then starts at their first hit, not at rest[0]
     LSet lead;
-    if (leading_literals(root.get(), &lead) && set_score(lead) < 1000 &&
-        (!have || set_score(lead) <= set_score(best) + kLeadScoreMargin)) {
+    int lead_dist = 0;
+    const bool has_lead = leading_literals(root.get(), &lead) || bounded_leading_literals(root.get(), &lead, &lead_dist);
+    if (has_lead && set_score(lead) < 1000 && (!have || set_score(lead) <= set_score(best) + kLeadScoreMargin)) {
       best = lead;
       have = true;
     }
@@ -1935,8 +2041,12 @@ int compile_regex(const std::string &pattern, CompiledRegex *out, std::string *e
         out->pref.push_back(pl);
       }
       out->pref_equivalent = prefilter_equivalent(root.get(), best);
-      LSet lead;
-      out->pref_lead = leading_literals(root.get(), &lead) && same_set(lead, best);
+      LSet l0;
+      out->pref_lead = leading_literals(root.get(), &l0) && same_set(l0, best);
+      if (!out->pref_lead && bounded_leading_literals(root.get(), &l0, &lead_dist) && same_set(l0, best)) {
+        out->pref_lead = true;
+        out->lead_dist = (uint8_t)lead_dist;
+      }
       out->required_literal = best[0].s;
     } else {
       out->mode = kModeScan;

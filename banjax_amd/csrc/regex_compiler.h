@@ -143,6 +143,10 @@ struct CompiledRegex {
   // leading assertion-free exact strings = pref): a DFA job may start at the
   // first occurrence of a pref literal instead of rest[0]
   bool pref_lead = false;
+  // with pref_lead: every match starts at most lead_dist bytes before the
+  // literal it begins with (a pure, bounded piece first, e.g. (?i)s in
+  // (?i)scrapy): the job starts lead_dist bytes (and a rune) before the hit
+  uint8_t lead_dist = 0;
   // kModeAnchored: every match starts with one of these (exact, ASCII-ci as above)
   std::vector<PrefLit> anchor;
   bool anchor_equivalent = false;  // match <=> text starts with one of `anchor`

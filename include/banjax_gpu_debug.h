@@ -18,6 +18,10 @@ extern "C" {
 int bjx_debug_rule_match_host(const bjx_ruleset *rs, size_t rule_idx, const uint8_t *text, size_t n);
 /* required literal the prefilter uses for a rule (bytes written, full length returned) */
 size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t rule_idx, char *out, size_t cap);
+/* a prefilter rule whose every match begins within a bounded distance of its
+   literals (its DFA jobs start near the first hit): that distance in bytes;
+   -1 for every other rule */
+int bjx_debug_rule_lead(const bjx_ruleset *rs, size_t rule_idx);
 /* device ms of the last batch's phases: framing count, scan, per-line resolve,
    emit, capacity check, IP/state slot claim, sort + automaton, trips
    (returns the phase count) */

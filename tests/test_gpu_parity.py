@@ -561,3 +561,26 @@ def test_shared_patterns_across_rules(engine):
                 rnd.choice(uris) + rnd.choice(["", " ", "x"]), j % 7))
         pair.feed("".join(lines).encode(), (base + b * 3 + 3) * S)
     pair.compare_state(["10.0.%d.%d" % (a, c) for a in range(4) for c in range(8)])
+
+
+def test_bounded_lead_rules(engine):
+    """Rules whose matches begin a bounded distance before their literals
+    (tests/test_lead_cpu.py): their DFA jobs start near the first literal hit.
+    Lines with 0..12 hits (past 4 the hit slots overflow and the first hit of
+    any literal bounds the start), cut runes and non-ASCII bytes before hits."""
+    from tests.test_lead_cpu import CASES
+    rnd = random.Random(17)
+    pats = [p for p, _, _ in CASES]
+    yaml_rules = ["regexes_with_rates:"]
+    for i, p in enumerate(pats):
+        yaml_rules.append("  - rule: 'l%d'\n    regex: '%s'\n    interval: 1\n    hits_per_interval: 1000000\n"
+                          "    decision: challenge" % (i, p.replace("'", "''")))
+    pair = Pair("\n".join(yaml_rules) + "\n", engine)
+    frags = [b"a", b"b", b"x", b"12", b" ", b"=", b"\xc3\xa9", b"\xc5\xbf", b"\xe2\x84\xaa", b"\xff", b"S", b"s",
+             b"crapy", b"CRAPY", b"mechanize", b"abcd", b"=token", b"wxyz", b"abwxyz1", b"Macintosh", b"Firefox/9",
+             b"Firefox/", b"qqqqqqqqqqqqqqqqqqqqqqqqqqqqqq"]
+    lines = []
+    for j in range(4000):
+        body = b"".join(rnd.choice(frags) for _ in range(rnd.randrange(0, 40)))
+        lines.append(b"1700000000 9.9.9.%d GET h%d.com " % (j % 250, j % 7) + body)
+    pair.feed(b"\n".join(lines) + b"\n", 1700000000 * S)

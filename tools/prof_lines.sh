@@ -5,6 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 o=gpurun_out/lp; mkdir -p $o
 BJX_DEBUG_IMG=1 BJX_PROF_LINES=1 timeout -k 10 120 python -u tools/scan_stats.py cfg3 40000000 2 > $o/prof.log 2>&1 || exit $?
+[ "${PROF_ONLY:-0}" = 1 ] && exit 0
 repo=$PWD
 cd /tmp && export TMPDIR=/tmp
 for v in hm nohm; do
