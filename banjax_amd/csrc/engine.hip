@@ -1521,6 +1521,8 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
               }
               cc = atomicAdd(&L.cand_meta[gline].cnt, 1u);
             }
+            if (B.cfirst) atomicMin(reinterpret_cast<unsigned long long *>(&L.cand_first[gline * kCandFirstLits + lit]),
+                                    (unsigned long long)q0);
             if (cc < (uint32_t)kCandSlots) {
               L.cand[gline * kCandSlots + cc] = ((uint64_t)q0 << 24) | ver | lit;
             } else {  // past the slots: the line's summary only (CandMeta)
@@ -1921,6 +1923,17 @@ __device__ __forceinline__ uint32_t lead_start(const Bind &B, const Lines &L, ui
   // a bounded piece may precede the literal (lead_dist; + 3 so a rune cut by
   // the start decodes to errors that end before the match)
   const uint32_t back = B.rules[r].lead_dist ? B.rules[r].lead_dist + 3u : 0u;
+  if (B.cfirst) {  // the first candidate of each literal of the line: exact, overflow or not
+    uint64_t f = ~0ull;
+    for (uint32_t k = 0; k < ln; ++k) {
+      const uint64_t q = L.cand_first[j * kCandFirstLits + B.rule_lits[lo + k]];
+      f = q < f ? q : f;
+    }
+    if (f == ~0ull) return rl;  // none of its literals occurs: no match
+    // a first candidate in the header still bounds the first one in rest from below
+    const uint32_t o = f <= rs ? 0u : (uint32_t)min<uint64_t>(f - rs, rl);
+    return o > back ? o - back : 0u;
+  }
   const CandMeta cm = L.cand_meta[j];
   const bool ovf = cm.cnt > (uint32_t)kCandSlots;
   uint64_t f = ~0ull;
@@ -2038,21 +2051,48 @@ __device__ __forceinline__ bool eq_certain(const Bind &B, const Lines &L, uint64
 __device__ __forceinline__ uint32_t lead_start_seek(const Bind &B, const DevRule &R, const Lines &L, const uint8_t *buf,
                                                     uint64_t n_buf, uint64_t j, uint32_t pos, uint64_t rs, uint32_t rl) {
   const uint32_t st0 = lead_start(B, L, j, pos, rs, rl);
-  if ((R.lead & 3u) != 3u || st0 >= rl || L.cand_meta[j].cnt <= (uint32_t)kCandSlots) return st0;
+  if ((R.lead & 3u) != 3u || st0 >= rl || B.cfirst || L.cand_meta[j].cnt <= (uint32_t)kCandSlots) return st0;
   const uint32_t back = R.lead_dist ? R.lead_dist + 3u : 0u;
   const uint64_t q = lead_seek(B, R, buf, n_buf, rs + st0 + (st0 ? back : 0u), rs + rl);
   const uint32_t o = (uint32_t)(q - rs);
   return o >= rl ? rl : (o > back && o - back > st0 ? o - back : st0);
 }
 
-constexpr uint32_t kDfaLdsEntries = 8192;  // u16 transitions staged per block (16 KB)
+constexpr uint32_t kDfaLdsEntries = 8192;
+constexpr uint32_t kDfaAccelLds = 2048;  // accel words staged per block (8 KB)  // u16 transitions staged per block (16 KB)
 
 // STAGED: tr / ac point into LDS (a distinct instantiation keeps the call
 // sites apart, so each keeps its address space instead of generic loads)
+// escape mask of 16 text bytes for an accelerated state (Bind::accel word ac):
+// bit i set when byte i is one of its n escape bytes or non-ASCII
+__device__ __forceinline__ uint32_t accel_mask(const uint4 v, uint32_t ac) {
+  const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+  const uint32_t ne = (ac >> 24) & 3u;
+  uint32_t m = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t hb = wv[q] & 0x80808080u;
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) {
+      if (k >= ne) break;
+      const uint32_t y = wv[q] ^ (((ac >> (8 * k)) & 0xFFu) * 0x01010101u);
+      hb |= ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;
+    }
+    m |= (((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u)) << (4 * q);
+  }
+  return m;
+}
+
+// STAGED: tr / ac point into LDS (a distinct instantiation keeps the call
+// sites apart, so each keeps its address space instead of generic loads).
+// acc: the rule's Bind::accel words (nullptr: none): at each 16 B boundary in
+// a self-loop state the text up to the next escape byte is skipped, 16 B per
+// step, instead of being stepped byte by byte (every skipped byte maps the
+// state to itself, so the result is the same)
 template <bool STAGED>
 __device__ __forceinline__ bool dfa_text(const Bind &B, const DevRule &R, const uint16_t *tr, const uint8_t *ac,
-                                         const uint8_t *__restrict__ buf, uint64_t n_buf, uint64_t t0, uint32_t len,
-                                         uint32_t st0) {
+                                         const uint32_t *acc, const uint8_t *__restrict__ buf, uint64_t n_buf, uint64_t t0,
+                                         uint32_t len, uint32_t st0) {
   const uint32_t ncls = R.ncls;
   uint32_t st = st0;
   uint64_t a = t0 & ~15ull;
@@ -2072,6 +2112,18 @@ __device__ __forceinline__ bool dfa_text(const Bind &B, const DevRule &R, const 
   // the current ones (each step is a dependent LDS lookup)
   uint4 v = a < end ? load16(a) : make_uint4(0, 0, 0, 0);
   while (a < end) {
+    const uint32_t aw = acc ? acc[st] : 0u;
+    if (aw >> 31) {
+      for (;;) {
+        uint32_t m = accel_mask(v, aw) & ~((1u << skip) - 1u);
+        if (end - a < 16) m &= (1u << (uint32_t)(end - a)) - 1u;
+        if (m) { skip = (uint32_t)__ffs(m) - 1; break; }
+        a += 16;
+        skip = 0;
+        if (a >= end) return B.accept_end[R.ae_off + st] != 0;
+        v = load16(a);
+      }
+    }
     const uint4 vn = a + 16 < end ? load16(a + 16) : make_uint4(0, 0, 0, 0);
     const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
     const uint32_t lim = end - a < 16 ? (uint32_t)(end - a) : 16u;
@@ -2117,6 +2169,7 @@ __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restric
                                                 const uint64_t *__restrict__ nl, const uint32_t *__restrict__ jkey,
                                                 const uint32_t *__restrict__ jline, uint64_t n, Lines L) {
   __shared__ uint16_t s_tr[kDfaLdsEntries];
+  __shared__ uint32_t s_acc[kDfaAccelLds];
   __shared__ uint8_t s_ac[128];
   const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x;
   const uint64_t t = t0 + threadIdx.x;
@@ -2130,6 +2183,8 @@ __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restric
     const uint16_t *g = B.trans + R0.trans_off;
     for (uint32_t i = threadIdx.x; i < (uint32_t)R0.ncls * R0.n_states; i += blockDim.x) s_tr[i] = g[i];
     if (threadIdx.x < 128) s_ac[threadIdx.x] = B.ascii_cls[(size_t)r0 * 128 + threadIdx.x];
+    if (R0.n_states <= kDfaAccelLds)
+      for (uint32_t i = threadIdx.x; i < R0.n_states; i += blockDim.x) s_acc[i] = B.accel[R0.ae_off + i];
   }
   __syncthreads();
   if (t >= n) return;
@@ -2149,16 +2204,18 @@ __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restric
     // begins at one, regex_compiler.h pref_lead)
     const uint32_t sk = R0.skip_len && R0.skip_len <= rl ? R0.skip_len : 0u;
     const uint32_t st0 = (R0.lead & 1u) ? lead_start_seek(B, R0, L, buf, n_buf, j, pos, rs, rl) : 0u;
-    m = st0 ? dfa_text<true>(B, R0, s_tr, s_ac, buf, n_buf, rs + st0, rl - st0, R0.start)
-            : dfa_text<true>(B, R0, s_tr, s_ac, buf, n_buf, rs + sk, rl - sk, sk ? R0.skip_state : R0.start);
+    const uint32_t *acc = R0.n_states <= kDfaAccelLds ? s_acc : B.accel + R0.ae_off;
+    m = st0 ? dfa_text<true>(B, R0, s_tr, s_ac, acc, buf, n_buf, rs + st0, rl - st0, R0.start)
+            : dfa_text<true>(B, R0, s_tr, s_ac, acc, buf, n_buf, rs + sk, rl - sk, sk ? R0.skip_state : R0.start);
   } else {
     const DevRule R = B.rules[r];
     if (R.flags & kRuleNfa) return;  // k_nfa's
     const uint32_t sk = R.skip_len && R.skip_len <= rl ? R.skip_len : 0u;
     const uint32_t st0 = (R.lead & 1u) ? lead_start_seek(B, R, L, buf, n_buf, j, pos, rs, rl) : 0u;
-    if (st0) m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, buf, n_buf, rs + st0, rl - st0,
-                                 R.start);
-    else m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, buf, n_buf, rs + sk, rl - sk,
+    const uint32_t *acc = B.accel + R.ae_off;
+    if (st0) m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, acc, buf, n_buf, rs + st0,
+                                 rl - st0, R.start);
+    else m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, acc, buf, n_buf, rs + sk, rl - sk,
                              sk ? R.skip_state : R.start);
   }
   if (!m) return;
@@ -3809,6 +3866,7 @@ struct bjx_engine {
   uint32_t scan_lds[2] = {0, 0};
   bool lines_attr = false;
   DevBuf<CandMeta> l_ccnt;
+  DevBuf<uint64_t> l_cfirst;  // Lines::cand_first
   unsigned long long scan_stats[6] = {0, 0, 0, 0, 0, 0};
   uint64_t last_slow = 0;
   DevBuf<uint8_t> l_flags;
@@ -4140,6 +4198,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   std::vector<uint32_t> lit_off, lit_len, lit_gram, rule_lits;
   std::vector<uint8_t> lit_pref;
   std::vector<uint64_t> nfa_blob;
+  std::vector<uint32_t> accel;  // per DFA state (indexed like accept_end): self-loop acceleration
   std::vector<uint32_t> rule_full;  // per rule_lits entry: (full literal << 8 | piece offset) of a host-split literal
   std::vector<const std::string *> site_host(rs->rules.size(), nullptr);
   for (auto &st : rs->sites)
@@ -4153,6 +4212,22 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     trans.insert(trans.end(), r.rx.trans.begin(), r.rx.trans.end());
     d.ae_off = (uint32_t)ae.size();
     ae.insert(ae.end(), r.rx.accept_end.begin(), r.rx.accept_end.end());
+    // self-loop acceleration (dfa_text): a state that every ASCII byte but at
+    // most 3 maps to itself is left only by those bytes or a non-ASCII one
+    for (uint32_t st = 0; st < r.rx.accept_end.size(); ++st) {
+      uint32_t a = 0;
+      if (st > 1 && !(r.rx.flags & kRuleNfa) && !r.rx.trans.empty()) {
+        uint32_t esc[3] = {0, 0, 0}, ne = 0;
+        bool ok = true;
+        for (uint32_t b = 0; b < 128 && ok; ++b)
+          if (r.rx.trans[(size_t)st * r.rx.ncls + r.rx.ascii_cls[b]] != st) {
+            if (ne == 3) ok = false;
+            else esc[ne++] = b;
+          }
+        if (ok) a = 0x80000000u | (ne << 24) | (esc[2] << 16) | (esc[1] << 8) | esc[0];
+      }
+      accel.push_back(a);
+    }
     d.na_off = (uint32_t)(nonascii.size() / 2);
     for (auto &p : r.rx.nonascii) { nonascii.push_back(p.first); nonascii.push_back(p.second); }
     d.n_na = (uint16_t)r.rx.nonascii.size();
@@ -4733,7 +4808,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
             img.size() - il.lrec, il.lbytes - il.lrec, lb_al.size(), plan.size() / 2, lr_ent.size(), hd.size());
 
   BlobBuilder bb;
-  size_t o_rules = bb.add(drules), o_trans = bb.add(trans), o_ae = bb.add(ae), o_ascii = bb.add(ascii),
+  size_t o_rules = bb.add(drules), o_trans = bb.add(trans), o_ae = bb.add(ae), o_accel = bb.add(accel), o_ascii = bb.add(ascii),
          o_na = bb.add(nonascii), o_lits = bb.add(lits), o_glob = bb.add(global_rules), o_soff = bb.add(site_off),
          o_srules = bb.add(site_rules), o_hdh = bb.add(hd_hash), o_hdid = bb.add(hd_id), o_hdoff = bb.add(hd_off),
          o_hdlen = bb.add(hd_len), o_hdb = bb.add(hd_bytes), o_hsc = bb.add(host_scope), o_skip = bb.add(skip),
@@ -4754,6 +4829,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.rules = reinterpret_cast<const DevRule *>(base + o_rules);
   B.trans = reinterpret_cast<const uint16_t *>(base + o_trans);
   B.accept_end = base + o_ae;
+  B.accel = reinterpret_cast<const uint32_t *>(base + o_accel);
   B.ascii_cls = base + o_ascii;
   B.nonascii = reinterpret_cast<const uint32_t *>(base + o_na);
   B.lits = base + o_lits;
@@ -4792,6 +4868,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.any_prefilter = use_pref ? 1 : 0;
   B.lit_nl = std::find(lit_bytes.begin(), lit_bytes.end(), (uint8_t)'\n') != lit_bytes.end() ? 1u : 0u;
   B.lits_small = lit_off.size() <= 32 ? 1u : 0u;
+  B.cfirst = lit_off.size() <= kCandFirstLits && use_pref ? 1u : 0u;
   B.img = base + o_img;
   B.img_bytes = (uint32_t)img.size();
   B.il = il;
@@ -5053,7 +5130,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   e->d_results.release(); e->q_out.release();
   e->ban_ips.release(); e->ban_log.release(); e->ban_off.release(); e->ban_kind.release(); e->ban_ipb.release();
   e->ban_ipo.release();
-  e->long_list.release(); e->l_ip16.release(); e->jline.release(); e->jkey.release(); e->jline2.release(); e->jkey2.release(); e->l_cand.release(); e->l_ccnt.release();
+  e->long_list.release(); e->l_ip16.release(); e->jline.release(); e->jkey.release(); e->jline2.release(); e->jkey2.release(); e->l_cand.release(); e->l_ccnt.release(); e->l_cfirst.release();
   (void)hipEventDestroy(e->ev0); (void)hipEventDestroy(e->ev1); (void)hipEventDestroy(e->evm0); (void)hipEventDestroy(e->evm1);
   for (auto &x : e->evk) (void)hipEventDestroy(x);
   for (auto &x : e->ph) (void)hipEventDestroy(x);
@@ -5390,6 +5467,12 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   L.host_len = e->l_hlen.p; L.rest_off = e->l_roff.p; L.host_id = e->l_hid.p; L.flags = e->l_flags.p;
   L.counts = e->l_counts.p; L.masks = e->l_masks.p;
   L.cand_meta = e->l_ccnt.p; L.cand = e->l_cand.p; L.ip16 = e->l_ip16.p;
+  L.cand_first = nullptr;
+  if (B.cfirst) {
+    e->l_cfirst.ensure(n_lines * kCandFirstLits);
+    L.cand_first = e->l_cfirst.p;
+    HIP_OK(hipMemsetAsync(e->l_cfirst.p, 0xFF, n_lines * kCandFirstLits * 8, st));
+  }
   e->jline.ensure(std::max<uint64_t>(e->jline.n, n_lines + (1u << 20)));
   e->jkey.ensure(e->jline.n);
   HIP_OK(hipMemsetAsync(e->scalars.p, 0, 16 * sizeof(unsigned long long), st));

@@ -90,6 +90,10 @@ struct Bind {
   const DevRule *rules;
   const uint16_t *trans;
   const uint8_t *accept_end;
+  // per DFA state (ae_off + state): 0, or 1 << 31 | n << 24 | e2 << 16 | e1 << 8 | e0
+  // when every ASCII byte but the n <= 3 escape bytes e0..e2 maps the state to
+  // itself (a `.*` loop waiting for a literal): dfa_text skips 16 B at a time
+  const uint32_t *accel;
   const uint8_t *ascii_cls;    // 128 per rule
   const uint32_t *nonascii;    // (lo, class) pairs
   const uint8_t *lits;
@@ -129,6 +133,7 @@ struct Bind {
   uint32_t any_prefilter;
   uint32_t lits_small;  // at most 32 interned literals: CandMeta bit id & 31 names one literal
   uint32_t lit_nl;  // some literal holds '\n' (k_scan then verifies only lines inside its window)
+  uint32_t cfirst;  // ruleset of <= kCandFirstLits literals: Lines::cand_first is kept (stride kCandFirstLits)
   ImgLayout il;
   // Lookup image for the scan pass (one blob, copied whole to LDS when it
   // fits; ImgLayout gives the offsets):
@@ -220,7 +225,11 @@ struct Lines {
   uint4 *ip16;         // key16 of the line's IP (see IpSlot)
   CandMeta *cand_meta;  // literal hits recorded by the scan pass (zeroed before it)
   uint64_t *cand;       // kCandSlots per line: (literal start << 24) | verified | literal id
+  // rulesets of at most kCandFirstLits literals (Bind::cfirst): per line and
+  // literal id, the lowest candidate position (~0: none), every hit counted
+  uint64_t *cand_first;
 };
+constexpr uint32_t kCandFirstLits = 8;
 
 // Persistent rate-limit state (RegexRateLimitStates, rate_limit.go:17-21),
 // keyed by IP string and rule name, never evicted (as in the reference).

@@ -584,3 +584,29 @@ def test_bounded_lead_rules(engine):
         body = b"".join(rnd.choice(frags) for _ in range(rnd.randrange(0, 40)))
         lines.append(b"1700000000 9.9.9.%d GET h%d.com " % (j % 250, j % 7) + body)
     pair.feed(b"\n".join(lines) + b"\n", 1700000000 * S)
+
+
+def test_dfa_self_loop_acceleration(engine):
+    """States left by at most 3 ASCII bytes (a `.*` waiting for a literal) are
+    skipped 16 B at a time (engine.hip dfa_text / Bind::accel): long texts with
+    sparse escape bytes at every offset of a 16 B chunk, non-ASCII bytes, cut
+    runes and matches ending at the last byte."""
+    rnd = random.Random(23)
+    pats = [r"Macintosh.*Firefox/\d+", r"ab.*cde.*f", r"[^z]*z.{3}", r"q.*[xy]\d", r"(?i)start.*stop$", r"wq.*é",
+            r"k.*\bend\b", r"zz[^\n]*zz"]
+    yaml_rules = ["regexes_with_rates:"]
+    for i, p in enumerate(pats):
+        yaml_rules.append("  - rule: 'a%d'\n    regex: '%s'\n    interval: 1\n    hits_per_interval: 1000000\n"
+                          "    decision: challenge" % (i, p.replace("'", "''")))
+    pair = Pair("\n".join(yaml_rules) + "\n", engine)
+    fill = [b"m", b"n", b"o", b"p", b" ", b"-", b"/", b"1"]
+    rare = [b"Macintosh", b"Firefox/7", b"Firefox/", b"ab", b"cde", b"f", b"z", b"zz", b"q", b"x", b"y9", b"START",
+            b"stop", b"wq", b"\xc3\xa9", b"\xc3", b"\xff", b"k", b"end", b" end "]
+    lines = []
+    for j in range(3000):
+        parts = []
+        for _ in range(rnd.randrange(0, 12)):
+            parts.append(b"".join(rnd.choice(fill) for _ in range(rnd.randrange(0, 300))))
+            parts.append(rnd.choice(rare))
+        lines.append(b"1700000000 9.9.9.%d GET h%d.com " % (j % 250, j % 7) + b"".join(parts))
+    pair.feed(b"\n".join(lines) + b"\n", 1700000000 * S)
