@@ -552,13 +552,75 @@ constexpr uint32_t kLinesBlocksPerCu = 3;       // k_lines' LDS budget: 3 blocks
 constexpr uint32_t kRulesImgMax = 48 * 1024;  // k_rules likewise (no line staging: 3+ blocks per CU)
 constexpr uint32_t kSpanBytes = 12 * 1024;    // k_lines: bytes of 64 lines staged per wave
 
-// first four spaces of the line [p, p + n): 16 B aligned loads, SWAR compare
+// 16-bit mask of the spaces among 16 bytes
+__device__ __forceinline__ uint32_t space_mask16(const uint4 v) {
+  const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+  uint32_t m16 = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t x = wv[k] ^ 0x20202020u;
+    const uint32_t hb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+    m16 |= (((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u)) << (4 * k);
+  }
+  return m16;
+}
+
+// 4 ASCII digits (first char lowest byte): exact test, and their value
+__device__ __forceinline__ bool digits4(uint32_t x) {
+  return (x & 0xF0F0F0F0u) == 0x30303030u && (((x & 0x0F0F0F0Fu) + 0x06060606u) & 0xF0F0F0F0u) == 0u;
+}
+__device__ __forceinline__ uint32_t value4(uint32_t x) {
+  x -= 0x30303030u;
+  x = x * 10u + (x >> 8);  // byte 0: d0 * 10 + d1, byte 2: d2 * 10 + d3
+  return (x & 0xFFu) * 100u + ((x >> 16) & 0xFFu);
+}
+// parseTimestamp's ParseFloat for the nginx $msec shape "dddddddddd.ddd"
+// (14 bytes: 10 integer digits, 3 fraction digits), loop-free from 4 words:
+// the same value parse_float_fast computes (the 13-digit mantissa is exact,
+// then one correctly rounded division by 1e3).  1: another shape (the caller
+// runs parse_float_fast).  Needs 2 readable bytes past the token (a header
+// token is followed by the rest of the line).
+__device__ __forceinline__ int parse_ts_msec(const uint8_t *p, uint32_t n, double *out) {
+  if (n != 14) return 1;
+  const uint32_t w0 = ld4(p), w1 = ld4(p + 4), w2 = ld4(p + 8), w3 = ld4(p + 12);
+  if (!digits4(w0) || !digits4(w1) || (w2 & 0x00FF0000u) != 0x002E0000u || !digits4((w2 & 0xFF00FFFFu) | 0x00300000u) ||
+      !digits4((w3 & 0xFFFFu) | 0x30300000u))
+    return 1;
+  const uint32_t d8 = w2 & 0xFFu, d9 = (w2 >> 8) & 0xFFu, d11 = w2 >> 24, d12 = w3 & 0xFFu, d13 = (w3 >> 8) & 0xFFu;
+  const uint64_t ip = (uint64_t)value4(w0) * 1000000ull + value4(w1) * 100u + (d8 - 48u) * 10u + (d9 - 48u);
+  const uint64_t m = ip * 1000ull + (d11 - 48u) * 100u + (d12 - 48u) * 10u + (d13 - 48u);
+  *out = (double)m / 1000.0;
+  return 0;
+}
+
+// first four spaces of the line [p, p + n): 16 B aligned loads, SWAR compare.
+// A line of 64 bytes or more (past the alignment skip) has its first 64 loaded
+// at once (four independent loads, one wait) and its spaces taken from one
+// 64-bit mask; the chunk loop covers the rest.
 __device__ __forceinline__ uint32_t find_spaces(const uint8_t *p, uint32_t n, uint32_t &sp0, uint32_t &sp1,
                                                 uint32_t &sp2, uint32_t &sp3) {
   const uint32_t skip = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15);
   const uint4 *base = reinterpret_cast<const uint4 *>(p - skip);  // keeps p's address space
-  uint32_t ns = 0;
-  for (uint32_t c = 0; c * 16 < n + skip && ns < 4; ++c) {
+  uint32_t ns = 0, c0 = 0;
+  if (n + skip >= 64) {
+    const uint4 v0 = base[0], v1 = base[1], v2 = base[2], v3 = base[3];
+    uint64_t m = (uint64_t)space_mask16(v0) | ((uint64_t)space_mask16(v1) << 16) | ((uint64_t)space_mask16(v2) << 32) |
+                 ((uint64_t)space_mask16(v3) << 48);
+    m &= ~((1ull << skip) - 1ull);  // all 64 bytes lie before p + n
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t pos = (uint32_t)__ffsll((unsigned long long)m) - 1 - skip;
+      const bool has = m != 0;
+      m &= m - 1;
+      if (k == 0) sp0 = has ? pos : sp0;
+      if (k == 1) sp1 = has ? pos : sp1;
+      if (k == 2) sp2 = has ? pos : sp2;
+      if (k == 3) sp3 = has ? pos : sp3;
+      ns += has ? 1u : 0u;
+    }
+    c0 = 4;
+  }
+  for (uint32_t c = c0; c * 16 < n + skip && ns < 4; ++c) {
     const uint4 v = base[c];
     // 16-bit mask of the spaces of this chunk inside [p, p + n)
     uint32_t m16 = 0;
@@ -1598,7 +1660,7 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
   HostRules H;
   bool slow = false;
   if (ns >= 4) {
-    slow = parse_float_fast(p, sp0, &f) != 0;
+    slow = parse_ts_msec(p, sp0, &f) != 0 && parse_float_fast(p, sp0, &f) != 0;
     if (PROF) P.mark(1);
     if (!slow) {
       hid = (A.dbg & 8) ? -1
@@ -2609,16 +2671,27 @@ __device__ __forceinline__ bool ip_claim_line(const EvSrc &E, const State &S, ui
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_ip_claim(EvSrc E, State S, uint32_t epoch, uint32_t *__restrict__ el_slot,
-                                                     uint32_t *__restrict__ el_id, uint64_t shard_budget) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool claimed = false;
-  if (i < E.n && ev_has(E, i) && !flag_set(S, 5)) claimed = ip_claim_line(E, S, epoch, i, el_slot, el_id, shard_budget);
-  count_claims(S, 0, 5, claimed, shard_budget);
-}
-
 // exclusive prefix of v over the wave and one atomicAdd of the wave's total
 // on ctr; returns ctr's old value + the prefix (every lane of the wave calls it)
+__device__ __forceinline__ uint64_t wave_alloc(unsigned long long *ctr, uint32_t v);
+
+// el_new / counters[4]: the event lines whose IP is new to the table (created
+// in this batch), listed for k_ip_commit
+__global__ __launch_bounds__(kBlock) void k_ip_claim(EvSrc E, State S, uint32_t epoch, uint32_t *__restrict__ el_slot,
+                                                     uint32_t *__restrict__ el_id, uint32_t *__restrict__ el_new,
+                                                     uint64_t shard_budget) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool claimed = false, isnew = false;
+  if (i < E.n && ev_has(E, i) && !flag_set(S, 5)) {
+    el_id[i] = 0;
+    claimed = ip_claim_line(E, S, epoch, i, el_slot, el_id, shard_budget);
+    isnew = el_id[i] == kNewIp;
+  }
+  count_claims(S, 0, 5, claimed, shard_budget);
+  const uint64_t at = wave_alloc((unsigned long long *)&S.counters[4], isnew ? 1u : 0u);
+  if (isnew) el_new[at] = (uint32_t)i;
+}
+
 __device__ __forceinline__ uint64_t wave_alloc(unsigned long long *ctr, uint32_t v) {
   const uint32_t lane = threadIdx.x & 63;
   uint32_t x = v;
@@ -2633,11 +2706,14 @@ __device__ __forceinline__ uint64_t wave_alloc(unsigned long long *ctr, uint32_t
   return base + (x - v);
 }
 
+// over the event lines k_ip_claim listed (el_new, n_new of them): IPs of
+// earlier batches were settled there
 __global__ __launch_bounds__(kBlock) void k_ip_commit(EvSrc E, State S, uint32_t epoch, const uint32_t *__restrict__ el_slot,
-                                                      uint32_t *__restrict__ el_id, uint32_t *__restrict__ coll) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  // IPs of earlier batches were settled by k_ip_claim
-  const bool act = i < E.n && ev_has(E, i) && el_id[i] == kNewIp;
+                                                      uint32_t *__restrict__ el_id, const uint32_t *__restrict__ el_new,
+                                                      uint64_t n_new, uint32_t *__restrict__ coll) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = t < n_new;
+  const uint64_t i = act ? el_new[t] : 0;
   uint32_t s = 0, f = 0, len = 0;
   const uint8_t *ip = nullptr;
   if (act) {
@@ -3876,6 +3952,7 @@ struct bjx_engine {
   DevBuf<uint32_t> res_rule, ev_el, ev_rule, ev_res, ev_st, ev_st2, ev_idx, ev_idx2, el_slot, coll, trip_idx;
   DevBuf<EvRec> ev_rec, ev_rec2;
   DevBuf<uint32_t> el_id;
+  DevBuf<uint32_t> el_new;  // event lines with a new IP (k_ip_claim -> k_ip_commit)
   DevBuf<uint8_t> rl_out, ev_out, ev_out_s, trip_flag;
   DevBuf<uint32_t> trip_ev, trip_ev2;
   DevBuf<bjx_trip> d_trips;
@@ -5111,7 +5188,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   e->l_hoff.release(); e->l_hlen.release(); e->l_roff.release(); e->slow_list.release(); e->l_hid.release();
   e->scalars.release(); e->res_seq.release(); e->res_rule.release(); e->ev_el.release(); e->ev_rule.release();
   e->ev_res.release(); e->ev_st.release(); e->ev_st2.release(); e->ev_idx.release(); e->ev_idx2.release();
-  e->el_slot.release(); e->coll.release(); e->ev_rec.release(); e->ev_rec2.release(); e->el_id.release();
+  e->el_slot.release(); e->coll.release(); e->el_new.release(); e->ev_rec.release(); e->ev_rec2.release(); e->el_id.release();
 
   for (auto *b : {&e->pk_key, &e->pk_key2, &e->pk_line, &e->pk_line2, &e->pack_src, &e->rx_len, &e->rx_ev_el}) b->release();
   for (auto *b : {&e->pk_nev, &e->pk_ipl, &e->pk_evoff, &e->pk_byoff, &e->pk_start, &e->pk_counts, &e->pk_bbase,
@@ -5187,7 +5264,8 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
   if (e->host_counters[0] + n_el >= 0x7FFFFFFFull) throw BjxError(BJX_ERR_CAPACITY, "more than 2^31 distinct IPs");
   if (++e->epoch == 0) ++e->epoch;  // 0 marks a slot being claimed
   const uint32_t epoch = e->epoch;
-  e->el_slot.ensure(E.n); e->el_id.ensure(E.n); e->coll.ensure(E.n);
+  e->el_slot.ensure(E.n); e->el_id.ensure(E.n); e->coll.ensure(E.n); e->el_new.ensure(E.n);
+  uint64_t nw_ovf[2] = {0, 0};  // new-IP event lines (k_ip_claim's list), IP table overflow flag
   e->ev_st.ensure(n_ev); e->ev_st2.ensure(n_ev); e->ev_rec.ensure(n_ev); e->ev_rec2.ensure(n_ev);
   e->ev_out.ensure(n_ev); e->ev_out_s.ensure(n_ev);
   mark(e, 5);
@@ -5199,20 +5277,21 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
     const bool forced = e->dbg_budget && attempt == 0 && e->dbg_budget < budget;  // test hook
     if (forced) budget = e->dbg_budget;
     hipLaunchKernelGGL(k_ip_claim, dim3(grid_for(E.n)), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p,
-                       budget / kClaimShards);
+                       e->el_new.p, budget / kClaimShards);
     HIP_OK(hipGetLastError());
-    uint64_t ovf = 0;
-    HIP_OK(hipMemcpyAsync(&ovf, e->S.counters + 5, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(nw_ovf, e->S.counters + 4, 16, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    if (!ovf) break;
+    if (!nw_ovf[1]) break;
     // more new IPs than the table had room for: undo, grow, claim again
     hipLaunchKernelGGL(k_ip_rollback, dim3(grid_for(e->ip_cap)), dim3(kBlock), 0, st, e->ip_cap, e->S, epoch);
     HIP_OK(hipGetLastError());
     if (!forced) grow_ip(e, attempt >= 2 ? n_ips + n_el : std::min<uint64_t>(n_ips + n_el, 4 * (e->ip_cap * 3 / 4)));
   }
-  hipLaunchKernelGGL(k_ip_commit, dim3(grid_for(E.n)), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p,
-                     e->coll.p);
-  HIP_OK(hipGetLastError());
+  if (nw_ovf[0]) {
+    hipLaunchKernelGGL(k_ip_commit, dim3(grid_for(nw_ovf[0])), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p,
+                       e->el_new.p, nw_ovf[0], e->coll.p);
+    HIP_OK(hipGetLastError());
+  }
   uint64_t n_coll = 0;
   HIP_OK(hipMemcpyAsync(&n_coll, e->S.counters + 3, 8, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
