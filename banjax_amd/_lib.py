@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libbanjax_gpu.so")
+# BJX_LIB_PATH: another build of the library (timing experiments only)
+LIB_PATH = os.environ.get("BJX_LIB_PATH") or os.path.join(HERE, "lib", "libbanjax_gpu.so")
 
 OK = 0
 ERR_REGEX, ERR_ARG, ERR_DEVICE, ERR_NOMEM, ERR_TOO_COMPLEX, ERR_CAPACITY, ERR_DECISION = -1, -2, -3, -4, -5, -6, -7

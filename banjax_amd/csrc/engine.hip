@@ -1244,10 +1244,28 @@ __device__ __forceinline__ void decide_plan_lds(const Bind &B, const Tabs &T, co
   if (P) { __builtin_amdgcn_s_waitcnt(0); P->mark(7); }
   if (hid >= 0) {
     const uint2 hi = LT.hinfo[hid];
-    const uint32_t cb = hi.x & 0xFFFFu, ce = cb + (hi.x >> 16);
-    for (uint32_t i = cb; i < ce; ++i)
-      plan_rule_lds<EMIT>(B, T, LT, LT.cls[2 * i], LT.cls[2 * i + 1], hi.y, rest, rest_len, host_rel, host_len, lits, lpos,
-                          nlit, ovf, ov, m0, m1, j, S);
+    // The wave's lines with a host nearly always share one plan class (hosts
+    // whose site rules differ only in their host name share it): its entries
+    // are then read with scalar loads from the blob in HBM and each entry's
+    // kind is dispatched once for the wave on the scalar unit; otherwise each
+    // lane walks its own class from LDS.
+    const uint32_t f = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1;
+    const uint32_t c0 = __builtin_amdgcn_readlane(hi.x, f);
+    if (__ballot(hi.x != c0) == 0) {
+      typedef const __attribute__((address_space(4))) uint32_t ConstU32;
+      ConstU32 *cg = (ConstU32 *)(uintptr_t)(B.hl + B.lt_cls);
+      const uint32_t cb = c0 & 0xFFFFu, ce = cb + (c0 >> 16);
+      for (uint32_t i = cb; i < ce; ++i) {
+        ConstU32 *q = cg + 8 * i;
+        plan_rule_lds<EMIT>(B, T, LT, make_uint4(q[0], q[1], q[2], q[3]), make_uint4(q[4], q[5], q[6], q[7]), hi.y, rest, rest_len,
+                            host_rel, host_len, lits, lpos, nlit, ovf, ov, m0, m1, j, S);
+      }
+    } else {
+      const uint32_t cb = hi.x & 0xFFFFu, ce = cb + (hi.x >> 16);
+      for (uint32_t i = cb; i < ce; ++i)
+        plan_rule_lds<EMIT>(B, T, LT, LT.cls[2 * i], LT.cls[2 * i + 1], hi.y, rest, rest_len, host_rel, host_len, lits, lpos,
+                            nlit, ovf, ov, m0, m1, j, S);
+    }
   }
   if (P) { __builtin_amdgcn_s_waitcnt(0); P->mark(8); }
   for (uint32_t i = 0; i < B.n_plan_glob; ++i)
@@ -4684,6 +4702,9 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   if (plan.empty()) plan.push_back(make_uint4(0, 0, 0, 0));
   if (plan_glob.empty()) plan_glob.push_back(make_uint4(0, 0, 0, 0));
 
+  std::vector<uint8_t> shared_pat(rs->rules.size(), 0);  // some other rule has this rule's pattern
+  for (uint32_t r = 0; r < (uint32_t)rs->rules.size(); ++r)
+    if (canon[r] != r) shared_pat[canon[r]] = 1;
   // plan classes for k_lines' LDS (decide_plan_lds), appended to the host
   // dictionary blob when both fit kLinesTabLdsMax
   uint32_t lt_hinfo = 0, lt_cls = 0, lt_trec = 0, lt_pool = 0;
@@ -4763,7 +4784,10 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
             b = make_uint4(0, 0, 0, 0);
           }
         }
-        if (canon[r] == r && r == per_host[h][0] + k) a.x = (a.x & ~0xFFFFFu) | kPlanOwn;
+        // "own" only for a pattern no other rule shares (a shared pattern is
+        // named by its first rule on every host alike, so hosts whose rules
+        // differ only in their host name keep one class)
+        if (canon[r] == r && !shared_pat[r] && r == per_host[h][0] + k) a.x = (a.x & ~0xFFFFFu) | kPlanOwn;
       }
       std::vector<uint32_t> key;
       for (auto &v : ents) { key.push_back(v.x); key.push_back(v.y); key.push_back(v.z); key.push_back(v.w); }
