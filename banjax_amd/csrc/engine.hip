@@ -3598,15 +3598,26 @@ __global__ void k_pack(uint64_t n_el, const uint32_t *__restrict__ key, const ui
     d_events[pe + t] = ev_rule[eo + t];
     pack_src[pe + t] = (uint32_t)(eo + t);
   }
+  // the IP bytes: word loads from the line (a log line continues past its
+  // IP), byte stores into the packed pool
   const uint8_t *ip = buf + line_start(nl, j) + L.ip_off[j];
   uint8_t *dst = d_bytes + by_off[p];
-  for (uint32_t k = 0; k < len; ++k) dst[k] = ip[k];
+  for (uint32_t k = 0; k < len; k += 4) {
+    const uint32_t w = ld4(ip + k);
+#pragma unroll
+    for (uint32_t b = 0; b < 4; ++b)
+      if (k + b < len) dst[k + b] = (uint8_t)(w >> (8 * b));
+  }
 }
 
 // received records of one source -> SoA rate-limit input (absolute IP offsets)
+// received event lines -> the rate-limit input arrays, with each IP's inline
+// key (IpSlot.key16) built once here from the byte pool (neighbouring lanes
+// read neighbouring bytes) instead of in every claim kernel
 __global__ void k_unpack_lines(uint64_t n, uint64_t first, uint64_t byte_base, const bjx_event_line *__restrict__ rec,
-                               int64_t *__restrict__ ts, uint64_t *__restrict__ hash, uint64_t *__restrict__ pos,
-                               uint32_t *__restrict__ len, uint64_t *__restrict__ nev) {
+                               const uint8_t *__restrict__ bytes, int64_t *__restrict__ ts, uint64_t *__restrict__ hash,
+                               uint64_t *__restrict__ pos, uint32_t *__restrict__ len, uint64_t *__restrict__ nev,
+                               uint4 *__restrict__ ip16) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const bjx_event_line r = rec[first + i];
@@ -3615,6 +3626,7 @@ __global__ void k_unpack_lines(uint64_t n, uint64_t first, uint64_t byte_base, c
   pos[first + i] = byte_base + r.ip_off;
   len[first + i] = r.ip_len;
   nev[first + i] = r.n_events;
+  ip16[first + i] = ip_key16_bytes(bytes + byte_base + r.ip_off, r.ip_len);
 }
 
 // event -> its line (events of line i are [off[i], off[i] + nev[i])); flags bad rule ids
@@ -3985,6 +3997,7 @@ struct bjx_engine {
   DevBuf<uint32_t> pk_key, pk_key2, pk_line, pk_line2, pack_src, rx_len, rx_ev_el;
   DevBuf<uint64_t> pk_nev, pk_ipl, pk_evoff, pk_byoff, pk_start, pk_counts, pk_bbase, rx_hash, rx_pos, rx_nev, rx_evoff;
   DevBuf<int64_t> rx_ts;
+  DevBuf<uint4> rx_ip16;  // received event lines: IpSlot.key16 of each IP (k_unpack_lines)
   uint32_t pk_parts = 0;
   uint64_t pk_n_ev = 0;
   bool partitioned = false;
@@ -5218,7 +5231,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   for (auto *b : {&e->pk_nev, &e->pk_ipl, &e->pk_evoff, &e->pk_byoff, &e->pk_start, &e->pk_counts, &e->pk_bbase,
                   &e->rx_hash, &e->rx_pos, &e->rx_nev, &e->rx_evoff})
     b->release();
-  e->rx_ts.release(); e->trip_idx.release(); e->d_trips.release();
+  e->rx_ts.release(); e->rx_ip16.release(); e->trip_idx.release(); e->d_trips.release();
   for (auto *b : {&e->bn_key, &e->bn_key2, &e->bn_len, &e->bn_off, &e->dl_hash}) b->release();
   for (auto *b : {&e->bn_val, &e->bn_val2, &e->bn_head, &e->bn_seg, &e->bn_first, &e->bn_cnt, &e->bn_ipt, &e->bn_coll,
                   &e->dl_off, &e->dl_len, &e->nm_off})
@@ -6249,13 +6262,13 @@ extern "C" int bjx_apply_events(bjx_engine *e, const bjx_ruleset *rs, const bjx_
     const Bind &B = e->bind;
     hipStream_t st = e->stream;
     e->rx_ts.ensure(n_lines); e->rx_hash.ensure(n_lines); e->rx_pos.ensure(n_lines); e->rx_len.ensure(n_lines);
-    e->rx_nev.ensure(n_lines + 1); e->rx_evoff.ensure(n_lines + 1); e->rx_ev_el.ensure(n_ev);
+    e->rx_nev.ensure(n_lines + 1); e->rx_evoff.ensure(n_lines + 1); e->rx_ev_el.ensure(n_ev); e->rx_ip16.ensure(n_lines);
     uint64_t first = 0, bbase = 0;
     for (uint32_t k = 0; k < n_src; ++k) {
       const uint64_t nk = src_counts[3 * k];
       if (nk)
-        hipLaunchKernelGGL(k_unpack_lines, dim3(grid_for(nk)), dim3(kBlock), 0, st, nk, first, bbase, d_lines, e->rx_ts.p,
-                           e->rx_hash.p, e->rx_pos.p, e->rx_len.p, e->rx_nev.p);
+        hipLaunchKernelGGL(k_unpack_lines, dim3(grid_for(nk)), dim3(kBlock), 0, st, nk, first, bbase, d_lines, d_bytes,
+                           e->rx_ts.p, e->rx_hash.p, e->rx_pos.p, e->rx_len.p, e->rx_nev.p, e->rx_ip16.p);
       first += nk;
       bbase += src_counts[3 * k + 2];
     }
@@ -6278,7 +6291,7 @@ extern "C" int bjx_apply_events(bjx_engine *e, const bjx_ruleset *rs, const bjx_
     if (chk[0] != n_ev || chk[1]) throw BjxError(BJX_ERR_ARG, "received event records are inconsistent");
     EvSrc E;
     E.bytes = d_bytes; E.nl = nullptr; E.ip_off = nullptr; E.ip_pos = e->rx_pos.p; E.ip_len = e->rx_len.p;
-    E.ip_hash = e->rx_hash.p; E.ts = e->rx_ts.p; E.counts = nullptr; E.ip16 = nullptr; E.n = n_lines;
+    E.ip_hash = e->rx_hash.p; E.ts = e->rx_ts.p; E.counts = nullptr; E.ip16 = e->rx_ip16.p; E.n = n_lines;
     rate_limit_stage(e, B, E, n_lines, n_bytes, n_ev, e->rx_ev_el.p, d_events);
     hipLaunchKernelGGL(k_unsort, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_rec2.p, e->ev_out_s.p, d_out);
     HIP_OK(hipGetLastError());
