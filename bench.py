@@ -350,8 +350,9 @@ def main():
                 "scan_stats_last_step_rank0": stats,
                 "state_tables": state_stats,
                 "parallelism": ("dp%d: chunk-sharded match, IP-hash-sharded rate-limit state, %s" % (
-                    n_parts, "one bjx_node (rank 0) of %d engines moving the event records between GPUs with "
-                    "hipMemcpyPeerAsync" % n_parts if node_mode else "RCCL all-to-all of the event records"))
+                    n_parts, "one bjx_node (rank 0) of %d engines moving the event records between them with %s" % (
+                        n_parts, "one RCCL group of ncclSend/ncclRecv over xGMI" if node is not None and node.exchange == "rccl"
+                        else "device copies (engines sharing a GPU)") if node_mode else "RCCL all-to-all of the event records"))
                 if n_parts > 1 else "dp1",
             },
             "roofline": roofline(kms, nbytes, args),
