@@ -1493,18 +1493,22 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
     // ---- 4-gram prefilter: positions [64 lane, 64 lane + 64) and the last line's halo part
     {
       const uint32_t nxt = *reinterpret_cast<const uint32_t *>(T + lane * 64u + 64u);
-      // per position: alignbyte, fold (shift, xor), mul24, word address, LDS
-      // read, bfe (its offset operand uses bits 0-4 only), shift-or
+      // positions in pairs (k, k + 1), k even: one LDS word keyed by the 3
+      // bytes the two grams share (gram_pair_word), bit (first byte & 15) for
+      // the gram at k and 16 + (last byte & 15) for the gram at k + 1
+      // (engine_types.h gram_pair_*): per pair two alignbytes, a mul24, the
+      // word address, one LDS read, two bfe (offset operand bits 0-4), shift-ors
       const uint8_t *sb = reinterpret_cast<const uint8_t *>(s_bits);
       uint32_t hlo = 0, hhi = 0;
 #pragma unroll
-      for (int k = 0; k < 64; ++k) {
+      for (int k = 0; k < 64; k += 2) {
         const uint32_t lo = w[k >> 2], hi = (k >> 2) < 15 ? w[(k >> 2) + 1] : nxt;
-        const uint32_t g = (k & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3)) : lo;
-        const uint32_t x = gram_fold(g);
-        const uint32_t word = *reinterpret_cast<const uint32_t *>(sb + ((gram_mix(x) >> 11) & ((kGramWords - 1) << 2)));
-        const uint32_t bit = __builtin_amdgcn_ubfe(word, x, 1);  // = gram_hash(g)'s bit
-        if (k < 32) hlo |= bit << k; else hhi |= bit << (k - 32);
+        const uint32_t g0 = (k & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3)) : lo;  // bytes k .. k + 3
+        const uint32_t g1 = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3) + 1u);           // bytes k + 1 .. k + 4
+        const uint32_t word = *reinterpret_cast<const uint32_t *>(sb + gram_pair_byte_off(g1 & 0xFFFFFFu));
+        const uint32_t b0 = __builtin_amdgcn_ubfe(word, g0 & 15u, 1), b1 = __builtin_amdgcn_ubfe(word, (g1 >> 24) | 16u, 1);
+        const uint32_t two = b0 | (b1 << 1);
+        if (k < 32) hlo |= two << k; else hhi |= two << (k - 32);
       }
       uint64_t hits = ((uint64_t)hhi << 32) | hlo;
       if (ts0 + lane * 64u + 64u > A.n) hits &= (ts0 + lane * 64u >= A.n) ? 0ull : ((1ull << (A.n - ts0 - lane * 64u)) - 1ull);
@@ -1512,8 +1516,8 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
       const uint32_t hend = last_in_halo ? hfirst : kWT;
       if (lane * 8u + kWT < hend) {
         for (uint32_t k = 0; k < 8 && kWT + lane * 8u + k < hend; ++k) {
-          const uint32_t h = gram_hash(ld4(T + kWT + lane * 8u + k));
-          hh |= ((s_bits[h >> 5] >> (h & 31)) & 1u) << k;
+          const uint32_t g = ld4(T + kWT + lane * 8u + k);  // one position: its gram's left-role bit
+          hh |= ((s_bits[gram_pair_word(g >> 8)] >> (g & 15u)) & 1u) << k;
         }
       }
       n_probe += __popcll(hits) + __popc(hh);
@@ -4448,8 +4452,11 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   std::vector<uint32_t> gt2(2 * gt2_cap, 0), gt2_ent;
   if (use_pref)
     for (auto &kv : gmap) {
-      const uint32_t h = gram_hash(kv.first);
-      gram_bits[h >> 5] |= 1u << (h & 31);
+      // both roles of the gram (k_scan tests even positions as the left gram
+      // of a pair and odd ones as the right gram)
+      const uint32_t g = kv.first;
+      gram_bits[gram_pair_word(g >> 8)] |= 1u << (g & 15u);
+      gram_bits[gram_pair_word(g & 0xFFFFFFu)] |= 1u << (16u + ((g >> 24) & 15u));
       uint32_t slot = gram_slot(kv.first, gt2_cap);
       while (gt2[2 * slot + 1] & 0xFFFF) slot = (slot + 1) & (gt2_cap - 1);
       gt2[2 * slot] = kv.first;

@@ -37,14 +37,11 @@ struct DevRule {
   uint16_t lead_dist;
 };
 
-// Prefilter gram bitset: one bit per hash of a 4-byte window (LDS resident).
-// Full-rate hash (24-bit multiply after folding the top byte in).
+// Prefilter gram bitset (LDS resident, 64K bits = 2048 words), tested two
+// positions per word (gram_pair_* below).  gram_mix: a full-rate 24 x 24-bit
+// multiply (one v_mul_u32_u24 on the device) whose bits 13..23 pick the word.
 constexpr uint32_t kGramLog2 = 16;
 constexpr uint32_t kGramWords = (1u << kGramLog2) / 32;
-// 4-gram -> bit of the 64K-bit prefilter set: word = bits 13..23 of a 24 x
-// 24-bit product of the folded gram (one full-rate v_mul_u32_u24 on the
-// device), bit = the folded gram's low 5 bits (a v_bfe offset operand as is)
-__host__ __device__ inline uint32_t gram_fold(uint32_t g) { return g ^ (g >> 15); }
 __host__ __device__ inline uint32_t gram_mix(uint32_t x) {
 #ifdef __HIP_DEVICE_COMPILE__
   return __umul24(x, 0x2C1B3Bu);
@@ -52,11 +49,14 @@ __host__ __device__ inline uint32_t gram_mix(uint32_t x) {
   return (x & 0xFFFFFFu) * 0x2C1B3Bu;
 #endif
 }
-__host__ __device__ inline uint32_t gram_hash(uint32_t g) {
-  const uint32_t x = gram_fold(g);
-  return (((gram_mix(x) >> 13) & 0x7FFu) << 5) | (x & 31u);
-}
-static_assert(kGramLog2 == 16, "gram_hash yields 16 bits");
+// The scan pass tests grams in pairs: positions k (even) and k + 1 share the
+// 3 bytes k + 1 .. k + 3, which pick one 32-bit word of the bitset; the gram
+// at k is bit (its first byte & 15), the gram at k + 1 bit 16 + (its last byte
+// & 15).  A registered gram sets its bit in both roles (word of its last three
+// bytes, low half; word of its first three bytes, high half), so no occurrence
+// is missed at either parity.  key = 3 bytes (24 bits).
+__host__ __device__ inline uint32_t gram_pair_word(uint32_t key) { return (gram_mix(key) >> 13) & (kGramWords - 1); }
+__host__ __device__ inline uint32_t gram_pair_byte_off(uint32_t key) { return (gram_mix(key) >> 11) & ((kGramWords - 1) << 2); }
 // home slot of a gram in the exact gram table (cap a power of two <= 2^18):
 // Fibonacci hashing, high product bits
 __host__ __device__ inline uint32_t gram_slot(uint32_t g, uint32_t cap) { return ((g * 0x9E3779B1u) >> 14) & (cap - 1); }
