@@ -174,12 +174,13 @@ class Zone:
         return cls(offset_s)
 
     @classmethod
-    def from_tzinfo(cls, tz, first_year: int = 1970, last_year: int = 2100) -> "Zone":
-        """Expand a tzinfo's offset changes over [first_year, last_year): daily
-        samples, each change pinned to the second by bisection."""
+    def from_tzinfo(cls, tz, first_year: int = 1970, last_year: int = 2100, start_s=None) -> "Zone":
+        """Expand a tzinfo's offset changes over [first_year, last_year) (or from
+        start_s): daily samples, each change pinned to the second by bisection.
+        For a tzinfo without its TZif data; named zones use from_tzif."""
         def off(sec):
             return int(_dt.datetime.fromtimestamp(sec, tz).utcoffset().total_seconds())
-        lo = int(_dt.datetime(first_year, 1, 1, tzinfo=_dt.timezone.utc).timestamp())
+        lo = int(_dt.datetime(first_year, 1, 1, tzinfo=_dt.timezone.utc).timestamp()) if start_s is None else int(start_s)
         hi = int(_dt.datetime(last_year, 1, 1, tzinfo=_dt.timezone.utc).timestamp())
         first = off(lo)
         trans, cur, t = [], first, lo
@@ -202,9 +203,63 @@ class Zone:
         return cls(first, trans)
 
     @classmethod
+    def from_tzif(cls, data: bytes, tz_after=None, last_year: int = 2400) -> "Zone":
+        """The zone as Go's time.LoadLocation reads a TZif file: every explicit
+        transition of the 64-bit (v2+) data block, the offset before the first
+        one chosen as Location.lookupFirstZone does (the first zone type if no
+        transition uses it, else the first non-DST type), and after the last
+        explicit transition the footer's rule, expanded (with tz_after, a tzinfo
+        of the same zone; daily samples pinned by bisection) up to last_year."""
+        import struct
+        if data[:4] != b"TZif":
+            raise ValueError("not a TZif file")
+        ver = data[4]
+
+        def counts(off):
+            return struct.unpack(">6l", data[off + 20:off + 44])  # isut, isstd, leap, time, type, char
+        isut, isstd, leap, timecnt, typecnt, charcnt = counts(0)
+        base, tsize = 44, 4
+        if ver >= ord("2"):
+            off = 44 + timecnt * 5 + typecnt * 6 + charcnt + leap * 8 + isstd + isut
+            isut, isstd, leap, timecnt, typecnt, charcnt = counts(off)
+            base, tsize = off + 44, 8
+        times = struct.unpack(">%d%s" % (timecnt, "q" if tsize == 8 else "l"), data[base:base + timecnt * tsize])
+        p = base + timecnt * tsize
+        idx = list(data[p:p + timecnt])
+        p += timecnt
+        types = [struct.unpack(">lBB", data[p + 6 * i:p + 6 * i + 6]) for i in range(typecnt)]  # utoff, isdst, desig
+        first = 0
+        if 0 in idx:  # time/zoneinfo.go lookupFirstZone, cases 2-4
+            first = None
+            if idx and types[idx[0]][1]:
+                first = next((z for z in range(idx[0] - 1, -1, -1) if not types[z][1]), None)
+            if first is None:
+                first = next((z for z in range(typecnt) if not types[z][1]), 0)
+        trans = [(int(t), int(types[i][0])) for t, i in zip(times, idx)]
+        offset = int(types[first][0]) if types else 0
+        if tz_after is not None:
+            start = trans[-1][0] if trans else int(_dt.datetime(1970, 1, 1, tzinfo=_dt.timezone.utc).timestamp())
+            ext = cls.from_tzinfo(tz_after, last_year=last_year, start_s=start)
+            trans += [(a, o) for a, o in ext.transitions if a > start]
+        return cls(offset, trans)
+
+    @classmethod
     def named(cls, name: str) -> "Zone":
+        """An IANA zone from its TZif file (zoneinfo.TZPATH, else the tzdata package)."""
+        import os
         import zoneinfo
-        return cls.from_tzinfo(zoneinfo.ZoneInfo(name))
+        data = None
+        for d in zoneinfo.TZPATH:
+            f = os.path.join(d, name)
+            if os.path.isfile(f):
+                with open(f, "rb") as fh:
+                    data = fh.read()
+                break
+        if data is None:
+            import importlib.resources
+            pkg, _, leaf = ("tzdata.zoneinfo/" + name).rpartition("/")
+            data = importlib.resources.files(pkg.replace("/", ".")).joinpath(leaf).read_bytes()
+        return cls.from_tzif(data, zoneinfo.ZoneInfo(name))
 
     def offset_at(self, sec: int) -> int:
         import bisect

@@ -66,3 +66,20 @@ def test_zone_table_matches_zoneinfo(name):
     for s in secs:
         want = dt.datetime.fromtimestamp(s, tz).strftime("%Y-%m-%dT%H:%M:%S")
         assert format_time(s * 1_000_000_000 + 999_999_999, z) == want, (name, s)
+
+
+@pytest.mark.parametrize("name", ["Europe/Berlin", "America/New_York", "Australia/Lord_Howe", "Asia/Kolkata"])
+def test_zone_from_tzif_wide_range(name):
+    """Zone.named reads the zone's TZif transitions (no daily sampling) and
+    expands the footer rule to 2400: offsets agree with zoneinfo from 1901 to
+    2380, before the first transition (Go's lookupFirstZone) and past 2100."""
+    import random
+    import zoneinfo
+    from banjax_amd import Zone
+    z, tz = Zone.named(name), zoneinfo.ZoneInfo(name)
+    rnd = random.Random(4)
+    secs = [rnd.randrange(-2 ** 31, 13_000_000_000) for _ in range(4000)]
+    for a, _ in z.transitions:
+        secs += [a - 1, a]
+    for s in secs:
+        assert z.offset_at(s) == int(dt.datetime.fromtimestamp(s, tz).utcoffset().total_seconds()), (name, s)
