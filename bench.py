@@ -299,6 +299,29 @@ def main():
                "ms_per_step": round(el2 * 1000.0 / args.bans_steps, 3), "steps": args.bans_steps,
                "what": "each step also builds the per-IP DynamicDecisionLists updates and all LogRegexBan JSON lines "
                        "on the device and copies them to pinned host memory (BJX_EMIT_BANS)"}
+        if not node_mode and not dist and ex is None:
+            # the host's side of the last step: Update per record into an empty
+            # decision map, ban-log lines appended to a file (workloads/host_apply.c)
+            import ctypes
+            import tempfile
+            from banjax_amd import _lib as bl
+            bb = bl.BanBatch()
+            if bl.lib().bjx_batch_bans(eng._h, ctypes.byref(bb)) == 0:
+                fd, path = tempfile.mkstemp(prefix="bjx_banlog_", dir="/tmp")
+                os.close(fd)
+                try:
+                    secs, changed = W.host_apply(bb, path)
+                finally:
+                    os.unlink(path)
+                dec["host_apply"] = {
+                    "ms": round(secs * 1000.0, 3), "records": int(bb.n_ips), "entries_changed": int(changed),
+                    "log_bytes": int(bb.log_bytes),
+                    "step_plus_host_lines_per_s": round(n_lines / (el2 / args.bans_steps + secs), 1),
+                    "what": "one step's per-IP records applied by a compiled stand-in for the Go host "
+                            "(DynamicDecisionLists.Update into an empty open-addressing map keyed by the IP "
+                            "bytes, decision.go:404-439) and its LogRegexBan lines appended to a file in /tmp "
+                            "(iptables.go:179-228); serial after the step (a pipelined host overlaps it with "
+                            "the next batch)"}
     # the decision records alone (BJX_BAN_RECORDS_ONLY: no LogRegexBan lines
     # built or copied), single-engine runs
     rec = None

@@ -26,6 +26,9 @@ class SynthCfg(C.Structure):
 IP_UNIFORM, IP_ZIPF, IP_DISTINCT = 0, 1, 2
 
 
+HOST_APPLY_LIB = os.path.join(HERE, "lib", "libbjx_host_apply.so")
+
+
 def build(force=False):
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     src = os.path.join(HERE, "synth.hip")
@@ -33,7 +36,22 @@ def build(force=False):
         subprocess.run(["hipcc", "-O3", "-std=c++17", "-fPIC", "-shared",
                         "--offload-arch=%s" % os.environ.get("BJX_OFFLOAD_ARCH", "gfx950"),
                         "-o", LIB, src], check=True)
+    ha = os.path.join(HERE, "host_apply.c")
+    if force or not os.path.exists(HOST_APPLY_LIB) or os.path.getmtime(ha) > os.path.getmtime(HOST_APPLY_LIB):
+        subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", HOST_APPLY_LIB, ha], check=True)
     return LIB
+
+
+def host_apply(ban_batch, log_path=None):
+    """workloads/host_apply.c over a bjx_ban_batch (ctypes struct): the
+    compiled stand-in for the Go host's Update per record + ban-log write.
+    Returns (seconds, entries changed)."""
+    L = C.CDLL(HOST_APPLY_LIB)
+    L.bjx_host_apply.restype = C.c_double
+    L.bjx_host_apply.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_uint64)]
+    ch = C.c_uint64(0)
+    secs = L.bjx_host_apply(C.addressof(ban_batch), log_path.encode() if log_path else None, C.byref(ch))
+    return secs, ch.value
 
 
 _lib = None
