@@ -5050,9 +5050,9 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     uint32_t hot = kNone;
     for (uint32_t g = 0; g < rs->n_global && hot == kNone; ++g)
       if (rs->rules[g].rx.mode == kModeAlways) hot = drules[g].name_id;
-    // opt-in (BJX_SLOT_CACHE=1): -1.1 ms of claim at cfg3, but two full GPU-suite
-    // runs with it on showed the intermittent outcome mismatch of DESIGN.md §3
-    static const bool slot_cache = getenv("BJX_SLOT_CACHE") && atoi(getenv("BJX_SLOT_CACHE")) == 1;
+    // on by default (-0.9 ms of claim at cfg3; full GPU suite green with it and
+    // BJX_CHECK=1, profiles/r03_final2/slot_cache.md); BJX_SLOT_CACHE=0 turns it off
+    static const bool slot_cache = !(getenv("BJX_SLOT_CACHE") && atoi(getenv("BJX_SLOT_CACHE")) == 0);
     if (!slot_cache || e->st_cap > (1ull << 32)) hot = kNone;
     if (hot != e->S.hot_name && e->S.ip_st) HIP_OK(hipMemsetAsync(e->S.ip_st, 0xFF, e->S.ip_st_cap * 4, e->stream));
     e->S.hot_name = hot;
