@@ -191,6 +191,8 @@ def lib():
     L.bjx_debug_scan_stats.argtypes = [vp, C.POINTER(C.c_uint64), sz]
     L.bjx_debug_set_claim_budget.restype = C.c_int
     L.bjx_debug_set_claim_budget.argtypes = [vp, C.c_uint64]
+    L.bjx_debug_set_slot_cache.restype = C.c_int
+    L.bjx_debug_set_slot_cache.argtypes = [vp, C.c_int]
     L.bjx_debug_set_ip_hash_mask.restype = C.c_int
     L.bjx_debug_set_ip_hash_mask.argtypes = [vp, C.c_uint64]
     L.bjx_debug_set_dfa_state_cap.restype = C.c_int

@@ -1611,8 +1611,11 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
               L.cand[gline * kCandSlots + cc] = ((uint64_t)q0 << 24) | ver | lit;
             } else {  // past the slots: the line's summary only (CandMeta)
               // a verified hit kCertainGap bytes past the line start lies in
-              // rest whenever the header is shorter (k_dfa checks rest_off)
-              const bool far = lk >= 0 ? s0 - (int32_t)ls[lk] >= (int32_t)kCertainGap : s0 >= (int32_t)kCertainGap;
+              // rest whenever the header is shorter (k_dfa checks rest_off).
+              // ls[] holds the first kLineCap line starts only: a later line's
+              // hit is never taken as far (an occurrence bit alone is exact)
+              const bool far = lk < 0 ? s0 >= (int32_t)kCertainGap
+                                      : lk < (int32_t)kLineCap && s0 - (int32_t)ls[lk] >= (int32_t)kCertainGap;
               const uint64_t bit = 1ull << (lit & 31);
               atomicOr(reinterpret_cast<unsigned long long *>(&L.cand_meta[gline].bits), ver && far ? bit | (bit << 32) : bit);
               atomicMax(&L.cand_meta[gline].first_inv, ~(uint32_t)((uint64_t)q0 >> 3));
@@ -3948,6 +3951,7 @@ struct bjx_engine {
   uint32_t epoch = 0;  // batch counter (IpSlot.born)
   uint64_t dbg_hash_mask = 0;  // bjx_debug_set_ip_hash_mask
   uint64_t dbg_budget = 0;     // bjx_debug_set_claim_budget (0 = off)
+  int dbg_slot_cache = -1;     // bjx_debug_set_slot_cache: -1 = BJX_SLOT_CACHE / default on, 0 off, 1 on
   uint64_t host_counters[3] = {0, 0, 0};
 
   // batch workspace
@@ -5052,7 +5056,8 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
       if (rs->rules[g].rx.mode == kModeAlways) hot = drules[g].name_id;
     // on by default (-0.9 ms of claim at cfg3; full GPU suite green with it and
     // BJX_CHECK=1, profiles/r03_final2/slot_cache.md); BJX_SLOT_CACHE=0 turns it off
-    static const bool slot_cache = !(getenv("BJX_SLOT_CACHE") && atoi(getenv("BJX_SLOT_CACHE")) == 0);
+    static const bool slot_cache_env = !(getenv("BJX_SLOT_CACHE") && atoi(getenv("BJX_SLOT_CACHE")) == 0);
+    const bool slot_cache = e->dbg_slot_cache < 0 ? slot_cache_env : e->dbg_slot_cache != 0;
     if (!slot_cache || e->st_cap > (1ull << 32)) hot = kNone;
     if (hot != e->S.hot_name && e->S.ip_st) HIP_OK(hipMemsetAsync(e->S.ip_st, 0xFF, e->S.ip_st_cap * 4, e->stream));
     e->S.hot_name = hot;
@@ -6582,6 +6587,13 @@ extern "C" int bjx_debug_set_claim_budget(bjx_engine *e, uint64_t max_new) {
   if (!e) return BJX_ERR_ARG;
   std::lock_guard<std::mutex> g(e->mu);
   e->dbg_budget = max_new;
+  return BJX_OK;
+}
+extern "C" int bjx_debug_set_slot_cache(bjx_engine *e, int on) {
+  if (!e) return BJX_ERR_ARG;
+  std::lock_guard<std::mutex> g(e->mu);
+  e->dbg_slot_cache = on < 0 ? -1 : on != 0;
+  e->bound_uid = 0;  // the next batch re-binds and applies it
   return BJX_OK;
 }
 extern "C" size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap) {

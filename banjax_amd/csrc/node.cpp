@@ -187,17 +187,25 @@ void exchange(bjx_node *n, Seg seg) {
     return;
   }
   nccl_ok(ncclGroupStart(), "ncclGroupStart");
-  for (size_t p = 0; p < N; ++p)
-    for (size_t k = 0; k < N; ++k) {
+  // the group is always closed on this thread, even when a call inside it
+  // fails: the first error is kept and raised after ncclGroupEnd
+  ncclResult_t first = ncclSuccess;
+  const char *what = "";
+  for (size_t p = 0; p < N && first == ncclSuccess; ++p)
+    for (size_t k = 0; k < N && first == ncclSuccess; ++k) {
       void *d;
       const void *s;
       size_t b;
       seg(p, k, &d, &s, &b);
       if (!b) continue;
-      nccl_ok(ncclSend(s, b, ncclUint8, (int)p, n->comms[k], n->parts[k].copy), "ncclSend");
-      nccl_ok(ncclRecv(d, b, ncclUint8, (int)k, n->comms[p], n->parts[p].copy), "ncclRecv");
+      ncclResult_t r = ncclSend(s, b, ncclUint8, (int)p, n->comms[k], n->parts[k].copy);
+      if (r != ncclSuccess) { first = r; what = "ncclSend"; break; }
+      r = ncclRecv(d, b, ncclUint8, (int)k, n->comms[p], n->parts[p].copy);
+      if (r != ncclSuccess) { first = r; what = "ncclRecv"; break; }
     }
-  nccl_ok(ncclGroupEnd(), "ncclGroupEnd");
+  const ncclResult_t end = ncclGroupEnd();
+  nccl_ok(first, what);
+  nccl_ok(end, "ncclGroupEnd");
 }
 
 void sync_copies(bjx_node *n) {

@@ -249,6 +249,10 @@ class Engine:
         """Test hook: cap the first claim launch per table and batch (0 = off)."""
         self._check(_lib.lib().bjx_debug_set_claim_budget(self._h, max_new), "debug_set_claim_budget")
 
+    def debug_set_slot_cache(self, on: int):
+        """Test hook: state-slot cache on (1), off (0), default (-1), from the next batch."""
+        self._check(_lib.lib().bjx_debug_set_slot_cache(self._h, on), "debug_set_slot_cache")
+
     def state_clear(self):
         self._check(_lib.lib().bjx_state_clear(self._h), "state_clear")
 

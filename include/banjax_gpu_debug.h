@@ -42,6 +42,9 @@ int bjx_debug_set_ip_hash_mask(bjx_engine *e, uint64_t mask);
 /* Test hook: the first claim launch of each table in a batch may add at most
    max_new entries (0 = off), forcing the roll-back / re-claim path. */
 int bjx_debug_set_claim_budget(bjx_engine *e, uint64_t max_new);
+/* Test hook: the per-IP state-slot cache of k_st_claim on (1), off (0) or as
+   BJX_SLOT_CACHE / the default says (-1), from the next batch on. */
+int bjx_debug_set_slot_cache(bjx_engine *e, int on);
 /* Test hook: rules compiled afterwards use the bit-parallel NFA once their DFA
    passes `cap` states (0 = default 4096; 1 = every rule that fits the NFA),
    process-wide; clears the compiled-pattern cache. */

@@ -21,13 +21,20 @@ def engine():
     e.close()
 
 
-def test_hot_key_workload(engine):
-    """cfg5h shape (one IP sends 25% of the lines), oracle-sized, two batches."""
+@pytest.mark.parametrize("slot_cache", [1, 0])
+def test_hot_key_workload(engine, slot_cache):
+    """cfg5h shape (one IP sends 25% of the lines), oracle-sized, two batches;
+    with the state-slot cache of k_st_claim on and off (bit-exact both ways)."""
     w = W.scaled(W.CFG5H, 160_000, n_ips=20_000)
-    pair = Pair(w.rules_yaml, engine)
-    pair.feed(w.host_lines(0, 80_000), w.now_ns(0, 80_000))
-    pair.feed(w.host_lines(80_000, 80_000), w.now_ns(80_000, 80_000))
-    pair.compare_state(["1.0.0.0", "2.0.0.0", "3.0.0.0"])
+    engine.debug_set_slot_cache(slot_cache)
+    try:
+        engine.state_clear()
+        pair = Pair(w.rules_yaml, engine)
+        pair.feed(w.host_lines(0, 80_000), w.now_ns(0, 80_000))
+        pair.feed(w.host_lines(80_000, 80_000), w.now_ns(80_000, 80_000))
+        pair.compare_state(["1.0.0.0", "2.0.0.0", "3.0.0.0"])
+    finally:
+        engine.debug_set_slot_cache(-1)
 
 
 HOT_CFG = """
@@ -70,12 +77,18 @@ def _hot_lines(t0_ms, n, step_ms=1, backwards_every=0, post_every=7):
     ("2", 37, "2", 5, 0),       # rules sharing the name with different limits: serial
     ("2", 37, "2", 37, 97),     # timestamps going backwards: serial
 ])
-def test_hot_key_runs(engine, iv1, lim1, iv2, lim2, back):
-    pair = Pair(HOT_CFG % (iv1, lim1, iv2, lim2), engine)
-    t0 = 1700000000_000
-    pair.feed(_hot_lines(t0, 30_000, backwards_every=back), t0 * 1_000_000)
-    pair.feed(_hot_lines(t0 + 30_000, 30_000, backwards_every=back), (t0 + 30_000) * 1_000_000)
-    pair.compare_state(["6.6.6.6", "7.7.7.1"])
+@pytest.mark.parametrize("slot_cache", [1, 0])
+def test_hot_key_runs(engine, iv1, lim1, iv2, lim2, back, slot_cache):
+    engine.debug_set_slot_cache(slot_cache)
+    try:
+        engine.state_clear()
+        pair = Pair(HOT_CFG % (iv1, lim1, iv2, lim2), engine)
+        t0 = 1700000000_000
+        pair.feed(_hot_lines(t0, 30_000, backwards_every=back), t0 * 1_000_000)
+        pair.feed(_hot_lines(t0 + 30_000, 30_000, backwards_every=back), (t0 + 30_000) * 1_000_000)
+        pair.compare_state(["6.6.6.6", "7.7.7.1"])
+    finally:
+        engine.debug_set_slot_cache(-1)
 
 
 def test_hot_key_reload_lowers_limit(engine):

@@ -397,6 +397,34 @@ def test_tile_geometry(engine, seed):
     pair.compare_state(["10.0.0.1", "10.0.1.2", "9.9.9.1"])
 
 
+def overflow_past_line_cap_lines(t, shift):
+    """A 4 KB scan tile whose last line starts after more than kLineCap (128)
+    other lines and overflows its hit slots: its IP field holds an
+    equivalent rule's literal ("needle", not in rest), and its rest -- in the
+    halo, so the scan pass verifies those hits first -- holds five hits of
+    another literal.  The IP-field hit then lands past the slots, where the
+    scan pass's "far from the line start" test must not read the line-start
+    array past its kLineCap entries (round-3 advisor finding)."""
+    tiny = b"x\n" * 140
+    target = b"%d needle GET h.com GET /a FooBar FooBar FooBar FooBar FooBar fOOBAR\n" % t
+    start = 4096 - 25 + shift  # the IP field ends just before the tile edge
+    filler_len = start - len(tiny) - 1
+    head = b"%d 10.0.0.1 GET h.com GET /a " % t
+    filler = head + b"a" * (filler_len - len(head)) + b"\n"
+    data = tiny + filler + target
+    assert data.index(target) == start
+    tail = b"%d 10.0.0.2 GET x.org GET /needle%d HTTP/1.1 ua\n" % (t, shift)
+    return data + tail * 3
+
+
+@pytest.mark.parametrize("shift", [0, 3, 9, 17])
+def test_overflow_hits_past_line_cap(engine, shift):
+    t = 1700000000
+    pair = Pair(GEOM_CFG, engine)
+    pair.feed(overflow_past_line_cap_lines(t, shift), t * S)
+    pair.compare_state(["needle", "10.0.0.1", "10.0.0.2"])
+
+
 @pytest.mark.parametrize("mask", [0xFF, 0xFFF])
 def test_ip_hash_collisions(engine, mask):
     """Distinct IPs forced onto a few 64-bit hash values (test hook): the IP
@@ -504,13 +532,15 @@ def test_sharded_engines_match_single_process(wl, world):
         e.close()
 
 
-@pytest.mark.parametrize("budget", [1, 97, 5000])
-def test_table_overflow_rollback(engine, budget):
+@pytest.mark.parametrize("budget,slot_cache", [(1, 1), (97, 1), (5000, 1), (1, 0), (97, 0)])
+def test_table_overflow_rollback(engine, budget, slot_cache):
     """The IP and state tables claim at most `budget` new entries in a batch's
     first claim launch (test hook): every batch overflows, rolls its claims
-    back and claims again - results stay bit-exact across batches."""
+    back and claims again - results stay bit-exact across batches, with the
+    state-slot cache on and off."""
     w = W.scaled(W.CFG5, 24_000, n_ips=8_000)
     engine.debug_set_claim_budget(budget)
+    engine.debug_set_slot_cache(slot_cache)
     try:
         pair = Pair(w.rules_yaml, engine)
         ips = set()
@@ -524,6 +554,7 @@ def test_table_overflow_rollback(engine, budget):
         pair.compare_state(sorted(ips)[:60])
     finally:
         engine.debug_set_claim_budget(0)
+        engine.debug_set_slot_cache(-1)
 
 
 def test_shared_patterns_across_rules(engine):

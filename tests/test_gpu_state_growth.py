@@ -14,8 +14,10 @@ pytestmark = pytest.mark.gpu
 S = 1_000_000_000
 
 
-def test_rolling_distinct_ips_grow_tables():
+@pytest.mark.parametrize("slot_cache", [1, 0])
+def test_rolling_distinct_ips_grow_tables(slot_cache):
     eng = Engine()
+    eng.debug_set_slot_cache(slot_cache)
     try:
         w = W.replace(W.CFG5, n_lines=9_000_000, n_ips=9_000_000, ipv6_pct=0)
         lim = RegexRateLimiter(Config.from_yaml(w.rules_yaml), engine=eng, banner=MockBanner())
