@@ -179,6 +179,8 @@ def lib():
     L.bjx_state_dump.argtypes = [vp, C.c_char_p, sz]
     L.bjx_debug_rule_match_host.restype = C.c_int
     L.bjx_debug_rule_match_host.argtypes = [vp, sz, C.c_char_p, sz]
+    L.bjx_debug_regex_parse.restype = C.c_int
+    L.bjx_debug_regex_parse.argtypes = [C.c_char_p, sz, C.c_char_p, sz]
     L.bjx_debug_rule_lead.restype = C.c_int
     L.bjx_debug_rule_lead.argtypes = [vp, sz]
     L.bjx_debug_rule_literal.restype = sz

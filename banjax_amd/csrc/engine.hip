@@ -1894,6 +1894,8 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
     for (int k = 0; k < 10; ++k) atomicAdd(&A.prof[k], (unsigned long long)P.acc[k]);
 }
 
+#include "lines2.h"
+
 // Rule decisions of the lines whose header the scan pass parsed (one lane per
 // line, regex_rate_limiter.go:175-211): host rules, anchored checks against
 // the line in HBM, the scan's literal hits; undecided (line, rule) pairs become
@@ -3951,6 +3953,7 @@ struct bjx_engine {
   uint32_t epoch = 0;  // batch counter (IpSlot.born)
   uint64_t dbg_hash_mask = 0;  // bjx_debug_set_ip_hash_mask
   uint64_t dbg_budget = 0;     // bjx_debug_set_claim_budget (0 = off)
+  uint32_t lines2_lds = 0;     // dynamic LDS k_lines2 was last configured for
   int dbg_slot_cache = -1;     // bjx_debug_set_slot_cache: -1 = BJX_SLOT_CACHE / default on, 0 off, 1 on
   uint64_t host_counters[3] = {0, 0, 0};
 
@@ -4732,6 +4735,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   // plan classes for k_lines' LDS (decide_plan_lds), appended to the host
   // dictionary blob when both fit kLinesTabLdsMax
   uint32_t lt_hinfo = 0, lt_cls = 0, lt_trec = 0, lt_pool = 0;
+  uint32_t l2_hdc = 0, l2_dcls = 0, l2_none = 0, l2_bytes = 0;  // k_lines2 tables (0 bytes: not eligible)
   if (use_plan && hl_bytes && n_hosts && !getenv("BJX_NO_PLAN_LDS")) {
     std::vector<uint2> hinfo(n_hosts, make_uint2(0, 0));
     std::vector<uint4> cls, trec;
@@ -4836,6 +4840,133 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
       if (!pool.empty()) memcpy(hl.data() + w_pool, pool.data(), pool.size());
       hl_bytes = w_end * 4;
       lt_hinfo = w_hi; lt_cls = w_cls; lt_trec = w_tr; lt_pool = w_pool;
+    }
+    // k_lines2 decision tables (lines2.h), appended to the blob after what
+    // k_lines reads: per decision class (site plan class, site rules, ALWAYS
+    // and hosts_to_skip masks) the per-literal rows, their checks, the rule of
+    // each position and the anchored / no-literal entries
+    // the literals a hit can carry (the scan pass's gram-table literals) must have
+    // ids below kL2Lits: they index the rows, and the overflow bits (id & 31) name
+    // them exactly
+    uint32_t pref_ids_ok = 1;
+    for (uint32_t id = 0; id < lit_pref.size(); ++id)
+      if (lit_pref[id] && id >= kL2Lits) pref_ids_ok = 0;
+    if (lt_cls && pref_ids_ok && max_app <= 64 && !getenv("BJX_NO_LINES2")) {
+      struct Dc {
+        uint64_t eq[kL2Lits] = {}, job[kL2Lits] = {}, lm[kL2Lits] = {};
+        std::vector<uint4> chk[kL2Lits];
+        uint32_t prule[64] = {};
+        std::vector<uint32_t> anc;  // kL2AncWords per entry
+        uint64_t alw = 0, skp = 0, anyhit = 0, anyovf = 0;
+      };
+      std::vector<Dc> dcs;
+      std::map<std::tuple<uint32_t, uint32_t, uint64_t, uint64_t>, uint32_t> dc_ids;
+      const uint32_t n_glob_ent = (uint32_t)(plan_glob.size() / 2);
+      bool ok = true;
+      auto add_entry = [&](Dc &D, uint4 a, const uint4 b, uint32_t p) {
+        const uint32_t kind = (a.x >> 27) & 7u, eq = (a.x >> 30) & 1u;
+        const uint64_t bit = 1ull << p;
+        a.x = (a.x & ~(0x7Fu << 20)) | (p << 20);
+        D.prule[p] = a.x;
+        auto ids = [&](auto fn) {
+          const uint32_t l4[4] = {a.y & 0xFFFFu, a.y >> 16, a.z & 0xFFFFu, a.z >> 16};
+          for (uint32_t l : l4)
+            if (l != 0xFFFFu) fn(l);
+        };
+        if (kind == kPlanLit) {
+          ids([&](uint32_t l) {
+            D.lm[l] |= bit;
+            if (a.w == kNone) (eq ? D.eq[l] : D.job[l]) |= bit;
+            else if (!eq) D.job[l] |= bit;
+            else {
+              const uint32_t off = a.w & 0xFFu, flen = b.y;
+              D.chk[l].push_back(make_uint4(p | (kL2ChkFull << 8) | (1u << 10), a.w, flen, flen > off ? flen - off : 0u));
+            }
+          });
+        } else if (kind == kPlanLitT) {
+          const uint4 rec = trec[a.w];
+          const uint32_t la = rec.x & 0xFF, lc = (rec.x >> 8) & 0xFF, side = (rec.x >> 16) & 1u;
+          ids([&](uint32_t l) {
+            D.lm[l] |= bit;
+            D.chk[l].push_back(make_uint4(p | (kL2ChkTmpl << 8) | (eq << 10) | ((side ? 0u : 1u) << 11), a.w, 0u,
+                                          side ? lc : la + lc));
+          });
+        } else if (kind == kPlanLitAny) {
+          D.anyhit |= bit;
+          D.anyovf |= bit;
+        } else {  // kPlanAnchor, kPlanAnchorT, kPlanScan: the bytes of rest each may read
+          uint32_t ext = 0;
+          if (kind == kPlanAnchorT) {
+            const uint4 rec = trec[a.w];
+            ext = ((rec.x & 0xFF) + ((rec.x >> 8) & 0xFF)) | 0x80000000u;
+          } else if (kind == kPlanAnchor) {
+            ext = std::max<uint32_t>((a.z & 0xFFu) + 8, a.w >> 16);
+            const uint32_t r = a.x & 0xFFFFFu;
+            for (uint32_t i = 0; i < drules[r].anc_len; ++i) ext = std::max<uint32_t>(ext, lit_len[rule_lits[drules[r].anc_off + i]]);
+          }
+          if (ext & 0x40000000u) ok = false;
+          const uint32_t w[kL2AncWords] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, ext, 0, 0, 0};
+          D.anc.insert(D.anc.end(), w, w + kL2AncWords);
+        }
+      };
+      auto dc_of = [&](uint32_t ci, uint32_t n_ent, uint32_t nsite, uint64_t alw, uint64_t skp) {
+        const auto key = std::make_tuple(ci | (n_ent << 16), nsite, alw, skp);
+        auto it = dc_ids.find(key);
+        if (it != dc_ids.end()) return it->second;
+        Dc D;
+        D.alw = alw;
+        D.skp = skp;
+        for (uint32_t e = 0; e < n_ent; ++e) add_entry(D, cls[2 * (ci + e)], cls[2 * (ci + e) + 1], (cls[2 * (ci + e)].x >> 20) & 0x7Fu);
+        for (uint32_t g = 0; g < n_glob_ent; ++g)
+          add_entry(D, plan_glob[2 * g], plan_glob[2 * g + 1], nsite + ((plan_glob[2 * g].x >> 20) & 0x7Fu));
+        const uint32_t id = (uint32_t)dcs.size();
+        dcs.push_back(std::move(D));
+        dc_ids.emplace(key, id);
+        return id;
+      };
+      std::vector<uint32_t> hdc(n_hosts, 0);
+      for (uint32_t h = 0; h < n_hosts; ++h)
+        hdc[h] = dc_of(hinfo[h].x & 0xFFFFu, hinfo[h].x >> 16, (uint32_t)per_host[h].size(), sc_always[2 * h], sc_skipm[2 * h]);
+      const uint32_t none = dc_of(0xFFFFu, 0, 0, sc_always[2 * n_hosts], sc_skipm[2 * n_hosts]);
+      // layout (words, 16 B aligned pieces)
+      std::vector<uint32_t> t(((hl.size() + 3) & ~size_t(3)), 0);
+      std::copy(hl.begin(), hl.end(), t.begin());
+      auto al4 = [&]() { t.resize((t.size() + 3) & ~size_t(3), 0); return (uint32_t)t.size(); };
+      const uint32_t w_hdc = al4();
+      t.insert(t.end(), hdc.begin(), hdc.end());
+      const uint32_t w_dc = al4();
+      t.resize(t.size() + kL2DclsWords * dcs.size(), 0);
+      for (uint32_t d = 0; d < dcs.size(); ++d) {
+        Dc &D = dcs[d];
+        const uint32_t w_rows = al4();
+        t.resize(t.size() + kL2RowWords * kL2Lits, 0);
+        for (uint32_t l = 0; l < kL2Lits; ++l) {
+          const uint32_t w_ck = al4();
+          for (const uint4 &c : D.chk[l]) { t.push_back(c.x); t.push_back(c.y); t.push_back(c.z); t.push_back(c.w); }
+          uint32_t *r = t.data() + w_rows + kL2RowWords * l;
+          r[0] = (uint32_t)D.eq[l]; r[1] = (uint32_t)(D.eq[l] >> 32);
+          r[2] = (uint32_t)D.job[l]; r[3] = (uint32_t)(D.job[l] >> 32);
+          r[4] = (uint32_t)D.lm[l]; r[5] = (uint32_t)(D.lm[l] >> 32);
+          r[6] = w_ck; r[7] = (uint32_t)D.chk[l].size();
+        }
+        const uint32_t w_pr = al4();
+        t.insert(t.end(), D.prule, D.prule + 64);
+        const uint32_t w_anc = al4();
+        t.insert(t.end(), D.anc.begin(), D.anc.end());
+        uint32_t *rec = t.data() + w_dc + kL2DclsWords * d;
+        const uint64_t v[4] = {D.alw, D.skp, D.anyhit, D.anyovf};
+        for (int k = 0; k < 4; ++k) { rec[2 * k] = (uint32_t)v[k]; rec[2 * k + 1] = (uint32_t)(v[k] >> 32); }
+        rec[8] = w_rows; rec[9] = w_pr; rec[10] = w_anc; rec[11] = (uint32_t)(D.anc.size() / kL2AncWords);
+      }
+      al4();
+      if (ok && t.size() * 4 <= kL2TabMax) {
+        l2_hdc = w_hdc; l2_dcls = w_dc; l2_none = none;
+        l2_bytes = (uint32_t)(t.size() * 4);
+        hl.swap(t);
+      }
+      if (getenv("BJX_DEBUG_IMG"))
+        fprintf(stderr, "[bjx] k_lines2 tables: %zu decision classes, %zu B (%s)\n", dcs.size(),
+                (l2_bytes ? hl.size() : t.size()) * 4, l2_bytes ? "on" : "off");
     }
     if (getenv("BJX_DEBUG_IMG"))
       fprintf(stderr, "[bjx] plan classes: %zu entries, %zu templates, pool %zu B, LDS tables %u B (%s)\n", cls.size() / 2,
@@ -5011,6 +5142,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.hl = reinterpret_cast<const uint32_t *>(base + o_hl);
   B.hl_bytes = hl_bytes;
   B.lt_hinfo = lt_hinfo; B.lt_cls = lt_cls; B.lt_trec = lt_trec; B.lt_pool = lt_pool;
+  B.l2_hdc = l2_hdc; B.l2_dcls = l2_dcls; B.l2_none = l2_none; B.l2_bytes = l2_bytes;
   B.plan = reinterpret_cast<const uint4 *>(base + o_plan);
   B.plan_off = reinterpret_cast<const uint32_t *>(base + o_plo);
   B.plan_glob = reinterpret_cast<const uint4 *>(base + o_plg);
@@ -5697,7 +5829,22 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       A.span_bytes = 0;
     }
     HIP_OK(hipEventRecord(e->evk[0], st));
-    if (!scan_hdr || n_todo) {
+    // k_lines2 (lines2.h) when the ruleset has its tables; BJX_LINES=1 keeps k_lines
+    static const int lines_env = getenv("BJX_LINES") ? atoi(getenv("BJX_LINES")) : 2;
+    const bool use_l2 = !scan_hdr && B.l2_bytes && lines_env != 1 && !getenv("BJX_PROF_LINES") && !A.dbg;
+    if (use_l2) {
+      const uint32_t lds = B.l2_bytes + (kL2Block / 64) * kL2WaveLds;
+      if (lds != e->lines2_lds) {
+        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_lines2), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        e->lines2_lds = lds;
+      }
+      int per_cu = 0;
+      HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&k_lines2), kL2Block, lds));
+      const uint64_t resident = (uint64_t)std::max(1, per_cu) * (uint64_t)std::max(1, n_cu);
+      const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n_lines + kL2Block - 1) / kL2Block, resident));
+      hipLaunchKernelGGL(k_lines2, dim3(grid), dim3(kL2Block), lds, st, B, A);
+      HIP_OK(hipGetLastError());
+    } else if (!scan_hdr || n_todo) {
       const bool img_lds = B.img_bytes <= kLinesImgMax;
       const bool host_lds = B.hl_bytes != 0;
       const uint32_t fixed = ((img_lds ? B.img_bytes : 0) + 15u & ~15u) + (host_lds ? B.hl_bytes + 15u & ~15u : 0u) +

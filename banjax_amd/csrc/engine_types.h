@@ -194,6 +194,10 @@ struct Bind {
   const uint32_t *hl;
   uint32_t hl_bytes;
   uint32_t lt_hinfo, lt_cls, lt_trec, lt_pool;
+  // k_lines2 decision tables after the plan classes in the same blob (word
+  // offsets; lines2.h): per-host decision class, class records, the class of
+  // lines without a host; l2_bytes = the blob with them (0: k_lines2 off)
+  uint32_t l2_hdc, l2_dcls, l2_none, l2_bytes;
   const uint4 *plan;
   const uint32_t *plan_off;  // n_hosts + 1
   const uint4 *plan_glob;

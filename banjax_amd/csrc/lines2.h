@@ -1,0 +1,409 @@
+// k_lines2: the per-line pass (consumeLine up to the rule loop,
+// internal/regex_rate_limiter.go:113-214) over 112-byte line windows, with the
+// rule decisions read from per-(decision class, literal) rows instead of a
+// walk over every rule of the line's scope.  Included by engine.hip after
+// k_lines, whose helpers it uses; DESIGN.md §4f.
+//
+// Window: each lane copies the 16 B-aligned 112 bytes that hold its line's
+// first bytes into its own LDS window (7 x 16 B loads, 7 ds_write_b128); the
+// header, the anchored windows at the start of rest and the template / literal
+// checks around hits read it there, anything past it from HBM.  112 B = 28
+// dwords per lane (an odd multiple of 4): lanes reading the same window offset
+// with ds_read_b128 hit distinct banks.
+//
+// Decisions.  A decision class is one (site plan class, number of site rules,
+// ALWAYS mask, hosts_to_skip mask) of the line's scope; its positions are the
+// host's site rules then the global rules (<= 64 in all).  Per class and
+// literal id (rulesets of <= 32 interned literals) one row holds:
+//   eq   positions a hit of the literal matches outright (equivalent literal
+//        rules, literal not host-split),
+//   job  positions a hit sends to the automaton (non-equivalent literal rules),
+//   lm   positions whose rule requires the literal (the overflow rule: a line
+//        with more hits than slots sends a literal rule to its automaton when
+//        one of its literals occurred),
+//   chk  checks run around the hit: a template A + host + C (kPlanLitT) or a
+//        host-split full literal (kPlanLit, equivalent), decided or sent to the
+//        automaton per plan_rule / plan_rule_lds.
+// Anchored and no-literal entries (kPlanAnchor, kPlanAnchorT, kPlanScan) are
+// listed per class and evaluated on every line of the class, as before.  The
+// decisions equal decide_plan_lds': the same entries, each decided by the same
+// test, a DFA job wherever that test leaves the rule open (k_dfa decides those
+// exactly, so a job for a rule also matched here is dropped, J & ~m).
+
+constexpr uint32_t kL2Win = 112;  // bytes of each line's window (odd multiple of 16)
+constexpr int kL2Block = 512;     // 8 waves; two blocks per CU
+constexpr uint32_t kL2WaveLds = 64 * kL2Win + kWaveJobBytes;
+constexpr uint32_t kL2TabMax = 20 * 1024;  // hl blob with the k_lines2 tables (LDS, per block)
+constexpr uint32_t kL2ChkTmpl = 1, kL2ChkFull = 2;
+constexpr uint32_t kL2DclsWords = 16, kL2RowWords = 8, kL2Lits = 32, kL2AncWords = 12;
+
+// positions <-> bits
+__device__ __forceinline__ uint64_t l2_bit(uint32_t p) { return 1ull << p; }
+
+// up to four spaces of mask m (bit i = line byte base + i) appended to sp0..sp3
+__device__ __forceinline__ void l2_take_spaces(uint64_t m, int32_t base, uint32_t &ns, uint32_t &sp0, uint32_t &sp1,
+                                               uint32_t &sp2, uint32_t &sp3) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool has = m != 0 && ns < 4;
+    const uint32_t pos = (uint32_t)((int32_t)__ffsll((unsigned long long)m) - 1 + base);
+    m &= m - 1;
+    sp0 = has && ns == 0 ? pos : sp0;
+    sp1 = has && ns == 1 ? pos : sp1;
+    sp2 = has && ns == 2 ? pos : sp2;
+    sp3 = has && ns == 3 ? pos : sp3;
+    ns += has ? 1u : 0u;
+  }
+}
+
+// first four spaces of line bytes [0, n): the window (line byte o at win[sk +
+// o]) 64 bytes at a time, then HBM past it (gp = line start)
+__device__ __forceinline__ uint32_t l2_spaces(const uint8_t *win, uint32_t sk, const uint8_t *gp, uint32_t n, uint32_t &sp0,
+                                              uint32_t &sp1, uint32_t &sp2, uint32_t &sp3) {
+  const uint4 *w = reinterpret_cast<const uint4 *>(win);
+  uint32_t ns = 0;
+  {
+    const uint4 v0 = w[0], v1 = w[1], v2 = w[2], v3 = w[3];
+    uint64_t m = (uint64_t)space_mask16(v0) | ((uint64_t)space_mask16(v1) << 16) | ((uint64_t)space_mask16(v2) << 32) |
+                 ((uint64_t)space_mask16(v3) << 48);
+    m &= ~((1ull << sk) - 1ull);
+    if (sk + n < 64) m &= (1ull << (sk + n)) - 1ull;
+    l2_take_spaces(m, -(int32_t)sk, ns, sp0, sp1, sp2, sp3);
+  }
+  if (ns < 4 && sk + n > 64) {
+    const uint4 v4 = w[4], v5 = w[5], v6 = w[6];
+    uint64_t m = (uint64_t)space_mask16(v4) | ((uint64_t)space_mask16(v5) << 16) | ((uint64_t)space_mask16(v6) << 32);
+    if (sk + n < kL2Win) m &= (1ull << (sk + n - 64)) - 1ull;
+    l2_take_spaces(m, 64 - (int32_t)sk, ns, sp0, sp1, sp2, sp3);
+  }
+  const uint32_t lim = kL2Win - sk;
+  if (ns < 4 && n > lim) {  // a header longer than the window: the rest from HBM
+    uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+    const uint32_t nq = find_spaces(gp + lim, n - lim, q0, q1, q2, q3);
+    const uint32_t q[4] = {q0, q1, q2, q3};
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const bool has = k < nq && ns < 4;
+      const uint32_t pos = q[k] + lim;
+      sp0 = has && ns == 0 ? pos : sp0;
+      sp1 = has && ns == 1 ? pos : sp1;
+      sp2 = has && ns == 2 ? pos : sp2;
+      sp3 = has && ns == 3 ? pos : sp3;
+      ns += has ? 1u : 0u;
+    }
+  }
+  return ns;
+}
+
+struct L2Line {
+  const uint8_t *wp;  // LDS: line byte 0 in the window
+  const uint8_t *gp;  // HBM: line byte 0
+  uint32_t lim;       // line bytes [0, lim) are in the window
+  uint32_t n;         // line length
+};
+// [o, o + len) plus ld4's slack lies in the window
+__device__ __forceinline__ bool l2_in(const L2Line &X, uint32_t o, uint32_t len) { return o + len + 8 <= X.lim; }
+
+// one anchored / no-literal entry (a, b) at position pos of the class
+// (plan_rule / plan_rule_lds for kinds kPlanAnchor, kPlanAnchorT, kPlanScan):
+// 1 = matched, 2 = DFA job, 0 = no match
+template <bool LDS_TEXT>
+__device__ __forceinline__ uint32_t l2_anchored(const Bind &B, const Tabs &T, const LdsTabs &LT, const uint4 a, const uint4 b,
+                                                uint32_t r, const uint8_t *rest, uint32_t rest_len, uint32_t host_rel,
+                                                uint32_t host_len) {
+  const uint32_t kind = (a.x >> 27) & 7u;
+  const bool eq = ((a.x >> 30) & 1u) != 0;
+  if (kind == kPlanScan) return 2;
+  if (kind == kPlanAnchorT) {
+    if (!tmpl_at(LT, a.w, rest, rest_len, host_rel, host_len, 0)) return 0;
+    return eq ? 1u : 2u;
+  }
+  // kPlanAnchor
+  const uint4 qa = make_uint4(a.y, a.z, b.x, b.y), qb = make_uint4(b.z, b.w, 0, 0);
+  const uint32_t qk = anchor_quick(qa, qb, rest, rest_len);
+  if (qk == 0) return 0;
+  if (qk == 1 && ((qa.y >> 9) & 1)) return 1;
+  if (a.w) {
+    if (!((a.w >> 16) <= rest_len && literal_at(T, (a.w & 0xFFFFu) - 1, rest))) return 0;
+    return eq ? 1u : 2u;
+  }
+  // dfa_rule's anchored branch: the rule's prefix literals
+  const DevRule &R = B.rules[r];
+  if (R.anc_len) {
+    bool any = false;
+    for (uint32_t i = 0; i < R.anc_len && !any; ++i) {
+      const uint32_t lit = B.rule_lits[R.anc_off + i];
+      any = lit_len_of(T, lit) <= rest_len && literal_at(T, lit, rest);
+    }
+    if (!any) return 0;
+    if (R.anc_equiv) return 1;
+  }
+  return 2;
+}
+
+// one check of a literal's row around its hit at rest offset hp: 1 matched,
+// 2 job, 0 not here (a later hit of the literal may still decide it)
+template <bool LDS_TEXT>
+__device__ __forceinline__ uint32_t l2_check(const Tabs &T, const LdsTabs &LT, const uint4 ck, const uint8_t *rest,
+                                             uint32_t rest_len, uint32_t host_rel, uint32_t host_len, uint32_t hp) {
+  const uint32_t kind = (ck.x >> 8) & 3u;
+  const bool eq = ((ck.x >> 10) & 1u) != 0;
+  if (kind == kL2ChkTmpl) {
+    const uint4 rec = LT.trec[ck.y];
+    const uint32_t la = rec.x & 0xFF;
+    const bool side_c = ((rec.x >> 16) & 1u) != 0;
+    const int32_t fs = side_c ? (int32_t)hp - (int32_t)host_len - (int32_t)la : (int32_t)hp;
+    if (!tmpl_at(LT, ck.y, rest, rest_len, host_rel, host_len, fs)) return 0;
+    return eq ? 1u : 2u;
+  }
+  // host-split full literal of an equivalent rule (plan_rule)
+  const uint32_t fl = ck.y >> 8, off = ck.y & 0xFFu;
+  return hp >= off && hp - off + ck.z <= rest_len && literal_at(T, fl, rest + (hp - off)) ? 1u : 0u;
+}
+
+__device__ __forceinline__ uint4 l2_ld4w(const uint32_t *hl, uint32_t w) { return *reinterpret_cast<const uint4 *>(hl + w); }
+
+__global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
+  uint32_t *s_hl = reinterpret_cast<uint32_t *>(s_dyn);
+  for (uint32_t i = threadIdx.x; i < B.l2_bytes / 16; i += blockDim.x)
+    reinterpret_cast<uint4 *>(s_hl)[i] = reinterpret_cast<const uint4 *>(B.hl)[i];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint8_t *wbase = s_dyn + B.l2_bytes + wave * kL2WaveLds;
+  uint8_t *win = wbase + lane * kL2Win;
+  JobSink S;
+  S.lds = reinterpret_cast<uint2 *>(wbase + 64 * kL2Win);
+  S.cnt = reinterpret_cast<uint32_t *>(S.lds + kWaveJobs);
+  S.jline = A.jline;
+  S.jkey = A.jkey;
+  S.count = A.job_count;
+  S.cap = A.job_cap;
+  if (lane == 0) *S.cnt = 0;
+  wave_sync();
+  const Tabs TB = make_tabs(B.img, B.il);
+  LdsTabs LT;
+  LT.hinfo = reinterpret_cast<const uint2 *>(s_hl + B.lt_hinfo);
+  LT.cls = reinterpret_cast<const uint4 *>(s_hl + B.lt_cls);
+  LT.trec = reinterpret_cast<const uint4 *>(s_hl + B.lt_trec);
+  LT.pool = reinterpret_cast<const uint8_t *>(s_hl + B.lt_pool);
+  const Lines &L = A.L;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + wave * 64u; base < A.n_lines; base += stride) {
+    const uint64_t j = base + lane;
+    const bool act = j < A.n_lines;
+    uint64_t s = 0;
+    uint32_t n = 0;
+    CandMeta cm{0, 0, 0};
+    uint64_t cv[kCandSlots] = {0, 0, 0, 0};
+    if (act) {
+      s = j ? A.nl[j - 1] + 1 : 0;
+      n = (uint32_t)(A.nl[j] - s);
+      if (B.any_prefilter) {
+        cm = L.cand_meta[j];
+        const ulonglong2 *cp = reinterpret_cast<const ulonglong2 *>(L.cand + j * kCandSlots);
+#pragma unroll
+        for (int k = 0; k < kCandSlots / 2; ++k) {
+          const ulonglong2 w = cp[k];
+          cv[2 * k] = w.x;
+          cv[2 * k + 1] = w.y;
+        }
+      }
+    }
+    // ---- the line's window: 16 B-aligned pieces from its first byte
+    const uint64_t a0 = s & ~15ull;
+    const uint32_t sk = (uint32_t)(s - a0);
+    {
+      uint4 v[kL2Win / 16];
+#pragma unroll
+      for (uint32_t k = 0; k < kL2Win / 16; ++k) {
+        const uint64_t a = a0 + 16ull * k;
+        if (a + 16 <= A.n) v[k] = *reinterpret_cast<const uint4 *>(A.buf + a);
+        else {
+          uint32_t w4[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            uint32_t x = 0;
+            for (int bb = 0; bb < 4; ++bb) {
+              const uint64_t p = a + 4 * q + bb;
+              if (p < A.n) x |= (uint32_t)A.buf[p] << (8 * bb);
+            }
+            w4[q] = x;
+          }
+          v[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kL2Win / 16; ++k) reinterpret_cast<uint4 *>(win)[k] = v[k];
+    }
+    if (act) {
+      L2Line X;
+      X.wp = win + sk;
+      X.gp = A.buf + s;
+      X.lim = kL2Win - sk;
+      X.n = n;
+      uint32_t sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
+      const uint32_t ns = l2_spaces(win, sk, X.gp, n, sp0, sp1, sp2, sp3);
+      double f = 0.0;
+      bool slow = false;
+      if (ns >= 4) slow = parse_ts_msec(X.wp, sp0, &f) != 0 && parse_float_fast(X.wp, sp0, &f) != 0;
+      if (ns < 4) {
+        L.flags[j] = kLineError;
+        L.counts[j] = 0;
+      } else if (slow) {  // exotic timestamp token: the per-line fallback
+        L.flags[j] = kLineSlowTs;
+        L.counts[j] = 0;
+        push_list(A.slow_list, A.slow_count, j);
+      } else {
+        const uint32_t ip_off = sp0 + 1, ip_len = sp1 - sp0 - 1;
+        const uint32_t rest_off = sp1 + 1, host_off = sp2 + 1, host_len = sp3 - sp2 - 1;
+        const bool hostw = l2_in(X, host_off, host_len);
+        const int32_t hid = hostw ? host_lookup_lds(s_hl, X.wp + host_off, host_len)
+                                  : host_lookup_lds(s_hl, X.gp + host_off, host_len);
+        const uint32_t dc = hid >= 0 ? s_hl[B.l2_hdc + (uint32_t)hid] : B.l2_none;
+        const uint32_t dw = B.l2_dcls + dc * kL2DclsWords;
+        const uint4 d0 = l2_ld4w(s_hl, dw), d1 = l2_ld4w(s_hl, dw + 4), d2 = l2_ld4w(s_hl, dw + 8), d3 = l2_ld4w(s_hl, dw + 12);
+        const uint64_t alw = ((uint64_t)d0.y << 32) | d0.x, skp = ((uint64_t)d0.w << 32) | d0.z;
+        const uint64_t anyhit = ((uint64_t)d1.y << 32) | d1.x, anyovf = ((uint64_t)d1.w << 32) | d1.z;
+        const uint32_t rows = d2.x, prule = d2.y, anc = d2.z, n_anc = d2.w;
+        const uint32_t first_rule = hid >= 0 ? LT.hinfo[hid].y : 0u;
+        (void)d3;
+        const bool exempt = B.any_allow && check_is_allowed(B, hid, X.gp + ip_off, ip_len);
+        const int64_t tsn = ns_from_seconds(f);
+        uint8_t fl = 0;
+        if (go_sub(A.now_ns, tsn) > 10000000000LL) fl = kLineOld;
+        else if (exempt) fl = kLineExempt;
+        const uint32_t rest_len = n - rest_off, host_rel = host_off - rest_off;
+        uint64_t m = alw, J = 0;
+        if (fl) {
+          L.counts[j] = 0;
+        } else {
+          // literal hits of the scan pass inside rest (unverified ones checked here)
+          const uint32_t cc = cm.cnt;
+          const bool ovf = cc > (uint32_t)kCandSlots;
+          const uint64_t rs = s + rest_off;
+          uint64_t ovbits = 0, done = 0;
+          uint32_t nlit = 0;
+#pragma unroll
+          for (uint32_t c = 0; c < (uint32_t)kCandSlots; ++c) {
+            if (c >= cc) break;
+            const uint64_t v = cv[c];
+            const uint32_t lit = (uint32_t)(v & 0x7FFFFF);
+            const uint64_t q = v >> 24;
+            if (q < rs) continue;
+            if (!(v & kCandVerified)) {
+              const uint32_t o = (uint32_t)(q - s), ll = lit_len_of(TB, lit);
+              if (o + ll > n) continue;
+              if (!(l2_in(X, o, ll) ? literal_at(TB, lit, X.wp + o) : literal_at(TB, lit, X.gp + o))) continue;
+            }
+            ovbits |= 1ull << (lit & 31);
+            ++nlit;
+            if (ovf) continue;
+            const uint32_t hp = q - rs < 0xFFFF ? (uint32_t)(q - rs) : 0xFFFFu;
+            const uint32_t rw = rows + (lit & 31) * kL2RowWords;
+            const uint4 ra = l2_ld4w(s_hl, rw), rb = l2_ld4w(s_hl, rw + 4);
+            m |= ((uint64_t)ra.y << 32) | ra.x;
+            J |= ((uint64_t)ra.w << 32) | ra.z;
+            for (uint32_t k = 0; k < rb.w; ++k) {
+              const uint4 ck = l2_ld4w(s_hl, rb.z + 4 * k);
+              const uint64_t bit = l2_bit(ck.x & 0xFFu);
+              if (done & bit) continue;
+              uint32_t out;
+              if (hp == 0xFFFFu) out = 2;  // hit offset unknown: the automaton decides
+              else {
+                // in the window: the checked text (ck.w bytes from the hit, plus the
+                // host for a template that spells it after the hit) and the host field
+                const uint32_t tail = ck.w + (((ck.x >> 11) & 1u) ? host_len : 0u);
+                const bool inw = hostw && rest_off + hp + tail + 8 <= X.lim;
+                out = inw ? l2_check<true>(TB, LT, ck, X.wp + rest_off, rest_len, host_rel, host_len, hp)
+                          : l2_check<false>(TB, LT, ck, X.gp + rest_off, rest_len, host_rel, host_len, hp);
+              }
+              if (out) {
+                done |= bit;
+                if (out == 1) m |= bit;
+                else J |= bit;
+              }
+            }
+          }
+          if (ovf) {
+            // more hits than slots: a literal rule none of whose literals occurred
+            // cannot match; the others go to their automaton
+            ovbits |= cm.bits & 0xFFFFFFFFull;
+            uint64_t ob = ovbits;
+            while (ob) {
+              const uint32_t l = (uint32_t)__ffsll((unsigned long long)ob) - 1;
+              ob &= ob - 1;
+              const uint4 rb = l2_ld4w(s_hl, rows + l * kL2RowWords + 4);
+              J |= ((uint64_t)rb.y << 32) | rb.x;
+            }
+            J |= anyovf;
+          } else if (nlit) {
+            J |= anyhit;
+          }
+          // anchored and no-literal entries of the class, wave-uniform per class
+          uint32_t todo_anc = n_anc ? 1u : 0u;
+          while (__ballot(todo_anc) != 0) {
+            const uint32_t f0 = (uint32_t)__ffsll((unsigned long long)__ballot(todo_anc)) - 1;
+            const uint32_t cur = __builtin_amdgcn_readlane(dc, f0);
+            if (todo_anc && dc == cur) {
+              todo_anc = 0;
+              const uint32_t na = __builtin_amdgcn_readlane(n_anc, f0), ab = __builtin_amdgcn_readlane(anc, f0);
+              for (uint32_t i = 0; i < na; ++i) {
+                const uint32_t ew = ab + kL2AncWords * i;
+                const uint4 a = l2_ld4w(s_hl, ew), bq = l2_ld4w(s_hl, ew + 4);
+                const uint32_t ext = s_hl[ew + 8];
+                const uint32_t pos = (a.x >> 20) & 0x7Fu;
+                const uint32_t r = (a.x & kPlanOwn) ? first_rule + pos : (a.x & 0xFFFFFu);
+                // in the window: the bytes of rest the entry may read (ext, plus the
+                // host for a template) and the host field
+                const uint32_t need = (ext & 0x7FFFFFFFu) + ((ext >> 31) ? host_len : 0u);
+                const bool inw = hostw && rest_off + need + 8 <= X.lim;
+                const uint32_t out = inw ? l2_anchored<true>(B, TB, LT, a, bq, r, X.wp + rest_off, rest_len, host_rel, host_len)
+                                         : l2_anchored<false>(B, TB, LT, a, bq, r, X.gp + rest_off, rest_len, host_rel, host_len);
+                if (out == 1) m |= l2_bit(pos);
+                else if (out == 2) J |= l2_bit(pos);
+              }
+            }
+          }
+          J &= ~m;
+          while (J) {
+            const uint32_t p = (uint32_t)__ffsll((unsigned long long)J) - 1;
+            J &= J - 1;
+            const uint32_t w = s_hl[prule + p];
+            emit_job(S, j, (w & kPlanOwn) ? first_rule + p : (w & 0xFFFFFu), p);
+          }
+          L.masks[j * B.mask_words] = m;
+          if (B.mask_words > 1) L.masks[j * B.mask_words + 1] = 0;
+          L.counts[j] = ((uint64_t)__popcll(m) << 32) | (uint64_t)__popcll(m & ~skp);
+        }
+        L.ip_off[j] = ip_off;
+        L.ip_len[j] = ip_len;
+        L.rest_off[j] = rest_off;
+        L.host_off[j] = host_off;
+        L.host_len[j] = host_len;
+        L.host_id[j] = hid;
+        if (l2_in(X, ip_off, ip_len > 16 ? ip_len : 16u)) {
+          L.ip_hash[j] = hash_bytes(X.wp + ip_off, ip_len);
+          L.ip16[j] = ip_key16(X.wp + ip_off, ip_len);
+        } else {
+          L.ip_hash[j] = hash_bytes(X.gp + ip_off, ip_len);
+          L.ip16[j] = ip_key16(X.gp + ip_off, ip_len);
+        }
+        L.ts[j] = tsn;
+        L.flags[j] = fl;
+      }
+    }
+    // ---- append this wave's DFA jobs (one global atomic per 64 lines)
+    wave_sync();
+    const uint32_t nj = min(*S.cnt, kWaveJobs);
+    if (nj) {
+      unsigned long long jb = 0;
+      if (lane == 0) jb = atomicAdd(A.job_count, (unsigned long long)nj);
+      jb = __shfl(jb, 0);
+      for (uint32_t i = lane; i < nj; i += 64)
+        if (jb + i < A.job_cap) { A.jline[jb + i] = S.lds[i].x; A.jkey[jb + i] = S.lds[i].y; }
+    }
+    wave_sync();
+    if (lane == 0) *S.cnt = 0;
+    wave_sync();
+  }
+}

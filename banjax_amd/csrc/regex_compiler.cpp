@@ -16,6 +16,7 @@
 // Accepting is absorbing (boolean match), so the device loop stops at the
 // first ACCEPT or DEAD state.
 #include "regex_compiler.h"
+#include "go_limits.h"
 
 #include <algorithm>
 #include <atomic>
@@ -196,6 +197,7 @@ const char *kErrMissingRepeatArg = "missing argument to repetition operator";
 const char *kErrTrailingBackslash = "trailing backslash at end of expression";
 const char *kErrUnexpectedParen = "unexpected )";
 const char *kErrNestingDepth = "expression nests too deeply";
+const char *kErrLarge = "expression too large";
 
 struct Group { const char *name; int sign; std::vector<int32_t> r; };
 const std::vector<Group> &perl_groups() {
@@ -233,11 +235,29 @@ const std::vector<Group> &posix_groups() {
   return g;
 }
 
+struct SimpleFold {
+  int32_t operator()(int32_t r) const { return simple_fold(r); }
+};
+
 class Parser {
  public:
-  Parser(const std::string &s) : whole_(s) {}
+  Parser(const std::string &s) : whole_(s), gs_(SimpleFold()) {}
 
+  // Go's size and nesting limits are checked on the way (go_limits.h), at the
+  // point of the parse where regexp/syntax would stop
   ReP parse() {
+    try {
+      return parse_all();
+    } catch (const gosh::Limit &l) {
+      throw ParseError{l.large ? kErrLarge : kErrNestingDepth, whole_};
+    }
+  }
+
+ private:
+  // Go's parse flags of the current position (FoldCase, NonGreedy)
+  uint32_t gf() const { return ((flags_ & kFold) ? gosh::fFold : 0u) | ((flags_ & kNonGreedy) ? gosh::fNonGreedy : 0u); }
+
+  ReP parse_all() {
     const char *t = whole_.data(), *end = whole_.data() + whole_.size();
     const char *last_repeat = nullptr;
     while (t < end) {
@@ -250,11 +270,13 @@ class Parser {
           ++t;
           break;
         case '|':
+          gs_.vertical_bar(gf());
           concat();
           if (!swap_vbar()) push(std::make_unique<Re>(kVBar, flags_));
           ++t;
           break;
         case ')': {
+          gs_.right_paren(gf());
           concat();
           if (swap_vbar()) stack_.pop_back();
           alternate();
@@ -270,9 +292,15 @@ class Parser {
           ++t;
           break;
         }
-        case '^': push(std::make_unique<Re>((flags_ & kOneLine) ? kBOT : kBOL, flags_)); ++t; break;
-        case '$': push(std::make_unique<Re>((flags_ & kOneLine) ? kEOT : kEOL, flags_)); ++t; break;
-        case '.': push(std::make_unique<Re>((flags_ & kDotNL) ? kAnyChar : kAnyNotNL, flags_)); ++t; break;
+        case '^':
+          gs_.op((flags_ & kOneLine) ? gosh::gBeginText : gosh::gBeginLine, gf());
+          push(std::make_unique<Re>((flags_ & kOneLine) ? kBOT : kBOL, flags_)); ++t; break;
+        case '$':
+          gs_.op((flags_ & kOneLine) ? gosh::gEndText : gosh::gEndLine, gf() | ((flags_ & kOneLine) ? gosh::fWasDollar : 0u));
+          push(std::make_unique<Re>((flags_ & kOneLine) ? kEOT : kEOL, flags_)); ++t; break;
+        case '.':
+          gs_.op((flags_ & kDotNL) ? gosh::gAnyChar : gosh::gAnyCharNotNL, gf());
+          push(std::make_unique<Re>((flags_ & kDotNL) ? kAnyChar : kAnyNotNL, flags_)); ++t; break;
         case '[': t = parse_class(t, end); break;
         case '*': case '+': case '?': {
           Op op = *t == '*' ? kStar : (*t == '+' ? kPlus : kQuest);
@@ -301,26 +329,19 @@ class Parser {
       }
       last_repeat = repeat;
     }
+    gs_.end(gf());
     concat();
     if (swap_vbar()) stack_.pop_back();
     alternate();
     if (stack_.size() != 1) throw ParseError{kErrMissingParen, whole_};
-    ReP root = std::move(stack_[0]);
-    if (height(root.get()) > 1000) throw ParseError{kErrNestingDepth, whole_};
-    return root;
+    return std::move(stack_[0]);
   }
 
- private:
   const std::string &whole_;
   uint32_t flags_ = kClassNL | kOneLine | kPerlX;
   int ncap_ = 0;
   std::vector<ReP> stack_;
-
-  static int height(const Re *r) {
-    int h = 0;
-    for (auto &s : r->sub) h = std::max(h, height(s.get()));
-    return h + 1;
-  }
+  gosh::GoShape<SimpleFold> gs_;
 
   int32_t next_rune(const char *t, const char *end, int *w) {
     int32_t c = decode_rune(reinterpret_cast<const uint8_t *>(t), static_cast<size_t>(end - t), w);
@@ -330,11 +351,13 @@ class Parser {
 
   void push(ReP r) { stack_.push_back(std::move(r)); }
   void push_paren(int cap) {
+    gs_.op(gosh::gLeftParen, gf(), cap);
     auto p = std::make_unique<Re>(kLParen, flags_);
     p->cap = cap;
     push(std::move(p));
   }
   void literal(int32_t r) {
+    gs_.literal(r, gf());
     auto n = std::make_unique<Re>(kLit, flags_);
     n->rune = r;
     push(std::move(n));
@@ -399,6 +422,8 @@ class Parser {
     n->max = mx;
     n->sub.push_back(std::move(stack_.back()));
     stack_.back() = std::move(n);
+    gs_.repeat(op == kStar ? gosh::gStar : op == kPlus ? gosh::gPlus : op == kQuest ? gosh::gQuest : gosh::gRepeat, mn, mx,
+               ((f & kFold) ? gosh::fFold : 0u) | ((f & kNonGreedy) ? gosh::fNonGreedy : 0u));
     if (op == kRepeat && (mn >= 2 || mx >= 2) && !repeat_valid(stack_.back().get(), 1000))
       throw ParseError{kErrInvalidRepeatSize, std::string(before, after)};
     return after;
@@ -608,6 +633,7 @@ class Parser {
     ++t;
     clean(re->cls);
     if (sign < 0) negate(re->cls);
+    gs_.char_class(re->cls, gf());
     push(std::move(re));
     return t;
   }
@@ -673,9 +699,9 @@ class Parser {
   const char *parse_backslash(const char *t, const char *end) {
     if ((flags_ & kPerlX) && end - t >= 2) {
       switch (t[1]) {
-        case 'A': push(std::make_unique<Re>(kBOT, flags_)); return t + 2;
-        case 'b': push(std::make_unique<Re>(kWB, flags_)); return t + 2;
-        case 'B': push(std::make_unique<Re>(kNWB, flags_)); return t + 2;
+        case 'A': gs_.op(gosh::gBeginText, gf()); push(std::make_unique<Re>(kBOT, flags_)); return t + 2;
+        case 'b': gs_.op(gosh::gWordBoundary, gf()); push(std::make_unique<Re>(kWB, flags_)); return t + 2;
+        case 'B': gs_.op(gosh::gNoWordBoundary, gf()); push(std::make_unique<Re>(kNWB, flags_)); return t + 2;
         case 'C': throw ParseError{kErrInvalidEscape, std::string(t, t + 2)};
         case 'Q': {
           const char *q = t + 2, *e = nullptr;
@@ -685,16 +711,18 @@ class Parser {
           while (q < lend) { int w; int32_t c = next_rune(q, lend, &w); literal(c); q += w; }
           return e ? e + 2 : end;
         }
-        case 'z': push(std::make_unique<Re>(kEOT, flags_)); return t + 2;
+        case 'z': gs_.op(gosh::gEndText, gf()); push(std::make_unique<Re>(kEOT, flags_)); return t + 2;
         default: break;
       }
     }
+    gs_.esc_alloc();  // parse's backslash case allocates a class node before it knows
     {
       Ranges u;
       if (const char *nt = parse_unicode_class(t, end, u)) {
         auto re = std::make_unique<Re>(kClass, flags_);
         re->cls.swap(u);
         clean(re->cls);
+        gs_.esc_class(re->cls, gf());
         push(std::move(re));
         return nt;
       }
@@ -703,9 +731,11 @@ class Parser {
       auto re = std::make_unique<Re>(kClass, flags_);
       append_group(re->cls, *g);
       clean(re->cls);
+      gs_.esc_class(re->cls, gf());
       push(std::move(re));
       return t + 2;
     }
+    gs_.esc_free();
     const char *rest;
     int32_t c = parse_escape(t, end, &rest);
     literal(c);
@@ -1958,6 +1988,19 @@ void set_force_wide_nfa(bool on) { g_force_wide = on; }
 void set_dfa_state_cap(uint32_t cap) { g_dfa_state_cap = cap ? cap : kDfaStateCap; }
 uint32_t dfa_state_cap() { return g_dfa_state_cap; }
 
+// syntax.Parse alone: Go's accept / reject decision and error text for a
+// pattern, without building its automaton (bjx_debug_regex_parse)
+int parse_regex_only(const std::string &pattern, std::string *err) {
+  try {
+    Parser p(pattern);
+    p.parse();
+  } catch (const ParseError &e) {
+    if (err) *err = "error parsing regexp: " + e.code + ": `" + e.expr + "`";
+    return BJX_ERR_REGEX;
+  }
+  return BJX_OK;
+}
+
 int compile_regex(const std::string &pattern, CompiledRegex *out, std::string *err, uint32_t max_dfa_states) {
   ReP root;
   try {
@@ -2177,3 +2220,16 @@ bool dfa_match_host(const CompiledRegex &rx, const uint8_t *text, size_t n) {
 }
 
 }  // namespace bjx
+
+// Test hook (banjax_gpu_debug.h): regexp/syntax's parse decision for one pattern
+extern "C" int bjx_debug_regex_parse(const char *pat, size_t len, char *err, size_t err_len) {
+  if (!pat && len) return BJX_ERR_ARG;
+  std::string e;
+  const int rc = bjx::parse_regex_only(std::string(pat ? pat : "", len), &e);
+  if (err && err_len) {
+    const size_t k = std::min(err_len - 1, e.size());
+    memcpy(err, e.data(), k);
+    err[k] = 0;
+  }
+  return rc;
+}

@@ -159,6 +159,7 @@ struct CompiledRegex {
 
 // Returns 0 on success; otherwise a negative bjx_status with *err set to the
 // Go-style message ("error parsing regexp: <code>: `<expr>`").
+int parse_regex_only(const std::string &pattern, std::string *err);
 int compile_regex(const std::string &pattern, CompiledRegex *out, std::string *err,
                   uint32_t max_dfa_states = 40000);
 

@@ -22,6 +22,9 @@ size_t bjx_debug_rule_literal(const bjx_ruleset *rs, size_t rule_idx, char *out,
    literals (its DFA jobs start near the first hit): that distance in bytes;
    -1 for every other rule */
 int bjx_debug_rule_lead(const bjx_ruleset *rs, size_t rule_idx);
+/* Test hook: regexp/syntax's parse of one pattern alone (accept / refuse and
+   Go's error text, e.g. the "expression too large" limits), no automaton. */
+int bjx_debug_regex_parse(const char *pattern, size_t len, char *err, size_t err_len);
 /* device ms of the last batch's phases: framing count, scan, per-line resolve,
    emit, capacity check, IP/state slot claim, sort + automaton, trips
    (returns the phase count) */

@@ -17,10 +17,11 @@
  * UnicodeGroups (\pL, \p{Greek}, \P{..}, \p{^..}) follow parse.go's
  * parseUnicodeClass / unicodeTable of Go 1.25 over the Unicode 15.0.0 tables of
  * third_party/unicode/unicode_tables.h (tools/gen_unicode_tables.py).
- * Known gap: Go's ErrLarge / ErrNestingDepth size limits are
- * approximated by a depth check.
+ * Go's ErrLarge / ErrNestingDepth parse limits are replayed on Go's own parse
+ * shapes by go_limits.c, event by event as the parser below runs.
  */
 #include "go_regexp.h"
+#include "go_limits.h"
 
 #include <stdint.h>
 #include <stdio.h>
@@ -164,6 +165,7 @@ typedef struct {
   int ncap;
   char *err; size_t errlen;
   int failed;
+  GoLim *gl;  /* Go's size / nesting limits (go_limits.c) */
 } P;
 
 static const char *E_INVALID_CHAR_CLASS = "invalid character class";
@@ -180,6 +182,7 @@ static const char *E_MISSING_REPEAT_ARG = "missing argument to repetition operat
 static const char *E_TRAILING_BACKSLASH = "trailing backslash at end of expression";
 static const char *E_UNEXPECTED_PAREN = "unexpected )";
 static const char *E_NESTING_DEPTH = "expression nests too deeply";
+static const char *E_LARGE = "expression too large";
 
 /* Go: "error parsing regexp: " + code + ": `" + expr + "`" */
 static void fail(P *p, const char *code, const char *expr, size_t elen) {
@@ -199,6 +202,15 @@ static void fail(P *p, const char *code, const char *expr, size_t elen) {
   }
 }
 
+/* Go flags of the current position for go_limits.c (FoldCase, NonGreedy) */
+static unsigned gfl(const P *p) { return (unsigned)(p->flags & (F_FOLD | F_NONGREEDY)); }
+/* a limit crossed at this point of the parse becomes the parse error */
+static int lim_check(P *p) {
+  const int f = p->gl ? golim_failed(p->gl) : 0;
+  if (f && !p->failed) fail(p, f == 1 ? E_LARGE : E_NESTING_DEPTH, p->whole, p->wlen);
+  return p->failed;
+}
+
 /* nextRune: decode one rune of the pattern; invalid UTF-8 is an error. */
 static int next_rune(P *p, const char *t, size_t tl, int *w) {
   int width;
@@ -216,9 +228,13 @@ static void push(P *p, Node *n) {
   if (p->nst == p->cst) { p->cst = p->cst ? p->cst * 2 : 16; p->st = realloc(p->st, sizeof(Node *) * p->cst); }
   p->st[p->nst++] = n;
 }
-static void op_push(P *p, int op) { push(p, node_new(op, p->flags)); }
+static void op_push(P *p, int op) {
+  golim_op(p->gl, op, gfl(p), 0);
+  push(p, node_new(op, p->flags));
+}
 
 static void literal(P *p, int r) {
+  golim_literal(p->gl, r, gfl(p));
   Node *n = node_new(OP_LIT, p->flags);
   n->rune = r;
   push(p, n);
@@ -289,6 +305,8 @@ static const char *do_repeat(P *p, int op, int min, int max, const char *before,
   n->min = min; n->max = max;
   node_add(n, p->st[p->nst - 1]);
   p->st[p->nst - 1] = n;
+  golim_repeat(p->gl, op, min, max, (unsigned)(flags & (F_FOLD | F_NONGREEDY)));
+  if (lim_check(p)) return NULL;
   if (op == OP_REPEAT && (min >= 2 || max >= 2) && !repeat_valid(n, 1000)) {
     fail(p, E_INVALID_REPEAT_SIZE, before, (size_t)(after - before));
     return NULL;
@@ -617,6 +635,7 @@ static const char *parse_class(P *p, const char *s, const char *end) {
   t++; /* ']' */
   rv_clean(&re->cls);
   if (sign < 0) rv_negate(&re->cls);
+  golim_class(p->gl, re->cls.r, re->cls.n / 2, gfl(p));
   push(p, re);
   return t;
 }
@@ -642,6 +661,7 @@ static const char *parse_perl_flags(P *p, const char *s, const char *end) {
     size_t nlen = (size_t)(gt - name);
     if (!valid_capture_name(name, nlen)) { fail(p, E_INVALID_NAMED_CAPTURE, s, (size_t)(gt + 1 - s)); return NULL; }
     p->ncap++;
+    golim_op(p->gl, OP_LPAREN, gfl(p), p->ncap);
     Node *lp = node_new(OP_LPAREN, p->flags);
     lp->cap = p->ncap;
     push(p, lp);
@@ -664,7 +684,7 @@ static const char *parse_perl_flags(P *p, const char *s, const char *end) {
       sign = -1; flags = ~flags; saw = 0; continue;
     case ':': case ')':
       if (sign < 0) { if (!saw) goto bad; flags = ~flags; }
-      if (c == ':') { Node *lp = node_new(OP_LPAREN, p->flags); lp->cap = 0; push(p, lp); }
+      if (c == ':') { golim_op(p->gl, OP_LPAREN, gfl(p), 0); Node *lp = node_new(OP_LPAREN, p->flags); lp->cap = 0; push(p, lp); }
       p->flags = flags;
       return t;
     default:
@@ -686,6 +706,7 @@ static Node *parse(const char *s, size_t len, char *err, size_t errlen) {
   P p = {0};
   p.whole = s; p.wlen = len; p.err = err; p.errlen = errlen;
   p.flags = F_CLASSNL | F_ONELINE | F_PERLX;
+  p.gl = golim_new(simple_fold);
   const char *t = s, *end = s + len;
   const char *last_repeat = NULL;
   while (t < end && !p.failed) {
@@ -697,15 +718,20 @@ static Node *parse(const char *s, size_t len, char *err, size_t errlen) {
         break;
       }
       p.ncap++;
+      golim_op(p.gl, OP_LPAREN, gfl(&p), p.ncap);
       { Node *lp = node_new(OP_LPAREN, p.flags); lp->cap = p.ncap; push(&p, lp); }
       t++;
       break;
     case '|':
+      golim_vertical_bar(p.gl, gfl(&p));
+      if (lim_check(&p)) break;
       concat(&p);
       if (!swap_vbar(&p)) op_push(&p, OP_VBAR);
       t++;
       break;
     case ')': {
+      golim_right_paren(p.gl, gfl(&p));
+      if (lim_check(&p)) break;
       concat(&p);
       if (swap_vbar(&p)) pop_free(&p);
       alternate(&p);
@@ -723,7 +749,8 @@ static Node *parse(const char *s, size_t len, char *err, size_t errlen) {
     case '^':
       op_push(&p, (p.flags & F_ONELINE) ? OP_BOT : OP_BOL); t++; break;
     case '$':
-      op_push(&p, (p.flags & F_ONELINE) ? OP_EOT : OP_EOL); t++; break;
+      golim_op(p.gl, (p.flags & F_ONELINE) ? OP_EOT : OP_EOL, gfl(&p) | ((p.flags & F_ONELINE) ? 256u : 0u), 0);
+      push(&p, node_new((p.flags & F_ONELINE) ? OP_EOT : OP_EOL, p.flags)); t++; break;
     case '.':
       op_push(&p, (p.flags & F_DOTNL) ? OP_ANY : OP_ANYNL); t++; break;
     case '[':
@@ -773,11 +800,13 @@ static Node *parse(const char *s, size_t len, char *err, size_t errlen) {
         }
         if (done) break;
       }
+      golim_esc_alloc(p.gl);  /* parse's backslash case allocates a class node first */
       if (end - t >= 2 && (t[1] == 'p' || t[1] == 'P')) {
         Node *re = node_new(OP_CLASS, p.flags);
         const char *nt = parse_unicode_class(&p, t, end, &re->cls);
         if (!nt) { node_free(re); break; }
         rv_clean(&re->cls);
+        golim_esc_class(p.gl, re->cls.r, re->cls.n / 2, gfl(&p));
         push(&p, re);
         t = nt;
         break;
@@ -787,10 +816,12 @@ static Node *parse(const char *s, size_t len, char *err, size_t errlen) {
         Node *re = node_new(OP_CLASS, p.flags);
         append_group(&p, &re->cls, g);
         rv_clean(&re->cls);
+        golim_esc_class(p.gl, re->cls.r, re->cls.n / 2, gfl(&p));
         push(&p, re);
         t += 2;
         break;
       }
+      golim_esc_free(p.gl);
       const char *rest;
       int c = parse_escape(&p, t, end, &rest);
       if (p.failed) break;
@@ -804,8 +835,13 @@ static Node *parse(const char *s, size_t len, char *err, size_t errlen) {
     }
     }
     last_repeat = repeat;
+    lim_check(&p);
   }
   Node *root = NULL;
+  if (!p.failed) {
+    golim_end(p.gl, gfl(&p));
+    lim_check(&p);
+  }
   if (!p.failed) {
     concat(&p);
     if (swap_vbar(&p)) pop_free(&p);
@@ -813,11 +849,11 @@ static Node *parse(const char *s, size_t len, char *err, size_t errlen) {
     if (p.nst != 1) fail(&p, E_MISSING_PAREN, p.whole, p.wlen);
     else {
       root = p.st[0]; p.nst = 0;
-      if (depth(root) > 1000) { fail(&p, E_NESTING_DEPTH, p.whole, p.wlen); node_free(root); root = NULL; }
     }
   }
   for (int i = 0; i < p.nst; i++) node_free(p.st[i]);
   free(p.st);
+  golim_free(p.gl);
   return root;
 }
 
@@ -1025,6 +1061,16 @@ static void compute_prefix(gre *g, Node *root) {
     memcpy(buf + len, tmp, (size_t)k); len += k;
   }
   if (len > 0) { g->prefix = malloc((size_t)len); memcpy(g->prefix, buf, (size_t)len); g->nprefix = len; }
+}
+
+/* syntax.Parse alone (regexp.Compile's accept / reject decision and its error
+   text, without building the program): 0 ok, 1 error (message in err) */
+int gre_parse_check(const char *pat, size_t len, char *err, size_t errlen) {
+  if (err && errlen) err[0] = 0;
+  Node *root = parse(pat, len, err, errlen);
+  if (!root) return 1;
+  node_free(root);
+  return 0;
 }
 
 gre *gre_compile(const char *pat, size_t len, char *err, size_t errlen) {

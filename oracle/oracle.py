@@ -45,6 +45,8 @@ def lib():
         vp, sz, i64, u8p = C.c_void_p, C.c_size_t, C.c_int64, C.POINTER(C.c_uint8)
         L.gre_compile.restype = vp
         L.gre_compile.argtypes = [C.c_char_p, sz, C.c_char_p, sz]
+        L.gre_parse_check.restype = C.c_int
+        L.gre_parse_check.argtypes = [C.c_char_p, sz, C.c_char_p, sz]
         L.gre_match.restype = C.c_int
         L.gre_match.argtypes = [vp, C.c_char_p, sz]
         L.gre_free.argtypes = [vp]
