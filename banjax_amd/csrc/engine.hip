@@ -845,6 +845,54 @@ __device__ __forceinline__ void emit_job(const JobSink &S, uint64_t j, uint32_t 
   if (g < S.cap) { S.jline[g] = v.x; S.jkey[g] = v.y; }
 }
 
+// A wave appends its staged jobs into a chunk of the batch's job array that it
+// takes kJobChunk slots at a time: one global atomic per chunk, not one per
+// 64 lines (a single counter serialises at ~88 atomics per microsecond:
+// MI355X_MICROARCH.md "dequeue").  The chunk's slots left unused at the end
+// become null jobs (key null_key, after every rule id in the job sort); the
+// wave's real jobs are added to *real once.
+constexpr uint32_t kJobChunk = 1024;
+struct JobChunk {
+  uint64_t base = 0;
+  uint32_t left = 0;
+  uint64_t real = 0;
+};
+__device__ __forceinline__ void wave_sync();
+__device__ __forceinline__ void flush_jobs(const JobSink &S, JobChunk &C, uint32_t lane) {
+  wave_sync();
+  const uint32_t cnt = *S.cnt;
+  const uint32_t nj = min(cnt, kWaveJobs);
+  C.real += cnt;  // the staged ones and those past the staging (emit_job's own slots)
+  uint32_t done = 0;
+  while (done < nj) {
+    if (C.left == 0) {
+      unsigned long long b = 0;
+      if (lane == 0) b = atomicAdd(S.count, (unsigned long long)kJobChunk);
+      C.base = __shfl(b, 0);
+      C.left = kJobChunk;
+    }
+    const uint32_t take = min(C.left, nj - done);
+    for (uint32_t i = lane; i < take; i += 64) {
+      const uint64_t g = C.base + i;
+      if (g < S.cap) { S.jline[g] = S.lds[done + i].x; S.jkey[g] = S.lds[done + i].y; }
+    }
+    C.base += take;
+    C.left -= take;
+    done += take;
+  }
+  wave_sync();
+  if (lane == 0) *S.cnt = 0;
+  wave_sync();
+}
+__device__ __forceinline__ void close_jobs(const JobSink &S, JobChunk &C, uint32_t lane, uint32_t null_key,
+                                           unsigned long long *real) {
+  for (uint32_t i = lane; i < C.left; i += 64) {
+    const uint64_t g = C.base + i;
+    if (g < S.cap) { S.jline[g] = 0; S.jkey[g] = null_key; }
+  }
+  if (lane == 0 && C.real) atomicAdd(real, (unsigned long long)C.real);
+}
+
 // One rule whose decision needs its automaton: an anchored prefix may decide
 // it first; otherwise run the DFA here (EMIT = false) or hand it to k_dfa.
 template <bool EMIT>
@@ -1655,7 +1703,9 @@ struct LinesArgs {
   uint32_t *slow_list;
   unsigned long long *slow_count;
   uint32_t *jline, *jkey;
-  unsigned long long *job_count;
+  unsigned long long *job_count;  // job slots taken (chunks)
+  unsigned long long *job_real;   // real jobs (the rest are null jobs, key null_key)
+  uint32_t null_key;
   uint64_t job_cap;
   uint32_t span_bytes;  // LDS staging per wave (0 = read lines from HBM)
   const uint32_t *list; // non-null: process only these lines (n_list of them), unstaged
@@ -1796,6 +1846,7 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
   S.cap = A.job_cap;
   if (lane == 0) *S.cnt = 0;
   wave_sync();
+  JobChunk JC;
   const Lines &L = A.L;
   // this wave's 64 lines, staged whole in LDS with coalesced 16 B loads when
   // they span at most kSpanBytes (otherwise read from HBM per lane)
@@ -1875,21 +1926,11 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
       else line_body<false, PROF, HOST_LDS>(B, TB, A, A.buf, 0, s, n, j, S, cm, cv, P, s_hl);
     }
     if (PROF) P.t = __builtin_amdgcn_s_memtime();
-    // ---- append this wave's DFA jobs (one global atomic per 64 lines)
-    wave_sync();
-    const uint32_t nj = min(*S.cnt, kWaveJobs);
-    if (nj) {
-      unsigned long long jb = 0;
-      if (lane == 0) jb = atomicAdd(A.job_count, (unsigned long long)nj);
-      jb = __shfl(jb, 0);
-      for (uint32_t i = lane; i < nj; i += 64)
-        if (jb + i < A.job_cap) { A.jline[jb + i] = S.lds[i].x; A.jkey[jb + i] = S.lds[i].y; }
-    }
-    wave_sync();
-    if (lane == 0) *S.cnt = 0;
-    wave_sync();
+    // ---- append this wave's DFA jobs (from its chunk of the job array)
+    flush_jobs(S, JC, lane);
     if (PROF) { __builtin_amdgcn_s_waitcnt(0); P.mark(6); }
   }
+  close_jobs(S, JC, lane, A.null_key, A.job_real);
   if (PROF && lane == 0)
     for (int k = 0; k < 10; ++k) atomicAdd(&A.prof[k], (unsigned long long)P.acc[k]);
 }
@@ -1910,6 +1951,8 @@ struct RulesArgs {
   unsigned long long *todo_count;
   uint32_t *jline, *jkey;
   unsigned long long *job_count;
+  unsigned long long *job_real;
+  uint32_t null_key;
   uint64_t job_cap;
 };
 
@@ -1932,6 +1975,7 @@ __global__ __launch_bounds__(kBlock) void k_rules(Bind B, RulesArgs A) {
   S.cap = A.job_cap;
   if (lane == 0) *S.cnt = 0;
   wave_sync();
+  JobChunk JC;
   const Lines &L = A.L;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + wave * 64u; base < A.n_lines; base += stride) {
@@ -1971,20 +2015,10 @@ __global__ __launch_bounds__(kBlock) void k_rules(Bind B, RulesArgs A) {
         }
       }
     }
-    // ---- append this wave's DFA jobs (one global atomic per 64 lines)
-    wave_sync();
-    const uint32_t nj = min(*S.cnt, kWaveJobs);
-    if (nj) {
-      unsigned long long jb = 0;
-      if (lane == 0) jb = atomicAdd(A.job_count, (unsigned long long)nj);
-      jb = __shfl(jb, 0);
-      for (uint32_t i = lane; i < nj; i += 64)
-        if (jb + i < A.job_cap) { A.jline[jb + i] = S.lds[i].x; A.jkey[jb + i] = S.lds[i].y; }
-    }
-    wave_sync();
-    if (lane == 0) *S.cnt = 0;
-    wave_sync();
+    // ---- append this wave's DFA jobs (from its chunk of the job array)
+    flush_jobs(S, JC, lane);
   }
+  close_jobs(S, JC, lane, A.null_key, A.job_real);
 }
 
 // DFA jobs of the line pass, sorted by rule: one (line, rule) per lane.  A
@@ -2864,6 +2898,192 @@ __global__ __launch_bounds__(kBlock) void k_st_claim(EvSrc E, uint64_t n_ev, con
   if (k < n_ev && !flag_set(S, 7)) claimed = st_claim_event(E, n_ev, k, ev_el, ev_rule, el_slot, el_id, rules, S, ev_st, ev_rec,
                                                             shard_budget);
   count_claims(S, 1, 7, claimed, shard_budget);
+}
+
+// ---- per-line claims of a local batch (no per-event line / rule arrays): the
+// events of a line are its match-mask positions in order, hosts_to_skip out
+// (k_emit's order), numbered from the line's exclusive event offset.
+
+// adds n claims of this lane to the block's shard (all lanes of the wave call it)
+__device__ __forceinline__ void count_claims_n(const State &S, uint32_t which, uint32_t ovf_flag, uint32_t n, uint64_t shard_budget) {
+  uint32_t tot = n;
+  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+  if (tot && (threadIdx.x & 63) == 0)
+    if (atomicAdd(claim_shard(S, which), (unsigned long long)tot) + tot > shard_budget) raise_flag(S, ovf_flag);
+}
+
+// fn(k, rule) for each event of line i, k from eo on
+template <typename F>
+__device__ __forceinline__ void for_line_events(const Bind &B, const Lines &L, uint64_t i, uint64_t eo, F fn) {
+  const int32_t hid = L.host_id[i];
+  uint32_t sb = 0, nsite = 0;
+  if (hid >= 0) { sb = B.site_off[hid]; nsite = B.site_off[hid + 1] - sb; }
+  const uint32_t napp = nsite + B.n_global;
+  const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
+  const uint64_t k0 = B.sc_skip[2 * sc], k1 = B.sc_skip[2 * sc + 1];
+  const uint64_t *mask = L.masks + i * B.mask_words;
+  uint64_t k = eo;
+  for (uint32_t w = 0; w * 64 < napp; ++w) {
+    uint64_t m = mask[w];
+    while (m) {
+      const uint32_t b = (uint32_t)__ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      const uint32_t pos = w * 64 + b;
+      const uint32_t r = pos < nsite ? B.site_rules[sb + pos] : B.global_rules[pos - nsite];
+      const bool skip = pos < 128 ? (((pos < 64 ? k0 >> pos : k1 >> (pos - 64)) & 1) != 0) : is_skip(B, r, hid);
+      if (!skip) fn(k++, r);
+    }
+  }
+}
+
+// one event's state slot (st_claim_event without the per-event arrays)
+__device__ __forceinline__ bool st_claim_rule(const State &S, const DevRule *__restrict__ rules, uint32_t id, uint32_t r,
+                                              int64_t ts, bool first, uint64_t k, uint32_t *__restrict__ ev_st,
+                                              EvRec *__restrict__ ev_rec, uint64_t shard_budget) {
+  const uint32_t nm = rules[r].name_id;
+  const uint64_t key = ((uint64_t)(id + 1) << 24) | nm;
+  const bool hot = nm == S.hot_name && id < S.ip_st_cap;
+  const uint32_t c = hot ? S.ip_st[id] : kNone;
+  uint64_t q = c;
+  bool claimed = false;
+  if (c == kNone) {
+    q = mix64(key) & S.st_mask;
+    for (;;) {
+      uint64_t cur = S.st[q].key;
+      if (cur == 0) {
+        if (flag_set(S, 7)) return false;
+        if (__hip_atomic_load(claim_shard(S, 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= shard_budget) {
+          raise_flag(S, 7);
+          return false;
+        }
+        cur = atomicCAS((unsigned long long *)&S.st[q].key, 0ull, (unsigned long long)key);
+        if (cur == 0) { claimed = true; break; }
+      }
+      if (cur == key) break;
+      q = (q + 1) & S.st_mask;
+    }
+    if (hot) S.ip_st[id] = (uint32_t)q;
+  }
+  ev_st[k] = (uint32_t)q;
+  EvRec rec;
+  rec.ts = ts;
+  rec.rule = r | (first ? 0x80000000u : 0u);
+  rec.ev = (uint32_t)k;
+  ev_rec[k] = rec;
+  return claimed;
+}
+
+// one lane per event line: the IP slot (k_ip_claim), then, for an IP of an
+// earlier batch, the state slots of the line's events right away; lines of
+// IPs new in this batch are listed (el_new) for k_ip_commit and k_line_st_claim
+__global__ __launch_bounds__(kBlock) void k_line_claim(Bind B, EvSrc E, Lines L, const uint64_t *__restrict__ offs, State S,
+                                                       uint32_t epoch, uint32_t *__restrict__ el_slot,
+                                                       uint32_t *__restrict__ el_id, uint32_t *__restrict__ el_new,
+                                                       uint64_t ip_budget, uint32_t *__restrict__ ev_st,
+                                                       EvRec *__restrict__ ev_rec, uint64_t st_budget) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool claimed = false, isnew = false;
+  const bool act = i < E.n && ev_has(E, i) && !flag_set(S, 5);
+  if (act) {
+    el_id[i] = 0;
+    claimed = ip_claim_line(E, S, epoch, i, el_slot, el_id, ip_budget);
+    isnew = el_id[i] == kNewIp;
+  }
+  count_claims(S, 0, 5, claimed, ip_budget);
+  const uint64_t at = wave_alloc((unsigned long long *)&S.counters[4], isnew ? 1u : 0u);
+  if (isnew) el_new[at] = (uint32_t)i;
+  uint32_t nst = 0;
+  if (act && !isnew && !flag_set(S, 7) && !flag_set(S, 5)) {
+    const uint32_t id = el_id[i] & ~kFirstIp;
+    const int64_t ts = E.ts[i];
+    for_line_events(B, L, i, offs[i] & 0xFFFFFFFFull, [&](uint64_t k, uint32_t r) {
+      nst += st_claim_rule(S, B.rules, id, r, ts, false, k, ev_st, ev_rec, st_budget) ? 1u : 0u;
+    });
+  }
+  count_claims_n(S, 1, 7, nst, st_budget);
+}
+
+// state slots of the listed event lines (list: IPs new in this batch, after
+// k_ip_commit), or of every event line (list == nullptr: the retry after a
+// state-table overflow).  seenIp is false only for the first event of the
+// first event line of a new IP (kFirstIp).
+__global__ __launch_bounds__(kBlock) void k_line_st_claim(Bind B, EvSrc E, Lines L, const uint64_t *__restrict__ offs, State S,
+                                                          const uint32_t *__restrict__ list, uint64_t n_list,
+                                                          const uint32_t *__restrict__ el_slot, const uint32_t *__restrict__ el_id,
+                                                          uint32_t *__restrict__ ev_st, EvRec *__restrict__ ev_rec,
+                                                          uint64_t st_budget) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t nst = 0;
+  const bool in = list ? t < n_list : t < E.n;
+  const uint64_t i = in ? (list ? list[t] : t) : 0;
+  if (in && ev_has(E, i) && !flag_set(S, 7)) {
+    uint32_t id = el_id[i];
+    const bool first_line = id != kNewIp && (id & kFirstIp);
+    id = id == kNewIp ? S.ip[el_slot[i]].id : (id & ~kFirstIp);
+    const int64_t ts = E.ts[i];
+    const uint64_t eo = offs[i] & 0xFFFFFFFFull;
+    for_line_events(B, L, i, eo, [&](uint64_t k, uint32_t r) {
+      nst += st_claim_rule(S, B.rules, id, r, ts, first_line && k == eo, k, ev_st, ev_rec, st_budget) ? 1u : 0u;
+    });
+  }
+  count_claims_n(S, 1, 7, nst, st_budget);
+}
+
+// lines with events and their IP bytes (bounds of the new IPs / arena bytes)
+__global__ __launch_bounds__(kBlock) void k_el_bounds(uint64_t n, const uint64_t *__restrict__ counts,
+                                                      const uint32_t *__restrict__ ip_len, unsigned long long *bounds) {
+  __shared__ unsigned long long s_acc[2][kBlock / 64];
+  unsigned long long a = 0, b = 0;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x)
+    if (counts[j] & 0xFFFFFFFFull) { ++a; b += ip_len[j]; }
+  for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o); b += __shfl_xor(b, o); }
+  if ((threadIdx.x & 63) == 0) { s_acc[0][threadIdx.x >> 6] = a; s_acc[1][threadIdx.x >> 6] = b; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long x = 0, y = 0;
+    for (int w = 0; w < kBlock / 64; ++w) { x += s_acc[0][w]; y += s_acc[1][w]; }
+    if (x) { atomicAdd(&bounds[0], x); atomicAdd(&bounds[1], y); }
+  }
+}
+
+// trip k (sorted record at pos[t]) -> (event << 32 | rule), for a batch without
+// per-event arrays
+__global__ void k_trip_events_rules(uint64_t n, const uint32_t *__restrict__ pos, const EvRec *__restrict__ rec,
+                                    uint64_t *__restrict__ evr) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) {
+    const EvRec v = rec[pos[t]];
+    evr[t] = ((uint64_t)v.ev << 32) | (v.rule & 0x7FFFFFFFu);
+  }
+}
+
+// k_build_trips from (event << 32 | rule): the event's line by binary search
+// over the lines' event offsets (the last line whose offset is <= k holds it)
+__global__ void k_build_trips_offs(uint64_t n_trips, const uint64_t *__restrict__ evr, uint64_t n_lines,
+                                   const uint64_t *__restrict__ offs, const uint64_t *__restrict__ nl, Lines L,
+                                   const DevRule *__restrict__ rules, bjx_trip *__restrict__ out) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_trips) return;
+  const uint64_t k = evr[t] >> 32;
+  uint64_t lo = 0, hi = n_lines;  // first line whose offset > k
+  while (lo < hi) {
+    const uint64_t m = (lo + hi) >> 1;
+    if ((offs[m] & 0xFFFFFFFFull) <= k) lo = m + 1; else hi = m;
+  }
+  const uint64_t line = lo - 1;
+  bjx_trip tr;
+  tr.line_idx = line;
+  tr.line_offset = line_start(nl, line);
+  tr.line_len = (uint32_t)(nl[line] - tr.line_offset);
+  tr.rule_idx = (uint32_t)(evr[t] & 0xFFFFFFFFull);
+  tr.ts_ns = L.ts[line];
+  tr.ip_off = L.ip_off[line];
+  tr.ip_len = L.ip_len[line];
+  tr.host_off = L.host_off[line];
+  tr.host_len = L.host_len[line];
+  tr.rest_off = L.rest_off[line];
+  tr.decision = rules[tr.rule_idx].decision;
+  out[t] = tr;
 }
 
 // state slots claimed by the last k_st_claim -> table load counters[2]; shards cleared
@@ -3990,8 +4210,10 @@ struct bjx_engine {
   DevBuf<unsigned long long> scalars;  // [0] slow count, [1..2] bounds, [3] selected
   DevBuf<uint64_t> res_seq;
   bool res_written = false;  // the last match phase wrote the RuleResult arrays
+  bool ev_arrays = false;    // ... and the per-event line / rule arrays (ev_el, ev_rule)
   DevBuf<uint32_t> res_rule, ev_el, ev_rule, ev_res, ev_st, ev_st2, ev_idx, ev_idx2, el_slot, coll, trip_idx;
   DevBuf<EvRec> ev_rec, ev_rec2;
+  DevBuf<uint64_t> trip_evr, trip_evr2;  // trips as (event << 32 | rule) (batches without per-event arrays)
   DevBuf<uint32_t> el_id;
   DevBuf<uint32_t> el_new;  // event lines with a new IP (k_ip_claim -> k_ip_commit)
   DevBuf<uint8_t> rl_out, ev_out, ev_out_s, trip_flag;
@@ -5368,6 +5590,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   e->l_counts.release(); e->l_offs.release(); e->l_masks.release(); e->l_ipoff.release(); e->l_iplen.release();
   e->l_hoff.release(); e->l_hlen.release(); e->l_roff.release(); e->slow_list.release(); e->l_hid.release();
   e->scalars.release(); e->res_seq.release(); e->res_rule.release(); e->ev_el.release(); e->ev_rule.release();
+  e->trip_evr.release(); e->trip_evr2.release();
   e->ev_res.release(); e->ev_st.release(); e->ev_st2.release(); e->ev_idx.release(); e->ev_idx2.release();
   e->el_slot.release(); e->coll.release(); e->el_new.release(); e->ev_rec.release(); e->ev_rec2.release(); e->el_id.release();
 
@@ -5435,37 +5658,42 @@ static void mark(bjx_engine *e, int k) {
 // RegexRateLimitStates.Apply for n_ev events (reference order) whose lines are
 // E; writes e->ev_out[k].  n_el / el_bytes bound the new IPs / arena bytes.
 // Phases 5 (IP + state slots), 6 (sort), 7 (automaton).
-static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t n_el, uint64_t el_bytes, uint64_t n_ev,
-                             const uint32_t *ev_el, const uint32_t *ev_rule) {
+// The claims of a local batch per line (k_line_claim: IP, then the states of
+// the lines whose IP is known; k_ip_commit / k_ip_collide for the IPs new in
+// this batch, then k_line_st_claim over their lines).  An IP-table overflow
+// rolls back both tables' claims of the batch; a state-table overflow rolls
+// back the states and claims them again for every event line.
+static void rl_claims_lines(bjx_engine *e, const Bind &B, const EvSrc &E, const Lines &L, const uint64_t *offs, uint64_t n_el,
+                            uint64_t n_ev, uint32_t epoch) {
   hipStream_t st = e->stream;
-  if (E.n >= 0x7FFFFFFFull || n_ev >= 0xFFFFFFFFull) throw BjxError(BJX_ERR_ARG, "batch too large (2^31 lines / 2^32 events)");
-  read_counters(e);
-  ensure_capacity(e, std::min<uint64_t>(n_el, std::max<uint64_t>(1u << 18, e->host_counters[0] / 8)), el_bytes,
-                  std::min<uint64_t>(n_ev, std::max<uint64_t>(1u << 20, e->host_counters[2] / 8)));
-  if (e->host_counters[0] + n_el >= 0x7FFFFFFFull) throw BjxError(BJX_ERR_CAPACITY, "more than 2^31 distinct IPs");
-  if (++e->epoch == 0) ++e->epoch;  // 0 marks a slot being claimed
-  const uint32_t epoch = e->epoch;
-  e->el_slot.ensure(E.n); e->el_id.ensure(E.n); e->coll.ensure(E.n); e->el_new.ensure(E.n);
-  uint64_t nw_ovf[2] = {0, 0};  // new-IP event lines (k_ip_claim's list), IP table overflow flag
-  e->ev_st.ensure(n_ev); e->ev_st2.ensure(n_ev); e->ev_rec.ensure(n_ev); e->ev_rec2.ensure(n_ev);
-  e->ev_out.ensure(n_ev); e->ev_out_s.ensure(n_ev);
-  mark(e, 5);
+  uint64_t nw_ovf[4] = {0, 0, 0, 0};  // counters 4 (new-IP lines), 5 (IP overflow), 6, 7 (state overflow)
+  auto st_rollback = [&]() {
+    HIP_OK(hipMemsetAsync(e->S.counters + 2, 0, 8, st));
+    hipLaunchKernelGGL(k_st_rollback, dim3(grid_for(e->st_cap)), dim3(kBlock), 0, st, e->st_cap, e->S);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemsetAsync(e->S.ip_st, 0xFF, e->S.ip_st_cap * 4, st));  // may name rolled-back slots
+    read_counters(e);
+  };
+  bool forced_st = false;
   for (int attempt = 0;; ++attempt) {
-    const uint64_t n_ips = e->host_counters[0];
-    HIP_OK(hipMemsetAsync(e->S.counters + 3, 0, 3 * 8, st));
+    const uint64_t n_ips = e->host_counters[0], n_st = e->host_counters[2];
+    HIP_OK(hipMemsetAsync(e->S.counters + 3, 0, 5 * 8, st));
     HIP_OK(hipMemsetAsync(e->S.counters + kShardBase, 0, kClaimShards * 128, st));
-    uint64_t budget = e->ip_cap * 3 / 4 - n_ips;
+    uint64_t budget = e->ip_cap * 3 / 4 - n_ips, st_budget = e->st_cap * 3 / 4 - n_st;
     const bool forced = e->dbg_budget && attempt == 0 && e->dbg_budget < budget;  // test hook
     if (forced) budget = e->dbg_budget;
-    hipLaunchKernelGGL(k_ip_claim, dim3(grid_for(E.n)), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p,
-                       e->el_new.p, budget / kClaimShards);
+    forced_st = e->dbg_budget && attempt == 0 && e->dbg_budget < st_budget;
+    if (forced_st) st_budget = e->dbg_budget;
+    hipLaunchKernelGGL(k_line_claim, dim3(grid_for(E.n)), dim3(kBlock), 0, st, B, E, L, offs, e->S, epoch, e->el_slot.p,
+                       e->el_id.p, e->el_new.p, budget / kClaimShards, e->ev_st.p, e->ev_rec.p, st_budget / kClaimShards);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(nw_ovf, e->S.counters + 4, 16, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(nw_ovf, e->S.counters + 4, 32, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     if (!nw_ovf[1]) break;
-    // more new IPs than the table had room for: undo, grow, claim again
+    // more new IPs than the table had room for: undo both tables' claims, grow, claim again
     hipLaunchKernelGGL(k_ip_rollback, dim3(grid_for(e->ip_cap)), dim3(kBlock), 0, st, e->ip_cap, e->S, epoch);
     HIP_OK(hipGetLastError());
+    st_rollback();
     if (!forced) grow_ip(e, attempt >= 2 ? n_ips + n_el : std::min<uint64_t>(n_ips + n_el, 4 * (e->ip_cap * 3 / 4)));
   }
   if (nw_ovf[0]) {
@@ -5487,18 +5715,30 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
     hipLaunchKernelGGL(k_ip_collide, dim3(1), dim3(64), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p, e->coll.p, n_coll);
     HIP_OK(hipGetLastError());
   }
+  // the states: the new IPs' lines (their state shard counts add to the first
+  // launch's), or, after an overflow, every event line again
+  bool all = nw_ovf[3] != 0;
   for (int attempt = 0;; ++attempt) {
-    read_counters(e);
-    const uint64_t n_st = e->host_counters[2];
-    HIP_OK(hipMemsetAsync(e->S.counters + 6, 0, 2 * 8, st));
-    HIP_OK(hipMemsetAsync(e->S.counters + kShardBase, 0, kClaimShards * 128, st));
-    uint64_t budget = e->st_cap * 3 / 4 - n_st;
-    const bool forced = e->dbg_budget && attempt == 0 && e->dbg_budget < budget;  // test hook
-    if (forced) budget = e->dbg_budget;
-    hipLaunchKernelGGL(k_st_claim, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, E, n_ev, ev_el, ev_rule, e->el_slot.p,
-                       e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_rec.p, budget / kClaimShards);
-    HIP_OK(hipGetLastError());
     uint64_t ovf = 0;
+    if (all) {
+      st_rollback();
+      if (!forced_st || attempt > 0)
+        grow_st(e, attempt >= 2 ? e->host_counters[2] + n_ev
+                                : std::min<uint64_t>(e->host_counters[2] + n_ev, 4 * (e->st_cap * 3 / 4)));
+      forced_st = false;
+      HIP_OK(hipMemsetAsync(e->S.counters + 6, 0, 2 * 8, st));
+      HIP_OK(hipMemsetAsync(e->S.counters + kShardBase, 0, kClaimShards * 128, st));
+      const uint64_t budget = e->st_cap * 3 / 4 - e->host_counters[2];
+      hipLaunchKernelGGL(k_line_st_claim, dim3(grid_for(E.n)), dim3(kBlock), 0, st, B, E, L, offs, e->S,
+                         (const uint32_t *)nullptr, (uint64_t)0, e->el_slot.p, e->el_id.p, e->ev_st.p, e->ev_rec.p,
+                         budget / kClaimShards);
+    } else if (nw_ovf[0]) {
+      const uint64_t budget = e->st_cap * 3 / 4 - e->host_counters[2];
+      hipLaunchKernelGGL(k_line_st_claim, dim3(grid_for(nw_ovf[0])), dim3(kBlock), 0, st, B, E, L, offs, e->S,
+                         e->el_new.p, nw_ovf[0], e->el_slot.p, e->el_id.p, e->ev_st.p, e->ev_rec.p,
+                         (forced_st ? e->dbg_budget : budget) / kClaimShards);
+    }
+    HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(&ovf, e->S.counters + 7, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     if (!ovf) {
@@ -5506,16 +5746,98 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
       HIP_OK(hipGetLastError());
       break;
     }
-    // more new (ip, rule name) states than the table had room for: undo this
-    // batch's claims, recount, grow, claim again
-    HIP_OK(hipMemsetAsync(e->S.counters + 2, 0, 8, st));
-    hipLaunchKernelGGL(k_st_rollback, dim3(grid_for(e->st_cap)), dim3(kBlock), 0, st, e->st_cap, e->S);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipMemsetAsync(e->S.ip_st, 0xFF, e->S.ip_st_cap * 4, st));  // may name rolled-back slots
-    read_counters(e);
-    if (!forced)
-      grow_st(e, attempt >= 2 ? e->host_counters[2] + n_ev
-                              : std::min<uint64_t>(e->host_counters[2] + n_ev, 4 * (e->st_cap * 3 / 4)));
+    all = true;  // more new (ip, rule name) states than the table had room for
+  }
+}
+
+// Lp / offs (a local batch): claims per line from the match masks
+// (k_line_claim, k_line_st_claim) instead of per event (ev_el / ev_rule)
+static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t n_el, uint64_t el_bytes, uint64_t n_ev,
+                             const uint32_t *ev_el, const uint32_t *ev_rule, const Lines *Lp = nullptr,
+                             const uint64_t *offs = nullptr) {
+  hipStream_t st = e->stream;
+  if (E.n >= 0x7FFFFFFFull || n_ev >= 0xFFFFFFFFull) throw BjxError(BJX_ERR_ARG, "batch too large (2^31 lines / 2^32 events)");
+  read_counters(e);
+  ensure_capacity(e, std::min<uint64_t>(n_el, std::max<uint64_t>(1u << 18, e->host_counters[0] / 8)), el_bytes,
+                  std::min<uint64_t>(n_ev, std::max<uint64_t>(1u << 20, e->host_counters[2] / 8)));
+  if (e->host_counters[0] + n_el >= 0x7FFFFFFFull) throw BjxError(BJX_ERR_CAPACITY, "more than 2^31 distinct IPs");
+  if (++e->epoch == 0) ++e->epoch;  // 0 marks a slot being claimed
+  const uint32_t epoch = e->epoch;
+  e->el_slot.ensure(E.n); e->el_id.ensure(E.n); e->coll.ensure(E.n); e->el_new.ensure(E.n);
+  uint64_t nw_ovf[2] = {0, 0};  // new-IP event lines (k_ip_claim's list), IP table overflow flag
+  e->ev_st.ensure(n_ev); e->ev_st2.ensure(n_ev); e->ev_rec.ensure(n_ev); e->ev_rec2.ensure(n_ev);
+  e->ev_out.ensure(n_ev); e->ev_out_s.ensure(n_ev);
+  mark(e, 5);
+  if (Lp) {
+    rl_claims_lines(e, B, E, *Lp, offs, n_el, n_ev, epoch);
+  } else {
+    for (int attempt = 0;; ++attempt) {
+      const uint64_t n_ips = e->host_counters[0];
+      HIP_OK(hipMemsetAsync(e->S.counters + 3, 0, 3 * 8, st));
+      HIP_OK(hipMemsetAsync(e->S.counters + kShardBase, 0, kClaimShards * 128, st));
+      uint64_t budget = e->ip_cap * 3 / 4 - n_ips;
+      const bool forced = e->dbg_budget && attempt == 0 && e->dbg_budget < budget;  // test hook
+      if (forced) budget = e->dbg_budget;
+      hipLaunchKernelGGL(k_ip_claim, dim3(grid_for(E.n)), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p,
+                         e->el_new.p, budget / kClaimShards);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(nw_ovf, e->S.counters + 4, 16, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      if (!nw_ovf[1]) break;
+      // more new IPs than the table had room for: undo, grow, claim again
+      hipLaunchKernelGGL(k_ip_rollback, dim3(grid_for(e->ip_cap)), dim3(kBlock), 0, st, e->ip_cap, e->S, epoch);
+      HIP_OK(hipGetLastError());
+      if (!forced) grow_ip(e, attempt >= 2 ? n_ips + n_el : std::min<uint64_t>(n_ips + n_el, 4 * (e->ip_cap * 3 / 4)));
+    }
+    if (nw_ovf[0]) {
+      hipLaunchKernelGGL(k_ip_commit, dim3(grid_for(nw_ovf[0])), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p,
+                         e->el_new.p, nw_ovf[0], e->coll.p);
+      HIP_OK(hipGetLastError());
+    }
+    uint64_t n_coll = 0;
+    HIP_OK(hipMemcpyAsync(&n_coll, e->S.counters + 3, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (n_coll) {  // distinct IPs with one 64-bit hash in this batch: resolve exactly, in line order
+      if (n_coll > 1) {
+        uint32_t *ki = e->coll.p, *ko = e->ev_st2.p;
+        cub_call(e, [&](void *tmp, size_t &bytes) {
+          return hipcub::DeviceRadixSort::SortKeys(tmp, bytes, ki, ko, (int)n_coll, 0, 32, st);
+        });
+        HIP_OK(hipMemcpyAsync(e->coll.p, e->ev_st2.p, n_coll * 4, hipMemcpyDeviceToDevice, st));
+      }
+      hipLaunchKernelGGL(k_ip_collide, dim3(1), dim3(64), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p, e->coll.p, n_coll);
+      HIP_OK(hipGetLastError());
+    }
+    for (int attempt = 0;; ++attempt) {
+      read_counters(e);
+      const uint64_t n_st = e->host_counters[2];
+      HIP_OK(hipMemsetAsync(e->S.counters + 6, 0, 2 * 8, st));
+      HIP_OK(hipMemsetAsync(e->S.counters + kShardBase, 0, kClaimShards * 128, st));
+      uint64_t budget = e->st_cap * 3 / 4 - n_st;
+      const bool forced = e->dbg_budget && attempt == 0 && e->dbg_budget < budget;  // test hook
+      if (forced) budget = e->dbg_budget;
+      hipLaunchKernelGGL(k_st_claim, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, E, n_ev, ev_el, ev_rule, e->el_slot.p,
+                         e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_rec.p, budget / kClaimShards);
+      HIP_OK(hipGetLastError());
+      uint64_t ovf = 0;
+      HIP_OK(hipMemcpyAsync(&ovf, e->S.counters + 7, 8, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      if (!ovf) {
+        hipLaunchKernelGGL(k_fold_claims, dim3(1), dim3(kClaimShards), 0, st, e->S);
+        HIP_OK(hipGetLastError());
+        break;
+      }
+      // more new (ip, rule name) states than the table had room for: undo this
+      // batch's claims, recount, grow, claim again
+      HIP_OK(hipMemsetAsync(e->S.counters + 2, 0, 8, st));
+      hipLaunchKernelGGL(k_st_rollback, dim3(grid_for(e->st_cap)), dim3(kBlock), 0, st, e->st_cap, e->S);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemsetAsync(e->S.ip_st, 0xFF, e->S.ip_st_cap * 4, st));  // may name rolled-back slots
+      read_counters(e);
+      if (!forced)
+        grow_st(e, attempt >= 2 ? e->host_counters[2] + n_ev
+                                : std::min<uint64_t>(e->host_counters[2] + n_ev, 4 * (e->st_cap * 3 / 4)));
+    }
   }
   mark(e, 6);
   {
@@ -5656,8 +5978,19 @@ static void run_nfa_jobs(bjx_engine *e, const Bind &B, const uint8_t *buf, uint6
 // consumeLine up to Apply for every line: framing, header, exemption, rule
 // matching, RuleResults and events in reference order (phases 0-4).  Leaves
 // the batch context in e->bc; false if the batch has no complete line.
+// BJX_FUSED_CLAIM=1: claims per line from the match masks (k_line_claim,
+// k_line_st_claim) instead of per event (k_emit, k_ip_claim, k_st_claim).  Off
+// by default: slower at cfg3 (profiles/r04_b: claims 11.6 ms + emit 1.2 against
+// 8.2 + 2.8; the serial per-line event loop's dependent loads)
+static bool fused_claims() {
+  static const bool on = getenv("BJX_FUSED_CLAIM") && atoi(getenv("BJX_FUSED_CLAIM")) == 1;
+  return on;
+}
+
+// need_ev: the per-event line / rule arrays are wanted (the node exchange);
+// a local batch without RuleResult copies claims from the per-line masks
 static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns, uint32_t flags,
-                        bjx_batch_result *out) {
+                        bjx_batch_result *out, bool need_ev = true) {
   e->bc = BatchCtx{};
   HIP_OK(hipSetDevice(e->device));
   if (e->bound_uid != rs->uid || e->bound_dec_version != e->decisions_version) {
@@ -5808,6 +6141,8 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     A.dbg = getenv("BJX_DEBUG_LINES") ? (uint32_t)atoi(getenv("BJX_DEBUG_LINES")) : 0u;
     A.slow_list = e->slow_list.p; A.slow_count = e->scalars.p;
     A.jline = e->jline.p; A.jkey = e->jkey.p; A.job_count = e->scalars.p + 11; A.job_cap = std::min(e->jline.n, e->jkey.n);
+    A.job_real = e->scalars.p + 14;
+    A.null_key = B.n_rules;  // sorts after every rule id (the job sort covers bit_width(n_rules) bits)
     A.span_bytes = getenv("BJX_SPAN_BYTES") ? (uint32_t)atoi(getenv("BJX_SPAN_BYTES")) & ~15u : kSpanBytes;
     A.list = nullptr; A.n_list = 0; A.prof = nullptr;
     unsigned long long n_todo = 0;
@@ -5815,6 +6150,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       RulesArgs R;
       R.buf = buf; R.nl = e->nl.p; R.n_lines = n_lines; R.L = L; R.todo = e->long_list.p; R.todo_count = e->scalars.p + 12;
       R.jline = A.jline; R.jkey = A.jkey; R.job_count = A.job_count; R.job_cap = A.job_cap;
+      R.job_real = A.job_real; R.null_key = A.null_key;
       const bool img_lds = B.img_bytes <= kRulesImgMax;
       const uint32_t lds = ((img_lds ? B.img_bytes : 0) + 15u & ~15u) + (kBlock / 64) * kWaveJobBytes;
       const void *fn = img_lds ? reinterpret_cast<const void *>(&k_rules<true>) : reinterpret_cast<const void *>(&k_rules<false>);
@@ -5905,21 +6241,27 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     e->jkey.ensure(sc4[3] + (1u << 20));
     HIP_OK(hipMemsetAsync(e->scalars.p, 0, 8, st));
     HIP_OK(hipMemsetAsync(e->scalars.p + 11, 0, 16, st));
+    HIP_OK(hipMemsetAsync(e->scalars.p + 14, 0, 8, st));
   }
   out->consumed_bytes = last_nl + 1;
-  const unsigned long long n_slow = sc4[4], n_jobs = sc4[3];
+  // job slots taken (sc4[3]; the chunks' unused ones hold null jobs) and real jobs
+  unsigned long long n_jobs = 0;
+  HIP_OK(hipMemcpyAsync(&n_jobs, e->scalars.p + 14, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  const unsigned long long n_slow = sc4[4], n_slots = sc4[3];
   e->last_jobs = n_jobs;
   e->scan_stats[0] = sc4[0]; e->scan_stats[1] = sc4[1]; e->scan_stats[2] = n_slow; e->scan_stats[3] = B.img_bytes;
   e->scan_stats[4] = n_jobs; e->scan_stats[5] = sc4[2];
   HIP_OK(hipEventRecord(e->evk[2], st));
   if (n_jobs) {
     // group the jobs by rule (stable: line order inside a rule), then one lane per job
-    e->jline2.ensure(n_jobs); e->jkey2.ensure(n_jobs);
+    e->jline2.ensure(n_slots); e->jkey2.ensure(n_slots);
     {
+      // null jobs (key n_rules) sort after the real ones: k_dfa takes the first n_jobs
       uint32_t *ki = e->jkey.p, *ko = e->jkey2.p, *vi = e->jline.p, *vo = e->jline2.p;
-      const int bits = std::max(1, bit_width(B.n_rules ? B.n_rules - 1 : 0));
+      const int bits = std::max(1, bit_width(B.n_rules));
       cub_call(e, [&](void *tmp, size_t &bytes) {
-        return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)n_jobs, 0, bits, st);
+        return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)n_slots, 0, bits, st);
       });
     }
     hipLaunchKernelGGL(k_dfa, dim3(grid_for(n_jobs)), dim3(kBlock), 0, st, B, buf, (uint64_t)n, e->nl.p, e->jkey2.p,
@@ -5984,10 +6326,21 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   e->res_seq.ensure(n_res + 1); e->res_rule.ensure(n_res + 1); e->rl_out.ensure(n_res + 1);
   e->ev_el.ensure(n_ev + 1); e->ev_rule.ensure(n_ev + 1); e->ev_res.ensure(n_ev + 1);
   HIP_OK(hipMemsetAsync(e->scalars.p + 1, 0, 2 * 8, st));
+  e->res_written = false;
+  e->ev_arrays = false;
   if (n_res) {
-    e->res_written = (flags & BJX_COPY_RESULTS) != 0;
-    hipLaunchKernelGGL(k_emit, dim3((unsigned)std::min<uint64_t>(grid_for(n_lines), 4096)), dim3(kBlock), 0, st, B, n_lines, L, e->l_offs.p, e->res_seq.p,
-                       e->res_rule.p, e->ev_el.p, e->ev_rule.p, e->ev_res.p, e->scalars.p + 1, e->res_written);
+    const bool want_res = (flags & BJX_COPY_RESULTS) != 0;
+    if (!want_res && !need_ev && fused_claims() && !getenv("BJX_CHECK")) {
+      // only the bounds: the claims read the per-line masks (k_line_claim)
+      hipLaunchKernelGGL(k_el_bounds, dim3((unsigned)std::min<uint64_t>(grid_for(n_lines), 4096)), dim3(kBlock), 0, st, n_lines,
+                         L.counts, L.ip_len, e->scalars.p + 1);
+    } else {
+      e->res_written = want_res;
+      e->ev_arrays = true;
+      hipLaunchKernelGGL(k_emit, dim3((unsigned)std::min<uint64_t>(grid_for(n_lines), 4096)), dim3(kBlock), 0, st, B, n_lines, L,
+                         e->l_offs.p, e->res_seq.p, e->res_rule.p, e->ev_el.p, e->ev_rule.p, e->ev_res.p, e->scalars.p + 1,
+                         e->res_written);
+    }
     HIP_OK(hipGetLastError());
     if (e->res_written) HIP_OK(hipMemsetAsync(e->rl_out.p, 0, n_res, st));
   }
@@ -6192,6 +6545,22 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
     if (n_trips) {
       // the selected trips in reference (event) order
       e->trip_ev.ensure(n_trips); e->trip_ev2.ensure(n_trips);
+      if (sorted && !e->ev_arrays) {
+        // no per-event arrays (claims from the line masks): the rule rides with
+        // the event index, the line comes from the lines' event offsets
+        e->trip_evr.ensure(n_trips); e->trip_evr2.ensure(n_trips);
+        hipLaunchKernelGGL(k_trip_events_rules, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_idx.p,
+                           e->ev_rec2.p, e->trip_evr.p);
+        uint64_t *ki = e->trip_evr.p, *ko = e->trip_evr2.p;
+        const int bits = std::max(1, bit_width(n_ev));
+        cub_call(e, [&](void *tmp, size_t &bytes) {
+          return hipcub::DeviceRadixSort::SortKeys(tmp, bytes, ki, ko, (int)n_trips, 32, 32 + bits, st);
+        });
+        e->d_trips.ensure(n_trips);
+        hipLaunchKernelGGL(k_build_trips_offs, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_evr2.p, n_lines,
+                           e->l_offs.p, e->nl.p, L, B.rules, e->d_trips.p);
+        HIP_OK(hipGetLastError());
+      } else {
       if (sorted)
         hipLaunchKernelGGL(k_trip_events, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_idx.p, e->ev_rec2.p,
                            e->trip_ev.p);
@@ -6205,6 +6574,7 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
       hipLaunchKernelGGL(k_build_trips, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, trip_ev, e->ev_el.p,
                          e->ev_rule.p, e->nl.p, L, B.rules, e->d_trips.p);
       HIP_OK(hipGetLastError());
+      }
       e->trips.resize(n_trips);
       HIP_OK(hipMemcpyAsync(e->trips.data(), e->d_trips.p, n_trips * sizeof(bjx_trip), hipMemcpyDeviceToHost, st));
       if (flags & BJX_EMIT_BANS) emit_bans(e, n_trips, (flags & BJX_BAN_RECORDS_ONLY) != 0);
@@ -6290,9 +6660,13 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
 
 static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns, uint32_t flags,
                       bjx_batch_result *out) {
-  if (!match_phase(e, rs, bytes, n, now_ns, flags, out)) return;
-  if (e->bc.n_ev)
-    rate_limit_stage(e, e->bind, local_evsrc(e), e->bc.n_el, e->bc.el_bytes, e->bc.n_ev, e->ev_el.p, e->ev_rule.p);
+  if (!match_phase(e, rs, bytes, n, now_ns, flags, out, false)) return;
+  if (e->bc.n_ev) {
+    if (fused_claims())
+      rate_limit_stage(e, e->bind, local_evsrc(e), e->bc.n_el, e->bc.el_bytes, e->bc.n_ev, nullptr, nullptr, &e->bc.L, e->l_offs.p);
+    else
+      rate_limit_stage(e, e->bind, local_evsrc(e), e->bc.n_el, e->bc.el_bytes, e->bc.n_ev, e->ev_el.p, e->ev_rule.p);
+  }
   finish_phase(e, flags, out, true);
 }
 

@@ -180,6 +180,7 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
   S.cap = A.job_cap;
   if (lane == 0) *S.cnt = 0;
   wave_sync();
+  JobChunk JC;
   const Tabs TB = make_tabs(B.img, B.il);
   LdsTabs LT;
   LT.hinfo = reinterpret_cast<const uint2 *>(s_hl + B.lt_hinfo);
@@ -392,18 +393,8 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
         L.flags[j] = fl;
       }
     }
-    // ---- append this wave's DFA jobs (one global atomic per 64 lines)
-    wave_sync();
-    const uint32_t nj = min(*S.cnt, kWaveJobs);
-    if (nj) {
-      unsigned long long jb = 0;
-      if (lane == 0) jb = atomicAdd(A.job_count, (unsigned long long)nj);
-      jb = __shfl(jb, 0);
-      for (uint32_t i = lane; i < nj; i += 64)
-        if (jb + i < A.job_cap) { A.jline[jb + i] = S.lds[i].x; A.jkey[jb + i] = S.lds[i].y; }
-    }
-    wave_sync();
-    if (lane == 0) *S.cnt = 0;
-    wave_sync();
+    // ---- append this wave's DFA jobs (from its chunk of the job array)
+    flush_jobs(S, JC, lane);
   }
+  close_jobs(S, JC, lane, A.null_key, A.job_real);
 }

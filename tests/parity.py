@@ -40,11 +40,18 @@ class Pair:
         self.lim = RegexRateLimiter(self.cfg, engine=self.engine, banner=MockBanner(), device_bans=device_bans)
         self.n_rules = len(self.cfg.all_rules())
 
-    def feed(self, data: bytes, now_ns: int, check=True):
+    def feed(self, data: bytes, now_ns: int, check=True, want_results=True):
+        """want_results=False: the engine's trip-only path (no RuleResult copies,
+        the bench's); the states, decisions and ban log compared by
+        compare_state still check every trip and its order."""
         before = self.engine.state_len()
         oflags, ores, oconsumed = self.ost.consume(self.ocfg, data, now_ns,
                                                    cap=(data.count(b"\n") + 1) * (self.n_rules + 1))
-        results, out = self.lim.consume_lines(data, now_ns, want_results=True)
+        results, out = self.lim.consume_lines(data, now_ns, want_results=want_results)
+        if not want_results:
+            assert out.consumed_bytes == oconsumed
+            assert out.n_trips == sum(1 for r in ores if r.exceeded)
+            return out
         if check:
             try:
                 compare_batch(oflags, ores, oconsumed, out)

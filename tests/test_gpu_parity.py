@@ -641,3 +641,40 @@ def test_dfa_self_loop_acceleration(engine):
             parts.append(rnd.choice(rare))
         lines.append(b"1700000000 9.9.9.%d GET h%d.com " % (j % 250, j % 7) + b"".join(parts))
     pair.feed(b"\n".join(lines) + b"\n", 1700000000 * S)
+
+
+@pytest.mark.parametrize("name,n_lines,batches", [("cfg3", 60_000, 2), ("cfg5", 40_000, 2), ("cfg1", 100_000, 2),
+                                                  ("cfg5h", 60_000, 2)])
+def test_workload_trips_only(engine, name, n_lines, batches):
+    """The bench's path: no RuleResult copies, so the state claims read the
+    per-line masks (k_line_claim) and the trips carry their rule from the sorted
+    records (k_build_trips_offs).  States, decisions and the ban log (every trip,
+    in order) against the oracle."""
+    w = W.scaled(W.ALL[name], n_lines, n_ips=min(W.ALL[name].n_ips, n_lines // 3 + 1))
+    pair = Pair(w.rules_yaml, engine)
+    per = (n_lines + batches - 1) // batches
+    ips = set()
+    for b in range(batches):
+        first, cnt = b * per, min(per, n_lines - b * per)
+        data = w.host_lines(first, cnt)
+        for ln in data.split(b"\n")[:200]:
+            parts = ln.split(b" ")
+            if len(parts) > 2:
+                ips.add(parts[1].decode())
+        pair.feed(data, w.now_ns(first, cnt), want_results=False)
+    pair.compare_state(sorted(ips)[:100])
+
+
+@pytest.mark.parametrize("budget", [1, 97])
+def test_trips_only_claim_rollback(engine, budget):
+    """k_line_claim's rollback paths (both tables) under the claim-budget hook,
+    on the trip-only path."""
+    w = W.scaled(W.CFG5, 24_000, n_ips=8_000)
+    engine.debug_set_claim_budget(budget)
+    try:
+        pair = Pair(w.rules_yaml, engine)
+        for b in range(3):
+            pair.feed(w.host_lines(b * 8_000, 8_000), w.now_ns(b * 8_000, 8_000), want_results=False)
+        pair.compare_state()
+    finally:
+        engine.debug_set_claim_budget(0)
