@@ -1343,6 +1343,20 @@ __device__ __forceinline__ void wave_sync() {
 
 extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
 
+// inclusive wave64 prefix sum on DPP (row_shr within 16-lane rows, then
+// row_bcast:15 / row_bcast:31 across rows): no LDS round trips, unlike __shfl_up
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+  uint32_t x = v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x113, 0xF, 0xF, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xE, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xC, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+  return x;
+}
+
+
 // consumeLine up to the rule loop for one line, from the scan tile in LDS
 // (regex_rate_limiter.go:120-172): SplitN header, parseTimestamp fast path,
 // host id (LDS host table), CheckIsAllowed, OldLine.  A line whose header runs
@@ -1466,13 +1480,8 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
       nlm |= (uint64_t)(((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u)) << (4 * k);
     }
     const uint32_t cnt = __popcll(nlm);
-    uint32_t pre = cnt;  // inclusive wave scan
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t v = __shfl_up(pre, o);
-      if (lane >= (uint32_t)o) pre += v;
-    }
-    const uint32_t tot = __shfl(pre, 63);
+    uint32_t pre = wave_incl_sum(cnt);
+    const uint32_t tot = __builtin_amdgcn_readlane(pre, 63);
     pre -= cnt;
     const uint64_t tb = A.tile_base[t];
     const bool head = prevb == '\n';
@@ -1544,29 +1553,57 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
       // positions in pairs (k, k + 1), k even: one LDS word keyed by the 3
       // bytes the two grams share (gram_pair_word), bit (first byte & 15) for
       // the gram at k and 16 + (last byte & 15) for the gram at k + 1
-      // (engine_types.h gram_pair_*): per pair two alignbytes, a mul24, the
-      // word address, one LDS read, two bfe (offset operand bits 0-4), shift-ors
+      // (engine_types.h gram_pair_*).  Eight word addresses, then their eight
+      // LDS reads in flight together, then the bits: per pair two alignbytes, a
+      // shift, a 24-bit mul_hi, an and, one LDS read, two bfe, two shift-ors
       const uint8_t *sb = reinterpret_cast<const uint8_t *>(s_bits);
       uint32_t hlo = 0, hhi = 0;
 #pragma unroll
-      for (int k = 0; k < 64; k += 2) {
-        const uint32_t lo = w[k >> 2], hi = (k >> 2) < 15 ? w[(k >> 2) + 1] : nxt;
-        const uint32_t g0 = (k & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3)) : lo;  // bytes k .. k + 3
-        const uint32_t g1 = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3) + 1u);           // bytes k + 1 .. k + 4
-        const uint32_t word = *reinterpret_cast<const uint32_t *>(sb + gram_pair_byte_off(g1 & 0xFFFFFFu));
-        const uint32_t b0 = __builtin_amdgcn_ubfe(word, g0 & 15u, 1), b1 = __builtin_amdgcn_ubfe(word, (g1 >> 24) | 16u, 1);
-        const uint32_t two = b0 | (b1 << 1);
-        if (k < 32) hlo |= two << k; else hhi |= two << (k - 32);
+      for (int k0 = 0; k0 < 64; k0 += 16) {
+        uint32_t word[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int k = k0 + 2 * i;
+          const uint32_t lo = w[k >> 2], hi = (k >> 2) < 15 ? w[(k >> 2) + 1] : nxt;
+          const uint32_t g0 = (k & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3)) : lo;  // bytes k .. k + 3
+          word[i] = *reinterpret_cast<const uint32_t *>(sb + gram_pair_byte_off(g0 >> 8));
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int k = k0 + 2 * i;
+          const uint32_t lo = w[k >> 2], hi = (k >> 2) < 15 ? w[(k >> 2) + 1] : nxt;
+          const uint32_t g0 = (k & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3)) : lo;
+          const uint32_t g1 = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3) + 1u);  // bytes k + 1 .. k + 4
+          const uint32_t b0 = __builtin_amdgcn_ubfe(word[i], g0 & 15u, 1), b1 = __builtin_amdgcn_ubfe(word[i], (g1 >> 24) | 16u, 1);
+          const uint32_t two = b0 | (b1 << 1);
+          if (k < 32) hlo |= two << k; else hhi |= two << (k - 32);
+        }
       }
       uint64_t hits = ((uint64_t)hhi << 32) | hlo;
       if (ts0 + lane * 64u + 64u > A.n) hits &= (ts0 + lane * 64u >= A.n) ? 0ull : ((1ull << (A.n - ts0 - lane * 64u)) - 1ull);
-      uint32_t hh = 0;  // halo positions of the last started line
+      // halo positions of the last started line: the lane's 8 halo bytes (hv)
+      // and the next lane's first 4, as four pairs with their reads in flight
+      uint32_t hh = 0;
       const uint32_t hend = last_in_halo ? hfirst : kWT;
       if (lane * 8u + kWT < hend) {
-        for (uint32_t k = 0; k < 8 && kWT + lane * 8u + k < hend; ++k) {
-          const uint32_t g = ld4(T + kWT + lane * 8u + k);  // one position: its gram's left-role bit
-          hh |= ((s_bits[gram_pair_word(g >> 8)] >> (g & 15u)) & 1u) << k;
+        const uint32_t hw[3] = {hv.x, hv.y, *reinterpret_cast<const uint32_t *>(T + kWT + lane * 8u + 8u)};
+        uint32_t word[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = 2 * i;
+          const uint32_t g0 = (k & 3) ? __builtin_amdgcn_alignbyte(hw[(k >> 2) + 1], hw[k >> 2], (uint32_t)(k & 3)) : hw[k >> 2];
+          word[i] = *reinterpret_cast<const uint32_t *>(sb + gram_pair_byte_off(g0 >> 8));
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = 2 * i;
+          const uint32_t lo = hw[k >> 2], hi = hw[(k >> 2) + 1];
+          const uint32_t g0 = (k & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3)) : lo;
+          const uint32_t g1 = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3) + 1u);
+          hh |= (__builtin_amdgcn_ubfe(word[i], g0 & 15u, 1) | (__builtin_amdgcn_ubfe(word[i], (g1 >> 24) | 16u, 1) << 1)) << k;
+        }
+        const uint32_t nv = hend - (kWT + lane * 8u);  // halo positions before hend
+        if (nv < 8) hh &= (1u << nv) - 1u;
       }
       n_probe += __popcll(hits) + __popc(hh);
       if (A.debug_skip & 2) { hits = 0; hh = 0; }
@@ -1580,13 +1617,8 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
       uint32_t remh = hh;
       for (;;) {
         const uint32_t cnt = __popcll(rem) + __popc(remh);
-        uint32_t off = cnt;  // inclusive scan
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t v = __shfl_up(off, o);
-          if (lane >= (uint32_t)o) off += v;
-        }
-        const uint32_t total = __shfl(off, 63);
+        uint32_t off = wave_incl_sum(cnt);
+        const uint32_t total = __builtin_amdgcn_readlane(off, 63);
         if (total == 0) break;
         off -= cnt;
         // append while the list has room (the rest waits for the next round)
@@ -6268,6 +6300,26 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
                        e->jline2.p, (uint64_t)n_jobs, L);
     HIP_OK(hipGetLastError());
     if (B.any_nfa && !e->nfa_rules.empty()) run_nfa_jobs(e, B, buf, n, n_jobs, L);
+    static const bool job_stats = getenv("BJX_JOB_STATS") != nullptr;  // diagnostics: jobs per rule (stderr)
+    if (job_stats) {
+      e->rb_first.ensure(B.n_rules); e->rb_last.ensure(B.n_rules);
+      HIP_OK(hipMemsetAsync(e->rb_first.p, 0, B.n_rules * 4ull, st));
+      HIP_OK(hipMemsetAsync(e->rb_last.p, 0, B.n_rules * 4ull, st));
+      hipLaunchKernelGGL(k_rule_bounds, dim3(grid_for(n_jobs)), dim3(kBlock), 0, st, (uint64_t)n_jobs, e->jkey2.p, e->rb_first.p,
+                         e->rb_last.p);
+      std::vector<uint32_t> f(B.n_rules), l(B.n_rules);
+      HIP_OK(hipMemcpyAsync(f.data(), e->rb_first.p, B.n_rules * 4ull, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(l.data(), e->rb_last.p, B.n_rules * 4ull, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      std::map<std::string, uint64_t> by_rx;
+      for (uint32_t r = 0; r < B.n_rules; ++r)
+        if (l[r] > f[r]) by_rx[r < rs->rules.size() ? rs->rules[r].regex.substr(0, 60) : "?"] += l[r] - f[r];
+      std::vector<std::pair<uint64_t, std::string>> v;
+      for (auto &kv : by_rx) v.push_back({kv.second, kv.first});
+      std::sort(v.rbegin(), v.rend());
+      fprintf(stderr, "BJX_JOB_STATS jobs=%llu lines=%llu\n", n_jobs, (unsigned long long)e->bc.n_lines);
+      for (size_t i = 0; i < v.size() && i < 16; ++i) fprintf(stderr, "  %10llu  %s\n", (unsigned long long)v[i].first, v[i].second.c_str());
+    }
   }
   HIP_OK(hipEventRecord(e->evk[3], st));
   if (n_slow) {
