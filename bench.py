@@ -139,6 +139,46 @@ def roofline(kms, nbytes, args):
     return r
 
 
+def rank_plan(world, rank, local, node_engines, exchange, n_devices, n_lines):
+    """Which engines this rank drives and which lines each engine holds.
+
+    node mode (N>1 with --exchange node, or --node-engines > 1): rank 0 drives
+    every engine through one bjx_node, engine k on device k % n_devices holding
+    lines [k n_lines, (k + 1) n_lines); the other ranks drive nothing and only
+    join the barriers.  Otherwise each rank drives one engine on its local GPU
+    over lines [rank n_lines, (rank + 1) n_lines) (weak scaling)."""
+    node_mode = (world > 1 and exchange == "node") or node_engines > 1
+    drives = not node_mode or rank == 0
+    n_parts = world if world > 1 else max(1, node_engines)
+    devices = [k % n_devices for k in range(n_parts)]
+    if node_mode:
+        chunks = [(devices[k], k * n_lines, n_lines) for k in range(n_parts)] if drives else []
+    else:
+        chunks = [(local, rank * n_lines, n_lines)]
+    return {"node_mode": node_mode, "drives": drives, "n_parts": n_parts, "devices": devices, "chunks": chunks}
+
+
+def timed_region(dist, step, sync_all, steps, clock_device):
+    """K steps bracketed by a barrier + device sync on both sides; the max over
+    ranks of the wall time (every rank calls this the same number of times, a
+    rank that drives nothing with a no-op step)."""
+    if dist:
+        dist.barrier()
+    sync_all()
+    t0 = time.perf_counter()
+    outs = [step() for _ in range(steps)]
+    sync_all()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], device=clock_device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, outs
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -178,17 +218,14 @@ def main():
     w0 = W.ALL[args.config]
     n_lines = args.lines or w0.n_lines
     w = W.scaled(w0, n_lines, n_ips=w0.n_ips) if args.lines else w0
-    node_mode = (world > 1 and args.exchange == "node") or args.node_engines > 1
-    drives = not node_mode or rank == 0  # node mode: rank 0 drives every GPU
-    n_parts = world if world > 1 else max(1, args.node_engines)
-    devices = [k % torch.cuda.device_count() for k in range(n_parts)]
-    # weak scaling: GPU r holds lines [r*n, (r+1)*n) of the workload's stream
+    P = rank_plan(world, rank, local, args.node_engines, args.exchange, torch.cuda.device_count(), n_lines)
+    node_mode, drives, n_parts, devices = P["node_mode"], P["drives"], P["n_parts"], P["devices"]
     first = rank * n_lines
     chunks, keep = [], []
     if node_mode and drives:
-        for k in range(n_parts):
-            with torch.cuda.device(devices[k]):
-                t, nb = w.device_lines(devices[k], k * n_lines, n_lines)
+        for dev, lo, n in P["chunks"]:
+            with torch.cuda.device(dev):
+                t, nb = w.device_lines(dev, lo, n)
                 torch.cuda.synchronize()
             keep.append(t)
             chunks.append((t.data_ptr(), nb))
@@ -240,32 +277,20 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    if dist:
-        dist.barrier()
-    sync_all()
     kacc = {"k_scan": 0.0, "k_lines": 0.0, "dfa_jobs": 0.0}
-    t0 = time.perf_counter()
-    outs = []
-    for _ in range(args.steps):
-        outs.append(step())
+
+    def timed_step():
+        o = step()
         if drives:  # HIP-event times of the step's kernels (host reads only, no sync)
             for k, v in eng.kernel_ms().items():
                 kacc[k] += v
-    sync_all()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        return o
+
+    elapsed, outs = timed_region(dist, timed_step, sync_all, args.steps, "cuda")
     ms_per_step = elapsed * 1000.0 / args.steps
     if not drives:  # node mode, rank > 0: only the barriers and the max-over-ranks clock
         if args.bans_steps > 0 and not bans:
-            dist.barrier()
-            dist.barrier()
-            t = torch.tensor([0.0], device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            timed_region(dist, step, sync_all, args.bans_steps, "cuda")
         dist.barrier()
         dist.destroy_process_group()
         return
@@ -280,20 +305,7 @@ def main():
     dec = None
     if args.bans_steps > 0 and not bans:
         bans = True
-        if dist:
-            dist.barrier()
-        sync_all()
-        t1 = time.perf_counter()
-        for _ in range(args.bans_steps):
-            step()
-        sync_all()
-        if dist:
-            dist.barrier()
-        el2 = time.perf_counter() - t1
-        if dist:
-            t = torch.tensor([el2], device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el2 = float(t.item())
+        el2, _ = timed_region(dist, step, sync_all, args.bans_steps, "cuda")
         bans = False
         dec = {"value": round(n_lines * n_parts / (el2 / args.bans_steps), 1), "unit": "lines/s",
                "ms_per_step": round(el2 * 1000.0 / args.bans_steps, 3), "steps": args.bans_steps,
