@@ -827,22 +827,38 @@ __device__ __forceinline__ bool has_pos(uint64_t m0, uint64_t m1, uint32_t pos) 
   return ((pos < 64 ? m0 >> pos : m1 >> (pos - 64)) & 1) != 0;
 }
 
-// DFA work found by the scan pass: staged per wave in LDS, appended to HBM
-// with one atomic per wave tile (overflow goes straight to HBM).
+// DFA work found by the line kernels: staged per wave in LDS, appended to HBM
+// with one atomic per wave tile (overflow goes straight to HBM).  A job is
+// its line, key (rule | position << 24), slot index (the job sort's value:
+// k_dfa finds the line and the window by it) and window record (jrec below).
 struct JobSink {
-  uint2 *lds;
+  uint4 *lds;
   uint32_t *cnt;
-  uint32_t *jline, *jkey;  // job = (line, rule | position << 24)
+  uint32_t *jline, *jkey, *jidx;
+  uint64_t *jrec;
   unsigned long long *count;
   uint64_t cap;
 };
-constexpr uint32_t kWaveJobBytes = kWaveJobs * 8 + 16;  // per wave: staged jobs + their counter
-__device__ __forceinline__ void emit_job(const JobSink &S, uint64_t j, uint32_t r, uint32_t pos) {
-  const uint2 v = make_uint2((uint32_t)j, r | (pos << 24));
+// Job window records (JobSink::jrec): where k_dfa starts the rule's automaton,
+// worked out by the line kernel from the line's hits in registers (k_dfa then
+// reads this record and the text, not the line's arrays):
+//   bits 0-39 absolute batch offset of the first byte, the text runs to the
+//   line's '\n'; kJobSkipState: start in the rule's skip_state (an anchored
+//   prefix already matched), else its start state; kJobNoCount: the rule is in
+//   the host's hosts_to_skip (a RuleResult, no event).  kJobLegacy: k_dfa
+//   derives the window from the line's arrays (kernels other than k_lines2,
+//   NFA rules, lead seeks past overflowed hit slots).
+constexpr uint64_t kJobOffMask = (1ull << 40) - 1;
+constexpr uint64_t kJobSkipState = 1ull << 40;
+constexpr uint64_t kJobNoCount = 1ull << 41;
+constexpr uint64_t kJobLegacy = 1ull << 63;
+constexpr uint32_t kWaveJobBytes = kWaveJobs * 16 + 16;  // per wave: staged jobs + their counter
+__device__ __forceinline__ void emit_job(const JobSink &S, uint64_t j, uint32_t r, uint32_t pos, uint64_t rec = kJobLegacy) {
+  const uint4 v = make_uint4((uint32_t)j, r | (pos << 24), (uint32_t)rec, (uint32_t)(rec >> 32));
   const uint32_t c = atomicAdd(S.cnt, 1u);
   if (c < kWaveJobs) { S.lds[c] = v; return; }
   const unsigned long long g = atomicAdd(S.count, 1ull);
-  if (g < S.cap) { S.jline[g] = v.x; S.jkey[g] = v.y; }
+  if (g < S.cap) { S.jline[g] = v.x; S.jkey[g] = v.y; S.jidx[g] = (uint32_t)g; S.jrec[g] = rec; }
 }
 
 // A wave appends its staged jobs into a chunk of the batch's job array that it
@@ -874,7 +890,11 @@ __device__ __forceinline__ void flush_jobs(const JobSink &S, JobChunk &C, uint32
     const uint32_t take = min(C.left, nj - done);
     for (uint32_t i = lane; i < take; i += 64) {
       const uint64_t g = C.base + i;
-      if (g < S.cap) { S.jline[g] = S.lds[done + i].x; S.jkey[g] = S.lds[done + i].y; }
+      const uint4 v = S.lds[done + i];
+      if (g < S.cap) {
+        S.jline[g] = v.x; S.jkey[g] = v.y; S.jidx[g] = (uint32_t)g;
+        S.jrec[g] = ((uint64_t)v.w << 32) | v.z;
+      }
     }
     C.base += take;
     C.left -= take;
@@ -888,7 +908,7 @@ __device__ __forceinline__ void close_jobs(const JobSink &S, JobChunk &C, uint32
                                            unsigned long long *real) {
   for (uint32_t i = lane; i < C.left; i += 64) {
     const uint64_t g = C.base + i;
-    if (g < S.cap) { S.jline[g] = 0; S.jkey[g] = null_key; }
+    if (g < S.cap) { S.jline[g] = 0; S.jkey[g] = null_key; S.jidx[g] = (uint32_t)g; S.jrec[g] = kJobLegacy; }
   }
   if (lane == 0 && C.real) atomicAdd(real, (unsigned long long)C.real);
 }
@@ -1734,7 +1754,8 @@ struct LinesArgs {
   int64_t now_ns;
   uint32_t *slow_list;
   unsigned long long *slow_count;
-  uint32_t *jline, *jkey;
+  uint32_t *jline, *jkey, *jidx;
+  uint64_t *jrec;
   unsigned long long *job_count;  // job slots taken (chunks)
   unsigned long long *job_real;   // real jobs (the rest are null jobs, key null_key)
   uint32_t null_key;
@@ -1870,10 +1891,12 @@ __global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
     __syncthreads();
   }
   JobSink S;
-  S.lds = reinterpret_cast<uint2 *>(s_dyn + img_al + hl_al + wave * kWaveJobBytes);
+  S.lds = reinterpret_cast<uint4 *>(s_dyn + img_al + hl_al + wave * kWaveJobBytes);
   S.cnt = reinterpret_cast<uint32_t *>(S.lds + kWaveJobs);
   S.jline = A.jline;
   S.jkey = A.jkey;
+  S.jidx = A.jidx;
+  S.jrec = A.jrec;
   S.count = A.job_count;
   S.cap = A.job_cap;
   if (lane == 0) *S.cnt = 0;
@@ -1981,7 +2004,8 @@ struct RulesArgs {
   Lines L;
   uint32_t *todo;
   unsigned long long *todo_count;
-  uint32_t *jline, *jkey;
+  uint32_t *jline, *jkey, *jidx;
+  uint64_t *jrec;
   unsigned long long *job_count;
   unsigned long long *job_real;
   uint32_t null_key;
@@ -1999,10 +2023,12 @@ __global__ __launch_bounds__(kBlock) void k_rules(Bind B, RulesArgs A) {
   const Tabs TB = make_tabs(IMG_LDS ? s_img : B.img, B.il);
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   JobSink S;
-  S.lds = reinterpret_cast<uint2 *>(s_dyn + ((IMG_LDS ? B.img_bytes : 0) + 15u & ~15u) + wave * kWaveJobBytes);
+  S.lds = reinterpret_cast<uint4 *>(s_dyn + ((IMG_LDS ? B.img_bytes : 0) + 15u & ~15u) + wave * kWaveJobBytes);
   S.cnt = reinterpret_cast<uint32_t *>(S.lds + kWaveJobs);
   S.jline = A.jline;
   S.jkey = A.jkey;
+  S.jidx = A.jidx;
+  S.jrec = A.jrec;
   S.count = A.job_count;
   S.cap = A.job_cap;
   if (lane == 0) *S.cnt = 0;
@@ -2320,9 +2346,103 @@ __device__ __forceinline__ bool dfa_text(const Bind &B, const DevRule &R, const 
   return B.accept_end[R.ae_off + st] != 0;
 }
 
+// dfa_text over the text from t0 to the line's '\n' (a job window record,
+// kJob*): the end is found in the 16 B loads the automaton steps over anyway
+__device__ __forceinline__ uint32_t nl_mask16(const uint4 v) {
+  const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+  uint32_t m = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t hb = nl_mask_word(wv[q]);
+    m |= (((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u)) << (4 * q);
+  }
+  return m;
+}
+template <bool STAGED>
+__device__ __forceinline__ bool dfa_line(const Bind &B, const DevRule &R, const uint16_t *tr, const uint8_t *ac,
+                                         const uint32_t *acc, const uint8_t *__restrict__ buf, uint64_t n_buf, uint64_t t0,
+                                         uint32_t st0) {
+  const uint32_t ncls = R.ncls;
+  uint32_t st = st0;
+  uint64_t a = t0 & ~15ull;
+  uint32_t skip = (uint32_t)(t0 - a);
+  auto load16 = [&](uint64_t p) -> uint4 {
+    if (p + 16 <= n_buf) return *reinterpret_cast<const uint4 *>(buf + p);
+    uint32_t w[4];
+    for (int k = 0; k < 4; ++k) {
+      uint32_t x = 0;
+      for (int b = 0; b < 4; ++b) x |= (p + 4 * k + b < n_buf ? (uint32_t)buf[p + 4 * k + b] : 0x0Au) << (8 * b);
+      w[k] = x;
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  };
+  uint4 v = load16(a);
+  for (;;) {
+    uint32_t nlm = nl_mask16(v) & ~((1u << skip) - 1u);
+    const uint32_t aw = acc ? acc[st] : 0u;
+    if ((aw >> 31) && !nlm) {
+      // self-loop state: skip 16 B at a time up to an escape byte or the '\n'
+      for (;;) {
+        const uint32_t m = accel_mask(v, aw) & ~((1u << skip) - 1u);
+        if (m || nlm) {
+          const uint32_t f = (uint32_t)__ffs(m | nlm) - 1;
+          skip = f;
+          break;
+        }
+        a += 16;
+        skip = 0;
+        v = load16(a);
+        nlm = nl_mask16(v);
+      }
+    } else if (aw >> 31) {
+      const uint32_t m = (accel_mask(v, aw) | nlm) & ~((1u << skip) - 1u);
+      skip = (uint32_t)__ffs(m) - 1;  // m != 0: nlm has a bit at or past skip
+    }
+    const uint32_t lim = nlm ? (uint32_t)__ffs(nlm) - 1 : 16u;  // bytes before the '\n'
+    const uint4 vn = lim == 16u ? load16(a + 16) : make_uint4(0, 0, 0, 0);
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) {
+      if (k < skip || k >= lim) continue;
+      const uint32_t b = (wv[k >> 2] >> (8 * (k & 3))) & 0xFF;
+      if (b >= 0x80) {
+        // non-ASCII: decode runes from here to the '\n' (Go's regexp steps by rune)
+        uint64_t i = a + k, end = i;
+        while (end < n_buf && buf[end] != '\n') ++end;
+        while (i < end) {
+          int w;
+          const int32_t rune = decode_rune_hd(buf + i, (uint32_t)(end - i), &w);
+          uint32_t c;
+          if (rune < 0x80) c = ac[rune];
+          else {
+            const uint32_t *na = B.nonascii + 2 * R.na_off;
+            uint32_t lo = 0, hi = R.n_na;
+            while (hi - lo > 1) {
+              const uint32_t m = (lo + hi) >> 1;
+              if (na[2 * m] <= (uint32_t)rune) lo = m; else hi = m;
+            }
+            c = na[2 * lo + 1];
+          }
+          i += (uint32_t)w;
+          st = tr[st * ncls + c];
+          if (st <= 1) break;
+        }
+        return B.accept_end[R.ae_off + st] != 0;
+      }
+      st = tr[st * ncls + ac[b]];
+      if (st <= 1) return st == kAccept;
+    }
+    if (lim < 16u) return B.accept_end[R.ae_off + st] != 0;
+    skip = 0;
+    a += 16;
+    v = vn;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restrict__ buf, uint64_t n_buf,
                                                 const uint64_t *__restrict__ nl, const uint32_t *__restrict__ jkey,
-                                                const uint32_t *__restrict__ jline, uint64_t n, Lines L) {
+                                                const uint32_t *__restrict__ jidx, const uint32_t *__restrict__ jline,
+                                                const uint64_t *__restrict__ jrec, uint64_t n, Lines L) {
   __shared__ uint16_t s_tr[kDfaLdsEntries];
   __shared__ uint32_t s_acc[kDfaAccelLds];
   __shared__ uint8_t s_ac[128];
@@ -2345,40 +2465,60 @@ __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restric
   if (t >= n) return;
   const uint32_t key = jkey[t];
   const uint32_t r = key & 0xFFFFFF, pos = key >> 24;
-  const uint64_t j = jline[t];
-  const uint64_t s = j ? nl[j - 1] + 1 : 0;
-  const uint64_t rs = s + L.rest_off[j];
-  const uint32_t rl = (uint32_t)(nl[j] - rs);
+  const uint32_t slot = jidx[t];
+  const uint64_t rec = jrec[slot];
   bool m;
+  uint64_t j = 0;
+  bool no_count;
   if (!staged && (B.rules[r].flags & kRuleNfa)) return;  // k_nfa's (a mixed block)
-  if ((staged ? R0.equiv : B.rules[r].equiv) && eq_certain(B, L, j, pos, rs)) {
-    m = true;
-  } else if (staged) {
-    // anchored prefix literal already matched by k_lines: step in past it;
-    // a lead rule's job starts at the first hit of its literals (every match
-    // begins at one, regex_compiler.h pref_lead)
-    const uint32_t sk = R0.skip_len && R0.skip_len <= rl ? R0.skip_len : 0u;
-    const uint32_t st0 = (R0.lead & 1u) ? lead_start_seek(B, R0, L, buf, n_buf, j, pos, rs, rl) : 0u;
-    const uint32_t *acc = R0.n_states <= kDfaAccelLds ? s_acc : B.accel + R0.ae_off;
-    m = st0 ? dfa_text<true>(B, R0, s_tr, s_ac, acc, buf, n_buf, rs + st0, rl - st0, R0.start)
-            : dfa_text<true>(B, R0, s_tr, s_ac, acc, buf, n_buf, rs + sk, rl - sk, sk ? R0.skip_state : R0.start);
+  if (!(rec & kJobLegacy)) {
+    // the window the line kernel worked out: the text from there to the '\n'
+    const uint64_t a = rec & kJobOffMask;
+    if (staged) {
+      const uint32_t *acc = R0.n_states <= kDfaAccelLds ? s_acc : B.accel + R0.ae_off;
+      m = dfa_line<true>(B, R0, s_tr, s_ac, acc, buf, n_buf, a, (rec & kJobSkipState) ? R0.skip_state : R0.start);
+    } else {
+      const DevRule R = B.rules[r];
+      m = dfa_line<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, B.accel + R.ae_off, buf, n_buf, a,
+                          (rec & kJobSkipState) ? R.skip_state : R.start);
+    }
+    if (!m) return;
+    j = jline[slot];
+    no_count = (rec & kJobNoCount) != 0;
   } else {
-    const DevRule R = B.rules[r];
-    if (R.flags & kRuleNfa) return;  // k_nfa's
-    const uint32_t sk = R.skip_len && R.skip_len <= rl ? R.skip_len : 0u;
-    const uint32_t st0 = (R.lead & 1u) ? lead_start_seek(B, R, L, buf, n_buf, j, pos, rs, rl) : 0u;
-    const uint32_t *acc = B.accel + R.ae_off;
-    if (st0) m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, acc, buf, n_buf, rs + st0,
-                                 rl - st0, R.start);
-    else m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, acc, buf, n_buf, rs + sk, rl - sk,
-                             sk ? R.skip_state : R.start);
+    j = jline[slot];
+    const uint64_t s = j ? nl[j - 1] + 1 : 0;
+    const uint64_t rs = s + L.rest_off[j];
+    const uint32_t rl = (uint32_t)(nl[j] - rs);
+    if ((staged ? R0.equiv : B.rules[r].equiv) && eq_certain(B, L, j, pos, rs)) {
+      m = true;
+    } else if (staged) {
+      // anchored prefix literal already matched by k_lines: step in past it;
+      // a lead rule's job starts at the first hit of its literals (every match
+      // begins at one, regex_compiler.h pref_lead)
+      const uint32_t sk = R0.skip_len && R0.skip_len <= rl ? R0.skip_len : 0u;
+      const uint32_t st0 = (R0.lead & 1u) ? lead_start_seek(B, R0, L, buf, n_buf, j, pos, rs, rl) : 0u;
+      const uint32_t *acc = R0.n_states <= kDfaAccelLds ? s_acc : B.accel + R0.ae_off;
+      m = st0 ? dfa_text<true>(B, R0, s_tr, s_ac, acc, buf, n_buf, rs + st0, rl - st0, R0.start)
+              : dfa_text<true>(B, R0, s_tr, s_ac, acc, buf, n_buf, rs + sk, rl - sk, sk ? R0.skip_state : R0.start);
+    } else {
+      const DevRule R = B.rules[r];
+      if (R.flags & kRuleNfa) return;  // k_nfa's
+      const uint32_t sk = R.skip_len && R.skip_len <= rl ? R.skip_len : 0u;
+      const uint32_t st0 = (R.lead & 1u) ? lead_start_seek(B, R, L, buf, n_buf, j, pos, rs, rl) : 0u;
+      const uint32_t *acc = B.accel + R.ae_off;
+      if (st0) m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, acc, buf, n_buf, rs + st0,
+                                   rl - st0, R.start);
+      else m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, acc, buf, n_buf, rs + sk, rl - sk,
+                               sk ? R.skip_state : R.start);
+    }
+    if (!m) return;
+    const int32_t hid = L.host_id[j];
+    const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
+    no_count = (B.sc_skip[2 * sc + (pos >> 6)] >> (pos & 63)) & 1;
   }
-  if (!m) return;
-  const int32_t hid = L.host_id[j];
-  const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
-  const bool skip = (B.sc_skip[2 * sc + (pos >> 6)] >> (pos & 63)) & 1;
   atomicOr(reinterpret_cast<unsigned long long *>(L.masks + j * B.mask_words + (pos >> 6)), 1ull << (pos & 63));
-  atomicAdd(reinterpret_cast<unsigned long long *>(L.counts + j), (1ull << 32) | (skip ? 0ull : 1ull));
+  atomicAdd(reinterpret_cast<unsigned long long *>(L.counts + j), (1ull << 32) | (no_count ? 0ull : 1ull));
 }
 
 // DFA jobs of one kRuleNfa rule (the sorted job range [j0, j1)): one job per
@@ -2388,7 +2528,8 @@ __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restric
 template <int WT>
 __global__ __launch_bounds__(kBlock) void k_nfa(Bind B, uint32_t rule, const uint8_t *__restrict__ buf, uint64_t n_buf,
                                                 const uint64_t *__restrict__ nl, const uint32_t *__restrict__ jkey,
-                                                const uint32_t *__restrict__ jline, uint64_t j0, uint64_t j1, Lines L) {
+                                                const uint32_t *__restrict__ jidx, const uint32_t *__restrict__ jline,
+                                                uint64_t j0, uint64_t j1, Lines L) {
   uint64_t *s_b = reinterpret_cast<uint64_t *>(s_dyn);
   const DevRule R = B.rules[rule];
   const uint64_t *g = B.nfa + R.nfa_off;
@@ -2400,7 +2541,7 @@ __global__ __launch_bounds__(kBlock) void k_nfa(Bind B, uint32_t rule, const uin
   const NfaLayout Ly = nfa_layout_of(reinterpret_cast<const uint32_t *>(s_b));
   const uint16_t *a16 = reinterpret_cast<const uint16_t *>(s_b + Ly.o_ascii);
   const uint32_t key = jkey[t], pos = key >> 24;
-  const uint64_t j = jline[t];
+  const uint64_t j = jline[jidx ? jidx[t] : t];
   const uint64_t s = j ? nl[j - 1] + 1 : 0;
   const uint64_t end = nl[j];
   uint64_t t0 = s + L.rest_off[j];
@@ -2479,7 +2620,8 @@ __device__ __forceinline__ void wide_sync() {
 template <bool GLB>
 __global__ __launch_bounds__(kBlock) void k_nfa_wide(Bind B, const uint8_t *__restrict__ buf, uint64_t n_buf,
                                                      const uint64_t *__restrict__ nl, const uint32_t *__restrict__ jkey,
-                                                     const uint32_t *__restrict__ jline, const uint32_t *__restrict__ jpos,
+                                                     const uint32_t *__restrict__ jidx, const uint32_t *__restrict__ jline,
+                                                     const uint32_t *__restrict__ jpos,
                                                      uint64_t j0, uint64_t j1, Lines L, uint64_t *scratch,
                                                      uint64_t scratch_words) {
   __shared__ uint32_t s_flag;
@@ -2487,7 +2629,7 @@ __global__ __launch_bounds__(kBlock) void k_nfa_wide(Bind B, const uint8_t *__re
   for (uint64_t t = j0 + blockIdx.x; t < j1; t += gridDim.x) {
     const uint32_t key = jkey[t], r = key & 0xFFFFFFu;
     const uint32_t pos = jpos ? jpos[t] : key >> 24;
-    const uint64_t j = jline[t];
+    const uint64_t j = jline[jidx ? jidx[t] : t];
     const DevRule R = B.rules[r];
     const uint64_t *b = B.nfa + R.nfa_off;
     const NfaWideLayout Ly = nfa_wide_layout_of(reinterpret_cast<const uint32_t *>(b));
@@ -4220,7 +4362,8 @@ struct bjx_engine {
   DevBuf<uint64_t> l_cand;
   DevBuf<uint4> l_ip16;
   DevBuf<uint32_t> long_list;
-  DevBuf<uint32_t> jline, jkey, jline2, jkey2;
+  DevBuf<uint32_t> jline, jkey, jidx, jidx2, jkey2;  // jobs by slot (line, key, slot), the sorted keys and slots
+  DevBuf<uint64_t> jrec;                           // job window records by slot (kJob*)
   uint64_t last_jobs = 0, last_todo = 0, last_long_runs = 0;
   DevBuf<uint64_t> long_heads;
   DevBuf<uint64_t> lr_end, lr_len, lr_off, lr_win;
@@ -5317,7 +5460,22 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
             "plan %zu entries, lit-rule ents %zu, hosts %zu\n", img.size(), il.ge - il.gt, il.ht - il.ge, il.lrec - il.ht,
             img.size() - il.lrec, il.lbytes - il.lrec, lb_al.size(), plan.size() / 2, lr_ent.size(), hd.size());
 
+  // per rule, what k_lines2 needs to work out a job's window (l2_job_rec):
+  // {literal-id mask (ids < 32), flags | lead_dist << 16, skip_len, 0}
+  std::vector<uint4> jinfo(drules.size());
+  for (size_t r = 0; r < drules.size(); ++r) {
+    const DevRule &d = drules[r];
+    uint32_t lm = 0, big = 0;
+    for (uint32_t k = 0; k < d.lits_len; ++k) {
+      const uint32_t id = rule_lits[d.lits_off + k];
+      if (id < 32) lm |= 1u << id; else big = 1;
+    }
+    jinfo[r] = make_uint4(lm, ((d.flags & kRuleNfa) ? kJiNfa : 0u) | (d.equiv ? kJiEquiv : 0u) | ((uint32_t)(d.lead & 3u) << 2) |
+                                  (big ? kJiBigLit : 0u) | ((uint32_t)d.lead_dist << 16),
+                          d.skip_len, 0u);
+  }
   BlobBuilder bb;
+  size_t o_jinfo = bb.add(jinfo);
   size_t o_rules = bb.add(drules), o_trans = bb.add(trans), o_ae = bb.add(ae), o_accel = bb.add(accel), o_ascii = bb.add(ascii),
          o_na = bb.add(nonascii), o_lits = bb.add(lits), o_glob = bb.add(global_rules), o_soff = bb.add(site_off),
          o_srules = bb.add(site_rules), o_hdh = bb.add(hd_hash), o_hdid = bb.add(hd_id), o_hdoff = bb.add(hd_off),
@@ -5337,6 +5495,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   uint8_t *base = e->bind_blob.p;
   Bind &B = e->bind;
   B.rules = reinterpret_cast<const DevRule *>(base + o_rules);
+  B.jinfo = reinterpret_cast<const uint4 *>(base + o_jinfo);
   B.trans = reinterpret_cast<const uint16_t *>(base + o_trans);
   B.accept_end = base + o_ae;
   B.accel = reinterpret_cast<const uint32_t *>(base + o_accel);
@@ -5643,7 +5802,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   e->d_results.release(); e->q_out.release();
   e->ban_ips.release(); e->ban_log.release(); e->ban_off.release(); e->ban_kind.release(); e->ban_ipb.release();
   e->ban_ipo.release();
-  e->long_list.release(); e->l_ip16.release(); e->jline.release(); e->jkey.release(); e->jline2.release(); e->jkey2.release(); e->l_cand.release(); e->l_ccnt.release(); e->l_cfirst.release();
+  e->long_list.release(); e->l_ip16.release(); e->jline.release(); e->jkey.release(); e->jidx.release(); e->jidx2.release(); e->jrec.release(); e->jkey2.release(); e->l_cand.release(); e->l_ccnt.release(); e->l_cfirst.release();
   (void)hipEventDestroy(e->ev0); (void)hipEventDestroy(e->ev1); (void)hipEventDestroy(e->evm0); (void)hipEventDestroy(e->evm1);
   for (auto &x : e->evk) (void)hipEventDestroy(x);
   for (auto &x : e->ph) (void)hipEventDestroy(x);
@@ -5956,7 +6115,7 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
 // k_nfa_wide over jobs [j0, j1): the state in LDS when it fits 64 KB, else
 // in a per-block HBM scratch (grid-stride over the jobs either way)
 static void launch_wide(bjx_engine *e, const Bind &B, const uint8_t *buf, uint64_t n, const uint32_t *jkey,
-                        const uint32_t *jline, const uint32_t *jpos, uint64_t j0, uint64_t j1, const Lines &L, uint32_t W,
+                        const uint32_t *jidx, const uint32_t *jline, const uint32_t *jpos, uint64_t j0, uint64_t j1, const Lines &L, uint32_t W,
                         uint32_t ng) {
   hipStream_t st = e->stream;
   const uint64_t words = 2ull * W + (ng + 63) / 64 + 1;
@@ -5964,11 +6123,11 @@ static void launch_wide(bjx_engine *e, const Bind &B, const uint8_t *buf, uint64
   if (words * 8 <= 64 * 1024 && !force_glb) {
     const unsigned grid = (unsigned)std::min<uint64_t>(j1 - j0, 8192);
     hipLaunchKernelGGL(k_nfa_wide<false>, dim3(grid), dim3(kBlock), (uint32_t)(words * 8), st, B, buf, n, e->nl.p, jkey,
-                       jline, jpos, j0, j1, L, nullptr, (uint64_t)0);
+                       jidx, jline, jpos, j0, j1, L, nullptr, (uint64_t)0);
   } else {
     const unsigned grid = (unsigned)std::min<uint64_t>(j1 - j0, 512);
     e->wide_scratch.ensure(grid * words);
-    hipLaunchKernelGGL(k_nfa_wide<true>, dim3(grid), dim3(kBlock), 0, st, B, buf, n, e->nl.p, jkey, jline, jpos, j0, j1, L,
+    hipLaunchKernelGGL(k_nfa_wide<true>, dim3(grid), dim3(kBlock), 0, st, B, buf, n, e->nl.p, jkey, jidx, jline, jpos, j0, j1, L,
                        e->wide_scratch.p, words);
   }
   HIP_OK(hipGetLastError());
@@ -5991,17 +6150,17 @@ static void run_nfa_jobs(bjx_engine *e, const Bind &B, const uint8_t *buf, uint6
     const uint64_t j0 = e->h_first[nr.x], j1 = e->h_last[nr.x];
     if (j1 <= j0) continue;
     if (nr.w) {  // kRuleNfaWide: nr.y = state words, nr.z = groups
-      launch_wide(e, B, buf, n, e->jkey2.p, e->jline2.p, nullptr, j0, j1, L, nr.y, nr.z);
+      launch_wide(e, B, buf, n, e->jkey2.p, e->jidx2.p, e->jline.p, nullptr, j0, j1, L, nr.y, nr.z);
       continue;
     }
     const unsigned grid = grid_for(j1 - j0);
     const uint32_t lds = nr.z * 8;
     switch (nr.y) {
-      case 1: hipLaunchKernelGGL(k_nfa<1>, dim3(grid), dim3(kBlock), lds, st, B, nr.x, buf, n, e->nl.p, e->jkey2.p, e->jline2.p, j0, j1, L); break;
-      case 2: hipLaunchKernelGGL(k_nfa<2>, dim3(grid), dim3(kBlock), lds, st, B, nr.x, buf, n, e->nl.p, e->jkey2.p, e->jline2.p, j0, j1, L); break;
-      case 4: hipLaunchKernelGGL(k_nfa<4>, dim3(grid), dim3(kBlock), lds, st, B, nr.x, buf, n, e->nl.p, e->jkey2.p, e->jline2.p, j0, j1, L); break;
-      case 8: hipLaunchKernelGGL(k_nfa<8>, dim3(grid), dim3(kBlock), lds, st, B, nr.x, buf, n, e->nl.p, e->jkey2.p, e->jline2.p, j0, j1, L); break;
-      default: hipLaunchKernelGGL(k_nfa<16>, dim3(grid), dim3(kBlock), lds, st, B, nr.x, buf, n, e->nl.p, e->jkey2.p, e->jline2.p, j0, j1, L); break;
+      case 1: hipLaunchKernelGGL(k_nfa<1>, dim3(grid), dim3(kBlock), lds, st, B, nr.x, buf, n, e->nl.p, e->jkey2.p, e->jidx2.p, e->jline.p, j0, j1, L); break;
+      case 2: hipLaunchKernelGGL(k_nfa<2>, dim3(grid), dim3(kBlock), lds, st, B, nr.x, buf, n, e->nl.p, e->jkey2.p, e->jidx2.p, e->jline.p, j0, j1, L); break;
+      case 4: hipLaunchKernelGGL(k_nfa<4>, dim3(grid), dim3(kBlock), lds, st, B, nr.x, buf, n, e->nl.p, e->jkey2.p, e->jidx2.p, e->jline.p, j0, j1, L); break;
+      case 8: hipLaunchKernelGGL(k_nfa<8>, dim3(grid), dim3(kBlock), lds, st, B, nr.x, buf, n, e->nl.p, e->jkey2.p, e->jidx2.p, e->jline.p, j0, j1, L); break;
+      default: hipLaunchKernelGGL(k_nfa<16>, dim3(grid), dim3(kBlock), lds, st, B, nr.x, buf, n, e->nl.p, e->jkey2.p, e->jidx2.p, e->jline.p, j0, j1, L); break;
     }
     HIP_OK(hipGetLastError());
   }
@@ -6099,7 +6258,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     HIP_OK(hipMemsetAsync(e->l_cfirst.p, 0xFF, n_lines * kCandFirstLits * 8, st));
   }
   e->jline.ensure(std::max<uint64_t>(e->jline.n, n_lines + (1u << 20)));
-  e->jkey.ensure(e->jline.n);
+  e->jkey.ensure(e->jline.n); e->jidx.ensure(e->jline.n); e->jrec.ensure(e->jline.n);
   HIP_OK(hipMemsetAsync(e->scalars.p, 0, 16 * sizeof(unsigned long long), st));
   if (B.any_prefilter) HIP_OK(hipMemsetAsync(e->l_ccnt.p, 0, n_lines * sizeof(CandMeta), st));
   // BJX_SCAN_HEADER=1: the scan pass parses the header of every line that fits
@@ -6172,7 +6331,8 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     A.buf = buf; A.n = n; A.nl = e->nl.p; A.n_lines = n_lines; A.L = L; A.now_ns = now_ns;
     A.dbg = getenv("BJX_DEBUG_LINES") ? (uint32_t)atoi(getenv("BJX_DEBUG_LINES")) : 0u;
     A.slow_list = e->slow_list.p; A.slow_count = e->scalars.p;
-    A.jline = e->jline.p; A.jkey = e->jkey.p; A.job_count = e->scalars.p + 11; A.job_cap = std::min(e->jline.n, e->jkey.n);
+    A.jline = e->jline.p; A.jkey = e->jkey.p; A.jidx = e->jidx.p; A.jrec = e->jrec.p; A.job_count = e->scalars.p + 11;
+    A.job_cap = std::min(std::min(e->jline.n, e->jkey.n), std::min(e->jidx.n, e->jrec.n));
     A.job_real = e->scalars.p + 14;
     A.null_key = B.n_rules;  // sorts after every rule id (the job sort covers bit_width(n_rules) bits)
     A.span_bytes = getenv("BJX_SPAN_BYTES") ? (uint32_t)atoi(getenv("BJX_SPAN_BYTES")) & ~15u : kSpanBytes;
@@ -6181,7 +6341,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     if (scan_hdr) {
       RulesArgs R;
       R.buf = buf; R.nl = e->nl.p; R.n_lines = n_lines; R.L = L; R.todo = e->long_list.p; R.todo_count = e->scalars.p + 12;
-      R.jline = A.jline; R.jkey = A.jkey; R.job_count = A.job_count; R.job_cap = A.job_cap;
+      R.jline = A.jline; R.jkey = A.jkey; R.jidx = A.jidx; R.jrec = A.jrec; R.job_count = A.job_count; R.job_cap = A.job_cap;
       R.job_real = A.job_real; R.null_key = A.null_key;
       const bool img_lds = B.img_bytes <= kRulesImgMax;
       const uint32_t lds = ((img_lds ? B.img_bytes : 0) + 15u & ~15u) + (kBlock / 64) * kWaveJobBytes;
@@ -6210,6 +6370,8 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&k_lines2), kL2Block, lds));
       const uint64_t resident = (uint64_t)std::max(1, per_cu) * (uint64_t)std::max(1, n_cu);
       const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n_lines + kL2Block - 1) / kL2Block, resident));
+      static const bool dbg_img = getenv("BJX_DEBUG_IMG") != nullptr;
+      if (dbg_img) fprintf(stderr, "[bjx] k_lines2: %u B LDS per block (tables %u), %d blocks per CU, grid %u\n", lds, B.l2_bytes, per_cu, grid);
       hipLaunchKernelGGL(k_lines2, dim3(grid), dim3(kL2Block), lds, st, B, A);
       HIP_OK(hipGetLastError());
     } else if (!scan_hdr || n_todo) {
@@ -6266,11 +6428,13 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     HIP_OK(hipMemcpyAsync(sc4, e->scalars.p + 8, 32, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(sc4 + 4, e->scalars.p, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    if (sc4[3] <= std::min(e->jline.n, e->jkey.n)) break;
+    if (sc4[3] <= std::min(std::min(e->jline.n, e->jkey.n), std::min(e->jidx.n, e->jrec.n))) break;
     // more DFA jobs than the buffer holds: grow it and redo the (idempotent) line pass
     if (attempt > 0) throw BjxError(BJX_ERR_DEVICE, "internal: DFA job buffer overflow");
     e->jline.ensure(sc4[3] + (1u << 20));
     e->jkey.ensure(sc4[3] + (1u << 20));
+    e->jidx.ensure(sc4[3] + (1u << 20));
+    e->jrec.ensure(sc4[3] + (1u << 20));
     HIP_OK(hipMemsetAsync(e->scalars.p, 0, 8, st));
     HIP_OK(hipMemsetAsync(e->scalars.p + 11, 0, 16, st));
     HIP_OK(hipMemsetAsync(e->scalars.p + 14, 0, 8, st));
@@ -6287,17 +6451,17 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   HIP_OK(hipEventRecord(e->evk[2], st));
   if (n_jobs) {
     // group the jobs by rule (stable: line order inside a rule), then one lane per job
-    e->jline2.ensure(n_slots); e->jkey2.ensure(n_slots);
+    e->jidx2.ensure(n_slots); e->jkey2.ensure(n_slots);
     {
       // null jobs (key n_rules) sort after the real ones: k_dfa takes the first n_jobs
-      uint32_t *ki = e->jkey.p, *ko = e->jkey2.p, *vi = e->jline.p, *vo = e->jline2.p;
+      uint32_t *ki = e->jkey.p, *ko = e->jkey2.p, *vi = e->jidx.p, *vo = e->jidx2.p;
       const int bits = std::max(1, bit_width(B.n_rules));
       cub_call(e, [&](void *tmp, size_t &bytes) {
         return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)n_slots, 0, bits, st);
       });
     }
     hipLaunchKernelGGL(k_dfa, dim3(grid_for(n_jobs)), dim3(kBlock), 0, st, B, buf, (uint64_t)n, e->nl.p, e->jkey2.p,
-                       e->jline2.p, (uint64_t)n_jobs, L);
+                       e->jidx2.p, e->jline.p, e->jrec.p, (uint64_t)n_jobs, L);
     HIP_OK(hipGetLastError());
     if (B.any_nfa && !e->nfa_rules.empty()) run_nfa_jobs(e, B, buf, n, n_jobs, L);
     static const bool job_stats = getenv("BJX_JOB_STATS") != nullptr;  // diagnostics: jobs per rule (stderr)
@@ -6338,7 +6502,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       HIP_OK(hipMemcpyAsync(&n_wl, e->scalars.p + 13, 8, hipMemcpyDeviceToHost, st));
       HIP_OK(hipStreamSynchronize(st));
       if (n_wl > WL.cap) throw BjxError(BJX_ERR_DEVICE, "internal: wide-NFA job list overflow");
-      if (n_wl) launch_wide(e, B, buf, n, e->wl_rule.p, e->wl_line.p, e->wl_pos.p, 0, n_wl, L, e->wide_max_w, e->wide_max_g);
+      if (n_wl) launch_wide(e, B, buf, n, e->wl_rule.p, nullptr, e->wl_line.p, e->wl_pos.p, 0, n_wl, L, e->wide_max_w, e->wide_max_g);
     }
   }
   e->last_slow = n_slow;

@@ -37,6 +37,9 @@ struct DevRule {
   uint16_t lead_dist;
 };
 
+// Bind::jinfo flags (word y; lead_dist in bits 16-31)
+constexpr uint32_t kJiNfa = 1, kJiEquiv = 2, kJiBigLit = 16;  // bits 2-3: lead & 3
+
 // Prefilter gram bitset (LDS resident, 64K bits = 2048 words), tested two
 // positions per word (gram_pair_* below).  gram_mix: bits 32..47 of a 24 x
 // 24-bit product (one full-rate v_mul_hi_u32_u24 on the device when the key is
@@ -90,6 +93,7 @@ struct HostSlot {
 // lists) pair.  All pointers are device pointers into one blob.
 struct Bind {
   const DevRule *rules;
+  const uint4 *jinfo;  // per rule: job-window facts for k_lines2 (engine.hip l2_job_rec; kJi* flags)
   const uint16_t *trans;
   const uint8_t *accept_end;
   // per DFA state (ae_off + state): 0, or 1 << 31 | n << 24 | e2 << 16 | e1 << 8 | e0

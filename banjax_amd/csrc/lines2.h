@@ -161,6 +161,70 @@ __device__ __forceinline__ uint32_t l2_check(const Tabs &T, const LdsTabs &LT, c
   return hp >= off && hp - off + ck.z <= rest_len && literal_at(T, fl, rest + (hp - off)) ? 1u : 0u;
 }
 
+// The window record of a DFA job (engine.hip kJob*), or kJobDecided when the
+// pair is decided here: k_dfa's eq_certain, skip and lead_start steps on the
+// line's hit slots in registers.  Lead seeks past overflowed slots, rules with
+// literal ids >= 32, NFA rules and first-hit tables (cfirst) stay with k_dfa
+// (kJobLegacy).
+constexpr uint64_t kJobDecided = ~0ull;
+__device__ __forceinline__ uint64_t l2_job_rec(const Bind &B, uint32_t r, const CandMeta &cm, const uint64_t (&cv)[kCandSlots],
+                                               uint64_t rs, uint32_t rl, uint32_t rest_off) {
+  // one 16 B load: Bind::jinfo[r] (a class entry naming another rule names one
+  // with the same pattern, so its literals and flags are the line's own)
+  const uint4 ji = B.jinfo[r];
+  const uint32_t lm = ji.x, fl = ji.y, lead = (fl >> 2) & 3u;
+  if (fl & (kJiNfa | kJiBigLit)) return kJobLegacy;
+  const bool ovf = cm.cnt > (uint32_t)kCandSlots;
+  const uint32_t ns = min(cm.cnt, (uint32_t)kCandSlots);
+  auto mine = [&](uint64_t v) {
+    const uint32_t id = (uint32_t)(v & 0x7FFFFF);
+    return id < 32 && ((lm >> id) & 1u);
+  };
+  if ((fl & kJiEquiv) && (lead & 2u)) {  // eq_certain
+#pragma unroll
+    for (uint32_t c = 0; c < (uint32_t)kCandSlots; ++c) {
+      if (c >= ns) break;
+      const uint64_t v = cv[c];
+      if ((v & kCandVerified) && (v >> 24) >= rs && mine(v)) return kJobDecided;
+    }
+    if (ovf && B.lits_small && rest_off <= kCertainGap && ((cm.bits >> 32) & lm) != 0) return kJobDecided;
+  }
+  const uint32_t skl = ji.z & 0xFFFFu;
+  const uint32_t sk = skl && skl <= rl ? skl : 0u;
+  uint32_t st0 = 0;
+  if (lead == 3u) {  // lead_start (lead & 1 gates it, lead & 3 == 3 runs it)
+    if (B.cfirst) return kJobLegacy;
+    const uint32_t ld = fl >> 16, back = ld ? ld + 3u : 0u;
+    uint64_t f = ~0ull;
+#pragma unroll
+    for (uint32_t c = 0; c < (uint32_t)kCandSlots; ++c) {
+      if (c >= ns) break;
+      const uint64_t v = cv[c];
+      const uint64_t q = v >> 24;
+      if (q < rs || q >= f) continue;
+      if (ovf || mine(v)) f = q;
+    }
+    bool zero = false;
+    if (ovf) {
+      const uint64_t mf = cm.first_inv ? (uint64_t)(~cm.first_inv) << 3 : ~0ull;
+      if (mf < rs) zero = true;
+      f = mf < f ? mf : f;
+    }
+    if (!zero) {
+      if (f == ~0ull) st0 = rl;
+      else {
+        const uint32_t o = (uint32_t)min<uint64_t>(f - rs, rl);
+        st0 = o > back ? o - back : 0u;
+      }
+    }
+    // lead_start_seek: past overflowed slots the start is the first hit of ANY
+    // literal; k_dfa seeks forward to the rule's own
+    if (st0 < rl && ovf) return kJobLegacy;
+  }
+  if (st0) return rs + st0;
+  return (rs + sk) | (sk ? kJobSkipState : 0ull);
+}
+
 __device__ __forceinline__ uint4 l2_ld4w(const uint32_t *hl, uint32_t w) { return *reinterpret_cast<const uint4 *>(hl + w); }
 
 __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
@@ -172,10 +236,12 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
   uint8_t *wbase = s_dyn + B.l2_bytes + wave * kL2WaveLds;
   uint8_t *win = wbase + lane * kL2Win;
   JobSink S;
-  S.lds = reinterpret_cast<uint2 *>(wbase + 64 * kL2Win);
+  S.lds = reinterpret_cast<uint4 *>(wbase + 64 * kL2Win);
   S.cnt = reinterpret_cast<uint32_t *>(S.lds + kWaveJobs);
   S.jline = A.jline;
   S.jkey = A.jkey;
+  S.jidx = A.jidx;
+  S.jrec = A.jrec;
   S.count = A.job_count;
   S.cap = A.job_cap;
   if (lane == 0) *S.cnt = 0;
@@ -370,7 +436,10 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
             const uint32_t p = (uint32_t)__ffsll((unsigned long long)J) - 1;
             J &= J - 1;
             const uint32_t w = s_hl[prule + p];
-            emit_job(S, j, (w & kPlanOwn) ? first_rule + p : (w & 0xFFFFFu), p);
+            const uint32_t r = (w & kPlanOwn) ? first_rule + p : (w & 0xFFFFFu);
+            const uint64_t rec = l2_job_rec(B, r, cm, cv, rs, rest_len, rest_off);
+            if (rec == kJobDecided) m |= l2_bit(p);
+            else emit_job(S, j, r, p, rec | (((skp >> p) & 1) ? kJobNoCount : 0ull));
           }
           L.masks[j * B.mask_words] = m;
           if (B.mask_words > 1) L.masks[j * B.mask_words + 1] = 0;

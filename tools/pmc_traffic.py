@@ -12,7 +12,7 @@ import json
 import os
 import sys
 
-KERNELS = {"k_scan": "k_scan<", "k_lines": "k_lines<", "dfa_jobs": "k_dfa("}
+KERNELS = {"k_scan": ("k_scan<",), "k_lines": ("k_lines2(", "k_lines<"), "dfa_jobs": ("k_dfa(",)}
 
 
 def last_value(d, counter, prefix):
@@ -32,11 +32,14 @@ def main():
     out = {"config": "cfg3 (bench.py defaults)", "source": note,
            "formula": "2 x FETCH_SIZE + WRITE_SIZE (KB; gfx950 reports half of a wide streaming read, "
                       "MI355X_MICROARCH.md HBM), last dispatch of the run", "kernels": {}}
-    for k, prefix in KERNELS.items():
-        fe, wr = last_value(d, "FETCH_SIZE", prefix), last_value(d, "WRITE_SIZE", prefix)
+    for k, prefixes in KERNELS.items():
+        for prefix in prefixes:  # the first kernel of the list that ran (k_lines2, else k_lines)
+            fe, wr = last_value(d, "FETCH_SIZE", prefix), last_value(d, "WRITE_SIZE", prefix)
+            if fe is not None and wr is not None:
+                break
         if fe is None or wr is None:
             continue
-        out["kernels"][k] = {"fetch_kb_per_launch": fe, "write_kb_per_launch": wr,
+        out["kernels"][k] = {"kernel": prefix.rstrip("(<"), "fetch_kb_per_launch": fe, "write_kb_per_launch": wr,
                              "hbm_gb_per_launch": round((2 * fe + wr) * 1024 / 1e9, 3)}
     json.dump(out, sys.stdout, indent=1)
     print()
