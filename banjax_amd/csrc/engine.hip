@@ -661,6 +661,14 @@ struct ScanArgs {
                               // 4 literal checks of gram table hits, 8 gram table probes
   uint32_t hdr;               // 1: parse the headers of the lines that start in each tile (scan_header)
   int64_t now_ns;
+  // decoupled look-back (tstat != nullptr): the newlines before each tile are
+  // found here instead of by the separate count pass (tile_base unused);
+  // n_lines is then the capacity of the per-line arrays, *lines_out gets the
+  // batch's line count and *lb_abort is raised by a wave that waited too long
+  // (the host then runs the two-pass way)
+  unsigned long long *tstat;
+  unsigned long long *lines_out;
+  unsigned long long *lb_abort;
 };
 
 // pass A: '\n' count per wave tile
@@ -1413,6 +1421,62 @@ __device__ __forceinline__ void scan_header(const Bind &B, const Tabs &TB, const
 }
 
 
+// Decoupled look-back over the wave tiles (ScanArgs::tstat, one word per
+// tile: flag << 62 | newlines in the tile << 48 | newlines up to and
+// including it; flag 1 = the tile's own count, 2 = the inclusive count too).
+// A wave publishes its tile's count as soon as it has it, then reads the
+// words of the 64 tiles before it at once: the nearest one with an inclusive
+// count ends the look-back, the counts of those in between are added; a tile
+// whose word is still empty is waited for.  Tiles go to waves grid-stride
+// from a grid that is resident as a whole (one block per CU), every wave
+// takes its tiles in order, so the lowest unfinished tile never waits.
+// Returns false if the wait ran past kLookbackSpins (*lb_abort raised).
+constexpr uint32_t kLookbackSpins = 1u << 22;
+constexpr uint64_t kTileIncl = (1ull << 48) - 1;
+__device__ __forceinline__ bool tile_lookback(const ScanArgs &A, uint64_t t, uint32_t tot, uint32_t lane, uint64_t &prefix,
+                                              uint32_t &prev_cnt) {
+  if (lane == 0)
+    __hip_atomic_store(&A.tstat[t], (1ull << 62) | ((unsigned long long)tot << 48), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t excl = 0;
+  int64_t base = (int64_t)t - 1;
+  uint32_t spins = 0;
+  bool first = true;
+  prev_cnt = 0;
+  while (base >= 0) {
+    const int64_t idx = base - (int64_t)lane;
+    const uint64_t v = idx >= 0 ? __hip_atomic_load(&A.tstat[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (2ull << 62);
+    const uint32_t fl = (uint32_t)(v >> 62);
+    const uint64_t incm = __ballot(fl == 2), miss = __ballot(fl == 0);
+    const uint32_t fi = incm ? (uint32_t)__ffsll((unsigned long long)incm) - 1 : 64u;
+    const uint64_t need = fi >= 63 ? ~0ull : ((2ull << fi) - 1ull);  // lanes 0 .. fi
+    if (miss & need) {
+      if (++spins > kLookbackSpins || __hip_atomic_load(A.lb_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        if (lane == 0) atomicOr(A.lb_abort, 1ull);
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    if (first) {
+      prev_cnt = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 48), 0) & 0x3FFFu;
+      first = false;
+    }
+    uint64_t c = (uint32_t)lane < fi ? ((v >> 48) & 0x3FFFull) : (uint32_t)lane == fi ? (v & kTileIncl) : 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    excl += c;
+    if (fi < 64) break;
+    base -= 64;
+  }
+  prefix = excl;
+  if (lane == 0) {
+    __hip_atomic_store(&A.tstat[t], (2ull << 62) | ((unsigned long long)tot << 48) | (excl + tot), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    if (t + 1 == A.n_tiles) *A.lines_out = excl + tot;
+  }
+  return true;
+}
+
 template <bool IMG_LDS>
 __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_scan(Bind B, ScanArgs A) {
   // ---- block-shared tables (read-only after this barrier): gram bitset, then
@@ -1503,7 +1567,14 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
     uint32_t pre = wave_incl_sum(cnt);
     const uint32_t tot = __builtin_amdgcn_readlane(pre, 63);
     pre -= cnt;
-    const uint64_t tb = A.tile_base[t];
+    uint64_t tb;
+    uint32_t prev_cnt = 0;
+    if (A.tstat) {
+      if (!tile_lookback(A, t, tot, lane, tb, prev_cnt)) return;  // the host redoes the batch the two-pass way
+    } else {
+      tb = A.tile_base[t];
+      prev_cnt = t ? (uint32_t)(tb - A.tile_base[t - 1]) : 0u;
+    }
     const bool head = prevb == '\n';
     const uint32_t nh = head ? 0u : 1u;
     const bool last_nl = (__shfl((uint32_t)(nlm >> 63), 63) & 1u) != 0;
@@ -1565,7 +1636,7 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
     const uint64_t win_end = A.n - ts0 < (uint64_t)(kWT + kHalo) ? A.n - ts0 : (uint64_t)(kWT + kHalo);
     // the line open at the tile start is long iff it started before the previous
     // tile (that tile has no '\n') or runs past the previous tile's halo
-    const bool open_long = !head && (p0 == kNone || p0 >= kHalo || tb == A.tile_base[t - 1]);
+    const bool open_long = !head && (p0 == kNone || p0 >= kHalo || prev_cnt == 0);
 
     // ---- 4-gram prefilter: positions [64 lane, 64 lane + 64) and the last line's halo part
     {
@@ -4377,6 +4448,14 @@ struct bjx_engine {
   DevBuf<unsigned long long> long_count;
   uint32_t scan_lds[2] = {0, 0};
   bool lines_attr = false;
+  // k_scan's newline look-back (tile_lookback): lines per byte of the batches
+  // so far (sizes the per-line arrays),
+  // off for an engine that shares its GPU with another one that may run
+  // concurrently (bjx_engine_set_scan_lookback), batches done again two-pass
+  double lines_per_byte = 1.0 / 128;  // access-log lines are rarely shorter; shorter ones redo the batch two-pass
+  bool scan_lookback = getenv("BJX_LOOKBACK") && atoi(getenv("BJX_LOOKBACK")) == 1;
+  uint64_t lb_fallbacks = 0;
+  DevBuf<unsigned long long> tstat;
   DevBuf<CandMeta> l_ccnt;
   DevBuf<uint64_t> l_cfirst;  // Lines::cand_first
   unsigned long long scan_stats[6] = {0, 0, 0, 0, 0, 0};
@@ -5777,7 +5856,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   for (auto *b : {&e->staging, &e->l_flags, &e->ev_out, &e->rl_out, &e->trip_flag, &e->bind_blob,
                   &e->cub_tmp, &e->q_ip})
     b->release();
-  e->tile_counts.release(); e->tile_base.release(); e->nl.release(); e->l_ts.release(); e->l_iph.release();
+  e->tile_counts.release(); e->tile_base.release(); e->tstat.release(); e->nl.release(); e->l_ts.release(); e->l_iph.release();
   e->l_counts.release(); e->l_offs.release(); e->l_masks.release(); e->l_ipoff.release(); e->l_iplen.release();
   e->l_hoff.release(); e->l_hlen.release(); e->l_roff.release(); e->slow_list.release(); e->l_hid.release();
   e->scalars.release(); e->res_seq.release(); e->res_rule.release(); e->ev_el.release(); e->ev_rule.release();
@@ -5811,6 +5890,15 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
 }
 
 extern "C" const char *bjx_engine_last_error(bjx_engine *e) { return e ? e->last_error.c_str() : "no engine"; }
+
+// k_scan's newline look-back needs its whole grid resident; an engine that
+// shares its GPU with another engine running concurrently (bjx_node with
+// repeated devices) uses the two-pass count instead
+extern "C" int bjx_engine_set_scan_lookback(bjx_engine *e, int on) {
+  if (!e) return BJX_ERR_ARG;
+  e->scan_lookback = on != 0;
+  return BJX_OK;
+}
 
 extern "C" int bjx_engine_set_decision_lists(bjx_engine *e, const bjx_decision_entry *entries, size_t n) {
   if (!e || (n && !entries)) return BJX_ERR_ARG;
@@ -6214,89 +6302,134 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   for (auto &r : e->phase_rec) r = false;
   mark(e, 0);
 
-  // ---- pass A: '\n' count per 4 KB wave tile, exclusive scan -> line index of each tile
+  // ---- line framing, two-pass by default: pass A counts the '\n' of each
+  // 4 KB wave tile and an exclusive scan gives every tile its first line
+  // index.  With the look-back (bjx_engine_set_scan_lookback, BJX_LOOKBACK=1)
+  // k_scan counts the newlines before each tile itself (tile_lookback), the
+  // per-line arrays sized from the lines per byte seen so far; a batch with
+  // more lines than that, or a look-back that waited too long, is done again
+  // two-pass.  Off by default: measured slower at cfg3 (profiles/r04_t3:
+  // k_scan 21.8 ms with it against 3.0 + 12.7 ms).
   const uint64_t n_tiles = (n + kWT - 1) / kWT;
   e->tile_counts.ensure(n_tiles);
   e->tile_base.ensure(n_tiles + 1);
-  hipLaunchKernelGGL(k_nl_count_wt, dim3((unsigned)((n_tiles + 3) / 4)), dim3(kBlock), 0, st, buf, (uint64_t)n, n_tiles,
-                     e->tile_counts.p);
-  HIP_OK(hipGetLastError());
-  {
-    uint32_t *in = e->tile_counts.p;
-    uint64_t *o = e->tile_base.p;
-    cub_call(e, [&](void *tmp, size_t &bytes) {
-      return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)n_tiles, st);
-    });
-  }
-  uint64_t last_base = 0;
-  uint32_t last_cnt = 0;
-  HIP_OK(hipMemcpyAsync(&last_base, e->tile_base.p + (n_tiles - 1), 8, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipMemcpyAsync(&last_cnt, e->tile_counts.p + (n_tiles - 1), 4, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
-  const uint64_t n_lines = last_base + last_cnt;
-  out->n_lines = n_lines;
-  if (n_lines == 0) return false;
-
-  // ---- per-line arrays
-  e->nl.ensure(n_lines);
-  e->l_ts.ensure(n_lines); e->l_iph.ensure(n_lines); e->l_counts.ensure(n_lines + 1); e->l_offs.ensure(n_lines + 1);
-  e->l_masks.ensure(n_lines * B.mask_words);
-  e->l_ipoff.ensure(n_lines); e->l_iplen.ensure(n_lines); e->l_hoff.ensure(n_lines); e->l_hlen.ensure(n_lines);
-  e->l_roff.ensure(n_lines); e->l_hid.ensure(n_lines); e->l_flags.ensure(n_lines); e->slow_list.ensure(n_lines);
-  e->long_list.ensure(n_lines); e->l_ccnt.ensure(n_lines); e->l_ip16.ensure(n_lines);
-  e->l_cand.ensure(B.any_prefilter ? n_lines * kCandSlots : 1);
-  e->scalars.ensure(16);
+  uint64_t n_lines = 0;
   Lines L;
-  L.ts = e->l_ts.p; L.ip_hash = e->l_iph.p; L.ip_off = e->l_ipoff.p; L.ip_len = e->l_iplen.p; L.host_off = e->l_hoff.p;
-  L.host_len = e->l_hlen.p; L.rest_off = e->l_roff.p; L.host_id = e->l_hid.p; L.flags = e->l_flags.p;
-  L.counts = e->l_counts.p; L.masks = e->l_masks.p;
-  L.cand_meta = e->l_ccnt.p; L.cand = e->l_cand.p; L.ip16 = e->l_ip16.p;
-  L.cand_first = nullptr;
-  if (B.cfirst) {
-    e->l_cfirst.ensure(n_lines * kCandFirstLits);
-    L.cand_first = e->l_cfirst.p;
-    HIP_OK(hipMemsetAsync(e->l_cfirst.p, 0xFF, n_lines * kCandFirstLits * 8, st));
-  }
-  e->jline.ensure(std::max<uint64_t>(e->jline.n, n_lines + (1u << 20)));
-  e->jkey.ensure(e->jline.n); e->jidx.ensure(e->jline.n); e->jrec.ensure(e->jline.n);
-  HIP_OK(hipMemsetAsync(e->scalars.p, 0, 16 * sizeof(unsigned long long), st));
-  if (B.any_prefilter) HIP_OK(hipMemsetAsync(e->l_ccnt.p, 0, n_lines * sizeof(CandMeta), st));
-  // BJX_SCAN_HEADER=1: the scan pass parses the header of every line that fits
-  // its window and k_rules decides their rules (the others keep kLineTodo for
-  // k_lines).  Off by default: measured slower at cfg3 (profiles/r02_v2: scan
-  // +19 ms, k_rules 24.8 ms against k_lines 30.4 ms), the rule decisions'
-  // reads of line bytes from HBM outweigh the saved staging.
-  static const bool scan_hdr_env = getenv("BJX_SCAN_HEADER") && atoi(getenv("BJX_SCAN_HEADER")) == 1;
-  const bool scan_hdr = scan_hdr_env;
-  if (scan_hdr) HIP_OK(hipMemsetAsync(e->l_flags.p, kLineTodo, n_lines, st));
-  mark(e, 1);
-
-  // ---- the scan kernel (the hot, HBM-bound kernel): line framing + literal hits
-  uint64_t last_nl = 0;
-  {
-    ScanArgs A;
-    A.buf = buf; A.n = n; A.n_tiles = n_tiles; A.n_lines = n_lines; A.tile_base = e->tile_base.p; A.nl = e->nl.p;
-    A.L = L; A.stats = e->scalars.p + 8;
-    A.debug_skip = getenv("BJX_DEBUG_SKIP") ? (uint32_t)atoi(getenv("BJX_DEBUG_SKIP")) : 0u;
-    A.hdr = scan_hdr ? 1u : 0u;
-    A.now_ns = now_ns;
-    // block-shared LDS: gram bitset, the lookup image when it fits, then 16 wave regions
-    const uint32_t fixed = kGramWords * 4 + kScanWaves * kWaveLds;
-    const bool img_lds = fixed + B.img_bytes <= kScanLdsMax;
-    A.shared_bytes = kGramWords * 4 + (img_lds ? B.img_bytes : 0);
-    const uint32_t lds = A.shared_bytes + kScanWaves * kWaveLds;
-    const void *kfn = img_lds ? reinterpret_cast<const void *>(&k_scan<true>) : reinterpret_cast<const void *>(&k_scan<false>);
-    if (lds != e->scan_lds[img_lds]) {
-      HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      e->scan_lds[img_lds] = lds;
+  bool scan_hdr = false;
+  for (int pass = 0;; ++pass) {
+    const bool lb = e->scan_lookback && pass == 0;
+    uint64_t cap = 0;
+    if (lb) {
+      cap = (uint64_t)((double)n * e->lines_per_byte * 1.25) + 65536;
+      cap = std::max<uint64_t>(cap, e->nl.n);
+    } else {
+      hipLaunchKernelGGL(k_nl_count_wt, dim3((unsigned)((n_tiles + 3) / 4)), dim3(kBlock), 0, st, buf, (uint64_t)n, n_tiles,
+                         e->tile_counts.p);
+      HIP_OK(hipGetLastError());
+      {
+        uint32_t *in = e->tile_counts.p;
+        uint64_t *o = e->tile_base.p;
+        cub_call(e, [&](void *tmp, size_t &bytes) {
+          return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)n_tiles, st);
+        });
+      }
+      uint64_t last_base = 0;
+      uint32_t last_cnt = 0;
+      HIP_OK(hipMemcpyAsync(&last_base, e->tile_base.p + (n_tiles - 1), 8, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(&last_cnt, e->tile_counts.p + (n_tiles - 1), 4, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      n_lines = last_base + last_cnt;
+      out->n_lines = n_lines;
+      if (n_lines == 0) return false;
+      cap = n_lines;
     }
-    HIP_OK(hipEventRecord(e->evm0, st));
-    const unsigned grid = (unsigned)std::min<uint64_t>((n_tiles + kScanWaves - 1) / kScanWaves, 256);
-    if (img_lds) hipLaunchKernelGGL(k_scan<true>, dim3(grid), dim3(kScanWaves * 64), lds, st, B, A);
-    else hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kScanWaves * 64), lds, st, B, A);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(e->evm1, st));
+
+    // ---- per-line arrays
+    e->nl.ensure(cap);
+    e->l_ts.ensure(cap); e->l_iph.ensure(cap); e->l_counts.ensure(cap + 1); e->l_offs.ensure(cap + 1);
+    e->l_masks.ensure(cap * B.mask_words);
+    e->l_ipoff.ensure(cap); e->l_iplen.ensure(cap); e->l_hoff.ensure(cap); e->l_hlen.ensure(cap);
+    e->l_roff.ensure(cap); e->l_hid.ensure(cap); e->l_flags.ensure(cap); e->slow_list.ensure(cap);
+    e->long_list.ensure(cap); e->l_ccnt.ensure(cap); e->l_ip16.ensure(cap);
+    e->l_cand.ensure(B.any_prefilter ? cap * kCandSlots : 1);
+    e->scalars.ensure(16);
+    L.ts = e->l_ts.p; L.ip_hash = e->l_iph.p; L.ip_off = e->l_ipoff.p; L.ip_len = e->l_iplen.p; L.host_off = e->l_hoff.p;
+    L.host_len = e->l_hlen.p; L.rest_off = e->l_roff.p; L.host_id = e->l_hid.p; L.flags = e->l_flags.p;
+    L.counts = e->l_counts.p; L.masks = e->l_masks.p;
+    L.cand_meta = e->l_ccnt.p; L.cand = e->l_cand.p; L.ip16 = e->l_ip16.p;
+    L.cand_first = nullptr;
+    if (B.cfirst) {
+      e->l_cfirst.ensure(cap * kCandFirstLits);
+      L.cand_first = e->l_cfirst.p;
+      HIP_OK(hipMemsetAsync(e->l_cfirst.p, 0xFF, cap * kCandFirstLits * 8, st));
+    }
+    e->jline.ensure(std::max<uint64_t>(e->jline.n, cap + (1u << 20)));
+    e->jkey.ensure(e->jline.n); e->jidx.ensure(e->jline.n); e->jrec.ensure(e->jline.n);
+    HIP_OK(hipMemsetAsync(e->scalars.p, 0, 16 * sizeof(unsigned long long), st));
+    if (B.any_prefilter) HIP_OK(hipMemsetAsync(e->l_ccnt.p, 0, cap * sizeof(CandMeta), st));
+    // BJX_SCAN_HEADER=1: the scan pass parses the header of every line that fits
+    // its window and k_rules decides their rules (the others keep kLineTodo for
+    // k_lines).  Off by default: measured slower at cfg3 (profiles/r02_v2: scan
+    // +19 ms, k_rules 24.8 ms against k_lines 30.4 ms), the rule decisions'
+    // reads of line bytes from HBM outweigh the saved staging.
+    static const bool scan_hdr_env = getenv("BJX_SCAN_HEADER") && atoi(getenv("BJX_SCAN_HEADER")) == 1;
+    scan_hdr = scan_hdr_env;
+    if (scan_hdr) HIP_OK(hipMemsetAsync(e->l_flags.p, kLineTodo, cap, st));
+    if (lb) {
+      e->tstat.ensure(n_tiles);
+      HIP_OK(hipMemsetAsync(e->tstat.p, 0, n_tiles * 8, st));
+    }
+    mark(e, 1);
+
+    // ---- the scan kernel (the hot, HBM-bound kernel): line framing + literal hits
+    {
+      ScanArgs A;
+      A.buf = buf; A.n = n; A.n_tiles = n_tiles; A.n_lines = cap; A.tile_base = e->tile_base.p; A.nl = e->nl.p;
+      A.L = L; A.stats = e->scalars.p + 8;
+      A.debug_skip = getenv("BJX_DEBUG_SKIP") ? (uint32_t)atoi(getenv("BJX_DEBUG_SKIP")) : 0u;
+      A.hdr = scan_hdr ? 1u : 0u;
+      A.now_ns = now_ns;
+      A.tstat = lb ? e->tstat.p : nullptr;
+      A.lines_out = e->scalars.p + 6;
+      A.lb_abort = e->scalars.p + 7;
+      // block-shared LDS: gram bitset, the lookup image when it fits, then 16 wave regions
+      const uint32_t fixed = kGramWords * 4 + kScanWaves * kWaveLds;
+      const bool img_lds = fixed + B.img_bytes <= kScanLdsMax;
+      A.shared_bytes = kGramWords * 4 + (img_lds ? B.img_bytes : 0);
+      const uint32_t lds = A.shared_bytes + kScanWaves * kWaveLds;
+      const void *kfn = img_lds ? reinterpret_cast<const void *>(&k_scan<true>) : reinterpret_cast<const void *>(&k_scan<false>);
+      if (lds != e->scan_lds[img_lds]) {
+        HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        e->scan_lds[img_lds] = lds;
+      }
+      // one block (16 waves) per CU: the whole grid resident, as the look-back needs
+      int n_cu_scan = 0;
+      HIP_OK(hipDeviceGetAttribute(&n_cu_scan, hipDeviceAttributeMultiprocessorCount, e->device));
+      HIP_OK(hipEventRecord(e->evm0, st));
+      const unsigned grid = (unsigned)std::min<uint64_t>((n_tiles + kScanWaves - 1) / kScanWaves, (uint64_t)std::max(1, n_cu_scan));
+      if (img_lds) hipLaunchKernelGGL(k_scan<true>, dim3(grid), dim3(kScanWaves * 64), lds, st, B, A);
+      else hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kScanWaves * 64), lds, st, B, A);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipEventRecord(e->evm1, st));
+    }
+    if (lb) {
+      unsigned long long r[2] = {0, 0};
+      HIP_OK(hipMemcpyAsync(r, e->scalars.p + 6, 16, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      if (r[1] || r[0] > cap) {  // the look-back gave up, or more lines than the arrays hold
+        e->lb_fallbacks += 1;
+        if (r[0] > cap && !r[1]) e->lines_per_byte = (double)r[0] / (double)n;
+        continue;
+      }
+      n_lines = r[0];
+      out->n_lines = n_lines;
+      if (n_lines == 0) return false;
+    }
+    const double lpb = (double)n_lines / (double)n;
+    e->lines_per_byte = std::max(e->lines_per_byte * 0.5, lpb);
+    break;
   }
+  uint64_t last_nl = 0;
   mark(e, 2);
 
   // ---- rule decisions (k_rules) for the lines the scan parsed; k_lines does

@@ -253,6 +253,10 @@ class Engine:
         """Test hook: state-slot cache on (1), off (0), default (-1), from the next batch."""
         self._check(_lib.lib().bjx_debug_set_slot_cache(self._h, on), "debug_set_slot_cache")
 
+    def set_scan_lookback(self, on: int):
+        """k_scan's newline look-back (on) or the two-pass count (off, the default)."""
+        self._check(_lib.lib().bjx_engine_set_scan_lookback(self._h, on), "set_scan_lookback")
+
     def state_clear(self):
         self._check(_lib.lib().bjx_state_clear(self._h), "state_clear")
 

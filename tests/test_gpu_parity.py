@@ -678,3 +678,30 @@ def test_trips_only_claim_rollback(engine, budget):
         pair.compare_state()
     finally:
         engine.debug_set_claim_budget(0)
+
+
+def short_lines(t, n, k):
+    """n lines of ~40 bytes: far more lines per byte than the batches before
+    them, so k_scan's look-back overflows its line arrays and the batch is done
+    again the two-pass way."""
+    return b"".join(b"%d 10.%d.0.%d GET s.com GET /%d h\n" % (t, k % 7, i % 50, i % 13) for i in range(n))
+
+
+@pytest.mark.parametrize("lookback", [1, 0])
+def test_scan_lookback_and_two_pass(engine, lookback):
+    """Line framing by k_scan's decoupled look-back and by the two-pass count
+    (default) give the same results: batches of ordinary lines, then a
+    batch of short lines that overflows the look-back's line arrays (redone
+    two-pass), then ordinary lines again."""
+    w = W.scaled(W.CFG3, 60_000, n_ips=3_000)
+    t = w.now_ns(0, 1) // S
+    engine.set_scan_lookback(lookback)
+    try:
+        pair = Pair(w.rules_yaml, engine)
+        for b in range(2):
+            pair.feed(w.host_lines(b * 20_000, 20_000), w.now_ns(b * 20_000, 20_000))
+        pair.feed(short_lines(t, 30_000, 1), t * S)
+        pair.feed(w.host_lines(40_000, 20_000), w.now_ns(40_000, 20_000))
+        pair.compare_state(["10.1.0.1", "10.1.0.2"])
+    finally:
+        engine.set_scan_lookback(0)
