@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("BJX_LIB_PATH") or os.path.join(HERE, "lib", "libbanja
 OK = 0
 ERR_REGEX, ERR_ARG, ERR_DEVICE, ERR_NOMEM, ERR_TOO_COMPLEX, ERR_CAPACITY, ERR_DECISION = -1, -2, -3, -4, -5, -6, -7
 TAIL_STOPPED, ERR_IO = -8, -9
-INPUT_DEVICE, COPY_RESULTS, EMIT_BANS, BAN_RECORDS_ONLY = 1, 2, 4, 8
+INPUT_DEVICE, COPY_RESULTS, EMIT_BANS, BAN_RECORDS_ONLY, TRIPS_COMPACT = 1, 2, 4, 8, 16
 
 
 class Str(C.Structure):
@@ -57,7 +57,7 @@ class BatchResult(C.Structure):
     _fields_ = [("n_lines", C.c_uint64), ("consumed_bytes", C.c_uint64), ("n_results", C.c_uint64),
                 ("n_events", C.c_uint64), ("n_trips", C.c_uint64), ("line_flags", C.POINTER(C.c_uint8)),
                 ("results", C.POINTER(RuleResult)), ("trips", C.POINTER(Trip)), ("device_ms", C.c_double),
-                ("match_kernel_ms", C.c_double)]
+                ("match_kernel_ms", C.c_double), ("trips_compact", C.POINTER(C.c_uint64))]
 
 
 class EventLine(C.Structure):

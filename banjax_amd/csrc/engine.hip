@@ -3825,6 +3825,12 @@ __global__ void k_build_trips(uint64_t n_trips, const uint32_t *__restrict__ idx
 // ---- trip -> decision emission (bans.h)
 
 // LogRegexBan line length of each trip (entry n_trips: 0, for the exclusive scan)
+// BJX_TRIPS_COMPACT: the 8-byte trip words (line offset << 24 | rule index)
+__global__ void k_pack_trips(uint64_t n, const bjx_trip *__restrict__ tr, uint64_t *__restrict__ out) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) out[t] = (tr[t].line_offset << 24) | (tr[t].rule_idx & 0xFFFFFFu);
+}
+
 __global__ void k_ban_len(BanDev A, uint64_t *__restrict__ len, uint8_t *__restrict__ kind) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t > A.n_trips) return;
@@ -4515,6 +4521,8 @@ struct bjx_engine {
 
   // host copies of the last batch
   HostBuf<bjx_trip> trips;
+  HostBuf<uint64_t> trips_c;     // BJX_TRIPS_COMPACT words
+  DevBuf<uint64_t> d_trips_c;
   HostBuf<bjx_rule_result> results;
   HostBuf<uint8_t> line_flags;
 };
@@ -5851,7 +5859,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   (void)hipSetDevice(e->device);
   (void)hipStreamSynchronize(e->stream);
   free_state(e);
-  e->trips.release(); e->results.release(); e->line_flags.release();
+  e->trips.release(); e->trips_c.release(); e->d_trips_c.release(); e->results.release(); e->line_flags.release();
   e->ev_out_s.release(); e->trip_ev.release(); e->trip_ev2.release();
   for (auto *b : {&e->staging, &e->l_flags, &e->ev_out, &e->rl_out, &e->trip_flag, &e->bind_blob,
                   &e->cub_tmp, &e->q_ip})
@@ -6288,6 +6296,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   hipStream_t st = e->stream;
   memset(out, 0, sizeof *out);
   e->trips.clear();
+  e->trips_c.clear();
   e->results.clear();
   e->line_flags.clear();
   if (n == 0) return false;
@@ -6924,8 +6933,16 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
                          e->ev_rule.p, e->nl.p, L, B.rules, e->d_trips.p);
       HIP_OK(hipGetLastError());
       }
-      e->trips.resize(n_trips);
-      HIP_OK(hipMemcpyAsync(e->trips.data(), e->d_trips.p, n_trips * sizeof(bjx_trip), hipMemcpyDeviceToHost, st));
+      if (flags & BJX_TRIPS_COMPACT) {
+        e->d_trips_c.ensure(n_trips);
+        hipLaunchKernelGGL(k_pack_trips, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->d_trips.p, e->d_trips_c.p);
+        HIP_OK(hipGetLastError());
+        e->trips_c.resize(n_trips);
+        HIP_OK(hipMemcpyAsync(e->trips_c.data(), e->d_trips_c.p, n_trips * 8, hipMemcpyDeviceToHost, st));
+      } else {
+        e->trips.resize(n_trips);
+        HIP_OK(hipMemcpyAsync(e->trips.data(), e->d_trips.p, n_trips * sizeof(bjx_trip), hipMemcpyDeviceToHost, st));
+      }
       if (flags & BJX_EMIT_BANS) emit_bans(e, n_trips, (flags & BJX_BAN_RECORDS_ONLY) != 0);
     }
     if ((flags & BJX_COPY_RESULTS) && !e->res_written) {
@@ -7002,7 +7019,9 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
     e->phase_ms[k] = x;
   }
   out->n_trips = n_trips;
-  out->trips = e->trips.empty() ? nullptr : e->trips.data();
+  const bool compact = (flags & BJX_TRIPS_COMPACT) != 0;
+  out->trips = compact || !n_trips ? nullptr : e->trips.data();
+  out->trips_compact = !compact || !n_trips ? nullptr : e->trips_c.data();
   out->results = e->results.empty() ? nullptr : e->results.data();
   out->line_flags = e->line_flags.empty() ? nullptr : e->line_flags.data();
 }

@@ -102,6 +102,7 @@ struct bjx_node {
   std::string last_error;
   // merged results of the last batch
   std::vector<bjx_trip> trips;
+  std::vector<uint64_t> trips_c;  // BJX_TRIPS_COMPACT words
   std::vector<bjx_rule_result> results;
   std::vector<uint8_t> line_flags;
   bool bans = false;
@@ -487,17 +488,22 @@ void run_batch(bjx_node *n, const bjx_ruleset *rs, const uint8_t *const *chunks,
   each(n, [&](size_t k) { return bjx_finish_batch(n->parts[k].e, n->parts[k].s_out.p, flags, &n->parts[k].res); });
   // 6. merge in chunk (= stream) order
   bjx_batch_result r{};
-  n->trips.clear(); n->results.clear(); n->line_flags.clear();
+  n->trips.clear(); n->trips_c.clear(); n->results.clear(); n->line_flags.clear();
   std::vector<uint64_t> trip_base(N, 0);
   uint64_t line_base = 0, byte_base = 0;
   for (size_t k = 0; k < N; ++k) {
     const bjx_batch_result &x = n->parts[k].res;
-    trip_base[k] = n->trips.size();
-    for (uint64_t t = 0; t < x.n_trips; ++t) {
-      bjx_trip tr = x.trips[t];
-      tr.line_idx += line_base;
-      tr.line_offset += byte_base;
-      n->trips.push_back(tr);
+    if (flags & BJX_TRIPS_COMPACT) {
+      trip_base[k] = n->trips_c.size();
+      for (uint64_t t = 0; t < x.n_trips; ++t) n->trips_c.push_back(x.trips_compact[t] + (byte_base << 24));
+    } else {
+      trip_base[k] = n->trips.size();
+      for (uint64_t t = 0; t < x.n_trips; ++t) {
+        bjx_trip tr = x.trips[t];
+        tr.line_idx += line_base;
+        tr.line_offset += byte_base;
+        n->trips.push_back(tr);
+      }
     }
     if (flags & BJX_COPY_RESULTS) {
       if (x.n_lines) n->line_flags.insert(n->line_flags.end(), x.line_flags, x.line_flags + x.n_lines);
@@ -514,8 +520,13 @@ void run_batch(bjx_node *n, const bjx_ruleset *rs, const uint8_t *const *chunks,
     byte_base += lens[k];
   }
   r.consumed_bytes = byte_base - lens[N - 1] + n->parts[N - 1].res.consumed_bytes;
-  r.n_trips = n->trips.size();
-  r.trips = r.n_trips ? n->trips.data() : nullptr;
+  if (flags & BJX_TRIPS_COMPACT) {
+    r.n_trips = n->trips_c.size();
+    r.trips_compact = r.n_trips ? n->trips_c.data() : nullptr;
+  } else {
+    r.n_trips = n->trips.size();
+    r.trips = r.n_trips ? n->trips.data() : nullptr;
+  }
   if (flags & BJX_COPY_RESULTS) {
     r.line_flags = r.n_lines ? n->line_flags.data() : nullptr;
     r.results = r.n_results ? n->results.data() : nullptr;

@@ -36,6 +36,14 @@ class BatchOutput:
             self._trips = [self._res.trips[i] for i in range(self.n_trips)] if self.n_trips else []
         return self._trips
 
+    def trips_compact(self):
+        """BJX_TRIPS_COMPACT: numpy uint64 words, line byte offset << 24 | rule index (zero-copy)."""
+        import numpy as np
+        if not self.n_trips or not self._res.trips_compact:
+            return np.zeros(0, dtype=np.uint64)
+        buf = (C.c_uint64 * self.n_trips).from_address(C.addressof(self._res.trips_compact.contents))
+        return np.ctypeslib.as_array(buf)
+
     def trips_array(self):
         import numpy as np
         if not self.n_trips:
@@ -152,12 +160,15 @@ class Engine:
         return BanBatch(bb)
 
     def process(self, rs: Ruleset, data, now_ns: int, copy_results: bool = False, device_ptr: Optional[int] = None,
-                nbytes: Optional[int] = None, emit_bans: bool = False, ban_log: bool = True) -> BatchOutput:
+                nbytes: Optional[int] = None, emit_bans: bool = False, ban_log: bool = True,
+                compact_trips: bool = False) -> BatchOutput:
         """consumeLine over every complete line of `data` (bytes) or of a device
         buffer (device_ptr, nbytes) already resident in HBM.  emit_bans with
-        ban_log=False: the per-IP decision records only (BJX_BAN_RECORDS_ONLY)."""
+        ban_log=False: the per-IP decision records only (BJX_BAN_RECORDS_ONLY).
+        compact_trips: trips as 8-byte words (BatchOutput.trips_compact)."""
         res = _lib.BatchResult()
-        flags = (_lib.COPY_RESULTS if copy_results else 0) | (_lib.EMIT_BANS if emit_bans else 0)
+        flags = (_lib.COPY_RESULTS if copy_results else 0) | (_lib.EMIT_BANS if emit_bans else 0) | \
+            (_lib.TRIPS_COMPACT if compact_trips else 0)
         if emit_bans and not ban_log:
             flags |= _lib.BAN_RECORDS_ONLY
         if device_ptr is not None:
@@ -343,10 +354,11 @@ class Node:
         return BatchOutput(res, copy_results)
 
     def process_chunks(self, rs: Ruleset, chunks: Sequence[Tuple[int, int]], now_ns: int, copy_results: bool = False,
-                       emit_bans: bool = False) -> BatchOutput:
+                       emit_bans: bool = False, compact_trips: bool = False) -> BatchOutput:
         """chunks[k] = (device pointer on engine k's GPU, bytes); all but the last end in '\\n'."""
         res = _lib.BatchResult()
-        flags = (_lib.COPY_RESULTS if copy_results else 0) | (_lib.EMIT_BANS if emit_bans else 0) | _lib.INPUT_DEVICE
+        flags = (_lib.COPY_RESULTS if copy_results else 0) | (_lib.EMIT_BANS if emit_bans else 0) | _lib.INPUT_DEVICE | \
+            (_lib.TRIPS_COMPACT if compact_trips else 0)
         ptrs = (C.c_void_p * len(chunks))(*[p for p, _ in chunks])
         lens = (C.c_size_t * len(chunks))(*[n for _, n in chunks])
         self._check(_lib.lib().bjx_node_process_chunks(self._h, rs.handle, ptrs, lens, now_ns, flags, C.byref(res)),

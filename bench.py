@@ -196,6 +196,9 @@ def main():
     ap.add_argument("--node-engines", type=int, default=0,
                     help="single process: one bjx_node of this many engines over the visible GPUs (round-robin), "
                          "e.g. to rehearse the N>1 node path on one GPU")
+    ap.add_argument("--trips", choices=("compact", "full"), default="compact",
+                    help="compact: the trip list crosses PCIe as 8-byte words (line byte offset, rule index: "
+                         "BJX_TRIPS_COMPACT; the host has the bytes for the rest); full: 56-byte bjx_trip records")
     ap.add_argument("--exchange", choices=("node", "rccl"), default="node",
                     help="N>1: node = rank 0 drives every local GPU through one bjx_node (the library moves the event "
                          "records over xGMI; the Go host's one-process shape), the other ranks only join the barriers; "
@@ -261,11 +264,14 @@ def main():
         from banjax_amd.distributed import TorchExchange, sharded_batch
         ex = TorchExchange(torch.device("cuda", local))
 
+    compact = args.trips == "compact"
+
     def step():
         if node_mode:
-            return node.process_chunks(rs, chunks, now, emit_bans=bans) if drives else None
+            return node.process_chunks(rs, chunks, now, emit_bans=bans, compact_trips=compact) if drives else None
         if ex is None:
-            return eng.process(rs, None, now, device_ptr=data.data_ptr(), nbytes=nbytes, emit_bans=bans)
+            return eng.process(rs, None, now, device_ptr=data.data_ptr(), nbytes=nbytes, emit_bans=bans,
+                               compact_trips=compact)
         return sharded_batch(eng, rs, now, data.data_ptr(), nbytes, ex, emit_bans=bans)
 
     def sync_all():
@@ -377,6 +383,8 @@ def main():
                 "rule_results_per_step_rank0": o.n_results,
                 "rate_limit_events_per_step_rank0": o.n_events,
                 "trips_per_step_rank0": o.n_trips,
+                "trip_records": ("8-byte words (line byte offset << 24 | rule index, BJX_TRIPS_COMPACT)" if compact
+                                 else "56-byte bjx_trip records"),
                 "decision_emission": ("device: per-IP decision updates + LogRegexBan JSON lines, in the step"
                                       if bans else "off (trip list only)"),
                 "device_ms_per_step_rank0": round(dev_ms, 3),

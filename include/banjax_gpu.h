@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define BJX_ABI_VERSION 3
+#define BJX_ABI_VERSION 4
 
 enum bjx_status {
   BJX_OK = 0,
@@ -155,9 +155,19 @@ enum bjx_batch_flags {
   BJX_INPUT_DEVICE = 1,   /* bytes is a device pointer already resident in HBM */
   BJX_COPY_RESULTS = 2,   /* also copy per-line flags and RuleResults to host memory */
   BJX_EMIT_BANS = 4,      /* also build the batch's decision updates and ban-log lines (bjx_batch_bans) */
-  BJX_BAN_RECORDS_ONLY = 8 /* with BJX_EMIT_BANS: the per-IP decision records only; no LogRegexBan lines
+  BJX_BAN_RECORDS_ONLY = 8, /* with BJX_EMIT_BANS: the per-IP decision records only; no LogRegexBan lines
                               are built or copied (log_bytes 0, every log_kind 0) */
+  BJX_TRIPS_COMPACT = 16    /* trips as 8-byte words in trips_compact (trips NULL): what the host cannot
+                              re-derive from its own copy of the bytes -- which line, which rule */
 };
+
+/* BJX_TRIPS_COMPACT trip word: the line's byte offset in the batch (40 bits)
+   and the rule index (24 bits).  Everything else in bjx_trip follows from the
+   line's bytes: line_len = up to its '\n', ts / IP / host / rest = the first
+   four space-separated fields (as consumeLine splits them), decision =
+   the rule's, line_idx = the newlines before it. */
+#define BJX_TRIP_OFFSET(w) ((uint64_t)(w) >> 24)
+#define BJX_TRIP_RULE(w) ((uint32_t)((w) & 0xFFFFFFu))
 
 typedef struct bjx_batch_result {
   uint64_t n_lines;        /* complete ('\n'-terminated) lines processed */
@@ -170,6 +180,7 @@ typedef struct bjx_batch_result {
   const bjx_trip *trips;            /* host, n_trips entries in reference order */
   double device_ms;                 /* device time of the batch (HIP events) */
   double match_kernel_ms;           /* device time of the match kernel alone */
+  const uint64_t *trips_compact;    /* host, n_trips trip words in reference order, if BJX_TRIPS_COMPACT (ABI 4) */
 } bjx_batch_result;
 
 /* consumeLine for every complete line of bytes[0..n) with injected clock

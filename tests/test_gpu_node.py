@@ -137,3 +137,35 @@ def test_node_rejects_chunk_without_newline():
     out = node.process(rs, data + b"1700000000.000 1.2.3.4 GET", w.now_ns(0, 1000))
     assert out.consumed_bytes == len(data) and out.n_lines == 1000
     node.close()
+
+
+def test_node_compact_trips_match_full():
+    """A node's BJX_TRIPS_COMPACT words (line offsets rebased to the whole
+    batch) equal its full trip records, over three engines."""
+    from banjax_amd import Ruleset
+
+    w = W.scaled(W.CFG5, 30_000, n_ips=3_000)
+    rs = Ruleset(Config.from_yaml(w.rules_yaml))
+    data = w.host_lines(0, 30_000)
+    now = w.now_ns(0, 30_000)
+    node = Node([0] * 3)
+    full = node.process(rs, data, now)
+    want = [(t.line_offset, t.rule_idx) for t in full.trips]
+    node.state_clear()
+    import torch
+    lines = data.split(b"\n")[:-1]
+    cuts = [0, len(lines) // 3, 2 * len(lines) // 3, len(lines)]
+    chunks, keep = [], []
+    for a, b in zip(cuts, cuts[1:]):
+        blob = b"".join(ln + b"\n" for ln in lines[a:b])
+        t = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to("cuda:0")
+        keep.append(t)
+        chunks.append((t.data_ptr(), len(blob)))
+    full2 = node.process_chunks(rs, chunks, now)
+    want2 = [(t.line_offset, t.rule_idx) for t in full2.trips]
+    node.state_clear()
+    comp = node.process_chunks(rs, chunks, now, compact_trips=True)
+    got = [(int(x) >> 24, int(x) & 0xFFFFFF) for x in comp.trips_compact()]
+    node.close()
+    assert comp.n_trips == len(want2) > 100
+    assert got == want2 and want2 == want

@@ -10,7 +10,7 @@ import random
 import pytest
 
 import workloads as W
-from banjax_amd import Config, Engine, MockBanner, RegexRateLimiter, consume_line
+from banjax_amd import Config, Engine, MockBanner, RegexRateLimiter, Ruleset, consume_line
 from oracle import oracle as O
 from tests.parity import Pair, oracle_config
 
@@ -705,3 +705,25 @@ def test_scan_lookback_and_two_pass(engine, lookback):
         pair.compare_state(["10.1.0.1", "10.1.0.2"])
     finally:
         engine.set_scan_lookback(0)
+
+
+def test_compact_trips_match_full(engine):
+    """BJX_TRIPS_COMPACT words carry each trip's line offset and rule index,
+    in reference order, equal to the full bjx_trip records of the same batch
+    on the same state."""
+    w = W.scaled(W.CFG5, 40_000, n_ips=4_000)
+    rs = Ruleset(Config.from_yaml(w.rules_yaml))
+    data = w.host_lines(0, 40_000)
+    now = w.now_ns(0, 40_000)
+    engine.state_clear()
+    full = engine.process(rs, data, now)
+    want = [(t.line_offset, t.rule_idx) for t in full.trips]
+    engine.state_clear()
+    comp = engine.process(rs, data, now, compact_trips=True)
+    words = comp.trips_compact()
+    got = [(int(x) >> 24, int(x) & 0xFFFFFF) for x in words]
+    engine.state_clear()
+    assert comp.n_trips == full.n_trips == len(want) > 100
+    assert got == want
+    for off, _ in got[:50]:  # the offset starts a line
+        assert off == 0 or data[off - 1:off] == b"\n"
