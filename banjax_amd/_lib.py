@@ -61,9 +61,8 @@ class BatchResult(C.Structure):
 
 
 class EventLine(C.Structure):
-    """bjx_event_line: one rate-limit record exchanged between GPUs (32 B)."""
-    _fields_ = [("ts_ns", C.c_int64), ("ip_hash", C.c_uint64), ("ip_off", C.c_uint32), ("ip_len", C.c_uint32),
-                ("n_events", C.c_uint32), ("_pad", C.c_uint32)]
+    """bjx_event_line: one rate-limit record exchanged between GPUs (16 B)."""
+    _fields_ = [("ts_ns", C.c_int64), ("ip_off", C.c_uint32), ("ip_len", C.c_uint16), ("n_events", C.c_uint16)]
 
 
 class TzTransition(C.Structure):

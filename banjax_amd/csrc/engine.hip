@@ -1944,7 +1944,7 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
 // SplitN header, parseTimestamp fast path, host lookup, CheckIsAllowed, OldLine,
 // then the rule decisions from the scan pass's literal hits (DFA work to k_dfa).
 template <bool IMG_LDS, bool PROF = false, bool HOST_LDS = false>
-__global__ __launch_bounds__(kBlock) void k_lines(Bind B, LinesArgs A) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_lines(Bind B, LinesArgs A) {
   LinesProf P;
   uint8_t *s_img = s_dyn;
   if (IMG_LDS) {
@@ -4054,39 +4054,60 @@ __global__ void k_part_counts(uint32_t n_parts, uint64_t n_el, uint64_t *__restr
   }
 }
 
-__global__ void k_pack(uint64_t n_el, const uint32_t *__restrict__ key, const uint32_t *__restrict__ line,
+constexpr uint32_t kPackWaveBytes = 2048;  // a wave's IP bytes staged in LDS for 16 B stores
+__global__ __launch_bounds__(kBlock) void k_pack(uint64_t n_el, const uint32_t *__restrict__ key, const uint32_t *__restrict__ line,
                        const uint64_t *__restrict__ ev_off, const uint64_t *__restrict__ by_off,
                        const uint64_t *__restrict__ part_byte_base, const uint8_t *__restrict__ buf,
                        const uint64_t *__restrict__ nl, Lines L, const uint64_t *__restrict__ offs,
                        const uint32_t *__restrict__ ev_rule, bjx_event_line *__restrict__ d_lines,
                        uint32_t *__restrict__ d_events, uint8_t *__restrict__ d_bytes, uint32_t *__restrict__ pack_src) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_ip[kBlock / 64][kPackWaveBytes + 32];
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n_el) return;
-  const uint32_t j = line[p];
-  const uint32_t ne = (uint32_t)(L.counts[j] & 0xFFFFFFFFull);
-  const uint32_t len = L.ip_len[j];
-  bjx_event_line r;
-  r.ts_ns = L.ts[j];
-  r.ip_hash = L.ip_hash[j];
-  r.ip_off = (uint32_t)(by_off[p] - part_byte_base[key[p]]);
-  r.ip_len = len;
-  r.n_events = ne;
-  r._pad = 0;
-  d_lines[p] = r;
-  const uint64_t eo = offs[j] & 0xFFFFFFFFull, pe = ev_off[p];
-  for (uint32_t t = 0; t < ne; ++t) {
-    d_events[pe + t] = ev_rule[eo + t];
-    pack_src[pe + t] = (uint32_t)(eo + t);
-  }
-  // the IP bytes: word loads from the line (a log line continues past its
-  // IP), byte stores into the packed pool
-  const uint8_t *ip = buf + line_start(nl, j) + L.ip_off[j];
-  uint8_t *dst = d_bytes + by_off[p];
-  for (uint32_t k = 0; k < len; k += 4) {
-    const uint32_t w = ld4(ip + k);
+  const uint32_t lane = threadIdx.x & 63;
+  uint8_t *sw = s_ip[threadIdx.x >> 6];
+  // the wave's packed IP bytes are one contiguous range [b0, b1) of d_bytes
+  const uint64_t p0 = p - lane, pl = min<uint64_t>(p0 + 64, n_el);
+  const uint64_t b0 = p0 < n_el ? by_off[p0] : 0, b1 = p0 < n_el ? by_off[pl] : 0;
+  const bool staged = p0 < n_el && b1 - b0 <= kPackWaveBytes;
+  const uint32_t head = (uint32_t)(b0 & 15);  // LDS byte of d_bytes[b0]: 16 B stores stay aligned
+  if (p < n_el) {
+    const uint32_t j = line[p];
+    const uint32_t ne = (uint32_t)(L.counts[j] & 0xFFFFFFFFull);
+    const uint32_t len = L.ip_len[j];
+    bjx_event_line r;
+    r.ts_ns = L.ts[j];
+    r.ip_off = (uint32_t)(by_off[p] - part_byte_base[key[p]]);
+    r.ip_len = (uint16_t)len;
+    r.n_events = (uint16_t)ne;
+    d_lines[p] = r;
+    const uint64_t eo = offs[j] & 0xFFFFFFFFull, pe = ev_off[p];
+    for (uint32_t t = 0; t < ne; ++t) {
+      d_events[pe + t] = ev_rule[eo + t];
+      pack_src[pe + t] = (uint32_t)(eo + t);
+    }
+    // the IP bytes: word loads from the line (a log line continues past its
+    // IP), byte stores into the wave's LDS stage (or the packed pool)
+    const uint8_t *ip = buf + line_start(nl, j) + L.ip_off[j];
+    uint8_t *dst = staged ? sw + head + (by_off[p] - b0) : d_bytes + by_off[p];
+    for (uint32_t k = 0; k < len; k += 4) {
+      const uint32_t w = ld4(ip + k);
 #pragma unroll
-    for (uint32_t b = 0; b < 4; ++b)
-      if (k + b < len) dst[k + b] = (uint8_t)(w >> (8 * b));
+      for (uint32_t b = 0; b < 4; ++b)
+        if (k + b < len) dst[k + b] = (uint8_t)(w >> (8 * b));
+    }
+  }
+  if (!staged) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // the range out with 16 B stores, the partial first and last pieces bytewise
+  const uint64_t a = b0 & ~15ull;
+  for (uint64_t q = a + 16ull * lane; q < b1; q += 16ull * 64) {
+    const uint32_t o = (uint32_t)(q - a);
+    if (q >= b0 && q + 16 <= b1) *reinterpret_cast<uint4 *>(d_bytes + q) = *reinterpret_cast<const uint4 *>(sw + o);
+    else
+      for (uint32_t k = 0; k < 16; ++k)
+        if (q + k >= b0 && q + k < b1) d_bytes[q + k] = sw[o + k];
   }
 }
 
@@ -4097,12 +4118,14 @@ __global__ void k_pack(uint64_t n_el, const uint32_t *__restrict__ key, const ui
 __global__ void k_unpack_lines(uint64_t n, uint64_t first, uint64_t byte_base, const bjx_event_line *__restrict__ rec,
                                const uint8_t *__restrict__ bytes, int64_t *__restrict__ ts, uint64_t *__restrict__ hash,
                                uint64_t *__restrict__ pos, uint32_t *__restrict__ len, uint64_t *__restrict__ nev,
-                               uint4 *__restrict__ ip16) {
+                               uint4 *__restrict__ ip16, uint64_t dbg_mask) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const bjx_event_line r = rec[first + i];
   ts[first + i] = r.ts_ns;
-  hash[first + i] = r.ip_hash;
+  // the IP's hash from its bytes (the source's hash_bytes; not on the wire)
+  const uint64_t h = hash_bytes(bytes + byte_base + r.ip_off, r.ip_len);
+  hash[first + i] = dbg_mask ? (h & dbg_mask) | 1 : h;
   pos[first + i] = byte_base + r.ip_off;
   len[first + i] = r.ip_len;
   nev[first + i] = r.n_events;
@@ -7169,7 +7192,7 @@ extern "C" int bjx_apply_events(bjx_engine *e, const bjx_ruleset *rs, const bjx_
       const uint64_t nk = src_counts[3 * k];
       if (nk)
         hipLaunchKernelGGL(k_unpack_lines, dim3(grid_for(nk)), dim3(kBlock), 0, st, nk, first, bbase, d_lines, d_bytes,
-                           e->rx_ts.p, e->rx_hash.p, e->rx_pos.p, e->rx_len.p, e->rx_nev.p, e->rx_ip16.p);
+                           e->rx_ts.p, e->rx_hash.p, e->rx_pos.p, e->rx_len.p, e->rx_nev.p, e->rx_ip16.p, e->dbg_hash_mask);
       first += nk;
       bbase += src_counts[3 * k + 2];
     }

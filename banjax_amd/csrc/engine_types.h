@@ -41,17 +41,18 @@ struct DevRule {
 constexpr uint32_t kJiNfa = 1, kJiEquiv = 2, kJiBigLit = 16;  // bits 2-3: lead & 3
 
 // Prefilter gram bitset (LDS resident, 64K bits = 2048 words), tested two
-// positions per word (gram_pair_* below).  gram_mix: bits 32..47 of a 24 x
-// 24-bit product (one full-rate v_mul_hi_u32_u24 on the device when the key is
-// visibly 24-bit); its bits 2..12 pick the word.
+// positions per word (gram_pair_* below).  gram_mix: the low 32 bits of a
+// 24 x 24-bit product (one full-rate v_mul_u32_u24 on the device when the key
+// is visibly 24-bit); its bits 13..23 pick the word.  (Bits 34..44 of the
+// full product spread cfg2's similar host literals worse: k_scan 17.5 -> 32 ms.)
 constexpr uint32_t kGramLog2 = 16;
 constexpr uint32_t kGramWords = (1u << kGramLog2) / 32;
-constexpr uint32_t kGramMul = 0x9E3779u;
+constexpr uint32_t kGramMul = 0x2C1B3Bu;
 __host__ __device__ inline uint32_t gram_mix(uint32_t x) {
 #ifdef __HIP_DEVICE_COMPILE__
-  return __umulhi(x & 0xFFFFFFu, kGramMul);
+  return __umul24(x, kGramMul);
 #else
-  return (uint32_t)(((uint64_t)(x & 0xFFFFFFu) * kGramMul) >> 32);
+  return (x & 0xFFFFFFu) * kGramMul;
 #endif
 }
 // The scan pass tests grams in pairs: positions k (even) and k + 1 share the
@@ -60,8 +61,8 @@ __host__ __device__ inline uint32_t gram_mix(uint32_t x) {
 // & 15).  A registered gram sets its bit in both roles (word of its last three
 // bytes, low half; word of its first three bytes, high half), so no occurrence
 // is missed at either parity.  key = 3 bytes (24 bits).
-__host__ __device__ inline uint32_t gram_pair_word(uint32_t key) { return (gram_mix(key) >> 2) & (kGramWords - 1); }
-__host__ __device__ inline uint32_t gram_pair_byte_off(uint32_t key) { return gram_mix(key) & ((kGramWords - 1) << 2); }
+__host__ __device__ inline uint32_t gram_pair_word(uint32_t key) { return (gram_mix(key) >> 13) & (kGramWords - 1); }
+__host__ __device__ inline uint32_t gram_pair_byte_off(uint32_t key) { return (gram_mix(key) >> 11) & ((kGramWords - 1) << 2); }
 // home slot of a gram in the exact gram table (cap a power of two <= 2^18):
 // Fibonacci hashing, high product bits
 __host__ __device__ inline uint32_t gram_slot(uint32_t g, uint32_t cap) { return ((g * 0x9E3779B1u) >> 14) & (cap - 1); }

@@ -265,16 +265,7 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
     if (act) {
       s = j ? A.nl[j - 1] + 1 : 0;
       n = (uint32_t)(A.nl[j] - s);
-      if (B.any_prefilter) {
-        cm = L.cand_meta[j];
-        const ulonglong2 *cp = reinterpret_cast<const ulonglong2 *>(L.cand + j * kCandSlots);
-#pragma unroll
-        for (int k = 0; k < kCandSlots / 2; ++k) {
-          const ulonglong2 w = cp[k];
-          cv[2 * k] = w.x;
-          cv[2 * k + 1] = w.y;
-        }
-      }
+      if (B.any_prefilter) cm = L.cand_meta[j];  // before the window loads: waited for alone
     }
     // ---- the line's window: 16 B-aligned pieces from its first byte
     const uint64_t a0 = s & ~15ull;
@@ -297,6 +288,18 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
             w4[q] = x;
           }
           v[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+      }
+      // the hit slots the scan filled (most lines have none or one: 16 B, not 32)
+      if (act && B.any_prefilter && cm.cnt) {
+        const ulonglong2 *cp = reinterpret_cast<const ulonglong2 *>(L.cand + j * kCandSlots);
+        const ulonglong2 w0 = cp[0];
+        cv[0] = w0.x;
+        cv[1] = w0.y;
+        if (cm.cnt > 2) {
+          const ulonglong2 w1 = cp[1];
+          cv[2] = w1.x;
+          cv[3] = w1.y;
         }
       }
 #pragma unroll

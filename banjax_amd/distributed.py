@@ -26,7 +26,7 @@ import torch
 from .config import Ruleset
 from .engine import BatchOutput
 
-LINE_REC = 32  # sizeof(bjx_event_line)
+LINE_REC = 16  # sizeof(bjx_event_line)
 
 
 def _sync(device: torch.device):

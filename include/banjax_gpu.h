@@ -201,13 +201,11 @@ int bjx_process_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
    Source order must be stream order (rank r holds the r-th chunk), which makes
    the owner's event order the reference's.  All buffers are device pointers
    allocated by the caller; the engine never retains them. */
-typedef struct bjx_event_line {
+typedef struct bjx_event_line {  /* 16 B (ABI 4; the owner hashes the IP bytes itself) */
   int64_t ts_ns;     /* parsed line timestamp */
-  uint64_t ip_hash;  /* engine hash of the IP bytes */
   uint32_t ip_off;   /* offset of the IP bytes in this owner's part of the byte buffer */
-  uint32_t ip_len;
-  uint32_t n_events; /* events of the line; their rule indices follow in the event buffer */
-  uint32_t _pad;
+  uint16_t ip_len;
+  uint16_t n_events; /* events of the line; their rule indices follow in the event buffer */
 } bjx_event_line;
 
 int bjx_match_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns, uint32_t flags,

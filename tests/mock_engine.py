@@ -16,7 +16,7 @@ import struct
 from oracle import oracle as O
 from tests.parity import oracle_config
 
-REC = struct.Struct("<qQIIII")  # bjx_event_line
+REC = struct.Struct("<qIHH")  # bjx_event_line
 
 
 def ip_hash(ip: bytes) -> int:
@@ -79,7 +79,7 @@ class MockEngine:
             base = len(ipb)
             for j, ev in part:
                 ip = self.line_ip[j]
-                recs += REC.pack(self.line_ts[j], ip_hash(ip), len(ipb) - base, len(ip), len(ev), 0)
+                recs += REC.pack(self.line_ts[j], len(ipb) - base, len(ip), len(ev))
                 ipb += ip
                 for e in ev:
                     evs += struct.pack("<I", self.results[self.events[e]][1])
@@ -100,7 +100,7 @@ class MockEngine:
         i, k, bbase = 0, 0, 0
         for (cl, ce, cb) in src_counts:
             for _ in range(cl):
-                ts, _h, off, ln, n_ev, _ = REC.unpack_from(recs, i * REC.size)
+                ts, off, ln, n_ev = REC.unpack_from(recs, i * REC.size)
                 ip = ipb[bbase + off:bbase + off + ln]
                 for _ in range(n_ev):
                     rule = self.rules[struct.unpack_from("<I", evs, 4 * k)[0]]
