@@ -846,6 +846,7 @@ struct JobSink {
   uint64_t *jrec;
   unsigned long long *count;
   uint64_t cap;
+  uint32_t n_rules;  // a legacy job's key names rule r as n_rules + r: the sort puts them after the windowed ones
 };
 // Job window records (JobSink::jrec): where k_dfa starts the rule's automaton,
 // worked out by the line kernel from the line's hits in registers (k_dfa then
@@ -862,7 +863,8 @@ constexpr uint64_t kJobNoCount = 1ull << 41;
 constexpr uint64_t kJobLegacy = 1ull << 63;
 constexpr uint32_t kWaveJobBytes = kWaveJobs * 16 + 16;  // per wave: staged jobs + their counter
 __device__ __forceinline__ void emit_job(const JobSink &S, uint64_t j, uint32_t r, uint32_t pos, uint64_t rec = kJobLegacy) {
-  const uint4 v = make_uint4((uint32_t)j, r | (pos << 24), (uint32_t)rec, (uint32_t)(rec >> 32));
+  const uint32_t rk = (rec & kJobLegacy) ? S.n_rules + r : r;
+  const uint4 v = make_uint4((uint32_t)j, rk | (pos << 24), (uint32_t)rec, (uint32_t)(rec >> 32));
   const uint32_t c = atomicAdd(S.cnt, 1u);
   if (c < kWaveJobs) { S.lds[c] = v; return; }
   const unsigned long long g = atomicAdd(S.count, 1ull);
@@ -1968,6 +1970,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
   S.jkey = A.jkey;
   S.jidx = A.jidx;
   S.jrec = A.jrec;
+  S.n_rules = B.n_rules;
   S.count = A.job_count;
   S.cap = A.job_cap;
   if (lane == 0) *S.cnt = 0;
@@ -2100,6 +2103,7 @@ __global__ __launch_bounds__(kBlock) void k_rules(Bind B, RulesArgs A) {
   S.jkey = A.jkey;
   S.jidx = A.jidx;
   S.jrec = A.jrec;
+  S.n_rules = B.n_rules;
   S.count = A.job_count;
   S.cap = A.job_cap;
   if (lane == 0) *S.cnt = 0;
@@ -2510,20 +2514,77 @@ __device__ __forceinline__ bool dfa_line(const Bind &B, const DevRule &R, const 
   }
 }
 
+// The windowed DFA jobs (kJob* records from k_lines2): one lane per job, the
+// rule's transition rows staged in LDS when the block's jobs share a rule
+// (jobs sorted by key; legacy jobs, keyed n_rules + rule, sort after them and
+// are k_dfa_legacy's).  Each job reads its window word and the text from
+// there to the line's '\n'; only a match reads the job's line.
 __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restrict__ buf, uint64_t n_buf,
-                                                const uint64_t *__restrict__ nl, const uint32_t *__restrict__ jkey,
-                                                const uint32_t *__restrict__ jidx, const uint32_t *__restrict__ jline,
-                                                const uint64_t *__restrict__ jrec, uint64_t n, Lines L) {
+                                                const uint32_t *__restrict__ jkey, const uint32_t *__restrict__ jidx,
+                                                const uint32_t *__restrict__ jline, const uint64_t *__restrict__ jrec, uint64_t n,
+                                                Lines L) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_dfa[];
+  uint16_t *s_tr = reinterpret_cast<uint16_t *>(s_dfa);
+  uint32_t *s_acc = reinterpret_cast<uint32_t *>(s_dfa + ((B.dfa_tr * 2 + 15) & ~15u));
+  uint8_t *s_ac = reinterpret_cast<uint8_t *>(s_acc + B.dfa_acc);
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x;
+  if ((jkey[t0] & 0xFFFFFF) >= B.n_rules) return;  // legacy jobs only (they sort last)
+  const uint64_t t = t0 + threadIdx.x;
+  const uint64_t tl = t0 + blockDim.x - 1 < n ? t0 + blockDim.x - 1 : n - 1;
+  const uint32_t r0 = jkey[t0] & 0xFFFFFF;
+  const DevRule R0 = B.rules[r0];
+  const bool uniform = (jkey[tl] & 0xFFFFFF) == r0;  // the whole block is r0's
+  const bool staged = uniform && (uint32_t)R0.ncls * R0.n_states <= B.dfa_tr;
+  if (staged) {
+    const uint16_t *g = B.trans + R0.trans_off;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)R0.ncls * R0.n_states; i += blockDim.x) s_tr[i] = g[i];
+    if (threadIdx.x < 128) s_ac[threadIdx.x] = B.ascii_cls[(size_t)r0 * 128 + threadIdx.x];
+    if (R0.n_states <= B.dfa_acc)
+      for (uint32_t i = threadIdx.x; i < R0.n_states; i += blockDim.x) s_acc[i] = B.accel[R0.ae_off + i];
+  }
+  __syncthreads();
+  if (t >= n) return;
+  const uint32_t key = jkey[t];
+  const uint32_t r = key & 0xFFFFFF, pos = key >> 24;
+  if (r >= B.n_rules) return;  // a legacy job
+  const uint32_t slot = jidx[t];
+  const uint64_t rec = jrec[slot];
+  const uint64_t a = rec & kJobOffMask;
+  bool m;
+  if (staged) {
+    const uint32_t *acc = R0.n_states <= B.dfa_acc ? s_acc : B.accel + R0.ae_off;
+    m = dfa_line<true>(B, R0, s_tr, s_ac, acc, buf, n_buf, a, (rec & kJobSkipState) ? R0.skip_state : R0.start);
+  } else {
+    const DevRule R = B.rules[r];
+    m = dfa_line<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, B.accel + R.ae_off, buf, n_buf, a,
+                        (rec & kJobSkipState) ? R.skip_state : R.start);
+  }
+  if (!m) return;
+  const uint64_t j = jline[slot];
+  atomicOr(reinterpret_cast<unsigned long long *>(L.masks + j * B.mask_words + (pos >> 6)), 1ull << (pos & 63));
+  atomicAdd(reinterpret_cast<unsigned long long *>(L.counts + j), (1ull << 32) | ((rec & kJobNoCount) ? 0ull : 1ull));
+}
+
+// The legacy DFA jobs (keys n_rules + rule: kernels other than k_lines2, and
+// k_lines2's NFA rules / seeks past overflowed slots / first-hit tables):
+// the start is derived from the line's arrays (eq_certain, skip prefix,
+// lead_start_seek), then dfa_text over rest.
+__global__ __launch_bounds__(kBlock) void k_dfa_legacy(Bind B, const uint8_t *__restrict__ buf, uint64_t n_buf,
+                                                       const uint64_t *__restrict__ nl, const uint32_t *__restrict__ jkey,
+                                                       const uint32_t *__restrict__ jidx, const uint32_t *__restrict__ jline,
+                                                       uint64_t n, Lines L) {
   __shared__ uint16_t s_tr[kDfaLdsEntries];
   __shared__ uint32_t s_acc[kDfaAccelLds];
   __shared__ uint8_t s_ac[128];
   const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x;
   const uint64_t t = t0 + threadIdx.x;
   const uint64_t tl = t0 + blockDim.x - 1 < n ? t0 + blockDim.x - 1 : n - 1;
-  const uint32_t r0 = jkey[t0] & 0xFFFFFF;
+  if ((jkey[tl] & 0xFFFFFF) < B.n_rules) return;  // windowed jobs only
+  const uint32_t k0 = jkey[t0] & 0xFFFFFF;
+  const uint32_t r0 = k0 >= B.n_rules ? k0 - B.n_rules : k0;
   const DevRule R0 = B.rules[r0];
-  const bool uniform = (jkey[tl] & 0xFFFFFF) == r0;  // jobs sorted by rule: the whole block is r0's
-  if (uniform && (R0.flags & kRuleNfa)) return;       // k_nfa's
+  const bool uniform = k0 >= B.n_rules && (jkey[tl] & 0xFFFFFF) == k0;  // the whole block is r0's
+  if (uniform && (R0.flags & kRuleNfa)) return;                        // k_nfa's
   const bool staged = uniform && (uint32_t)R0.ncls * R0.n_states <= kDfaLdsEntries;
   if (staged) {
     const uint16_t *g = B.trans + R0.trans_off;
@@ -2535,59 +2596,40 @@ __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restric
   __syncthreads();
   if (t >= n) return;
   const uint32_t key = jkey[t];
-  const uint32_t r = key & 0xFFFFFF, pos = key >> 24;
-  const uint32_t slot = jidx[t];
-  const uint64_t rec = jrec[slot];
+  const uint32_t rk = key & 0xFFFFFF, pos = key >> 24;
+  if (rk < B.n_rules) return;  // a windowed job
+  const uint32_t r = rk - B.n_rules;
+  const uint64_t j = jline[jidx[t]];
+  const uint64_t s = j ? nl[j - 1] + 1 : 0;
+  const uint64_t rs = s + L.rest_off[j];
+  const uint32_t rl = (uint32_t)(nl[j] - rs);
   bool m;
-  uint64_t j = 0;
-  bool no_count;
   if (!staged && (B.rules[r].flags & kRuleNfa)) return;  // k_nfa's (a mixed block)
-  if (!(rec & kJobLegacy)) {
-    // the window the line kernel worked out: the text from there to the '\n'
-    const uint64_t a = rec & kJobOffMask;
-    if (staged) {
-      const uint32_t *acc = R0.n_states <= kDfaAccelLds ? s_acc : B.accel + R0.ae_off;
-      m = dfa_line<true>(B, R0, s_tr, s_ac, acc, buf, n_buf, a, (rec & kJobSkipState) ? R0.skip_state : R0.start);
-    } else {
-      const DevRule R = B.rules[r];
-      m = dfa_line<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, B.accel + R.ae_off, buf, n_buf, a,
-                          (rec & kJobSkipState) ? R.skip_state : R.start);
-    }
-    if (!m) return;
-    j = jline[slot];
-    no_count = (rec & kJobNoCount) != 0;
+  if ((staged ? R0.equiv : B.rules[r].equiv) && eq_certain(B, L, j, pos, rs)) {
+    m = true;
+  } else if (staged) {
+    // anchored prefix literal already matched by k_lines: step in past it;
+    // a lead rule's job starts at the first hit of its literals (every match
+    // begins at one, regex_compiler.h pref_lead)
+    const uint32_t sk = R0.skip_len && R0.skip_len <= rl ? R0.skip_len : 0u;
+    const uint32_t st0 = (R0.lead & 1u) ? lead_start_seek(B, R0, L, buf, n_buf, j, pos, rs, rl) : 0u;
+    const uint32_t *acc = R0.n_states <= kDfaAccelLds ? s_acc : B.accel + R0.ae_off;
+    m = st0 ? dfa_text<true>(B, R0, s_tr, s_ac, acc, buf, n_buf, rs + st0, rl - st0, R0.start)
+            : dfa_text<true>(B, R0, s_tr, s_ac, acc, buf, n_buf, rs + sk, rl - sk, sk ? R0.skip_state : R0.start);
   } else {
-    j = jline[slot];
-    const uint64_t s = j ? nl[j - 1] + 1 : 0;
-    const uint64_t rs = s + L.rest_off[j];
-    const uint32_t rl = (uint32_t)(nl[j] - rs);
-    if ((staged ? R0.equiv : B.rules[r].equiv) && eq_certain(B, L, j, pos, rs)) {
-      m = true;
-    } else if (staged) {
-      // anchored prefix literal already matched by k_lines: step in past it;
-      // a lead rule's job starts at the first hit of its literals (every match
-      // begins at one, regex_compiler.h pref_lead)
-      const uint32_t sk = R0.skip_len && R0.skip_len <= rl ? R0.skip_len : 0u;
-      const uint32_t st0 = (R0.lead & 1u) ? lead_start_seek(B, R0, L, buf, n_buf, j, pos, rs, rl) : 0u;
-      const uint32_t *acc = R0.n_states <= kDfaAccelLds ? s_acc : B.accel + R0.ae_off;
-      m = st0 ? dfa_text<true>(B, R0, s_tr, s_ac, acc, buf, n_buf, rs + st0, rl - st0, R0.start)
-              : dfa_text<true>(B, R0, s_tr, s_ac, acc, buf, n_buf, rs + sk, rl - sk, sk ? R0.skip_state : R0.start);
-    } else {
-      const DevRule R = B.rules[r];
-      if (R.flags & kRuleNfa) return;  // k_nfa's
-      const uint32_t sk = R.skip_len && R.skip_len <= rl ? R.skip_len : 0u;
-      const uint32_t st0 = (R.lead & 1u) ? lead_start_seek(B, R, L, buf, n_buf, j, pos, rs, rl) : 0u;
-      const uint32_t *acc = B.accel + R.ae_off;
-      if (st0) m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, acc, buf, n_buf, rs + st0,
-                                   rl - st0, R.start);
-      else m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, acc, buf, n_buf, rs + sk, rl - sk,
-                               sk ? R.skip_state : R.start);
-    }
-    if (!m) return;
-    const int32_t hid = L.host_id[j];
-    const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
-    no_count = (B.sc_skip[2 * sc + (pos >> 6)] >> (pos & 63)) & 1;
+    const DevRule R = B.rules[r];
+    const uint32_t sk = R.skip_len && R.skip_len <= rl ? R.skip_len : 0u;
+    const uint32_t st0 = (R.lead & 1u) ? lead_start_seek(B, R, L, buf, n_buf, j, pos, rs, rl) : 0u;
+    const uint32_t *acc = B.accel + R.ae_off;
+    if (st0) m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, acc, buf, n_buf, rs + st0,
+                                 rl - st0, R.start);
+    else m = dfa_text<false>(B, R, B.trans + R.trans_off, B.ascii_cls + (size_t)r * 128, acc, buf, n_buf, rs + sk, rl - sk,
+                             sk ? R.skip_state : R.start);
   }
+  if (!m) return;
+  const int32_t hid = L.host_id[j];
+  const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
+  const bool no_count = (B.sc_skip[2 * sc + (pos >> 6)] >> (pos & 63)) & 1;
   atomicOr(reinterpret_cast<unsigned long long *>(L.masks + j * B.mask_words + (pos >> 6)), 1ull << (pos & 63));
   atomicAdd(reinterpret_cast<unsigned long long *>(L.counts + j), (1ull << 32) | (no_count ? 0ull : 1ull));
 }
@@ -2698,7 +2740,7 @@ __global__ __launch_bounds__(kBlock) void k_nfa_wide(Bind B, const uint8_t *__re
   __shared__ uint32_t s_flag;
   const uint32_t tid = threadIdx.x;
   for (uint64_t t = j0 + blockIdx.x; t < j1; t += gridDim.x) {
-    const uint32_t key = jkey[t], r = key & 0xFFFFFFu;
+    const uint32_t key = jkey[t], rk = key & 0xFFFFFFu, r = rk >= B.n_rules ? rk - B.n_rules : rk;
     const uint32_t pos = jpos ? jpos[t] : key >> 24;
     const uint64_t j = jline[jidx ? jidx[t] : t];
     const DevRule R = B.rules[r];
@@ -5666,6 +5708,20 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.hl_bytes = hl_bytes;
   B.lt_hinfo = lt_hinfo; B.lt_cls = lt_cls; B.lt_trec = lt_trec; B.lt_pool = lt_pool;
   B.l2_hdc = l2_hdc; B.l2_dcls = l2_dcls; B.l2_none = l2_none; B.l2_bytes = l2_bytes;
+  {
+    // k_dfa stages the block's rule in LDS when it fits: size that LDS by the
+    // ruleset's largest DFA, not the cap, so smaller rulesets run more blocks
+    uint32_t tr = 0, acc = 0;
+    for (const DevRule &d : drules) {
+      if (d.flags & kRuleNfa) continue;
+      const uint32_t ne = (uint32_t)d.ncls * d.n_states;
+      if (ne <= kDfaLdsEntries) tr = std::max(tr, ne);
+      if (d.n_states <= kDfaAccelLds) acc = std::max(acc, d.n_states);
+    }
+    B.dfa_tr = tr;
+    B.dfa_acc = acc;
+    B.dfa_lds = ((tr * 2 + 15) & ~15u) + acc * 4 + 128;
+  }
   B.plan = reinterpret_cast<const uint4 *>(base + o_plan);
   B.plan_off = reinterpret_cast<const uint32_t *>(base + o_plo);
   B.plan_glob = reinterpret_cast<const uint4 *>(base + o_plg);
@@ -6256,17 +6312,20 @@ static void launch_wide(bjx_engine *e, const Bind &B, const uint8_t *buf, uint64
 // (k_rule_bounds), then one k_nfa launch per rule with its state width.
 static void run_nfa_jobs(bjx_engine *e, const Bind &B, const uint8_t *buf, uint64_t n, uint64_t n_jobs, const Lines &L) {
   hipStream_t st = e->stream;
-  e->rb_first.ensure(B.n_rules); e->rb_last.ensure(B.n_rules);
-  HIP_OK(hipMemsetAsync(e->rb_first.p, 0, B.n_rules * 4ull, st));
-  HIP_OK(hipMemsetAsync(e->rb_last.p, 0, B.n_rules * 4ull, st));
+  // bounds per job key: rule r's windowed jobs under r, its legacy ones (every
+  // NFA job) under n_rules + r
+  const uint32_t nk = 2 * B.n_rules;
+  e->rb_first.ensure(nk); e->rb_last.ensure(nk);
+  HIP_OK(hipMemsetAsync(e->rb_first.p, 0, nk * 4ull, st));
+  HIP_OK(hipMemsetAsync(e->rb_last.p, 0, nk * 4ull, st));
   hipLaunchKernelGGL(k_rule_bounds, dim3(grid_for(n_jobs)), dim3(kBlock), 0, st, n_jobs, e->jkey2.p, e->rb_first.p, e->rb_last.p);
   HIP_OK(hipGetLastError());
-  e->h_first.resize(B.n_rules); e->h_last.resize(B.n_rules);
-  HIP_OK(hipMemcpyAsync(e->h_first.data(), e->rb_first.p, B.n_rules * 4ull, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipMemcpyAsync(e->h_last.data(), e->rb_last.p, B.n_rules * 4ull, hipMemcpyDeviceToHost, st));
+  e->h_first.resize(nk); e->h_last.resize(nk);
+  HIP_OK(hipMemcpyAsync(e->h_first.data(), e->rb_first.p, nk * 4ull, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(e->h_last.data(), e->rb_last.p, nk * 4ull, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
   for (const uint4 &nr : e->nfa_rules) {
-    const uint64_t j0 = e->h_first[nr.x], j1 = e->h_last[nr.x];
+    const uint64_t j0 = e->h_first[B.n_rules + nr.x], j1 = e->h_last[B.n_rules + nr.x];
     if (j1 <= j0) continue;
     if (nr.w) {  // kRuleNfaWide: nr.y = state words, nr.z = groups
       launch_wide(e, B, buf, n, e->jkey2.p, e->jidx2.p, e->jline.p, nullptr, j0, j1, L, nr.y, nr.z);
@@ -6499,7 +6558,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     A.jline = e->jline.p; A.jkey = e->jkey.p; A.jidx = e->jidx.p; A.jrec = e->jrec.p; A.job_count = e->scalars.p + 11;
     A.job_cap = std::min(std::min(e->jline.n, e->jkey.n), std::min(e->jidx.n, e->jrec.n));
     A.job_real = e->scalars.p + 14;
-    A.null_key = B.n_rules;  // sorts after every rule id (the job sort covers bit_width(n_rules) bits)
+    A.null_key = 2 * B.n_rules;  // sorts after every job key (windowed r, legacy n_rules + r)
     A.span_bytes = getenv("BJX_SPAN_BYTES") ? (uint32_t)atoi(getenv("BJX_SPAN_BYTES")) & ~15u : kSpanBytes;
     A.list = nullptr; A.n_list = 0; A.prof = nullptr;
     unsigned long long n_todo = 0;
@@ -6620,33 +6679,42 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     {
       // null jobs (key n_rules) sort after the real ones: k_dfa takes the first n_jobs
       uint32_t *ki = e->jkey.p, *ko = e->jkey2.p, *vi = e->jidx.p, *vo = e->jidx2.p;
-      const int bits = std::max(1, bit_width(B.n_rules));
+      const int bits = std::max(1, bit_width(2 * B.n_rules));
       cub_call(e, [&](void *tmp, size_t &bytes) {
         return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)n_slots, 0, bits, st);
       });
     }
-    hipLaunchKernelGGL(k_dfa, dim3(grid_for(n_jobs)), dim3(kBlock), 0, st, B, buf, (uint64_t)n, e->nl.p, e->jkey2.p,
+    hipLaunchKernelGGL(k_dfa, dim3(grid_for(n_jobs)), dim3(kBlock), B.dfa_lds, st, B, buf, (uint64_t)n, e->jkey2.p,
                        e->jidx2.p, e->jline.p, e->jrec.p, (uint64_t)n_jobs, L);
+    hipLaunchKernelGGL(k_dfa_legacy, dim3(grid_for(n_jobs)), dim3(kBlock), 0, st, B, buf, (uint64_t)n, e->nl.p, e->jkey2.p,
+                       e->jidx2.p, e->jline.p, (uint64_t)n_jobs, L);
     HIP_OK(hipGetLastError());
     if (B.any_nfa && !e->nfa_rules.empty()) run_nfa_jobs(e, B, buf, n, n_jobs, L);
     static const bool job_stats = getenv("BJX_JOB_STATS") != nullptr;  // diagnostics: jobs per rule (stderr)
     if (job_stats) {
-      e->rb_first.ensure(B.n_rules); e->rb_last.ensure(B.n_rules);
-      HIP_OK(hipMemsetAsync(e->rb_first.p, 0, B.n_rules * 4ull, st));
-      HIP_OK(hipMemsetAsync(e->rb_last.p, 0, B.n_rules * 4ull, st));
+      const uint32_t nk = 2 * B.n_rules;
+      e->rb_first.ensure(nk); e->rb_last.ensure(nk);
+      HIP_OK(hipMemsetAsync(e->rb_first.p, 0, nk * 4ull, st));
+      HIP_OK(hipMemsetAsync(e->rb_last.p, 0, nk * 4ull, st));
       hipLaunchKernelGGL(k_rule_bounds, dim3(grid_for(n_jobs)), dim3(kBlock), 0, st, (uint64_t)n_jobs, e->jkey2.p, e->rb_first.p,
                          e->rb_last.p);
-      std::vector<uint32_t> f(B.n_rules), l(B.n_rules);
-      HIP_OK(hipMemcpyAsync(f.data(), e->rb_first.p, B.n_rules * 4ull, hipMemcpyDeviceToHost, st));
-      HIP_OK(hipMemcpyAsync(l.data(), e->rb_last.p, B.n_rules * 4ull, hipMemcpyDeviceToHost, st));
+      std::vector<uint32_t> f(nk), l(nk);
+      HIP_OK(hipMemcpyAsync(f.data(), e->rb_first.p, nk * 4ull, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(l.data(), e->rb_last.p, nk * 4ull, hipMemcpyDeviceToHost, st));
       HIP_OK(hipStreamSynchronize(st));
       std::map<std::string, uint64_t> by_rx;
-      for (uint32_t r = 0; r < B.n_rules; ++r)
-        if (l[r] > f[r]) by_rx[r < rs->rules.size() ? rs->rules[r].regex.substr(0, 60) : "?"] += l[r] - f[r];
+      uint64_t n_legacy = 0;
+      for (uint32_t k = 0; k < nk; ++k) {
+        const uint32_t r = k % B.n_rules;
+        if (l[k] <= f[k]) continue;
+        by_rx[r < rs->rules.size() ? rs->rules[r].regex.substr(0, 60) : "?"] += l[k] - f[k];
+        if (k >= B.n_rules) n_legacy += l[k] - f[k];
+      }
       std::vector<std::pair<uint64_t, std::string>> v;
       for (auto &kv : by_rx) v.push_back({kv.second, kv.first});
       std::sort(v.rbegin(), v.rend());
-      fprintf(stderr, "BJX_JOB_STATS jobs=%llu lines=%llu\n", n_jobs, (unsigned long long)e->bc.n_lines);
+      fprintf(stderr, "BJX_JOB_STATS jobs=%llu (legacy %llu) lines=%llu\n", n_jobs, (unsigned long long)n_legacy,
+              (unsigned long long)e->bc.n_lines);
       for (size_t i = 0; i < v.size() && i < 16; ++i) fprintf(stderr, "  %10llu  %s\n", (unsigned long long)v[i].first, v[i].second.c_str());
     }
   }

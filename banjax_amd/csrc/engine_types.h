@@ -205,6 +205,9 @@ struct Bind {
   // offsets; lines2.h): per-host decision class, class records, the class of
   // lines without a host; l2_bytes = the blob with them (0: k_lines2 off)
   uint32_t l2_hdc, l2_dcls, l2_none, l2_bytes;
+  // k_dfa's LDS: transition entries / accel words staged per block (the
+  // ruleset's largest DFA within kDfaLdsEntries / kDfaAccelLds), dynamic bytes
+  uint32_t dfa_tr, dfa_acc, dfa_lds;
   const uint4 *plan;
   const uint32_t *plan_off;  // n_hosts + 1
   const uint4 *plan_glob;

@@ -242,6 +242,7 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
   S.jkey = A.jkey;
   S.jidx = A.jidx;
   S.jrec = A.jrec;
+  S.n_rules = B.n_rules;
   S.count = A.job_count;
   S.cap = A.job_cap;
   if (lane == 0) *S.cnt = 0;
