@@ -3019,6 +3019,41 @@ __device__ __forceinline__ bool ip_claim_line(const EvSrc &E, const State &S, ui
   }
 }
 
+// The IP of every parsed line looked up among the IPs of earlier batches
+// (read-only: no claim), on its own stream while the DFA jobs run (both are
+// latency-bound, so they share the CUs).  el_id = the IP's id, or kUnresolved
+// (not there, or the line's header is parsed later); k_ip_claim then only
+// claims the unresolved event lines.  Ids survive a table rehash.
+constexpr uint32_t kUnresolved = 0xFFFFFFFEu;
+__global__ __launch_bounds__(kBlock) void k_ip_lookup(EvSrc E, const uint8_t *__restrict__ flags, State S,
+                                                      uint32_t *__restrict__ el_id) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E.n; i += (uint64_t)gridDim.x * blockDim.x) {
+  uint32_t out = kUnresolved;
+  if (flags[i] == 0) {
+    const uint64_t h = E.ip_hash[i];
+    const uint32_t len = E.ip_len[i];
+    const bool inl = len <= 15;
+    const uint4 k16 = inl ? E.ip16[i] : make_uint4(0, 0, 0, 0);
+    uint64_t s = h & S.ip_mask;
+    for (;;) {
+      const uint4 *sp = reinterpret_cast<const uint4 *>(&S.ip[s]);
+      const uint4 q0 = sp[0], q1 = sp[1];
+      const uint64_t cur = ((uint64_t)q0.y << 32) | q0.x;
+      if (cur == 0) break;
+      if (cur == h && q0.w != 0) {
+        const uint32_t id = q0.z;
+        if (inl ? key16_eq(q1, k16) : (S.ip_len[id] == len && bytes_eq(S.arena + S.ip_off[id], ev_ip(E, i), len))) {
+          out = id;
+          break;
+        }
+      }
+      s = (s + 1) & S.ip_mask;
+    }
+  }
+  el_id[i] = out;
+  }
+}
+
 // exclusive prefix of v over the wave and one atomicAdd of the wave's total
 // on ctr; returns ctr's old value + the prefix (every lane of the wave calls it)
 __device__ __forceinline__ uint64_t wave_alloc(unsigned long long *ctr, uint32_t v);
@@ -3027,10 +3062,11 @@ __device__ __forceinline__ uint64_t wave_alloc(unsigned long long *ctr, uint32_t
 // in this batch), listed for k_ip_commit
 __global__ __launch_bounds__(kBlock) void k_ip_claim(EvSrc E, State S, uint32_t epoch, uint32_t *__restrict__ el_slot,
                                                      uint32_t *__restrict__ el_id, uint32_t *__restrict__ el_new,
-                                                     uint64_t shard_budget) {
+                                                     uint64_t shard_budget, uint32_t pre) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool claimed = false, isnew = false;
-  if (i < E.n && ev_has(E, i) && !flag_set(S, 5)) {
+  // pre: k_ip_lookup resolved the lines whose IP an earlier batch created
+  if (i < E.n && ev_has(E, i) && !(pre && el_id[i] != kUnresolved) && !flag_set(S, 5)) {
     el_id[i] = 0;
     claimed = ip_claim_line(E, S, epoch, i, el_slot, el_id, shard_budget);
     isnew = el_id[i] == kNewIp;
@@ -4456,6 +4492,10 @@ struct bjx_engine {
   std::mutex mu;
   std::string last_error;
   hipStream_t stream = nullptr;
+  // IP pre-lookup (k_ip_lookup) on its own stream beside the DFA jobs
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_lines = nullptr, ev_lookup = nullptr;
+  bool pre_looked = false;  // this batch's el_id holds the pre-lookup (k_ip_claim skips resolved lines)
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evm0 = nullptr, evm1 = nullptr;
   hipEvent_t evk[4] = {};      // k_lines launch, DFA-job sort + k_dfa / k_nfa (bench: per-kernel roofline)
   double kernel_ms[3] = {};   // last batch: k_scan, k_lines, DFA jobs
@@ -5913,6 +5953,9 @@ extern "C" int bjx_engine_create(int device, const bjx_engine_options *opts, bjx
     e->device = device;
     HIP_OK(hipSetDevice(device));
     HIP_OK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&e->ev_lines, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&e->ev_lookup, hipEventDisableTiming));
     HIP_OK(hipEventCreate(&e->ev0));
     HIP_OK(hipEventCreate(&e->ev1));
     HIP_OK(hipEventCreate(&e->evm0));
@@ -5973,6 +6016,9 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   for (auto &x : e->evk) (void)hipEventDestroy(x);
   for (auto &x : e->ph) (void)hipEventDestroy(x);
   (void)hipStreamDestroy(e->stream);
+  if (e->aux) (void)hipStreamDestroy(e->aux);
+  if (e->ev_lines) (void)hipEventDestroy(e->ev_lines);
+  if (e->ev_lookup) (void)hipEventDestroy(e->ev_lookup);
   delete e;
 }
 
@@ -6123,6 +6169,8 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
                              const uint64_t *offs = nullptr) {
   hipStream_t st = e->stream;
   if (E.n >= 0x7FFFFFFFull || n_ev >= 0xFFFFFFFFull) throw BjxError(BJX_ERR_ARG, "batch too large (2^31 lines / 2^32 events)");
+  // the pre-lookup reads the IP table: done before any growth or claim
+  if (e->pre_looked) HIP_OK(hipStreamWaitEvent(st, e->ev_lookup, 0));
   read_counters(e);
   ensure_capacity(e, std::min<uint64_t>(n_el, std::max<uint64_t>(1u << 18, e->host_counters[0] / 8)), el_bytes,
                   std::min<uint64_t>(n_ev, std::max<uint64_t>(1u << 20, e->host_counters[2] / 8)));
@@ -6144,8 +6192,10 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
       uint64_t budget = e->ip_cap * 3 / 4 - n_ips;
       const bool forced = e->dbg_budget && attempt == 0 && e->dbg_budget < budget;  // test hook
       if (forced) budget = e->dbg_budget;
+      // a retry after an overflow claims every line again (the rolled-back
+      // claims left their lines' el_id set)
       hipLaunchKernelGGL(k_ip_claim, dim3(grid_for(E.n)), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p,
-                         e->el_new.p, budget / kClaimShards);
+                         e->el_new.p, budget / kClaimShards, e->pre_looked && attempt == 0 ? 1u : 0u);
       HIP_OK(hipGetLastError());
       HIP_OK(hipMemcpyAsync(nw_ovf, e->S.counters + 4, 16, hipMemcpyDeviceToHost, st));
       HIP_OK(hipStreamSynchronize(st));
@@ -6362,6 +6412,10 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
                         bjx_batch_result *out, bool need_ev = true) {
   e->bc = BatchCtx{};
   HIP_OK(hipSetDevice(e->device));
+  // a previous batch's pre-lookup (side stream) is done before this batch
+  // rewrites the line arrays it read
+  if (e->aux) HIP_OK(hipStreamWaitEvent(e->stream, e->ev_lookup, 0));
+  e->pre_looked = false;
   if (e->bound_uid != rs->uid || e->bound_dec_version != e->decisions_version) {
     // (re)binding: calibrate the gram filter on the head of this batch
     const size_t sn = std::min<size_t>(n, 4u << 20);
@@ -6664,6 +6718,28 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     HIP_OK(hipMemsetAsync(e->scalars.p + 14, 0, 8, st));
   }
   out->consumed_bytes = last_nl + 1;
+  // BJX_IP_PRELOOKUP=1: the IPs of the parsed lines looked up on a side stream
+  // while the DFA jobs run (k_ip_lookup), k_ip_claim then claims only the
+  // unresolved lines; only for this engine's own rate-limit stage, when every
+  // header is parsed by now (no per-line fallback lines) and no test hook
+  // rewrites the IP hashes afterwards.  Off by default: the two did not
+  // overlap (profiles/r04_t8: the lookup's blocks fill the CUs first, the
+  // step 63.5 -> 65.4 ms; a 2-blocks-per-CU lookup grid left it latency-bound,
+  // 13.8 ms, and slowed k_dfa: 69.0 ms)
+  e->pre_looked = false;
+  static const bool pre_env = getenv("BJX_IP_PRELOOKUP") && atoi(getenv("BJX_IP_PRELOOKUP")) == 1;
+  if (pre_env && !need_ev && !scan_hdr && sc4[4] == 0 && !e->dbg_hash_mask && e->ip_cap && e->S.ip && !getenv("BJX_CHECK")) {
+    e->el_id.ensure(n_lines);
+    EvSrc E;
+    E.bytes = buf; E.nl = e->nl.p; E.ip_off = L.ip_off; E.ip_pos = nullptr; E.ip_len = L.ip_len;
+    E.ip_hash = L.ip_hash; E.ts = L.ts; E.counts = L.counts; E.ip16 = L.ip16; E.n = n_lines;
+    HIP_OK(hipEventRecord(e->ev_lines, st));
+    HIP_OK(hipStreamWaitEvent(e->aux, e->ev_lines, 0));
+    hipLaunchKernelGGL(k_ip_lookup, dim3(grid_for(n_lines)), dim3(kBlock), 0, e->aux, E, L.flags, e->S, e->el_id.p);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(e->ev_lookup, e->aux));
+    e->pre_looked = true;
+  }
   // job slots taken (sc4[3]; the chunks' unused ones hold null jobs) and real jobs
   unsigned long long n_jobs = 0;
   HIP_OK(hipMemcpyAsync(&n_jobs, e->scalars.p + 14, 8, hipMemcpyDeviceToHost, st));
@@ -6969,6 +7045,8 @@ static void emit_bans(bjx_engine *e, uint64_t n, bool records_only) {
 static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, bool sorted) {
   const Bind &B = e->bind;
   hipStream_t st = e->stream;
+  if (e->aux) HIP_OK(hipStreamWaitEvent(st, e->ev_lookup, 0));  // the batch ends after its side-stream work
+  e->pre_looked = false;
   const BatchCtx &c = e->bc;
   const uint64_t n_lines = c.n_lines, n_res = c.n_res, n_ev = c.n_ev;
   const Lines &L = c.L;
