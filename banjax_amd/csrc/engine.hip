@@ -3168,11 +3168,14 @@ __global__ void k_ip_collide(EvSrc E, State S, uint32_t epoch, uint32_t *__restr
 
 // event k -> state slot and its sort record.  seenIp is false only for the
 // first event of an IP created in this batch.
+// A record whose timestamp the 12-B form cannot hold raises flag 8 (the host
+// claims the batch again in the 16-B form).
+template <typename R>
 __device__ __forceinline__ bool st_claim_event(const EvSrc &E, uint64_t n_ev, uint64_t k, const uint32_t *__restrict__ ev_el,
                                                const uint32_t *__restrict__ ev_rule, const uint32_t *__restrict__ el_slot,
                                                const uint32_t *__restrict__ el_id, const DevRule *__restrict__ rules,
-                                               const State &S, uint32_t *__restrict__ ev_st, EvRec *__restrict__ ev_rec,
-                                               uint64_t shard_budget) {
+                                               const State &S, uint32_t *__restrict__ ev_st, R *__restrict__ ev_rec,
+                                               int64_t base, uint64_t shard_budget) {
   const uint32_t i = ev_el[k];
   const uint32_t r = ev_rule[k];
   uint32_t id = el_id[i];
@@ -3203,23 +3206,22 @@ __device__ __forceinline__ bool st_claim_event(const EvSrc &E, uint64_t n_ev, ui
     if (hot) S.ip_st[id] = (uint32_t)q;
   }
   ev_st[k] = (uint32_t)q;
-  EvRec rec;
-  rec.ts = E.ts[i];
-  rec.rule = r | (first ? 0x80000000u : 0u);
-  rec.ev = (uint32_t)k;
-  ev_rec[k] = rec;
+  const int64_t ts = E.ts[i];
+  if (!R::fits(ts, base)) raise_flag(S, 8);
+  ev_rec[k] = R::make(ts, r, first, (uint32_t)k, base);
   return claimed;
 }
 
+template <typename R>
 __global__ __launch_bounds__(kBlock) void k_st_claim(EvSrc E, uint64_t n_ev, const uint32_t *__restrict__ ev_el,
                                                      const uint32_t *__restrict__ ev_rule, const uint32_t *__restrict__ el_slot,
                                                      const uint32_t *__restrict__ el_id, const DevRule *__restrict__ rules,
-                                                     State S, uint32_t *__restrict__ ev_st, EvRec *__restrict__ ev_rec,
-                                                     uint64_t shard_budget) {
+                                                     State S, uint32_t *__restrict__ ev_st, R *__restrict__ ev_rec,
+                                                     int64_t base, uint64_t shard_budget) {
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool claimed = false;
   if (k < n_ev && !flag_set(S, 7)) claimed = st_claim_event(E, n_ev, k, ev_el, ev_rule, el_slot, el_id, rules, S, ev_st, ev_rec,
-                                                            shard_budget);
+                                                            base, shard_budget);
   count_claims(S, 1, 7, claimed, shard_budget);
 }
 
@@ -3288,11 +3290,7 @@ __device__ __forceinline__ bool st_claim_rule(const State &S, const DevRule *__r
     if (hot) S.ip_st[id] = (uint32_t)q;
   }
   ev_st[k] = (uint32_t)q;
-  EvRec rec;
-  rec.ts = ts;
-  rec.rule = r | (first ? 0x80000000u : 0u);
-  rec.ev = (uint32_t)k;
-  ev_rec[k] = rec;
+  ev_rec[k] = EvRec::make(ts, r, first, (uint32_t)k, 0);
   return claimed;
 }
 
@@ -3376,7 +3374,7 @@ __global__ void k_trip_events_rules(uint64_t n, const uint32_t *__restrict__ pos
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < n) {
     const EvRec v = rec[pos[t]];
-    evr[t] = ((uint64_t)v.ev << 32) | (v.rule & 0x7FFFFFFFu);
+    evr[t] = ((uint64_t)v.ev << 32) | v.rule_id();
   }
 }
 
@@ -3431,27 +3429,30 @@ __global__ void k_fold_claims(State S) {
 // sorted order: bit0 seenIp, bits1-2 MatchType, bit3 Exceeded, bit7 valid.
 constexpr uint32_t kApplyChunk = 2048;
 
-__device__ __forceinline__ uint8_t apply_step(const EvRec &v, const DevRule *__restrict__ rules, uint32_t &pr, int64_t &interval,
-                                              int64_t &limit, bool &valid, int64_t &hits, int64_t &start) {
-  const uint32_t r = v.rule & 0x7FFFFFFFu;
-  const bool seen = (v.rule >> 31) == 0;
+template <typename R>
+__device__ __forceinline__ uint8_t apply_step(const R &v, int64_t base, const DevRule *__restrict__ rules, uint32_t &pr,
+                                              int64_t &interval, int64_t &limit, bool &valid, int64_t &hits, int64_t &start) {
+  const uint32_t r = v.rule_id();
+  const bool seen = v.seen();
+  const int64_t ts = v.time(base);
   if (r != pr) { pr = r; interval = rules[r].interval_ns; limit = rules[r].hits; }  // rules sharing a name share the state
   uint8_t mt;
-  if (!valid) { hits = 1; start = v.ts; mt = BJX_FIRST_TIME; valid = true; }
-  else if (go_sub(v.ts, start) > interval) { mt = BJX_OUTSIDE_INTERVAL; hits = 1; start = v.ts; }
+  if (!valid) { hits = 1; start = ts; mt = BJX_FIRST_TIME; valid = true; }
+  else if (go_sub(ts, start) > interval) { mt = BJX_OUTSIDE_INTERVAL; hits = 1; start = ts; }
   else { mt = BJX_INSIDE_INTERVAL; ++hits; }
   const bool ex = hits > limit;
   if (ex) hits = 0;
   return (uint8_t)(0x80 | (seen ? 1 : 0) | (mt << 1) | (ex ? 8 : 0));
 }
 
-__global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const uint32_t *__restrict__ key, const EvRec *__restrict__ rec,
-                                                  const DevRule *__restrict__ rules, StSlot *__restrict__ st,
+template <typename R>
+__global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const uint32_t *__restrict__ key, const R *__restrict__ rec,
+                                                  int64_t tbase, const DevRule *__restrict__ rules, StSlot *__restrict__ st,
                                                   uint8_t *__restrict__ out_sorted, uint64_t *__restrict__ long_heads,
                                                   unsigned long long *__restrict__ n_long, uint32_t *__restrict__ wcnt) {
   constexpr uint32_t kPer = kApplyChunk / kBlock;  // positions per thread for the head scan
   constexpr uint32_t kLongRun = 8;                 // runs at least this long go to the first lanes
-  __shared__ EvRec s_rec[kApplyChunk];
+  __shared__ R s_rec[kApplyChunk];
   __shared__ uint32_t s_key[kApplyChunk + 1];  // s_key[i + 1] = slot of record i; s_key[0] = slot before the chunk
   __shared__ uint8_t s_out[kApplyChunk];
   __shared__ uint16_t s_head[kApplyChunk];  // run heads in position order
@@ -3514,11 +3515,11 @@ __global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const uint32_t 
       long_heads[atomicAdd(n_long, 1ull)] = u0 + b;
       continue;
     }
-    EvRec v = s_rec[b];
+    R v = s_rec[b];
     for (uint32_t u = b; u < e; ++u) {
-      EvRec nx;
+      R nx;
       if (u + 1 < e) nx = s_rec[u + 1];  // next record in flight while this one is applied
-      s_out[u] = apply_step(v, rules, pr, interval, limit, valid, hits, start);
+      s_out[u] = apply_step(v, tbase, rules, pr, interval, limit, valid, hits, start);
       v = nx;
     }
     st[q].hits = hits;
@@ -3589,8 +3590,9 @@ struct LongRuns {
 };
 
 // 1. run end (block-parallel search), the stored state and the first window
+template <typename Rec>
 __global__ __launch_bounds__(kBlock) void k_long_ends(uint64_t n_ev, const uint32_t *__restrict__ key,
-                                                      const EvRec *__restrict__ rec, const StSlot *__restrict__ st,
+                                                      const Rec *__restrict__ rec, int64_t base, const StSlot *__restrict__ st,
                                                       const DevRule *__restrict__ rules, LongRuns R, uint64_t *__restrict__ len) {
   __shared__ uint32_t s_red[kBlock / 64];
   const uint64_t r = blockIdx.x;
@@ -3601,10 +3603,11 @@ __global__ __launch_bounds__(kBlock) void k_long_ends(uint64_t n_ev, const uint3
   R.end[r] = end;
   len[r] = end - head;
   const StSlot cur = st[q];
-  const int64_t I = rules[rec[head].rule & 0x7FFFFFFFu].interval_ns;
+  const int64_t I = rules[rec[head].rule_id()].interval_ns;
+  const int64_t ts = rec[head].time(base);
   const bool valid = cur.valid != 0;
-  const bool cont = valid && go_sub(rec[head].ts, cur.start) <= I;
-  R.t0[r] = cont ? cur.start : rec[head].ts;
+  const bool cont = valid && go_sub(ts, cur.start) <= I;
+  R.t0[r] = cont ? cur.start : ts;
   R.h0[r] = cont ? cur.hits : 0;
   R.flags[r] = (cont ? 1u : 0u) | ((uint32_t)(valid ? BJX_OUTSIDE_INTERVAL : BJX_FIRST_TIME) << 1) |
                (end - head <= kLongSerial ? 16u : 0u);
@@ -3621,15 +3624,16 @@ __device__ __forceinline__ uint64_t long_run_of(const LongRuns &R, uint64_t k) {
 
 // 2. every record of every long run, in parallel: same interval / limit as the
 // head's rule and timestamps that never decrease, or the run is applied serially
-__global__ __launch_bounds__(kBlock) void k_long_check(uint64_t total, const EvRec *__restrict__ rec,
+template <typename Rec>
+__global__ __launch_bounds__(kBlock) void k_long_check(uint64_t total, const Rec *__restrict__ rec, int64_t base,
                                                        const DevRule *__restrict__ rules, LongRuns R) {
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= total) return;
   const uint64_t r = long_run_of(R, k);
   const uint64_t head = R.head[r], i = head + (k - R.off[r]);
   if (i == head) return;
-  const uint32_t r0 = rec[head].rule & 0x7FFFFFFFu, ri = rec[i].rule & 0x7FFFFFFFu;
-  bool bad = rec[i].ts < rec[i - 1].ts;
+  const uint32_t r0 = rec[head].rule_id(), ri = rec[i].rule_id();
+  bool bad = rec[i].time(base) < rec[i - 1].time(base);
   if (ri != r0) bad = bad || rules[ri].interval_ns != rules[r0].interval_ns || rules[ri].hits != rules[r0].hits;
   if (bad && !(__hip_atomic_load(&R.flags[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 8u)) atomicOr(&R.flags[r], 8u);
 }
@@ -3637,8 +3641,9 @@ __global__ __launch_bounds__(kBlock) void k_long_check(uint64_t total, const EvR
 // 3. per run: the serial walk (short or irregular runs), else the window
 // starts one after another (block-parallel search per window) and the final
 // state in closed form
-__global__ __launch_bounds__(kBlock) void k_long_windows(const uint32_t *__restrict__ key, const EvRec *__restrict__ rec,
-                                                         const DevRule *__restrict__ rules, StSlot *__restrict__ st,
+template <typename Rec>
+__global__ __launch_bounds__(kBlock) void k_long_windows(const uint32_t *__restrict__ key, const Rec *__restrict__ rec,
+                                                         int64_t base, const DevRule *__restrict__ rules, StSlot *__restrict__ st,
                                                          uint8_t *__restrict__ out_sorted, LongRuns R) {
   __shared__ uint32_t s_red[kBlock / 64];
   const uint32_t tid = threadIdx.x;
@@ -3653,7 +3658,7 @@ __global__ __launch_bounds__(kBlock) void k_long_windows(const uint32_t *__restr
       int64_t hits = cur.hits, start = cur.start, interval = 0, limit = 0;
       uint32_t pr = 0xFFFFFFFFu;
       for (uint64_t i = head; i < end; ++i) {
-        out_sorted[i] = apply_step(rec[i], rules, pr, interval, limit, valid, hits, start);
+        out_sorted[i] = apply_step(rec[i], base, rules, pr, interval, limit, valid, hits, start);
         if (R.wcnt) atomicAdd(&R.wcnt[i], 1u);
       }
       st[q].hits = hits;
@@ -3663,7 +3668,7 @@ __global__ __launch_bounds__(kBlock) void k_long_windows(const uint32_t *__restr
     }
     return;
   }
-  const uint32_t r0 = rec[head].rule & 0x7FFFFFFFu;
+  const uint32_t r0 = rec[head].rule_id();
   const int64_t I = rules[r0].interval_ns, Lim = rules[r0].hits;
   uint64_t *win = R.win + R.off[r];
   uint32_t nw = 0;
@@ -3673,7 +3678,7 @@ __global__ __launch_bounds__(kBlock) void k_long_windows(const uint32_t *__restr
     if (tid == 0) win[nw] = a;
     ++nw;
     const int64_t Tw = T;
-    const uint64_t b = block_first(a + 1, end, [&](uint64_t i) { return go_sub(rec[i].ts, Tw) > I; }, s_red);
+    const uint64_t b = block_first(a + 1, end, [&](uint64_t i) { return go_sub(rec[i].time(base), Tw) > I; }, s_red);
     if (b >= end) {
       if (tid == 0) {
         const int64_t e = (int64_t)(b - a);
@@ -3689,14 +3694,15 @@ __global__ __launch_bounds__(kBlock) void k_long_windows(const uint32_t *__restr
       return;
     }
     a = b;
-    T = rec[b].ts;
+    T = rec[b].time(base);
     h0 = 0;
   }
 }
 
 // 4. every record of the windowed runs, in parallel: its window (binary
 // search over the run's window starts) and the closed-form outcome
-__global__ __launch_bounds__(kBlock) void k_long_fill(uint64_t total, const EvRec *__restrict__ rec,
+template <typename Rec>
+__global__ __launch_bounds__(kBlock) void k_long_fill(uint64_t total, const Rec *__restrict__ rec,
                                                       const DevRule *__restrict__ rules, uint8_t *__restrict__ out_sorted,
                                                       LongRuns R) {
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3711,7 +3717,7 @@ __global__ __launch_bounds__(kBlock) void k_long_fill(uint64_t total, const EvRe
     const uint32_t m = (lo + hi) >> 1;
     if (win[m] <= i) lo = m; else hi = m;
   }
-  const uint32_t r0 = rec[head].rule & 0x7FFFFFFFu;
+  const uint32_t r0 = rec[head].rule_id();
   const int64_t Lim = rules[r0].hits;
   const bool first_win = lo == 0, cont = first_win && (fl & 1u);
   const int64_t h0 = first_win ? R.h0[r] : 0;
@@ -3723,7 +3729,7 @@ __global__ __launch_bounds__(kBlock) void k_long_fill(uint64_t total, const EvRe
   else ex = (h0 + e) % (Lim + 1) == 0;
   const uint8_t first_mt = first_win ? (uint8_t)((fl >> 1) & 3u) : (uint8_t)BJX_OUTSIDE_INTERVAL;
   const uint8_t mt = (!cont && i == a) ? first_mt : (uint8_t)BJX_INSIDE_INTERVAL;
-  const bool seen = (rec[i].rule >> 31) == 0;
+  const bool seen = rec[i].seen();
   out_sorted[i] = (uint8_t)(0x80 | (seen ? 1 : 0) | (mt << 1) | (ex ? 8 : 0));
   if (R.wcnt) atomicAdd(&R.wcnt[i], 1u);
 }
@@ -3804,17 +3810,19 @@ __global__ void k_dbg_mask_hash(uint64_t n, uint64_t *__restrict__ h, uint64_t m
   if (i < n) h[i] = (h[i] & mask) | 1;
 }
 
-// sorted outcomes -> event order
-__global__ void k_unsort(uint64_t n, const EvRec *__restrict__ rec, const uint8_t *__restrict__ in, uint8_t *__restrict__ out) {
+// sorted outcomes -> event order (evw: the sorted records' event index words,
+// `stride` words apart: either record form)
+__global__ void k_unsort(uint64_t n, const uint32_t *__restrict__ evw, uint32_t stride, const uint8_t *__restrict__ in,
+                         uint8_t *__restrict__ out) {
   const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (u < n) out[rec[u].ev] = in[u];
+  if (u < n) out[evw[u * stride]] = in[u];
 }
 
 // event index of each trip found in sorted order
-__global__ void k_trip_events(uint64_t n, const uint32_t *__restrict__ pos, const EvRec *__restrict__ rec,
+__global__ void k_trip_events(uint64_t n, const uint32_t *__restrict__ pos, const uint32_t *__restrict__ evw, uint32_t stride,
                               uint32_t *__restrict__ ev) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < n) ev[t] = rec[pos[t]].ev;
+  if (t < n) ev[t] = evw[(uint64_t)pos[t] * stride];
 }
 
 struct TripBit {
@@ -4577,7 +4585,9 @@ struct bjx_engine {
   bool res_written = false;  // the last match phase wrote the RuleResult arrays
   bool ev_arrays = false;    // ... and the per-event line / rule arrays (ev_el, ev_rule)
   DevBuf<uint32_t> res_rule, ev_el, ev_rule, ev_res, ev_st, ev_st2, ev_idx, ev_idx2, el_slot, coll, trip_idx;
-  DevBuf<EvRec> ev_rec, ev_rec2;
+  DevBuf<EvRec> ev_rec, ev_rec2;  // EvRec12 records when rec12 (the last rate-limit stage's form), from rec_base
+  bool rec12 = false;
+  int64_t rec_base = 0;
   DevBuf<uint64_t> trip_evr, trip_evr2;  // trips as (event << 32 | rule) (batches without per-event arrays)
   DevBuf<uint32_t> el_id;
   DevBuf<uint32_t> el_new;  // event lines with a new IP (k_ip_claim -> k_ip_commit)
@@ -5849,6 +5859,13 @@ void free_state(bjx_engine *e) {
   S = State{};
 }
 
+// the sorted records' event index words and their stride, in the form the
+// last rate-limit stage used
+static const uint32_t *ev_words(const bjx_engine *e) {
+  return reinterpret_cast<const uint32_t *>(e->ev_rec2.p) + (e->rec12 ? 2 : 3);
+}
+static uint32_t rec_stride(const bjx_engine *e) { return e->rec12 ? 3u : 4u; }
+
 void read_counters(bjx_engine *e) {
   HIP_OK(hipMemcpyAsync(e->host_counters, e->S.counters, 24, hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
@@ -6162,12 +6179,107 @@ static void rl_claims_lines(bjx_engine *e, const Bind &B, const EvSrc &E, const 
   }
 }
 
+// the event sort (state slot keys, records as values) and the Apply kernels,
+// for either record form
+template <typename Rec>
+static void rl_sort_apply(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t n_ev, const uint32_t *ev_el,
+                          const uint32_t *ev_rule, int64_t base) {
+  hipStream_t st = e->stream;
+  const Rec *rec2 = reinterpret_cast<const Rec *>(e->ev_rec2.p);
+  {
+    uint32_t *ki = e->ev_st.p, *ko = e->ev_st2.p;
+    Rec *vi = reinterpret_cast<Rec *>(e->ev_rec.p), *vo = reinterpret_cast<Rec *>(e->ev_rec2.p);
+    const int bits = std::max(1, bit_width(e->st_cap - 1));
+    cub_call(e, [&](void *tmp, size_t &bytes) {
+      return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)n_ev, 0, bits, st);
+    });
+  }
+  const uint64_t n_chunks = (n_ev + kApplyChunk - 1) / kApplyChunk;
+  const bool check = getenv("BJX_CHECK") != nullptr;
+  uint32_t *wcnt = nullptr;
+  if (check) {
+    HIP_OK(hipMemsetAsync(e->ev_out_s.p, 0, n_ev, st));
+    e->chk_w.ensure(2 * n_ev);
+    wcnt = e->chk_w.p;
+    HIP_OK(hipMemsetAsync(wcnt, 0, 2 * n_ev * 4, st));
+  }
+  e->long_heads.ensure(n_chunks + 1);
+  e->long_count.ensure(1);
+  HIP_OK(hipMemsetAsync(e->long_count.p, 0, 8, st));
+  hipLaunchKernelGGL(k_apply<Rec>, dim3((unsigned)n_chunks), dim3(kBlock), 0, st, n_ev, e->ev_st2.p, rec2, base, B.rules, e->S.st,
+                     e->ev_out_s.p, e->long_heads.p, e->long_count.p, wcnt);
+  HIP_OK(hipGetLastError());
+  unsigned long long n_long = 0;
+  HIP_OK(hipMemcpyAsync(&n_long, e->long_count.p, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  e->last_long_runs = n_long;
+  if (n_long) {
+    // runs crossing a k_apply chunk (hot keys): ends, a parallel regularity
+    // check, the window starts per run, then every record in parallel
+    LongRuns R;
+    e->lr_end.ensure(n_long); e->lr_len.ensure(n_long + 1); e->lr_off.ensure(n_long + 1); e->lr_t0.ensure(n_long);
+    e->lr_h0.ensure(n_long); e->lr_flags.ensure(n_long); e->lr_nwin.ensure(n_long);
+    R.head = e->long_heads.p; R.end = e->lr_end.p; R.off = e->lr_off.p; R.t0 = e->lr_t0.p; R.h0 = e->lr_h0.p;
+    R.flags = e->lr_flags.p; R.nwin = e->lr_nwin.p; R.n = n_long; R.win = nullptr; R.wcnt = wcnt;
+    HIP_OK(hipMemsetAsync(e->lr_len.p + n_long, 0, 8, st));
+    hipLaunchKernelGGL(k_long_ends<Rec>, dim3((unsigned)n_long), dim3(kBlock), 0, st, n_ev, e->ev_st2.p, rec2, base, e->S.st,
+                       B.rules, R, e->lr_len.p);
+    HIP_OK(hipGetLastError());
+    {
+      uint64_t *in = e->lr_len.p, *o = e->lr_off.p;
+      cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)(n_long + 1), st); });
+    }
+    uint64_t total = 0;
+    HIP_OK(hipMemcpyAsync(&total, e->lr_off.p + n_long, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    e->lr_win.ensure(total + 1);
+    R.win = e->lr_win.p;
+    hipLaunchKernelGGL(k_long_check<Rec>, dim3(grid_for(total)), dim3(kBlock), 0, st, total, rec2, base, B.rules, R);
+    hipLaunchKernelGGL(k_long_windows<Rec>, dim3((unsigned)n_long), dim3(kBlock), 0, st, e->ev_st2.p, rec2, base, B.rules,
+                       e->S.st, e->ev_out_s.p, R);
+    hipLaunchKernelGGL(k_long_fill<Rec>, dim3(grid_for(total)), dim3(kBlock), 0, st, total, rec2, B.rules, e->ev_out_s.p, R);
+    HIP_OK(hipGetLastError());
+  }
+  if (check) {
+    e->chk.ensure(16);
+    HIP_OK(hipMemsetAsync(e->chk.p, 0, 128, st));
+    uint32_t *pc = wcnt + n_ev;
+    hipLaunchKernelGGL(k_check_count, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev,
+                       ev_words(e), rec_stride(e), n_ev, pc, e->chk.p + 14);
+    hipLaunchKernelGGL(k_check_rl, dim3(grid_for(std::max<uint64_t>(E.n, n_ev))), dim3(kBlock), 0, st, E, n_ev, ev_el, ev_rule,
+                       e->el_slot.p, e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_out_s.p, wcnt, pc, e->chk.p);
+    HIP_OK(hipGetLastError());
+    unsigned long long c[16];
+    HIP_OK(hipMemcpyAsync(c, e->chk.p, 128, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (c[0] || c[3] || c[6] || c[8] || c[10] || c[12] || c[14]) {
+      char msg[768];
+      snprintf(msg, sizeof msg,
+               "BJX_CHECK: %llu event lines with a wrong IP id (first line %llu id %llu), %llu events in a wrong state slot "
+               "(first %llu slot %llu), %llu unwritten outcomes (first %llu), %llu outcomes not written exactly once (first "
+               "%llu), %llu seenIp=false outcomes that are not FirstTime (first %llu), %llu sorted positions whose event "
+               "index is not a permutation (first %llu; %llu out of range); epoch %u, %llu long runs, n_ev %llu",
+               c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9], c[10], c[11], c[12], c[13], c[14], e->epoch,
+               (unsigned long long)n_long, (unsigned long long)n_ev);
+      fprintf(stderr, "%s\n", msg);
+      throw BjxError(BJX_ERR_DEVICE, msg);
+    }
+  }
+}
+
 // Lp / offs (a local batch): claims per line from the match masks
-// (k_line_claim, k_line_st_claim) instead of per event (ev_el / ev_rule)
+// (k_line_claim, k_line_st_claim) instead of per event (ev_el / ev_rule).
+// rec_base (kNoRecBase: none): the events' timestamps are expected within
+// 2^43 ns of it either way, so the sort carries 12-B records (EvRec12).
+constexpr int64_t kNoRecBase = INT64_MIN;
 static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t n_el, uint64_t el_bytes, uint64_t n_ev,
-                             const uint32_t *ev_el, const uint32_t *ev_rule, const Lines *Lp = nullptr,
+                             const uint32_t *ev_el, const uint32_t *ev_rule, int64_t rec_base, const Lines *Lp = nullptr,
                              const uint64_t *offs = nullptr) {
   hipStream_t st = e->stream;
+  const bool force16 = getenv("BJX_REC16") != nullptr;  // test hook: the 16-B records throughout
+  bool use12 = !Lp && rec_base != kNoRecBase && B.n_rules < (1u << EvRec12::kRuleBits) && !force16;
+  if (use12) rec_base = (int64_t)((uint64_t)rec_base - (EvRec12::kSpan >> 1));
+  else rec_base = 0;
   if (E.n >= 0x7FFFFFFFull || n_ev >= 0xFFFFFFFFull) throw BjxError(BJX_ERR_ARG, "batch too large (2^31 lines / 2^32 events)");
   // the pre-lookup reads the IP table: done before any growth or claim
   if (e->pre_looked) HIP_OK(hipStreamWaitEvent(st, e->ev_lookup, 0));
@@ -6227,20 +6339,34 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
     for (int attempt = 0;; ++attempt) {
       read_counters(e);
       const uint64_t n_st = e->host_counters[2];
-      HIP_OK(hipMemsetAsync(e->S.counters + 6, 0, 2 * 8, st));
+      HIP_OK(hipMemsetAsync(e->S.counters + 6, 0, 3 * 8, st));
       HIP_OK(hipMemsetAsync(e->S.counters + kShardBase, 0, kClaimShards * 128, st));
       uint64_t budget = e->st_cap * 3 / 4 - n_st;
       const bool forced = e->dbg_budget && attempt == 0 && e->dbg_budget < budget;  // test hook
       if (forced) budget = e->dbg_budget;
-      hipLaunchKernelGGL(k_st_claim, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, E, n_ev, ev_el, ev_rule, e->el_slot.p,
-                         e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_rec.p, budget / kClaimShards);
+      if (use12)
+        hipLaunchKernelGGL(k_st_claim<EvRec12>, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, E, n_ev, ev_el, ev_rule,
+                           e->el_slot.p, e->el_id.p, B.rules, e->S, e->ev_st.p, reinterpret_cast<EvRec12 *>(e->ev_rec.p),
+                           rec_base, budget / kClaimShards);
+      else
+        hipLaunchKernelGGL(k_st_claim<EvRec>, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, E, n_ev, ev_el, ev_rule,
+                           e->el_slot.p, e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_rec.p, rec_base, budget / kClaimShards);
       HIP_OK(hipGetLastError());
-      uint64_t ovf = 0;
-      HIP_OK(hipMemcpyAsync(&ovf, e->S.counters + 7, 8, hipMemcpyDeviceToHost, st));
+      uint64_t ovf[2] = {0, 0};  // state table overflow, a timestamp outside the 12-B records' span
+      HIP_OK(hipMemcpyAsync(ovf, e->S.counters + 7, 16, hipMemcpyDeviceToHost, st));
       HIP_OK(hipStreamSynchronize(st));
-      if (!ovf) {
+      if (!ovf[0]) {
         hipLaunchKernelGGL(k_fold_claims, dim3(1), dim3(kClaimShards), 0, st, e->S);
         HIP_OK(hipGetLastError());
+        if (use12 && ovf[1]) {
+          // the same claims again (every key is in the table now, so nothing
+          // is claimed twice), writing 16-B records
+          use12 = false;
+          rec_base = 0;
+          hipLaunchKernelGGL(k_st_claim<EvRec>, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, E, n_ev, ev_el, ev_rule,
+                             e->el_slot.p, e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_rec.p, rec_base, budget / kClaimShards);
+          HIP_OK(hipGetLastError());
+        }
         break;
       }
       // more new (ip, rule name) states than the table had room for: undo this
@@ -6256,85 +6382,10 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
     }
   }
   mark(e, 6);
-  {
-    uint32_t *ki = e->ev_st.p, *ko = e->ev_st2.p;
-    EvRec *vi = e->ev_rec.p, *vo = e->ev_rec2.p;
-    const int bits = std::max(1, bit_width(e->st_cap - 1));
-    cub_call(e, [&](void *tmp, size_t &bytes) {
-      return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)n_ev, 0, bits, st);
-    });
-  }
-  const uint64_t n_chunks = (n_ev + kApplyChunk - 1) / kApplyChunk;
-  const bool check = getenv("BJX_CHECK") != nullptr;
-  uint32_t *wcnt = nullptr;
-  if (check) {
-    HIP_OK(hipMemsetAsync(e->ev_out_s.p, 0, n_ev, st));
-    e->chk_w.ensure(2 * n_ev);
-    wcnt = e->chk_w.p;
-    HIP_OK(hipMemsetAsync(wcnt, 0, 2 * n_ev * 4, st));
-  }
-  e->long_heads.ensure(n_chunks + 1);
-  e->long_count.ensure(1);
-  HIP_OK(hipMemsetAsync(e->long_count.p, 0, 8, st));
-  hipLaunchKernelGGL(k_apply, dim3((unsigned)n_chunks), dim3(kBlock), 0, st, n_ev, e->ev_st2.p, e->ev_rec2.p, B.rules, e->S.st,
-                     e->ev_out_s.p, e->long_heads.p, e->long_count.p, wcnt);
-  HIP_OK(hipGetLastError());
-  unsigned long long n_long = 0;
-  HIP_OK(hipMemcpyAsync(&n_long, e->long_count.p, 8, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
-  e->last_long_runs = n_long;
-  if (n_long) {
-    // runs crossing a k_apply chunk (hot keys): ends, a parallel regularity
-    // check, the window starts per run, then every record in parallel
-    LongRuns R;
-    e->lr_end.ensure(n_long); e->lr_len.ensure(n_long + 1); e->lr_off.ensure(n_long + 1); e->lr_t0.ensure(n_long);
-    e->lr_h0.ensure(n_long); e->lr_flags.ensure(n_long); e->lr_nwin.ensure(n_long);
-    R.head = e->long_heads.p; R.end = e->lr_end.p; R.off = e->lr_off.p; R.t0 = e->lr_t0.p; R.h0 = e->lr_h0.p;
-    R.flags = e->lr_flags.p; R.nwin = e->lr_nwin.p; R.n = n_long; R.win = nullptr; R.wcnt = wcnt;
-    HIP_OK(hipMemsetAsync(e->lr_len.p + n_long, 0, 8, st));
-    hipLaunchKernelGGL(k_long_ends, dim3((unsigned)n_long), dim3(kBlock), 0, st, n_ev, e->ev_st2.p, e->ev_rec2.p, e->S.st,
-                       B.rules, R, e->lr_len.p);
-    HIP_OK(hipGetLastError());
-    {
-      uint64_t *in = e->lr_len.p, *o = e->lr_off.p;
-      cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)(n_long + 1), st); });
-    }
-    uint64_t total = 0;
-    HIP_OK(hipMemcpyAsync(&total, e->lr_off.p + n_long, 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    e->lr_win.ensure(total + 1);
-    R.win = e->lr_win.p;
-    hipLaunchKernelGGL(k_long_check, dim3(grid_for(total)), dim3(kBlock), 0, st, total, e->ev_rec2.p, B.rules, R);
-    hipLaunchKernelGGL(k_long_windows, dim3((unsigned)n_long), dim3(kBlock), 0, st, e->ev_st2.p, e->ev_rec2.p, B.rules, e->S.st,
-                       e->ev_out_s.p, R);
-    hipLaunchKernelGGL(k_long_fill, dim3(grid_for(total)), dim3(kBlock), 0, st, total, e->ev_rec2.p, B.rules, e->ev_out_s.p, R);
-    HIP_OK(hipGetLastError());
-  }
-  if (check) {
-    e->chk.ensure(16);
-    HIP_OK(hipMemsetAsync(e->chk.p, 0, 128, st));
-    uint32_t *pc = wcnt + n_ev;
-    hipLaunchKernelGGL(k_check_count, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev,
-                       reinterpret_cast<const uint32_t *>(e->ev_rec2.p) + 3, 4u, n_ev, pc, e->chk.p + 14);
-    hipLaunchKernelGGL(k_check_rl, dim3(grid_for(std::max<uint64_t>(E.n, n_ev))), dim3(kBlock), 0, st, E, n_ev, ev_el, ev_rule,
-                       e->el_slot.p, e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_out_s.p, wcnt, pc, e->chk.p);
-    HIP_OK(hipGetLastError());
-    unsigned long long c[16];
-    HIP_OK(hipMemcpyAsync(c, e->chk.p, 128, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    if (c[0] || c[3] || c[6] || c[8] || c[10] || c[12] || c[14]) {
-      char msg[768];
-      snprintf(msg, sizeof msg,
-               "BJX_CHECK: %llu event lines with a wrong IP id (first line %llu id %llu), %llu events in a wrong state slot "
-               "(first %llu slot %llu), %llu unwritten outcomes (first %llu), %llu outcomes not written exactly once (first "
-               "%llu), %llu seenIp=false outcomes that are not FirstTime (first %llu), %llu sorted positions whose event "
-               "index is not a permutation (first %llu; %llu out of range); epoch %u, %llu long runs, n_ev %llu",
-               c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9], c[10], c[11], c[12], c[13], c[14], e->epoch,
-               (unsigned long long)n_long, (unsigned long long)n_ev);
-      fprintf(stderr, "%s\n", msg);
-      throw BjxError(BJX_ERR_DEVICE, msg);
-    }
-  }
+  e->rec12 = use12;
+  e->rec_base = rec_base;
+  if (use12) rl_sort_apply<EvRec12>(e, B, E, n_ev, ev_el, ev_rule, rec_base);
+  else rl_sort_apply<EvRec>(e, B, E, n_ev, ev_el, ev_rule, rec_base);
 }
 
 // k_nfa_wide over jobs [j0, j1): the state in LDS when it fits 64 KB, else
@@ -7089,8 +7140,8 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
         HIP_OK(hipGetLastError());
       } else {
       if (sorted)
-        hipLaunchKernelGGL(k_trip_events, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_idx.p, e->ev_rec2.p,
-                           e->trip_ev.p);
+        hipLaunchKernelGGL(k_trip_events, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_idx.p, ev_words(e),
+                           rec_stride(e), e->trip_ev.p);
       uint32_t *ki = sorted ? e->trip_ev.p : e->trip_idx.p, *ko = e->trip_ev2.p;
       const int bits = std::max(1, bit_width(n_ev));
       cub_call(e, [&](void *tmp, size_t &bytes) {
@@ -7127,7 +7178,8 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
     }
     if (flags & BJX_COPY_RESULTS) {
       if (sorted)
-        hipLaunchKernelGGL(k_unsort, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_rec2.p, e->ev_out_s.p, e->ev_out.p);
+        hipLaunchKernelGGL(k_unsort, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, ev_words(e), rec_stride(e), e->ev_out_s.p,
+                           e->ev_out.p);
       hipLaunchKernelGGL(k_scatter_rl, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_res.p, e->ev_out.p, e->rl_out.p);
       HIP_OK(hipGetLastError());
       if (getenv("BJX_CHECK")) {  // every event names its own RuleResult (ev_res injective)
@@ -7200,9 +7252,11 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
   if (!match_phase(e, rs, bytes, n, now_ns, flags, out, false)) return;
   if (e->bc.n_ev) {
     if (fused_claims())
-      rate_limit_stage(e, e->bind, local_evsrc(e), e->bc.n_el, e->bc.el_bytes, e->bc.n_ev, nullptr, nullptr, &e->bc.L, e->l_offs.p);
+      rate_limit_stage(e, e->bind, local_evsrc(e), e->bc.n_el, e->bc.el_bytes, e->bc.n_ev, nullptr, nullptr, kNoRecBase, &e->bc.L,
+                       e->l_offs.p);
     else
-      rate_limit_stage(e, e->bind, local_evsrc(e), e->bc.n_el, e->bc.el_bytes, e->bc.n_ev, e->ev_el.p, e->ev_rule.p);
+      rate_limit_stage(e, e->bind, local_evsrc(e), e->bc.n_el, e->bc.el_bytes, e->bc.n_ev, e->ev_el.p, e->ev_rule.p,
+                       e->bc.now_ns);
   }
   finish_phase(e, flags, out, true);
 }
@@ -7362,8 +7416,11 @@ extern "C" int bjx_apply_events(bjx_engine *e, const bjx_ruleset *rs, const bjx_
     EvSrc E;
     E.bytes = d_bytes; E.nl = nullptr; E.ip_off = nullptr; E.ip_pos = e->rx_pos.p; E.ip_len = e->rx_len.p;
     E.ip_hash = e->rx_hash.p; E.ts = e->rx_ts.p; E.counts = nullptr; E.ip16 = e->rx_ip16.p; E.n = n_lines;
-    rate_limit_stage(e, B, E, n_lines, n_bytes, n_ev, e->rx_ev_el.p, d_events);
-    hipLaunchKernelGGL(k_unsort, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_rec2.p, e->ev_out_s.p, d_out);
+    // the clock of this engine's last match phase (the node's batch) as the
+    // 12-B records' base; a stale or foreign one only costs the 16-B re-claim
+    rate_limit_stage(e, B, E, n_lines, n_bytes, n_ev, e->rx_ev_el.p, d_events, e->bc.now_ns ? e->bc.now_ns : kNoRecBase);
+    hipLaunchKernelGGL(k_unsort, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, ev_words(e), rec_stride(e), e->ev_out_s.p,
+                       d_out);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(st));
     return BJX_OK;

@@ -727,3 +727,21 @@ def test_compact_trips_match_full(engine):
     assert got == want
     for off, _ in got[:50]:  # the offset starts a line
         assert off == 0 or data[off - 1:off] == b"\n"
+
+
+@pytest.mark.parametrize("rec16", [0, 1])
+def test_event_record_forms(engine, rec16, monkeypatch):
+    """The event sort carries 12-B records (engine_types.h EvRec12: timestamps
+    within 2^43 ns of the batch's clock); a batch whose events lie 3 h past
+    its clock is claimed again and sorted in the 16-B form, and BJX_REC16=1
+    forces that form throughout.  Results stay bit-exact against the oracle
+    through state carried across the batches."""
+    if rec16:
+        monkeypatch.setenv("BJX_REC16", "1")
+    w = W.scaled(W.CFG3, 40_000, n_ips=2_000)
+    pair = Pair(w.rules_yaml, engine)
+    pair.feed(w.host_lines(0, 10_000), w.now_ns(0, 10_000))
+    pair.feed(w.host_lines(10_000, 10_000), w.now_ns(10_000, 10_000) - 3 * 3600 * S)
+    pair.feed(w.host_lines(20_000, 10_000), w.now_ns(20_000, 10_000), want_results=False)
+    pair.feed(w.host_lines(30_000, 10_000), w.now_ns(30_000, 10_000) - 3 * 3600 * S, want_results=False)
+    pair.compare_state()
