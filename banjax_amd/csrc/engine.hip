@@ -4297,11 +4297,12 @@ struct HostBuf {
   size_t n = 0, cap = 0;
   void resize(size_t want) {
     if (want > cap) {
+      // geometric growth with headroom: a pinned (re)allocation stalls the
+      // batch for ~0.1 ms/MB, and per-batch counts (trips) drift upwards
+      const size_t c = std::max<size_t>({want * 2, cap * 2, 1u << 16});
       if (p) (void)hipHostFree(p);
       p = nullptr;
       cap = 0;
-      // geometric growth: a pinned (re)allocation stalls the batch for ~0.1 ms/MB
-      const size_t c = want < 1024 ? 1024 : std::max(want + want / 2, 2 * cap);
       HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&p), c * sizeof(T), hipHostMallocDefault));
       cap = c;
     }
