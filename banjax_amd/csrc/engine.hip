@@ -658,15 +658,18 @@ struct ScanArgs {
   unsigned long long *stats;  // [0] bitset hits, [1] recorded literal hits
   uint32_t shared_bytes;      // per-wave LDS regions start here
   uint32_t debug_skip;        // timing experiments only (BJX_DEBUG_SKIP, results invalid): 1 gram phase, 2 candidates,
-                              // 4 literal checks of gram table hits, 8 gram table probes
+                              // 4 literal checks of gram table hits, 8 gram table probes; line index: 0x10000 no
+                              // group_wait, 0x20000 no count-ahead reads
   uint32_t hdr;               // 1: parse the headers of the lines that start in each tile (scan_header)
   int64_t now_ns;
-  // decoupled look-back (tstat != nullptr): the newlines before each tile are
-  // found here instead of by the separate count pass (tile_base unused);
-  // n_lines is then the capacity of the per-line arrays, *lines_out gets the
-  // batch's line count and *lb_abort is raised by a wave that waited too long
-  // (the host then runs the two-pass way)
+  // in-kernel line index (tstat != nullptr): the newlines before each tile
+  // are found here instead of by the separate count pass (tile_base unused;
+  // see group_wait); n_lines is then the capacity of the per-line arrays,
+  // *lines_out gets the batch's line count and *lb_abort is raised by a wave
+  // that waited too long (the host then runs the two-pass way).  tstat: 4
+  // kRing iteration slots x gridDim.x block words, zeroed by the host.
   unsigned long long *tstat;
+  unsigned long long *lbprof;  // BJX_LB_PROF: clocks in group_wait, count-ahead, publish, the loop (timing aid)
   unsigned long long *lines_out;
   unsigned long long *lb_abort;
 };
@@ -1423,63 +1426,186 @@ __device__ __forceinline__ void scan_header(const Bind &B, const Tabs &TB, const
 }
 
 
-// Decoupled look-back over the wave tiles (ScanArgs::tstat, one word per
-// tile: flag << 62 | newlines in the tile << 48 | newlines up to and
-// including it; flag 1 = the tile's own count, 2 = the inclusive count too).
-// A wave publishes its tile's count as soon as it has it, then reads the
-// words of the 64 tiles before it at once: the nearest one with an inclusive
-// count ends the look-back, the counts of those in between are added; a tile
-// whose word is still empty is waited for.  Tiles go to waves grid-stride
-// from a grid that is resident as a whole (one block per CU), every wave
-// takes its tiles in order, so the lowest unfinished tile never waits.
-// Returns false if the wait ran past kLookbackSpins (*lb_abort raised).
+// In-kernel line index (ScanArgs::tstat): counted ahead, summed per block.
+// All of its atomics are relaxed: the grid words carry their data in the word
+// itself, and LDS operations of a wave complete in order (compiler fences keep
+// that order), so no release / acquire (an agent-scope release writes back the
+// XCD's L2) is needed.
+// The grid (one block per CU, resident as a whole) takes the tiles in
+// iterations: iteration r gives block b the 16 consecutive tiles
+// r * nw + 16 b + wave.  Each wave counts the newlines of its tile kAhead
+// iterations ahead (an extra 64 B read per lane) and adds the count to its
+// block's sum in LDS; the block's last wave to arrive publishes the sum (and
+// its last tile's count) as one tagged word per (iteration slot, block), then
+// reads the grid's words of the iteration before (group_read: the newlines of
+// the blocks before this one and of the whole iteration).  Each wave keeps
+// its running base (the newlines of the iterations before) and finds the rest
+// in LDS when it gets to the iteration (group_wait).  Nothing chains from
+// tile to tile, unlike the per-tile decoupled look-back it replaces
+// (profiles/r04_t3).  Still slower than the two-pass count at cfg3
+// (profiles/r04_lbp, BJX_LB_PROF=1: 23 % of wave clocks waiting for the
+// grid's slowest waves, 10 % counting ahead; k_scan 25.8 ms against 3.0 +
+// 12.9 ms), so it stays opt-in (BJX_LOOKBACK=1).
+constexpr uint32_t kAhead = 6;   // iterations counted ahead
+constexpr uint32_t kRing = 16;   // iteration slots (>= 2 kAhead + 2: a block is at most kAhead iterations ahead of any other)
+static_assert((kRing & (kRing - 1)) == 0 && kRing >= 2 * kAhead + 2, "ring of iteration slots");
+struct ScanGroup {
+  uint32_t cnt[kRing][kScanWaves];  // newlines of each wave's tile, by iteration slot
+  uint32_t sum[kRing], arr[kRing];  // block sum / arrivals of the slot being counted
+  uint32_t done[kRing];             // ready tag (iteration + 1) per slot
+  uint32_t pre[kRing];              // newlines of the iteration's tiles before the block's
+  uint32_t tot[kRing];              // newlines of the iteration
+  uint32_t prevb[kRing];            // newlines of the previous block's last tile
+  uint32_t lastg[kRing];            // newlines of the iteration's last tile
+  unsigned long long wbase[kScanWaves];  // per wave: newlines before its current iteration
+  unsigned long long wtb[kScanWaves];    // per wave: newlines before its tile (kept out of VGPRs)
+  uint32_t wprev[kScanWaves];            // and newlines in the tile before it
+};
+constexpr uint32_t kScanGroupLds = (sizeof(ScanGroup) + 15) & ~15u;
+static_assert(kWaveLds % 16 == 0, "ScanGroup follows the wave regions 16-B aligned");
 constexpr uint32_t kLookbackSpins = 1u << 22;
-constexpr uint64_t kTileIncl = (1ull << 48) - 1;
-__device__ __forceinline__ bool tile_lookback(const ScanArgs &A, uint64_t t, uint32_t tot, uint32_t lane, uint64_t &prefix,
-                                              uint32_t &prev_cnt) {
-  if (lane == 0)
-    __hip_atomic_store(&A.tstat[t], (1ull << 62) | ((unsigned long long)tot << 48), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  uint64_t excl = 0;
-  int64_t base = (int64_t)t - 1;
-  uint32_t spins = 0;
-  bool first = true;
-  prev_cnt = 0;
-  while (base >= 0) {
-    const int64_t idx = base - (int64_t)lane;
-    const uint64_t v = idx >= 0 ? __hip_atomic_load(&A.tstat[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (2ull << 62);
-    const uint32_t fl = (uint32_t)(v >> 62);
-    const uint64_t incm = __ballot(fl == 2), miss = __ballot(fl == 0);
-    const uint32_t fi = incm ? (uint32_t)__ffsll((unsigned long long)incm) - 1 : 64u;
-    const uint64_t need = fi >= 63 ? ~0ull : ((2ull << fi) - 1ull);  // lanes 0 .. fi
-    if (miss & need) {
+constexpr uint32_t kGroupAbort = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t wave_total(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(v), 63);
+}
+
+// newlines in wave tile tt (0 past the batch), every lane reading 64 B
+__device__ __forceinline__ uint32_t tile_nl_count(const ScanArgs &A, uint64_t tt, uint32_t lane) {
+  uint32_t c = 0;
+  if (tt < A.n_tiles) {
+    const uint64_t base = tt * kWT + lane * 64u;
+    if (base + 64 <= A.n) {
+      const uint4 *src = reinterpret_cast<const uint4 *>(A.buf + base);
+      uint4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = src[k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        c += __popc(nl_mask_word(v[k].x)) + __popc(nl_mask_word(v[k].y)) + __popc(nl_mask_word(v[k].z)) +
+             __popc(nl_mask_word(v[k].w));
+    } else {
+      for (uint64_t q = base; q < A.n && q < base + 64; ++q) c += A.buf[q] == '\n' ? 1u : 0u;
+    }
+  }
+  return wave_total(c);
+}
+
+// iteration r's grid words -> G (slot r % kRing): the newlines of the blocks
+// before this one, of the whole iteration, and the last tile counts this
+// block's first wave needs; run by one wave of the block (group_publish).  One
+// round trip per poll: every lane loads its share of the words at once.
+// Iterations are read independently (the running base is kept per wave,
+// ScanGroup::wbase).  False if the wait ran past kLookbackSpins or another
+// wave gave up (*lb_abort).
+constexpr uint32_t kReadPer = 4;  // words per lane: grids of up to 256 blocks in one load round
+__device__ __forceinline__ bool group_read(const ScanArgs &A, ScanGroup &G, uint32_t r, uint32_t lane) {
+  const uint32_t s = r & (kRing - 1), tg = r + 1u;
+  const uint32_t b = blockIdx.x, ng = gridDim.x;
+  uint32_t pre = 0, tot = 0, prevb = 0, lastg = 0, spins = 0;
+  for (uint32_t c0 = 0; c0 < ng; c0 += 64 * kReadPer) {
+    unsigned long long v[kReadPer];
+    for (;;) {
+#pragma unroll
+      for (uint32_t k = 0; k < kReadPer; ++k) {
+        const uint32_t idx = c0 + k * 64 + lane;
+        v[k] = idx < ng ? __hip_atomic_load(&A.tstat[(uint64_t)s * ng + idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : ((unsigned long long)tg << 32);
+      }
+      bool ok = true;
+#pragma unroll
+      for (uint32_t k = 0; k < kReadPer; ++k) ok = ok && (uint32_t)(v[k] >> 32) == tg;
+      if (__ballot(!ok) == 0) break;
       if (++spins > kLookbackSpins || __hip_atomic_load(A.lb_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        if (lane == 0) atomicOr(A.lb_abort, 1ull);
+        if (lane == 0) {
+          atomicOr(A.lb_abort, 1ull);
+          __hip_atomic_store(&G.done[s], kGroupAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         return false;
       }
-      __builtin_amdgcn_s_sleep(1);
-      continue;
+      __builtin_amdgcn_s_sleep(8);
     }
-    if (first) {
-      prev_cnt = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 48), 0) & 0x3FFFu;
-      first = false;
-    }
-    uint64_t c = (uint32_t)lane < fi ? ((v >> 48) & 0x3FFFull) : (uint32_t)lane == fi ? (v & kTileIncl) : 0ull;
+    uint32_t ct = 0, cp = 0;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-    excl += c;
-    if (fi < 64) break;
-    base -= 64;
+    for (uint32_t k = 0; k < kReadPer; ++k) {
+      const uint32_t idx = c0 + k * 64 + lane;
+      const uint32_t c = idx < ng ? (uint32_t)(v[k] & 0x1FFFFu) : 0u;
+      const uint32_t l = (uint32_t)(v[k] >> 17) & 0x1FFFu;
+      ct += c;
+      cp += idx < b ? c : 0u;
+      if (idx + 1 == b) prevb = l;
+      if (idx + 1 == ng) lastg = l;
+    }
+    tot += wave_total(ct);
+    pre += wave_total(cp);
   }
-  prefix = excl;
+  // prevb / lastg sit in one lane each
+  prevb = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_total(prevb));
+  lastg = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_total(lastg));
   if (lane == 0) {
-    __hip_atomic_store(&A.tstat[t], (2ull << 62) | ((unsigned long long)tot << 48) | (excl + tot), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    if (t + 1 == A.n_tiles) *A.lines_out = excl + tot;
+    G.pre[s] = pre;
+    G.tot[s] = tot;
+    G.prevb[s] = prevb;
+    G.lastg[s] = lastg;
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __hip_atomic_store(&G.done[s], tg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   return true;
 }
 
-template <bool IMG_LDS>
+// this wave's count for iteration r into its block's slot.  The last of the
+// block's waves to arrive publishes the block word, then reads iteration
+// r - 1 (whose words went out about an iteration earlier), and r itself if it
+// is the last iteration, so the block's waves find their tb ready some
+// kAhead iterations before they need it (group_wait).
+__device__ __forceinline__ bool group_publish(const ScanArgs &A, ScanGroup &G, uint32_t r, uint32_t n_iter, uint32_t c,
+                                              uint32_t wave, uint32_t lane) {
+  const uint32_t s = r & (kRing - 1);
+  uint32_t last = 0;
+  if (lane == 0) {
+    __hip_atomic_store(&G.cnt[s][wave], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(&G.sum[s], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const uint32_t old = __hip_atomic_fetch_add(&G.arr[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (old == kScanWaves - 1) {
+      last = 1;
+      const uint32_t tot = __hip_atomic_load(&G.sum[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const uint32_t lc = __hip_atomic_load(&G.cnt[s][kScanWaves - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // reset for iteration r + kRing before the word goes out (a wave that
+      // sees the word sees the reset)
+      __hip_atomic_store(&G.sum[s], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_store(&G.arr[s], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the resets are done
+      __hip_atomic_store(&A.tstat[(uint64_t)s * gridDim.x + blockIdx.x],
+                         ((unsigned long long)(r + 1u) << 32) | ((unsigned long long)lc << 17) | tot, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (!__builtin_amdgcn_readfirstlane((int)last)) return true;
+  if (r >= 1 && !group_read(A, G, r - 1, lane)) return false;
+  if (r + 1 == n_iter && !group_read(A, G, r, lane)) return false;
+  return true;
+}
+
+// waits until iteration r's tb / prev are in G; false if a wave gave up
+__device__ __forceinline__ bool group_wait(const ScanArgs &A, ScanGroup &G, uint32_t r) {
+  const uint32_t s = r & (kRing - 1), tg = r + 1u;
+  uint32_t spins = 0;
+  for (;;) {
+    const uint32_t d = __hip_atomic_load(&G.done[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (d == tg) {
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      return true;
+    }
+    if (d == kGroupAbort || ++spins > kLookbackSpins ||
+        __hip_atomic_load(A.lb_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// LB: the in-kernel line index (group_wait) instead of the count pass's tile_base
+template <bool IMG_LDS, bool LB>
 __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_scan(Bind B, ScanArgs A) {
   // ---- block-shared tables (read-only after this barrier): gram bitset, then
   // the lookup image when it fits
@@ -1490,11 +1616,14 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
   if (IMG_LDS)
     for (uint32_t i = threadIdx.x; i < B.img_bytes / 16; i += blockDim.x)
       reinterpret_cast<uint4 *>(s_img)[i] = reinterpret_cast<const uint4 *>(B.img)[i];
+  for (uint32_t i = threadIdx.x; i < kScanGroupLds / 4; i += blockDim.x)
+    reinterpret_cast<uint32_t *>(s_dyn + A.shared_bytes + kScanWaves * kWaveLds)[i] = 0;
   __syncthreads();
   const Tabs TB = make_tabs(IMG_LDS ? s_img : B.img, B.il);
   const uint32_t *gt = TB.gt, *ge = TB.ge;
 
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  ScanGroup &G = *reinterpret_cast<ScanGroup *>(s_dyn + A.shared_bytes + kScanWaves * kWaveLds);
   uint8_t *T = s_dyn + A.shared_bytes + wave * kWaveLds;
   uint16_t *ls = reinterpret_cast<uint16_t *>(T + kTileLds);
   uint16_t *le = ls + kLineCap;
@@ -1528,8 +1657,40 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
       for (int k = 0; k < 4; ++k) q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
     }
   };
+  const uint64_t n_iter = (A.n_tiles + nw - 1) / nw;
+  uint64_t pw = 0, pc = 0, pp = 0;
+  const uint64_t p_start = __builtin_amdgcn_s_memtime();
+  if (LB)  // the counts of iterations 0 .. kAhead - 1 (group_wait)
+    for (uint32_t q = 0; q < kAhead && q < n_iter; ++q)
+      if (!group_publish(A, G, q, (uint32_t)n_iter, tile_nl_count(A, t + (uint64_t)q * nw, lane), wave, lane)) return;
   if (t < A.n_tiles) load_tile(t);
-  for (; t < A.n_tiles; t += nw) {
+  for (uint32_t r = 0; r < n_iter; ++r, t += nw) {
+    if (LB) {
+      const uint64_t c0 = __builtin_amdgcn_s_memtime();
+      if (!(A.debug_skip & 0x10000) && !group_wait(A, G, r)) return;  // the host redoes the batch the two-pass way
+      const uint64_t c1 = __builtin_amdgcn_s_memtime();
+      pw += c1 - c0;
+      const uint32_t s = r & (kRing - 1);
+      if (lane == 0) {
+        const uint64_t base = G.wbase[wave];
+        uint64_t x = base + G.pre[s];
+        for (uint32_t w2 = 0; w2 < wave; ++w2) x += G.cnt[s][w2];
+        G.wtb[wave] = x;
+        G.wprev[wave] = wave ? G.cnt[s][wave - 1] : blockIdx.x ? G.prevb[s] : r ? G.lastg[(r - 1) & (kRing - 1)] : 0u;
+        G.wbase[wave] = base + G.tot[s];
+      }
+      // read before this wave's count for r + kAhead goes out (group_publish)
+      if (r + kAhead < n_iter) {
+        const uint64_t c2 = __builtin_amdgcn_s_memtime();
+        const uint32_t cnt_ahead = (A.debug_skip & 0x20000) ? 0u : tile_nl_count(A, t + (uint64_t)kAhead * nw, lane);
+        const uint64_t c3 = __builtin_amdgcn_s_memtime();
+        if (!group_publish(A, G, r + kAhead, (uint32_t)n_iter, cnt_ahead, wave, lane)) return;
+        const uint64_t c4 = __builtin_amdgcn_s_memtime();
+        pc += c3 - c2;
+        pp += c4 - c3;
+      }
+    }
+    if (t >= A.n_tiles) continue;
     const uint64_t ts0 = t * kWT;
     uint32_t w[16];
 #pragma unroll
@@ -1571,8 +1732,10 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
     pre -= cnt;
     uint64_t tb;
     uint32_t prev_cnt = 0;
-    if (A.tstat) {
-      if (!tile_lookback(A, t, tot, lane, tb, prev_cnt)) return;  // the host redoes the batch the two-pass way
+    if (LB) {
+      tb = G.wtb[wave];
+      prev_cnt = G.wprev[wave];
+      if (t + 1 == A.n_tiles && lane == 0) *A.lines_out = tb + tot;
     } else {
       tb = A.tile_base[t];
       prev_cnt = t ? (uint32_t)(tb - A.tile_base[t - 1]) : 0u;
@@ -1809,6 +1972,12 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
     n_probe += __shfl_xor(n_probe, o);
     n_hit += __shfl_xor(n_hit, o);
     n_gram += __shfl_xor(n_gram, o);
+  }
+  if (LB && A.lbprof && lane == 0) {
+    atomicAdd(&A.lbprof[0], (unsigned long long)pw);
+    atomicAdd(&A.lbprof[1], (unsigned long long)pc);
+    atomicAdd(&A.lbprof[2], (unsigned long long)pp);
+    atomicAdd(&A.lbprof[3], (unsigned long long)(__builtin_amdgcn_s_memtime() - p_start));
   }
   if (lane == 0 && (n_probe | n_hit)) {
     atomicAdd(&A.stats[0], (unsigned long long)n_probe);
@@ -4566,16 +4735,16 @@ struct bjx_engine {
   DevBuf<int64_t> lr_t0, lr_h0;
   DevBuf<uint32_t> lr_flags, lr_nwin;
   DevBuf<unsigned long long> long_count;
-  uint32_t scan_lds[2] = {0, 0};
+  uint32_t scan_lds[2][2] = {{0, 0}, {0, 0}};
   bool lines_attr = false;
-  // k_scan's newline look-back (tile_lookback): lines per byte of the batches
+  // k_scan's in-kernel line index (group_wait): lines per byte of the batches
   // so far (sizes the per-line arrays),
   // off for an engine that shares its GPU with another one that may run
   // concurrently (bjx_engine_set_scan_lookback), batches done again two-pass
   double lines_per_byte = 1.0 / 128;  // access-log lines are rarely shorter; shorter ones redo the batch two-pass
   bool scan_lookback = getenv("BJX_LOOKBACK") && atoi(getenv("BJX_LOOKBACK")) == 1;
   uint64_t lb_fallbacks = 0;
-  DevBuf<unsigned long long> tstat;
+  DevBuf<unsigned long long> tstat, lbprof;
   DevBuf<CandMeta> l_ccnt;
   DevBuf<uint64_t> l_cfirst;  // Lines::cand_first
   unsigned long long scan_stats[6] = {0, 0, 0, 0, 0, 0};
@@ -6502,11 +6671,10 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   // ---- line framing, two-pass by default: pass A counts the '\n' of each
   // 4 KB wave tile and an exclusive scan gives every tile its first line
   // index.  With the look-back (bjx_engine_set_scan_lookback, BJX_LOOKBACK=1)
-  // k_scan counts the newlines before each tile itself (tile_lookback), the
+  // k_scan counts the newlines before each tile itself (group_wait), the
   // per-line arrays sized from the lines per byte seen so far; a batch with
-  // more lines than that, or a look-back that waited too long, is done again
-  // two-pass.  Off by default: measured slower at cfg3 (profiles/r04_t3:
-  // k_scan 21.8 ms with it against 3.0 + 12.7 ms).
+  // more lines than that, or a wait that ran too long, is done again
+  // two-pass.
   const uint64_t n_tiles = (n + kWT - 1) / kWT;
   e->tile_counts.ensure(n_tiles);
   e->tile_base.ensure(n_tiles + 1);
@@ -6572,9 +6740,13 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     static const bool scan_hdr_env = getenv("BJX_SCAN_HEADER") && atoi(getenv("BJX_SCAN_HEADER")) == 1;
     scan_hdr = scan_hdr_env;
     if (scan_hdr) HIP_OK(hipMemsetAsync(e->l_flags.p, kLineTodo, cap, st));
+    int n_cu_scan = 0;
+    HIP_OK(hipDeviceGetAttribute(&n_cu_scan, hipDeviceAttributeMultiprocessorCount, e->device));
+    // one block (16 waves) per CU: the whole grid resident, as the in-kernel line index needs
+    const unsigned scan_grid = (unsigned)std::min<uint64_t>((n_tiles + kScanWaves - 1) / kScanWaves, (uint64_t)std::max(1, n_cu_scan));
     if (lb) {
-      e->tstat.ensure(n_tiles);
-      HIP_OK(hipMemsetAsync(e->tstat.p, 0, n_tiles * 8, st));
+      e->tstat.ensure((uint64_t)kRing * scan_grid);
+      HIP_OK(hipMemsetAsync(e->tstat.p, 0, (uint64_t)kRing * scan_grid * 8, st));
     }
     mark(e, 1);
 
@@ -6583,6 +6755,13 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       ScanArgs A;
       A.buf = buf; A.n = n; A.n_tiles = n_tiles; A.n_lines = cap; A.tile_base = e->tile_base.p; A.nl = e->nl.p;
       A.L = L; A.stats = e->scalars.p + 8;
+      static const bool lbprof = getenv("BJX_LB_PROF") != nullptr;
+      A.lbprof = nullptr;
+      if (lbprof && lb) {
+        e->lbprof.ensure(4);
+        HIP_OK(hipMemsetAsync(e->lbprof.p, 0, 32, st));
+        A.lbprof = e->lbprof.p;
+      }
       A.debug_skip = getenv("BJX_DEBUG_SKIP") ? (uint32_t)atoi(getenv("BJX_DEBUG_SKIP")) : 0u;
       A.hdr = scan_hdr ? 1u : 0u;
       A.now_ns = now_ns;
@@ -6590,22 +6769,21 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       A.lines_out = e->scalars.p + 6;
       A.lb_abort = e->scalars.p + 7;
       // block-shared LDS: gram bitset, the lookup image when it fits, then 16 wave regions
-      const uint32_t fixed = kGramWords * 4 + kScanWaves * kWaveLds;
+      // (and the block's ScanGroup with the in-kernel line index)
+      const uint32_t grp = lb ? kScanGroupLds : 0u;
+      const uint32_t fixed = kGramWords * 4 + kScanWaves * kWaveLds + grp;
       const bool img_lds = fixed + B.img_bytes <= kScanLdsMax;
       A.shared_bytes = kGramWords * 4 + (img_lds ? B.img_bytes : 0);
-      const uint32_t lds = A.shared_bytes + kScanWaves * kWaveLds;
-      const void *kfn = img_lds ? reinterpret_cast<const void *>(&k_scan<true>) : reinterpret_cast<const void *>(&k_scan<false>);
-      if (lds != e->scan_lds[img_lds]) {
-        HIP_OK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        e->scan_lds[img_lds] = lds;
+      const uint32_t lds = A.shared_bytes + kScanWaves * kWaveLds + grp;
+      using ScanFn = void (*)(Bind, ScanArgs);
+      const ScanFn fns[2][2] = {{k_scan<false, false>, k_scan<false, true>}, {k_scan<true, false>, k_scan<true, true>}};
+      const ScanFn kfn = fns[img_lds][lb];
+      if (lds != e->scan_lds[img_lds][lb]) {
+        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        e->scan_lds[img_lds][lb] = lds;
       }
-      // one block (16 waves) per CU: the whole grid resident, as the look-back needs
-      int n_cu_scan = 0;
-      HIP_OK(hipDeviceGetAttribute(&n_cu_scan, hipDeviceAttributeMultiprocessorCount, e->device));
       HIP_OK(hipEventRecord(e->evm0, st));
-      const unsigned grid = (unsigned)std::min<uint64_t>((n_tiles + kScanWaves - 1) / kScanWaves, (uint64_t)std::max(1, n_cu_scan));
-      if (img_lds) hipLaunchKernelGGL(k_scan<true>, dim3(grid), dim3(kScanWaves * 64), lds, st, B, A);
-      else hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kScanWaves * 64), lds, st, B, A);
+      hipLaunchKernelGGL(kfn, dim3(scan_grid), dim3(kScanWaves * 64), lds, st, B, A);
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(e->evm1, st));
     }
@@ -6613,6 +6791,12 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       unsigned long long r[2] = {0, 0};
       HIP_OK(hipMemcpyAsync(r, e->scalars.p + 6, 16, hipMemcpyDeviceToHost, st));
       HIP_OK(hipStreamSynchronize(st));
+      if (e->lbprof.p && getenv("BJX_LB_PROF")) {
+        unsigned long long q[4];
+        HIP_OK(hipMemcpy(q, e->lbprof.p, 32, hipMemcpyDeviceToHost));
+        fprintf(stderr, "lbprof wait %.3f count %.3f publish %.3f loop %.3f (share of wave clocks)\n", (double)q[0] / q[3],
+                (double)q[1] / q[3], (double)q[2] / q[3], 1.0);
+      }
       if (r[1] || r[0] > cap) {  // the look-back gave up, or more lines than the arrays hold
         e->lb_fallbacks += 1;
         if (r[0] > cap && !r[1]) e->lines_per_byte = (double)r[0] / (double)n;
