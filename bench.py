@@ -105,8 +105,8 @@ def pmc_traffic(kernel):
 
 KERNELS = {
     "k_scan": "k_scan (framing + line index + literal prefilter over every byte of the batch)",
-    "k_lines": "k_lines (one lane per line: header, host, CheckIsAllowed, rule decisions from the hits; "
-               "the batch's line bytes staged in LDS)",
+    "k_lines": "k_lines2 (one lane per line: header from a 64 B window, host, CheckIsAllowed, rule decisions "
+               "from the literal hits; undecided pairs emitted as DFA-job windows)",
     "dfa_jobs": "DFA-job sort + k_dfa / k_nfa (the (line, rule) pairs the literals cannot decide)",
 }
 
