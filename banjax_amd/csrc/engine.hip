@@ -3198,7 +3198,7 @@ __global__ __launch_bounds__(kBlock) void k_ip_lookup(EvSrc E, const uint8_t *__
                                                       uint32_t *__restrict__ el_id) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E.n; i += (uint64_t)gridDim.x * blockDim.x) {
   uint32_t out = kUnresolved;
-  if (flags[i] == 0) {
+  if (flags[i] == 0 && E.ip_len[i] != 0) {  // ip_len 0: no event line (k_lines2) or an empty IP, claimed as usual
     const uint64_t h = E.ip_hash[i];
     const uint32_t len = E.ip_len[i];
     const bool inl = len <= 15;

@@ -345,6 +345,7 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
         else if (exempt) fl = kLineExempt;
         const uint32_t rest_len = n - rest_off, host_rel = host_off - rest_off;
         uint64_t m = alw, J = 0;
+        bool evl = false;  // the line has or may get (through its jobs) a rate-limit event
         if (fl) {
           L.counts[j] = 0;
         } else {
@@ -436,6 +437,7 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
             }
           }
           J &= ~m;
+          evl = ((m | J) & ~skp) != 0;
           while (J) {
             const uint32_t p = (uint32_t)__ffsll((unsigned long long)J) - 1;
             J &= J - 1;
@@ -449,18 +451,23 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
           if (B.mask_words > 1) L.masks[j * B.mask_words + 1] = 0;
           L.counts[j] = ((uint64_t)__popcll(m) << 32) | (uint64_t)__popcll(m & ~skp);
         }
-        L.ip_off[j] = ip_off;
-        L.ip_len[j] = ip_len;
         L.rest_off[j] = rest_off;
-        L.host_off[j] = host_off;
-        L.host_len[j] = host_len;
         L.host_id[j] = hid;
-        if (l2_in(X, ip_off, ip_len > 16 ? ip_len : 16u)) {
-          L.ip_hash[j] = hash_bytes(X.wp + ip_off, ip_len);
-          L.ip16[j] = ip_key16(X.wp + ip_off, ip_len);
-        } else {
-          L.ip_hash[j] = hash_bytes(X.gp + ip_off, ip_len);
-          L.ip16[j] = ip_key16(X.gp + ip_off, ip_len);
+        // the IP and host fields are read only for event lines (claims, node
+        // exchange, trips, bans): the others get ip_len 0 (k_ip_lookup skips
+        // them) and 36 B fewer stores
+        L.ip_len[j] = evl ? ip_len : 0u;
+        if (evl) {
+          L.ip_off[j] = ip_off;
+          L.host_off[j] = host_off;
+          L.host_len[j] = host_len;
+          if (l2_in(X, ip_off, ip_len > 16 ? ip_len : 16u)) {
+            L.ip_hash[j] = hash_bytes(X.wp + ip_off, ip_len);
+            L.ip16[j] = ip_key16(X.wp + ip_off, ip_len);
+          } else {
+            L.ip_hash[j] = hash_bytes(X.gp + ip_off, ip_len);
+            L.ip16[j] = ip_key16(X.gp + ip_off, ip_len);
+          }
         }
         L.ts[j] = tsn;
         L.flags[j] = fl;
