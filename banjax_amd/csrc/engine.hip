@@ -4340,12 +4340,16 @@ __global__ __launch_bounds__(kBlock) void k_pack(uint64_t n_el, const uint32_t *
       d_events[pe + t] = ev_rule[eo + t];
       pack_src[pe + t] = (uint32_t)(eo + t);
     }
-    // the IP bytes: word loads from the line (a log line continues past its
-    // IP), byte stores into the wave's LDS stage (or the packed pool)
-    const uint8_t *ip = buf + line_start(nl, j) + L.ip_off[j];
+    // the IP bytes, byte stores into the wave's LDS stage (or the packed
+    // pool): an IP of <= 15 bytes from its inline key (L.ip16, k_lines2 wrote
+    // it beside the line's other fields), a longer one by word loads from the
+    // line (a log line continues past its IP; a random 128 B fetch per line)
+    const bool inl = len <= 15;
+    const uint4 k16 = inl ? L.ip16[j] : make_uint4(0, 0, 0, 0);
+    const uint8_t *ip = inl ? nullptr : buf + line_start(nl, j) + L.ip_off[j];
     uint8_t *dst = staged ? sw + head + (by_off[p] - b0) : d_bytes + by_off[p];
     for (uint32_t k = 0; k < len; k += 4) {
-      const uint32_t w = ld4(ip + k);
+      const uint32_t w = inl ? (k < 4 ? k16.x : k < 8 ? k16.y : k < 12 ? k16.z : k16.w) : ld4(ip + k);
 #pragma unroll
       for (uint32_t b = 0; b < 4; ++b)
         if (k + b < len) dst[k + b] = (uint8_t)(w >> (8 * b));
