@@ -200,8 +200,6 @@ def lib():
     L.bjx_debug_set_dfa_state_cap.argtypes = [C.c_uint32]
     L.bjx_debug_force_wide_nfa.restype = C.c_int
     L.bjx_debug_force_wide_nfa.argtypes = [C.c_int]
-    L.bjx_engine_set_scan_lookback.restype = C.c_int
-    L.bjx_engine_set_scan_lookback.argtypes = [C.c_void_p, C.c_int]
     L.bjx_tailer_open.restype = C.c_int
     L.bjx_tailer_open.argtypes = [C.c_char_p, sz, C.POINTER(TailerOptions), C.POINTER(vp), C.c_char_p, sz]
     L.bjx_tailer_next.restype = C.c_int

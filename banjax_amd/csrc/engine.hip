@@ -5,16 +5,19 @@
 // per-(ip, rule-name) fixed-window counters of RegexRateLimitStates.Apply
 // (internal/rate_limit.go:37-78) kept resident in HBM across batches.
 //
-// Pipeline (DESIGN.md "Kernels"):
-//   k_nl_count / k_nl_write    line framing: '\n' positions (coalesced 16 B/lane)
-//   k_parse_match<FAST>        per line: SplitN header parse, ParseFloat fast path,
-//                              host lookup, CheckIsAllowed, then every applicable
-//                              rule's DFA over the rest -> match bitmask
+// Pipeline of one batch:
+//   k_nl_count_wt + scan       '\n' count per 4 KB wave tile -> each tile's first line
+//   k_scan                     line framing (nl[]) and the prefilter literal hits of
+//                              every line, from the tile staged in LDS
+//   k_lines2 (k_lines)         per line: SplitN header, ParseFloat fast path, host
+//                              lookup, CheckIsAllowed, OldLine, rule decisions from
+//                              the literal hits; undecided (line, rule) pairs -> jobs
+//   job sort + k_dfa / k_nfa   the automaton of every undecided pair
 //   k_parse_match<SLOW>        lines whose timestamp needs the general ParseFloat
-//   scan + k_emit              RuleResults in reference order + rate-limit events
-//   radix sort by IP hash      groups events per IP, preserving (line, rule) order
-//   k_heads + k_ratelimit      one thread per IP: the Apply state machine in order
-//   trip compaction            RateLimitResult.Exceeded -> host replays the Banner
+//   k_emit                     RuleResults and rate-limit events in reference order
+//   k_ip_claim / k_st_claim    IP and (ip, rule name) state slots in HBM hash tables
+//   radix sort + k_apply       events by state slot (stable), the Apply automaton
+//   k_select_trips / k_build_trips   RateLimitResult.Exceeded -> the host's Banner replay
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -56,7 +59,6 @@ struct BjxError : std::runtime_error {
       throw BjxError(BJX_ERR_DEVICE, std::string(#expr " failed: ") + hipGetErrorString(e_));          \
   } while (0)
 
-constexpr uint32_t kTile = 4096;   // bytes per framing tile (256 lanes x 16 B)
 constexpr int kBlock = 256;
 
 // =====================================================================
@@ -70,69 +72,6 @@ __device__ __forceinline__ uint32_t nl_mask_word(uint32_t v) {
   uint32_t x = v ^ 0x0A0A0A0Au;
   uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;
   return ~t & 0x80808080u;
-}
-
-__global__ __launch_bounds__(kBlock) void k_nl_count(const uint8_t *__restrict__ buf, uint64_t n,
-                                                     uint32_t *__restrict__ tile_counts) {
-  typedef hipcub::BlockReduce<uint32_t, kBlock> BR;
-  __shared__ typename BR::TempStorage tmp;
-  const uint64_t base = (uint64_t)blockIdx.x * kTile + threadIdx.x * 16u;
-  uint32_t cnt = 0;
-  if (base + 16 <= n) {
-    uint4 v = *reinterpret_cast<const uint4 *>(buf + base);
-    cnt = __popc(nl_mask_word(v.x)) + __popc(nl_mask_word(v.y)) + __popc(nl_mask_word(v.z)) + __popc(nl_mask_word(v.w));
-  } else {
-    for (uint64_t k = base; k < n && k < base + 16; ++k) cnt += buf[k] == '\n';
-  }
-  uint32_t tot = BR(tmp).Sum(cnt);
-  if (threadIdx.x == 0) tile_counts[blockIdx.x] = tot;
-}
-
-// pass A of the v2 pipeline: '\n' count per 8 KB scan tile (32 B per lane)
-__global__ __launch_bounds__(kBlock) void k_nl_count8(const uint8_t *__restrict__ buf, uint64_t n,
-                                                      uint32_t *__restrict__ tile_counts) {
-  typedef hipcub::BlockReduce<uint32_t, kBlock> BR;
-  __shared__ typename BR::TempStorage tmp;
-  const uint64_t base = (uint64_t)blockIdx.x * 8192u + threadIdx.x * 32u;
-  uint32_t cnt = 0;
-  if (base + 32 <= n) {
-    const uint4 *src = reinterpret_cast<const uint4 *>(buf + base);
-    const uint4 a = src[0], b = src[1];
-    cnt = __popc(nl_mask_word(a.x)) + __popc(nl_mask_word(a.y)) + __popc(nl_mask_word(a.z)) + __popc(nl_mask_word(a.w)) +
-          __popc(nl_mask_word(b.x)) + __popc(nl_mask_word(b.y)) + __popc(nl_mask_word(b.z)) + __popc(nl_mask_word(b.w));
-  } else {
-    for (uint64_t k = base; k < n && k < base + 32; ++k) cnt += buf[k] == '\n';
-  }
-  const uint32_t tot = BR(tmp).Sum(cnt);
-  if (threadIdx.x == 0) tile_counts[blockIdx.x] = tot;
-}
-
-__global__ __launch_bounds__(kBlock) void k_nl_write(const uint8_t *__restrict__ buf, uint64_t n,
-                                                     const uint64_t *__restrict__ tile_base, uint64_t *__restrict__ nl) {
-  typedef hipcub::BlockScan<uint32_t, kBlock> BS;
-  __shared__ typename BS::TempStorage tmp;
-  const uint64_t base = (uint64_t)blockIdx.x * kTile + threadIdx.x * 16u;
-  uint32_t m[4] = {0, 0, 0, 0};
-  uint32_t cnt = 0;
-  if (base + 16 <= n) {
-    uint4 v = *reinterpret_cast<const uint4 *>(buf + base);
-    m[0] = nl_mask_word(v.x); m[1] = nl_mask_word(v.y); m[2] = nl_mask_word(v.z); m[3] = nl_mask_word(v.w);
-  } else {
-    for (uint64_t k = base; k < n && k < base + 16; ++k)
-      if (buf[k] == '\n') m[(k - base) >> 2] |= 0x80u << (8 * ((k - base) & 3));
-  }
-  cnt = __popc(m[0]) + __popc(m[1]) + __popc(m[2]) + __popc(m[3]);
-  uint32_t off;
-  BS(tmp).ExclusiveSum(cnt, off);
-  uint64_t o = tile_base[blockIdx.x] + off;
-  for (int w = 0; w < 4; ++w) {
-    uint32_t x = m[w];
-    while (x) {
-      int b = __ffs(x) - 1;
-      nl[o++] = base + 4 * w + (b >> 3);
-      x &= x - 1;
-    }
-  }
 }
 
 // --------------------------------------------------------------- lookups
@@ -549,7 +488,6 @@ constexpr uint32_t kLinesImgMax = 16 * 1024;  // k_lines copies the lookup image
 constexpr uint32_t kLinesHostLdsMax = 6 * 1024;  // k_lines copies the compact host dictionary up to this size
 constexpr uint32_t kLinesTabLdsMax = 10 * 1024;  // ... and the plan classes after it, up to this size in all
 constexpr uint32_t kLinesBlocksPerCu = 3;       // k_lines' LDS budget: 3 blocks of 4 waves per CU
-constexpr uint32_t kRulesImgMax = 48 * 1024;  // k_rules likewise (no line staging: 3+ blocks per CU)
 constexpr uint32_t kSpanBytes = 12 * 1024;    // k_lines: bytes of 64 lines staged per wave
 
 // 16-bit mask of the spaces among 16 bytes
@@ -658,20 +596,7 @@ struct ScanArgs {
   unsigned long long *stats;  // [0] bitset hits, [1] recorded literal hits
   uint32_t shared_bytes;      // per-wave LDS regions start here
   uint32_t debug_skip;        // timing experiments only (BJX_DEBUG_SKIP, results invalid): 1 gram phase, 2 candidates,
-                              // 4 literal checks of gram table hits, 8 gram table probes; line index: 0x10000 no
-                              // group_wait, 0x20000 no count-ahead reads
-  uint32_t hdr;               // 1: parse the headers of the lines that start in each tile (scan_header)
-  int64_t now_ns;
-  // in-kernel line index (tstat != nullptr): the newlines before each tile
-  // are found here instead of by the separate count pass (tile_base unused;
-  // see group_wait); n_lines is then the capacity of the per-line arrays,
-  // *lines_out gets the batch's line count and *lb_abort is raised by a wave
-  // that waited too long (the host then runs the two-pass way).  tstat: 4
-  // kRing iteration slots x gridDim.x block words, zeroed by the host.
-  unsigned long long *tstat;
-  unsigned long long *lbprof;  // BJX_LB_PROF: clocks in group_wait, count-ahead, publish, the loop (timing aid)
-  unsigned long long *lines_out;
-  unsigned long long *lb_abort;
+                              // 4 literal checks of gram table hits, 8 gram table probes
 };
 
 // pass A: '\n' count per wave tile
@@ -1390,222 +1315,7 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
 }
 
 
-// consumeLine up to the rule loop for one line, from the scan tile in LDS
-// (regex_rate_limiter.go:120-172): SplitN header, parseTimestamp fast path,
-// host id (LDS host table), CheckIsAllowed, OldLine.  A line whose header runs
-// past the window or whose timestamp needs the general ParseFloat keeps
-// kLineTodo and goes to k_lines.  complete: the line's '\n' is in the window.
 template <bool IMG_LDS>
-__device__ __forceinline__ void scan_header(const Bind &B, const Tabs &TB, const ScanArgs &A, const uint8_t *p, uint32_t n,
-                                            bool complete, uint64_t j) {
-  const Lines &L = A.L;
-  uint32_t sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
-  const uint32_t ns = find_spaces(p, n, sp0, sp1, sp2, sp3);
-  if (ns < 4) {
-    if (complete) { L.flags[j] = kLineError; L.counts[j] = 0; }
-    return;
-  }
-  double f;
-  if (parse_float_fast(p, sp0, &f) != 0) return;
-  const uint32_t ip_off = sp0 + 1, ip_len = sp1 - sp0 - 1;
-  const uint32_t rest_off = sp1 + 1, host_off = sp2 + 1, host_len = sp3 - sp2 - 1;
-  const int32_t hid = host_lookup_ht(B, TB, p + host_off, host_len);
-  const bool exempt = B.any_allow && check_is_allowed(B, hid, p + ip_off, ip_len);
-  L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
-  L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
-  L.host_id[j] = hid;
-  L.ip_hash[j] = hash_bytes(p + ip_off, ip_len);
-  L.ip16[j] = ip_key16(p + ip_off, ip_len);
-  const int64_t tsn = ns_from_seconds(f);
-  L.ts[j] = tsn;
-  uint8_t fl = 0;
-  if (go_sub(A.now_ns, tsn) > 10000000000LL) fl = kLineOld;
-  else if (exempt) fl = kLineExempt;
-  L.flags[j] = fl;
-  if (fl) L.counts[j] = 0;
-}
-
-
-// In-kernel line index (ScanArgs::tstat): counted ahead, summed per block.
-// All of its atomics are relaxed: the grid words carry their data in the word
-// itself, and LDS operations of a wave complete in order (compiler fences keep
-// that order), so no release / acquire (an agent-scope release writes back the
-// XCD's L2) is needed.
-// The grid (one block per CU, resident as a whole) takes the tiles in
-// iterations: iteration r gives block b the 16 consecutive tiles
-// r * nw + 16 b + wave.  Each wave counts the newlines of its tile kAhead
-// iterations ahead (an extra 64 B read per lane) and adds the count to its
-// block's sum in LDS; the block's last wave to arrive publishes the sum (and
-// its last tile's count) as one tagged word per (iteration slot, block), then
-// reads the grid's words of the iteration before (group_read: the newlines of
-// the blocks before this one and of the whole iteration).  Each wave keeps
-// its running base (the newlines of the iterations before) and finds the rest
-// in LDS when it gets to the iteration (group_wait).  Nothing chains from
-// tile to tile, unlike the per-tile decoupled look-back it replaces
-// (profiles/r04_t3).  Still slower than the two-pass count at cfg3
-// (profiles/r04_lbp, BJX_LB_PROF=1: 23 % of wave clocks waiting for the
-// grid's slowest waves, 10 % counting ahead; k_scan 25.8 ms against 3.0 +
-// 12.9 ms), so it stays opt-in (BJX_LOOKBACK=1).
-constexpr uint32_t kAhead = 6;   // iterations counted ahead
-constexpr uint32_t kRing = 16;   // iteration slots (>= 2 kAhead + 2: a block is at most kAhead iterations ahead of any other)
-static_assert((kRing & (kRing - 1)) == 0 && kRing >= 2 * kAhead + 2, "ring of iteration slots");
-struct ScanGroup {
-  uint32_t cnt[kRing][kScanWaves];  // newlines of each wave's tile, by iteration slot
-  uint32_t sum[kRing], arr[kRing];  // block sum / arrivals of the slot being counted
-  uint32_t done[kRing];             // ready tag (iteration + 1) per slot
-  uint32_t pre[kRing];              // newlines of the iteration's tiles before the block's
-  uint32_t tot[kRing];              // newlines of the iteration
-  uint32_t prevb[kRing];            // newlines of the previous block's last tile
-  uint32_t lastg[kRing];            // newlines of the iteration's last tile
-  unsigned long long wbase[kScanWaves];  // per wave: newlines before its current iteration
-  unsigned long long wtb[kScanWaves];    // per wave: newlines before its tile (kept out of VGPRs)
-  uint32_t wprev[kScanWaves];            // and newlines in the tile before it
-};
-constexpr uint32_t kScanGroupLds = (sizeof(ScanGroup) + 15) & ~15u;
-static_assert(kWaveLds % 16 == 0, "ScanGroup follows the wave regions 16-B aligned");
-constexpr uint32_t kLookbackSpins = 1u << 22;
-constexpr uint32_t kGroupAbort = 0xFFFFFFFFu;
-
-__device__ __forceinline__ uint32_t wave_total(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(v), 63);
-}
-
-// newlines in wave tile tt (0 past the batch), every lane reading 64 B
-__device__ __forceinline__ uint32_t tile_nl_count(const ScanArgs &A, uint64_t tt, uint32_t lane) {
-  uint32_t c = 0;
-  if (tt < A.n_tiles) {
-    const uint64_t base = tt * kWT + lane * 64u;
-    if (base + 64 <= A.n) {
-      const uint4 *src = reinterpret_cast<const uint4 *>(A.buf + base);
-      uint4 v[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = src[k];
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        c += __popc(nl_mask_word(v[k].x)) + __popc(nl_mask_word(v[k].y)) + __popc(nl_mask_word(v[k].z)) +
-             __popc(nl_mask_word(v[k].w));
-    } else {
-      for (uint64_t q = base; q < A.n && q < base + 64; ++q) c += A.buf[q] == '\n' ? 1u : 0u;
-    }
-  }
-  return wave_total(c);
-}
-
-// iteration r's grid words -> G (slot r % kRing): the newlines of the blocks
-// before this one, of the whole iteration, and the last tile counts this
-// block's first wave needs; run by one wave of the block (group_publish).  One
-// round trip per poll: every lane loads its share of the words at once.
-// Iterations are read independently (the running base is kept per wave,
-// ScanGroup::wbase).  False if the wait ran past kLookbackSpins or another
-// wave gave up (*lb_abort).
-constexpr uint32_t kReadPer = 4;  // words per lane: grids of up to 256 blocks in one load round
-__device__ __forceinline__ bool group_read(const ScanArgs &A, ScanGroup &G, uint32_t r, uint32_t lane) {
-  const uint32_t s = r & (kRing - 1), tg = r + 1u;
-  const uint32_t b = blockIdx.x, ng = gridDim.x;
-  uint32_t pre = 0, tot = 0, prevb = 0, lastg = 0, spins = 0;
-  for (uint32_t c0 = 0; c0 < ng; c0 += 64 * kReadPer) {
-    unsigned long long v[kReadPer];
-    for (;;) {
-#pragma unroll
-      for (uint32_t k = 0; k < kReadPer; ++k) {
-        const uint32_t idx = c0 + k * 64 + lane;
-        v[k] = idx < ng ? __hip_atomic_load(&A.tstat[(uint64_t)s * ng + idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                        : ((unsigned long long)tg << 32);
-      }
-      bool ok = true;
-#pragma unroll
-      for (uint32_t k = 0; k < kReadPer; ++k) ok = ok && (uint32_t)(v[k] >> 32) == tg;
-      if (__ballot(!ok) == 0) break;
-      if (++spins > kLookbackSpins || __hip_atomic_load(A.lb_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        if (lane == 0) {
-          atomicOr(A.lb_abort, 1ull);
-          __hip_atomic_store(&G.done[s], kGroupAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        return false;
-      }
-      __builtin_amdgcn_s_sleep(8);
-    }
-    uint32_t ct = 0, cp = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kReadPer; ++k) {
-      const uint32_t idx = c0 + k * 64 + lane;
-      const uint32_t c = idx < ng ? (uint32_t)(v[k] & 0x1FFFFu) : 0u;
-      const uint32_t l = (uint32_t)(v[k] >> 17) & 0x1FFFu;
-      ct += c;
-      cp += idx < b ? c : 0u;
-      if (idx + 1 == b) prevb = l;
-      if (idx + 1 == ng) lastg = l;
-    }
-    tot += wave_total(ct);
-    pre += wave_total(cp);
-  }
-  // prevb / lastg sit in one lane each
-  prevb = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_total(prevb));
-  lastg = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_total(lastg));
-  if (lane == 0) {
-    G.pre[s] = pre;
-    G.tot[s] = tot;
-    G.prevb[s] = prevb;
-    G.lastg[s] = lastg;
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __hip_atomic_store(&G.done[s], tg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-  return true;
-}
-
-// this wave's count for iteration r into its block's slot.  The last of the
-// block's waves to arrive publishes the block word, then reads iteration
-// r - 1 (whose words went out about an iteration earlier), and r itself if it
-// is the last iteration, so the block's waves find their tb ready some
-// kAhead iterations before they need it (group_wait).
-__device__ __forceinline__ bool group_publish(const ScanArgs &A, ScanGroup &G, uint32_t r, uint32_t n_iter, uint32_t c,
-                                              uint32_t wave, uint32_t lane) {
-  const uint32_t s = r & (kRing - 1);
-  uint32_t last = 0;
-  if (lane == 0) {
-    __hip_atomic_store(&G.cnt[s][wave], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_add(&G.sum[s], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    const uint32_t old = __hip_atomic_fetch_add(&G.arr[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (old == kScanWaves - 1) {
-      last = 1;
-      const uint32_t tot = __hip_atomic_load(&G.sum[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const uint32_t lc = __hip_atomic_load(&G.cnt[s][kScanWaves - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      // reset for iteration r + kRing before the word goes out (a wave that
-      // sees the word sees the reset)
-      __hip_atomic_store(&G.sum[s], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_store(&G.arr[s], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the resets are done
-      __hip_atomic_store(&A.tstat[(uint64_t)s * gridDim.x + blockIdx.x],
-                         ((unsigned long long)(r + 1u) << 32) | ((unsigned long long)lc << 17) | tot, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  if (!__builtin_amdgcn_readfirstlane((int)last)) return true;
-  if (r >= 1 && !group_read(A, G, r - 1, lane)) return false;
-  if (r + 1 == n_iter && !group_read(A, G, r, lane)) return false;
-  return true;
-}
-
-// waits until iteration r's tb / prev are in G; false if a wave gave up
-__device__ __forceinline__ bool group_wait(const ScanArgs &A, ScanGroup &G, uint32_t r) {
-  const uint32_t s = r & (kRing - 1), tg = r + 1u;
-  uint32_t spins = 0;
-  for (;;) {
-    const uint32_t d = __hip_atomic_load(&G.done[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (d == tg) {
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      return true;
-    }
-    if (d == kGroupAbort || ++spins > kLookbackSpins ||
-        __hip_atomic_load(A.lb_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-      return false;
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-// LB: the in-kernel line index (group_wait) instead of the count pass's tile_base
-template <bool IMG_LDS, bool LB>
 __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_scan(Bind B, ScanArgs A) {
   // ---- block-shared tables (read-only after this barrier): gram bitset, then
   // the lookup image when it fits
@@ -1616,14 +1326,11 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
   if (IMG_LDS)
     for (uint32_t i = threadIdx.x; i < B.img_bytes / 16; i += blockDim.x)
       reinterpret_cast<uint4 *>(s_img)[i] = reinterpret_cast<const uint4 *>(B.img)[i];
-  for (uint32_t i = threadIdx.x; i < kScanGroupLds / 4; i += blockDim.x)
-    reinterpret_cast<uint32_t *>(s_dyn + A.shared_bytes + kScanWaves * kWaveLds)[i] = 0;
   __syncthreads();
   const Tabs TB = make_tabs(IMG_LDS ? s_img : B.img, B.il);
   const uint32_t *gt = TB.gt, *ge = TB.ge;
 
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  ScanGroup &G = *reinterpret_cast<ScanGroup *>(s_dyn + A.shared_bytes + kScanWaves * kWaveLds);
   uint8_t *T = s_dyn + A.shared_bytes + wave * kWaveLds;
   uint16_t *ls = reinterpret_cast<uint16_t *>(T + kTileLds);
   uint16_t *le = ls + kLineCap;
@@ -1658,38 +1365,8 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
     }
   };
   const uint64_t n_iter = (A.n_tiles + nw - 1) / nw;
-  uint64_t pw = 0, pc = 0, pp = 0;
-  const uint64_t p_start = __builtin_amdgcn_s_memtime();
-  if (LB)  // the counts of iterations 0 .. kAhead - 1 (group_wait)
-    for (uint32_t q = 0; q < kAhead && q < n_iter; ++q)
-      if (!group_publish(A, G, q, (uint32_t)n_iter, tile_nl_count(A, t + (uint64_t)q * nw, lane), wave, lane)) return;
   if (t < A.n_tiles) load_tile(t);
   for (uint32_t r = 0; r < n_iter; ++r, t += nw) {
-    if (LB) {
-      const uint64_t c0 = __builtin_amdgcn_s_memtime();
-      if (!(A.debug_skip & 0x10000) && !group_wait(A, G, r)) return;  // the host redoes the batch the two-pass way
-      const uint64_t c1 = __builtin_amdgcn_s_memtime();
-      pw += c1 - c0;
-      const uint32_t s = r & (kRing - 1);
-      if (lane == 0) {
-        const uint64_t base = G.wbase[wave];
-        uint64_t x = base + G.pre[s];
-        for (uint32_t w2 = 0; w2 < wave; ++w2) x += G.cnt[s][w2];
-        G.wtb[wave] = x;
-        G.wprev[wave] = wave ? G.cnt[s][wave - 1] : blockIdx.x ? G.prevb[s] : r ? G.lastg[(r - 1) & (kRing - 1)] : 0u;
-        G.wbase[wave] = base + G.tot[s];
-      }
-      // read before this wave's count for r + kAhead goes out (group_publish)
-      if (r + kAhead < n_iter) {
-        const uint64_t c2 = __builtin_amdgcn_s_memtime();
-        const uint32_t cnt_ahead = (A.debug_skip & 0x20000) ? 0u : tile_nl_count(A, t + (uint64_t)kAhead * nw, lane);
-        const uint64_t c3 = __builtin_amdgcn_s_memtime();
-        if (!group_publish(A, G, r + kAhead, (uint32_t)n_iter, cnt_ahead, wave, lane)) return;
-        const uint64_t c4 = __builtin_amdgcn_s_memtime();
-        pc += c3 - c2;
-        pp += c4 - c3;
-      }
-    }
     if (t >= A.n_tiles) continue;
     const uint64_t ts0 = t * kWT;
     uint32_t w[16];
@@ -1730,16 +1407,8 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
     uint32_t pre = wave_incl_sum(cnt);
     const uint32_t tot = __builtin_amdgcn_readlane(pre, 63);
     pre -= cnt;
-    uint64_t tb;
-    uint32_t prev_cnt = 0;
-    if (LB) {
-      tb = G.wtb[wave];
-      prev_cnt = G.wprev[wave];
-      if (t + 1 == A.n_tiles && lane == 0) *A.lines_out = tb + tot;
-    } else {
-      tb = A.tile_base[t];
-      prev_cnt = t ? (uint32_t)(tb - A.tile_base[t - 1]) : 0u;
-    }
+    const uint64_t tb = A.tile_base[t];
+    const uint32_t prev_cnt = t ? (uint32_t)(tb - A.tile_base[t - 1]) : 0u;
     const bool head = prevb == '\n';
     const uint32_t nh = head ? 0u : 1u;
     const bool last_nl = (__shfl((uint32_t)(nlm >> 63), 63) & 1u) != 0;
@@ -1785,17 +1454,6 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
     const bool last_long = n_st && !last_nl && hfirst == kNone;
     if (lane == 0 && last_in_halo && n_st - 1 < kLineCap) le[n_st - 1] = (uint16_t)hfirst;
     wave_sync();
-    // ---- headers of the lines that start in this tile (one lane per line)
-    if (A.hdr) {
-      const uint32_t n_hl = min(n_st, kLineCap);
-      for (uint32_t k = lane; k < n_hl; k += 64) {
-        const uint64_t gline = tb + nh + k;
-        if (gline >= A.n_lines) continue;
-        const bool complete = k + 1 < n_st || !last_long;
-        const uint32_t b0 = ls[k], e0 = complete ? (uint32_t)le[k] : kWT + kHalo;
-        scan_header<IMG_LDS>(B, TB, A, T + b0, e0 - b0, complete, gline);
-      }
-    }
     if (!B.any_prefilter || (A.debug_skip & 1)) continue;
     // bytes of the batch held by the tile + halo in LDS
     const uint64_t win_end = A.n - ts0 < (uint64_t)(kWT + kHalo) ? A.n - ts0 : (uint64_t)(kWT + kHalo);
@@ -1972,12 +1630,6 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
     n_probe += __shfl_xor(n_probe, o);
     n_hit += __shfl_xor(n_hit, o);
     n_gram += __shfl_xor(n_gram, o);
-  }
-  if (LB && A.lbprof && lane == 0) {
-    atomicAdd(&A.lbprof[0], (unsigned long long)pw);
-    atomicAdd(&A.lbprof[1], (unsigned long long)pc);
-    atomicAdd(&A.lbprof[2], (unsigned long long)pp);
-    atomicAdd(&A.lbprof[3], (unsigned long long)(__builtin_amdgcn_s_memtime() - p_start));
   }
   if (lane == 0 && (n_probe | n_hit)) {
     atomicAdd(&A.stats[0], (unsigned long long)n_probe);
@@ -2235,93 +1887,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
 
 #include "lines2.h"
 
-// Rule decisions of the lines whose header the scan pass parsed (one lane per
-// line, regex_rate_limiter.go:175-211): host rules, anchored checks against
-// the line in HBM, the scan's literal hits; undecided (line, rule) pairs become
-// DFA jobs.  kLineTodo lines (and lines with more than 128 applicable rules)
-// are listed for k_lines.
-struct RulesArgs {
-  const uint8_t *buf;
-  const uint64_t *nl;
-  uint64_t n_lines;
-  Lines L;
-  uint32_t *todo;
-  unsigned long long *todo_count;
-  uint32_t *jline, *jkey, *jidx;
-  uint64_t *jrec;
-  unsigned long long *job_count;
-  unsigned long long *job_real;
-  uint32_t null_key;
-  uint64_t job_cap;
-};
-
-template <bool IMG_LDS>
-__global__ __launch_bounds__(kBlock) void k_rules(Bind B, RulesArgs A) {
-  uint8_t *s_img = s_dyn;
-  if (IMG_LDS) {
-    for (uint32_t i = threadIdx.x; i < B.img_bytes / 16; i += blockDim.x)
-      reinterpret_cast<uint4 *>(s_img)[i] = reinterpret_cast<const uint4 *>(B.img)[i];
-    __syncthreads();
-  }
-  const Tabs TB = make_tabs(IMG_LDS ? s_img : B.img, B.il);
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  JobSink S;
-  S.lds = reinterpret_cast<uint4 *>(s_dyn + ((IMG_LDS ? B.img_bytes : 0) + 15u & ~15u) + wave * kWaveJobBytes);
-  S.cnt = reinterpret_cast<uint32_t *>(S.lds + kWaveJobs);
-  S.jline = A.jline;
-  S.jkey = A.jkey;
-  S.jidx = A.jidx;
-  S.jrec = A.jrec;
-  S.n_rules = B.n_rules;
-  S.count = A.job_count;
-  S.cap = A.job_cap;
-  if (lane == 0) *S.cnt = 0;
-  wave_sync();
-  JobChunk JC;
-  const Lines &L = A.L;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + wave * 64u; base < A.n_lines; base += stride) {
-    const uint64_t j = base + lane;
-    if (j < A.n_lines) {
-      const uint8_t fl = L.flags[j];
-      if (fl & kLineTodo) {
-        push_list(A.todo, A.todo_count, j);
-      } else if (fl == 0) {
-        const int32_t hid = L.host_id[j];
-        const HostRules H = host_rules(B, hid);
-        if ((H.s_end - H.s_begin) + B.n_global > 128) {
-          L.flags[j] = kLineTodo;  // the per-line kernel sends it to the general path
-          push_list(A.todo, A.todo_count, j);
-        } else {
-          const uint64_t s = j ? A.nl[j - 1] + 1 : 0;
-          const uint32_t n = (uint32_t)(A.nl[j] - s);
-          const uint32_t ro = L.rest_off[j];
-          uint64_t lits = 0, lpos = 0;
-          uint32_t nlit = 0, cc = 0;
-          if (B.any_prefilter) {
-            cc = L.cand_meta[j].cnt;
-            const uint64_t rs = s + ro;
-#pragma unroll
-            for (uint32_t c = 0; c < (uint32_t)kCandSlots; ++c) {
-              if (c >= cc) break;
-              const uint64_t v = L.cand[j * kCandSlots + c];
-              const uint32_t lit = (uint32_t)(v & 0x7FFFFF);
-              const uint64_t q = v >> 24;
-              if (q < rs) continue;
-              if (!(v & kCandVerified) && (q + lit_len_of(TB, lit) > s + n || !literal_at(TB, lit, A.buf + q))) continue;
-              lpos |= (uint64_t)(q - rs < 0xFFFF ? (uint32_t)(q - rs) : 0xFFFFu) << (16 * nlit);
-              lits |= (uint64_t)lit << (16 * nlit++);
-            }
-          }
-          decide_rules<true>(B, TB, A.buf + s + ro, n - ro, hid, H, lits, lpos, nlit, cc > (uint32_t)kCandSlots, j, L, S);
-        }
-      }
-    }
-    // ---- append this wave's DFA jobs (from its chunk of the job array)
-    flush_jobs(S, JC, lane);
-  }
-  close_jobs(S, JC, lane, A.null_key, A.job_real);
-}
 
 // DFA jobs of the line pass, sorted by rule: one (line, rule) per lane.  A
 // block whose jobs share one rule (the common case) stages that rule's
@@ -3188,41 +2753,6 @@ __device__ __forceinline__ bool ip_claim_line(const EvSrc &E, const State &S, ui
   }
 }
 
-// The IP of every parsed line looked up among the IPs of earlier batches
-// (read-only: no claim), on its own stream while the DFA jobs run (both are
-// latency-bound, so they share the CUs).  el_id = the IP's id, or kUnresolved
-// (not there, or the line's header is parsed later); k_ip_claim then only
-// claims the unresolved event lines.  Ids survive a table rehash.
-constexpr uint32_t kUnresolved = 0xFFFFFFFEu;
-__global__ __launch_bounds__(kBlock) void k_ip_lookup(EvSrc E, const uint8_t *__restrict__ flags, State S,
-                                                      uint32_t *__restrict__ el_id) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E.n; i += (uint64_t)gridDim.x * blockDim.x) {
-  uint32_t out = kUnresolved;
-  if (flags[i] == 0 && E.ip_len[i] != 0) {  // ip_len 0: no event line (k_lines2) or an empty IP, claimed as usual
-    const uint64_t h = E.ip_hash[i];
-    const uint32_t len = E.ip_len[i];
-    const bool inl = len <= 15;
-    const uint4 k16 = inl ? E.ip16[i] : make_uint4(0, 0, 0, 0);
-    uint64_t s = h & S.ip_mask;
-    for (;;) {
-      const uint4 *sp = reinterpret_cast<const uint4 *>(&S.ip[s]);
-      const uint4 q0 = sp[0], q1 = sp[1];
-      const uint64_t cur = ((uint64_t)q0.y << 32) | q0.x;
-      if (cur == 0) break;
-      if (cur == h && q0.w != 0) {
-        const uint32_t id = q0.z;
-        if (inl ? key16_eq(q1, k16) : (S.ip_len[id] == len && bytes_eq(S.arena + S.ip_off[id], ev_ip(E, i), len))) {
-          out = id;
-          break;
-        }
-      }
-      s = (s + 1) & S.ip_mask;
-    }
-  }
-  el_id[i] = out;
-  }
-}
-
 // exclusive prefix of v over the wave and one atomicAdd of the wave's total
 // on ctr; returns ctr's old value + the prefix (every lane of the wave calls it)
 __device__ __forceinline__ uint64_t wave_alloc(unsigned long long *ctr, uint32_t v);
@@ -3231,11 +2761,10 @@ __device__ __forceinline__ uint64_t wave_alloc(unsigned long long *ctr, uint32_t
 // in this batch), listed for k_ip_commit
 __global__ __launch_bounds__(kBlock) void k_ip_claim(EvSrc E, State S, uint32_t epoch, uint32_t *__restrict__ el_slot,
                                                      uint32_t *__restrict__ el_id, uint32_t *__restrict__ el_new,
-                                                     uint64_t shard_budget, uint32_t pre) {
+                                                     uint64_t shard_budget) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool claimed = false, isnew = false;
-  // pre: k_ip_lookup resolved the lines whose IP an earlier batch created
-  if (i < E.n && ev_has(E, i) && !(pre && el_id[i] != kUnresolved) && !flag_set(S, 5)) {
+  if (i < E.n && ev_has(E, i) && !flag_set(S, 5)) {
     el_id[i] = 0;
     claimed = ip_claim_line(E, S, epoch, i, el_slot, el_id, shard_budget);
     isnew = el_id[i] == kNewIp;
@@ -3392,188 +2921,6 @@ __global__ __launch_bounds__(kBlock) void k_st_claim(EvSrc E, uint64_t n_ev, con
   if (k < n_ev && !flag_set(S, 7)) claimed = st_claim_event(E, n_ev, k, ev_el, ev_rule, el_slot, el_id, rules, S, ev_st, ev_rec,
                                                             base, shard_budget);
   count_claims(S, 1, 7, claimed, shard_budget);
-}
-
-// ---- per-line claims of a local batch (no per-event line / rule arrays): the
-// events of a line are its match-mask positions in order, hosts_to_skip out
-// (k_emit's order), numbered from the line's exclusive event offset.
-
-// adds n claims of this lane to the block's shard (all lanes of the wave call it)
-__device__ __forceinline__ void count_claims_n(const State &S, uint32_t which, uint32_t ovf_flag, uint32_t n, uint64_t shard_budget) {
-  uint32_t tot = n;
-  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
-  if (tot && (threadIdx.x & 63) == 0)
-    if (atomicAdd(claim_shard(S, which), (unsigned long long)tot) + tot > shard_budget) raise_flag(S, ovf_flag);
-}
-
-// fn(k, rule) for each event of line i, k from eo on
-template <typename F>
-__device__ __forceinline__ void for_line_events(const Bind &B, const Lines &L, uint64_t i, uint64_t eo, F fn) {
-  const int32_t hid = L.host_id[i];
-  uint32_t sb = 0, nsite = 0;
-  if (hid >= 0) { sb = B.site_off[hid]; nsite = B.site_off[hid + 1] - sb; }
-  const uint32_t napp = nsite + B.n_global;
-  const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
-  const uint64_t k0 = B.sc_skip[2 * sc], k1 = B.sc_skip[2 * sc + 1];
-  const uint64_t *mask = L.masks + i * B.mask_words;
-  uint64_t k = eo;
-  for (uint32_t w = 0; w * 64 < napp; ++w) {
-    uint64_t m = mask[w];
-    while (m) {
-      const uint32_t b = (uint32_t)__ffsll((unsigned long long)m) - 1;
-      m &= m - 1;
-      const uint32_t pos = w * 64 + b;
-      const uint32_t r = pos < nsite ? B.site_rules[sb + pos] : B.global_rules[pos - nsite];
-      const bool skip = pos < 128 ? (((pos < 64 ? k0 >> pos : k1 >> (pos - 64)) & 1) != 0) : is_skip(B, r, hid);
-      if (!skip) fn(k++, r);
-    }
-  }
-}
-
-// one event's state slot (st_claim_event without the per-event arrays)
-__device__ __forceinline__ bool st_claim_rule(const State &S, const DevRule *__restrict__ rules, uint32_t id, uint32_t r,
-                                              int64_t ts, bool first, uint64_t k, uint32_t *__restrict__ ev_st,
-                                              EvRec *__restrict__ ev_rec, uint64_t shard_budget) {
-  const uint32_t nm = rules[r].name_id;
-  const uint64_t key = ((uint64_t)(id + 1) << 24) | nm;
-  const bool hot = nm == S.hot_name && id < S.ip_st_cap;
-  const uint32_t c = hot ? S.ip_st[id] : kNone;
-  uint64_t q = c;
-  bool claimed = false;
-  if (c == kNone) {
-    q = mix64(key) & S.st_mask;
-    for (;;) {
-      uint64_t cur = S.st[q].key;
-      if (cur == 0) {
-        if (flag_set(S, 7)) return false;
-        if (__hip_atomic_load(claim_shard(S, 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= shard_budget) {
-          raise_flag(S, 7);
-          return false;
-        }
-        cur = atomicCAS((unsigned long long *)&S.st[q].key, 0ull, (unsigned long long)key);
-        if (cur == 0) { claimed = true; break; }
-      }
-      if (cur == key) break;
-      q = (q + 1) & S.st_mask;
-    }
-    if (hot) S.ip_st[id] = (uint32_t)q;
-  }
-  ev_st[k] = (uint32_t)q;
-  ev_rec[k] = EvRec::make(ts, r, first, (uint32_t)k, 0);
-  return claimed;
-}
-
-// one lane per event line: the IP slot (k_ip_claim), then, for an IP of an
-// earlier batch, the state slots of the line's events right away; lines of
-// IPs new in this batch are listed (el_new) for k_ip_commit and k_line_st_claim
-__global__ __launch_bounds__(kBlock) void k_line_claim(Bind B, EvSrc E, Lines L, const uint64_t *__restrict__ offs, State S,
-                                                       uint32_t epoch, uint32_t *__restrict__ el_slot,
-                                                       uint32_t *__restrict__ el_id, uint32_t *__restrict__ el_new,
-                                                       uint64_t ip_budget, uint32_t *__restrict__ ev_st,
-                                                       EvRec *__restrict__ ev_rec, uint64_t st_budget) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool claimed = false, isnew = false;
-  const bool act = i < E.n && ev_has(E, i) && !flag_set(S, 5);
-  if (act) {
-    el_id[i] = 0;
-    claimed = ip_claim_line(E, S, epoch, i, el_slot, el_id, ip_budget);
-    isnew = el_id[i] == kNewIp;
-  }
-  count_claims(S, 0, 5, claimed, ip_budget);
-  const uint64_t at = wave_alloc((unsigned long long *)&S.counters[4], isnew ? 1u : 0u);
-  if (isnew) el_new[at] = (uint32_t)i;
-  uint32_t nst = 0;
-  if (act && !isnew && !flag_set(S, 7) && !flag_set(S, 5)) {
-    const uint32_t id = el_id[i] & ~kFirstIp;
-    const int64_t ts = E.ts[i];
-    for_line_events(B, L, i, offs[i] & 0xFFFFFFFFull, [&](uint64_t k, uint32_t r) {
-      nst += st_claim_rule(S, B.rules, id, r, ts, false, k, ev_st, ev_rec, st_budget) ? 1u : 0u;
-    });
-  }
-  count_claims_n(S, 1, 7, nst, st_budget);
-}
-
-// state slots of the listed event lines (list: IPs new in this batch, after
-// k_ip_commit), or of every event line (list == nullptr: the retry after a
-// state-table overflow).  seenIp is false only for the first event of the
-// first event line of a new IP (kFirstIp).
-__global__ __launch_bounds__(kBlock) void k_line_st_claim(Bind B, EvSrc E, Lines L, const uint64_t *__restrict__ offs, State S,
-                                                          const uint32_t *__restrict__ list, uint64_t n_list,
-                                                          const uint32_t *__restrict__ el_slot, const uint32_t *__restrict__ el_id,
-                                                          uint32_t *__restrict__ ev_st, EvRec *__restrict__ ev_rec,
-                                                          uint64_t st_budget) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t nst = 0;
-  const bool in = list ? t < n_list : t < E.n;
-  const uint64_t i = in ? (list ? list[t] : t) : 0;
-  if (in && ev_has(E, i) && !flag_set(S, 7)) {
-    uint32_t id = el_id[i];
-    const bool first_line = id != kNewIp && (id & kFirstIp);
-    id = id == kNewIp ? S.ip[el_slot[i]].id : (id & ~kFirstIp);
-    const int64_t ts = E.ts[i];
-    const uint64_t eo = offs[i] & 0xFFFFFFFFull;
-    for_line_events(B, L, i, eo, [&](uint64_t k, uint32_t r) {
-      nst += st_claim_rule(S, B.rules, id, r, ts, first_line && k == eo, k, ev_st, ev_rec, st_budget) ? 1u : 0u;
-    });
-  }
-  count_claims_n(S, 1, 7, nst, st_budget);
-}
-
-// lines with events and their IP bytes (bounds of the new IPs / arena bytes)
-__global__ __launch_bounds__(kBlock) void k_el_bounds(uint64_t n, const uint64_t *__restrict__ counts,
-                                                      const uint32_t *__restrict__ ip_len, unsigned long long *bounds) {
-  __shared__ unsigned long long s_acc[2][kBlock / 64];
-  unsigned long long a = 0, b = 0;
-  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x)
-    if (counts[j] & 0xFFFFFFFFull) { ++a; b += ip_len[j]; }
-  for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o); b += __shfl_xor(b, o); }
-  if ((threadIdx.x & 63) == 0) { s_acc[0][threadIdx.x >> 6] = a; s_acc[1][threadIdx.x >> 6] = b; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long x = 0, y = 0;
-    for (int w = 0; w < kBlock / 64; ++w) { x += s_acc[0][w]; y += s_acc[1][w]; }
-    if (x) { atomicAdd(&bounds[0], x); atomicAdd(&bounds[1], y); }
-  }
-}
-
-// trip k (sorted record at pos[t]) -> (event << 32 | rule), for a batch without
-// per-event arrays
-__global__ void k_trip_events_rules(uint64_t n, const uint32_t *__restrict__ pos, const EvRec *__restrict__ rec,
-                                    uint64_t *__restrict__ evr) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < n) {
-    const EvRec v = rec[pos[t]];
-    evr[t] = ((uint64_t)v.ev << 32) | v.rule_id();
-  }
-}
-
-// k_build_trips from (event << 32 | rule): the event's line by binary search
-// over the lines' event offsets (the last line whose offset is <= k holds it)
-__global__ void k_build_trips_offs(uint64_t n_trips, const uint64_t *__restrict__ evr, uint64_t n_lines,
-                                   const uint64_t *__restrict__ offs, const uint64_t *__restrict__ nl, Lines L,
-                                   const DevRule *__restrict__ rules, bjx_trip *__restrict__ out) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_trips) return;
-  const uint64_t k = evr[t] >> 32;
-  uint64_t lo = 0, hi = n_lines;  // first line whose offset > k
-  while (lo < hi) {
-    const uint64_t m = (lo + hi) >> 1;
-    if ((offs[m] & 0xFFFFFFFFull) <= k) lo = m + 1; else hi = m;
-  }
-  const uint64_t line = lo - 1;
-  bjx_trip tr;
-  tr.line_idx = line;
-  tr.line_offset = line_start(nl, line);
-  tr.line_len = (uint32_t)(nl[line] - tr.line_offset);
-  tr.rule_idx = (uint32_t)(evr[t] & 0xFFFFFFFFull);
-  tr.ts_ns = L.ts[line];
-  tr.ip_off = L.ip_off[line];
-  tr.ip_len = L.ip_len[line];
-  tr.host_off = L.host_off[line];
-  tr.host_len = L.host_len[line];
-  tr.rest_off = L.rest_off[line];
-  tr.decision = rules[tr.rule_idx].decision;
-  out[t] = tr;
 }
 
 // state slots claimed by the last k_st_claim -> table load counters[2]; shards cleared
@@ -4273,15 +3620,20 @@ __global__ void k_part_keys(uint64_t n_lines, const uint64_t *__restrict__ count
   val[j] = (uint32_t)j;
 }
 
-// scan inputs per packed line (index n_el: 0, so the exclusive scans end in totals)
+// scan inputs per packed line (index n_el: 0, so the exclusive scans end in
+// totals).  *wide is raised for a line whose IP length or event count does
+// not fit bjx_event_line's 16-bit fields (the batch then fails with
+// BJX_ERR_CAPACITY instead of packing a truncated key)
 __global__ void k_pack_prep(uint64_t n_el, const uint32_t *__restrict__ line, const uint64_t *__restrict__ counts,
-                            const uint32_t *__restrict__ ip_len, uint64_t *__restrict__ nev, uint64_t *__restrict__ ipl) {
+                            const uint32_t *__restrict__ ip_len, uint64_t *__restrict__ nev, uint64_t *__restrict__ ipl,
+                            unsigned long long *__restrict__ wide) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p > n_el) return;
   if (p == n_el) { nev[p] = 0; ipl[p] = 0; return; }
   const uint32_t j = line[p];
   nev[p] = counts[j] & 0xFFFFFFFFull;
   ipl[p] = ip_len[j];
+  if (nev[p] > 0xFFFFu || ip_len[j] > 0xFFFFu) atomicOr(wide, 1ull);
 }
 
 // first packed index of each owner (keys sorted); start[] preset to n_el
@@ -4674,10 +4026,6 @@ struct bjx_engine {
   std::mutex mu;
   std::string last_error;
   hipStream_t stream = nullptr;
-  // IP pre-lookup (k_ip_lookup) on its own stream beside the DFA jobs
-  hipStream_t aux = nullptr;
-  hipEvent_t ev_lines = nullptr, ev_lookup = nullptr;
-  bool pre_looked = false;  // this batch's el_id holds the pre-lookup (k_ip_claim skips resolved lines)
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evm0 = nullptr, evm1 = nullptr;
   hipEvent_t evk[4] = {};      // k_lines launch, DFA-job sort + k_dfa / k_nfa (bench: per-kernel roofline)
   double kernel_ms[3] = {};   // last batch: k_scan, k_lines, DFA jobs
@@ -4725,10 +4073,9 @@ struct bjx_engine {
   DevBuf<int32_t> l_hid;
   DevBuf<uint64_t> l_cand;
   DevBuf<uint4> l_ip16;
-  DevBuf<uint32_t> long_list;
   DevBuf<uint32_t> jline, jkey, jidx, jidx2, jkey2;  // jobs by slot (line, key, slot), the sorted keys and slots
   DevBuf<uint64_t> jrec;                           // job window records by slot (kJob*)
-  uint64_t last_jobs = 0, last_todo = 0, last_long_runs = 0;
+  uint64_t last_jobs = 0, last_long_runs = 0;
   DevBuf<uint64_t> long_heads;
   DevBuf<uint64_t> lr_end, lr_len, lr_off, lr_win;
   DevBuf<unsigned long long> chk;
@@ -4739,16 +4086,8 @@ struct bjx_engine {
   DevBuf<int64_t> lr_t0, lr_h0;
   DevBuf<uint32_t> lr_flags, lr_nwin;
   DevBuf<unsigned long long> long_count;
-  uint32_t scan_lds[2][2] = {{0, 0}, {0, 0}};
+  uint32_t scan_lds[2] = {0, 0};
   bool lines_attr = false;
-  // k_scan's in-kernel line index (group_wait): lines per byte of the batches
-  // so far (sizes the per-line arrays),
-  // off for an engine that shares its GPU with another one that may run
-  // concurrently (bjx_engine_set_scan_lookback), batches done again two-pass
-  double lines_per_byte = 1.0 / 128;  // access-log lines are rarely shorter; shorter ones redo the batch two-pass
-  bool scan_lookback = getenv("BJX_LOOKBACK") && atoi(getenv("BJX_LOOKBACK")) == 1;
-  uint64_t lb_fallbacks = 0;
-  DevBuf<unsigned long long> tstat, lbprof;
   DevBuf<CandMeta> l_ccnt;
   DevBuf<uint64_t> l_cfirst;  // Lines::cand_first
   unsigned long long scan_stats[6] = {0, 0, 0, 0, 0, 0};
@@ -4757,12 +4096,10 @@ struct bjx_engine {
   DevBuf<unsigned long long> scalars;  // [0] slow count, [1..2] bounds, [3] selected
   DevBuf<uint64_t> res_seq;
   bool res_written = false;  // the last match phase wrote the RuleResult arrays
-  bool ev_arrays = false;    // ... and the per-event line / rule arrays (ev_el, ev_rule)
   DevBuf<uint32_t> res_rule, ev_el, ev_rule, ev_res, ev_st, ev_st2, ev_idx, ev_idx2, el_slot, coll, trip_idx;
   DevBuf<EvRec> ev_rec, ev_rec2;  // EvRec12 records when rec12 (the last rate-limit stage's form), from rec_base
   bool rec12 = false;
   int64_t rec_base = 0;
-  DevBuf<uint64_t> trip_evr, trip_evr2;  // trips as (event << 32 | rule) (batches without per-event arrays)
   DevBuf<uint32_t> el_id;
   DevBuf<uint32_t> el_new;  // event lines with a new IP (k_ip_claim -> k_ip_commit)
   DevBuf<uint8_t> rl_out, ev_out, ev_out_s, trip_flag;
@@ -5055,6 +4392,10 @@ static bool split_at_host(const PrefLit &pl, const std::string &h, PrefLit *piec
 
 void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, size_t sample_n) {
   if (e->bound_uid == rs->uid && e->bound_dec_version == e->decisions_version) return;
+  // DFA job keys: a rule id (windowed jobs r, legacy n_rules + r, null jobs
+  // 2 n_rules) in the low 24 bits, the rule's position above them
+  if (rs->rules.size() >= (1u << 23))
+    throw BjxError(BJX_ERR_TOO_COMPLEX, "ruleset of 2^23 rules or more (DFA job keys hold 2 * n_rules in 24 bits)");
   // host dictionary: per-site hosts, skip hosts, allow-list sites
   std::map<std::string, uint32_t> hosts;
   auto host_id = [&](const std::string &h) {
@@ -6144,9 +5485,6 @@ extern "C" int bjx_engine_create(int device, const bjx_engine_options *opts, bjx
     e->device = device;
     HIP_OK(hipSetDevice(device));
     HIP_OK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-    HIP_OK(hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking));
-    HIP_OK(hipEventCreateWithFlags(&e->ev_lines, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&e->ev_lookup, hipEventDisableTiming));
     HIP_OK(hipEventCreate(&e->ev0));
     HIP_OK(hipEventCreate(&e->ev1));
     HIP_OK(hipEventCreate(&e->evm0));
@@ -6177,11 +5515,11 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   for (auto *b : {&e->staging, &e->l_flags, &e->ev_out, &e->rl_out, &e->trip_flag, &e->bind_blob,
                   &e->cub_tmp, &e->q_ip})
     b->release();
-  e->tile_counts.release(); e->tile_base.release(); e->tstat.release(); e->nl.release(); e->l_ts.release(); e->l_iph.release();
+  e->tile_counts.release(); e->tile_base.release(); e->nl.release(); e->l_ts.release(); e->l_iph.release();
   e->l_counts.release(); e->l_offs.release(); e->l_masks.release(); e->l_ipoff.release(); e->l_iplen.release();
   e->l_hoff.release(); e->l_hlen.release(); e->l_roff.release(); e->slow_list.release(); e->l_hid.release();
   e->scalars.release(); e->res_seq.release(); e->res_rule.release(); e->ev_el.release(); e->ev_rule.release();
-  e->trip_evr.release(); e->trip_evr2.release();
+
   e->ev_res.release(); e->ev_st.release(); e->ev_st2.release(); e->ev_idx.release(); e->ev_idx2.release();
   e->el_slot.release(); e->coll.release(); e->el_new.release(); e->ev_rec.release(); e->ev_rec2.release(); e->el_id.release();
 
@@ -6202,27 +5540,15 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   e->d_results.release(); e->q_out.release();
   e->ban_ips.release(); e->ban_log.release(); e->ban_off.release(); e->ban_kind.release(); e->ban_ipb.release();
   e->ban_ipo.release();
-  e->long_list.release(); e->l_ip16.release(); e->jline.release(); e->jkey.release(); e->jidx.release(); e->jidx2.release(); e->jrec.release(); e->jkey2.release(); e->l_cand.release(); e->l_ccnt.release(); e->l_cfirst.release();
+  e->l_ip16.release(); e->jline.release(); e->jkey.release(); e->jidx.release(); e->jidx2.release(); e->jrec.release(); e->jkey2.release(); e->l_cand.release(); e->l_ccnt.release(); e->l_cfirst.release();
   (void)hipEventDestroy(e->ev0); (void)hipEventDestroy(e->ev1); (void)hipEventDestroy(e->evm0); (void)hipEventDestroy(e->evm1);
   for (auto &x : e->evk) (void)hipEventDestroy(x);
   for (auto &x : e->ph) (void)hipEventDestroy(x);
   (void)hipStreamDestroy(e->stream);
-  if (e->aux) (void)hipStreamDestroy(e->aux);
-  if (e->ev_lines) (void)hipEventDestroy(e->ev_lines);
-  if (e->ev_lookup) (void)hipEventDestroy(e->ev_lookup);
   delete e;
 }
 
 extern "C" const char *bjx_engine_last_error(bjx_engine *e) { return e ? e->last_error.c_str() : "no engine"; }
-
-// k_scan's newline look-back needs its whole grid resident; an engine that
-// shares its GPU with another engine running concurrently (bjx_node with
-// repeated devices) uses the two-pass count instead
-extern "C" int bjx_engine_set_scan_lookback(bjx_engine *e, int on) {
-  if (!e) return BJX_ERR_ARG;
-  e->scan_lookback = on != 0;
-  return BJX_OK;
-}
 
 extern "C" int bjx_engine_set_decision_lists(bjx_engine *e, const bjx_decision_entry *entries, size_t n) {
   if (!e || (n && !entries)) return BJX_ERR_ARG;
@@ -6261,98 +5587,6 @@ static void mark(bjx_engine *e, int k) {
 // RegexRateLimitStates.Apply for n_ev events (reference order) whose lines are
 // E; writes e->ev_out[k].  n_el / el_bytes bound the new IPs / arena bytes.
 // Phases 5 (IP + state slots), 6 (sort), 7 (automaton).
-// The claims of a local batch per line (k_line_claim: IP, then the states of
-// the lines whose IP is known; k_ip_commit / k_ip_collide for the IPs new in
-// this batch, then k_line_st_claim over their lines).  An IP-table overflow
-// rolls back both tables' claims of the batch; a state-table overflow rolls
-// back the states and claims them again for every event line.
-static void rl_claims_lines(bjx_engine *e, const Bind &B, const EvSrc &E, const Lines &L, const uint64_t *offs, uint64_t n_el,
-                            uint64_t n_ev, uint32_t epoch) {
-  hipStream_t st = e->stream;
-  uint64_t nw_ovf[4] = {0, 0, 0, 0};  // counters 4 (new-IP lines), 5 (IP overflow), 6, 7 (state overflow)
-  auto st_rollback = [&]() {
-    HIP_OK(hipMemsetAsync(e->S.counters + 2, 0, 8, st));
-    hipLaunchKernelGGL(k_st_rollback, dim3(grid_for(e->st_cap)), dim3(kBlock), 0, st, e->st_cap, e->S);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipMemsetAsync(e->S.ip_st, 0xFF, e->S.ip_st_cap * 4, st));  // may name rolled-back slots
-    read_counters(e);
-  };
-  bool forced_st = false;
-  for (int attempt = 0;; ++attempt) {
-    const uint64_t n_ips = e->host_counters[0], n_st = e->host_counters[2];
-    HIP_OK(hipMemsetAsync(e->S.counters + 3, 0, 5 * 8, st));
-    HIP_OK(hipMemsetAsync(e->S.counters + kShardBase, 0, kClaimShards * 128, st));
-    uint64_t budget = e->ip_cap * 3 / 4 - n_ips, st_budget = e->st_cap * 3 / 4 - n_st;
-    const bool forced = e->dbg_budget && attempt == 0 && e->dbg_budget < budget;  // test hook
-    if (forced) budget = e->dbg_budget;
-    forced_st = e->dbg_budget && attempt == 0 && e->dbg_budget < st_budget;
-    if (forced_st) st_budget = e->dbg_budget;
-    hipLaunchKernelGGL(k_line_claim, dim3(grid_for(E.n)), dim3(kBlock), 0, st, B, E, L, offs, e->S, epoch, e->el_slot.p,
-                       e->el_id.p, e->el_new.p, budget / kClaimShards, e->ev_st.p, e->ev_rec.p, st_budget / kClaimShards);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(nw_ovf, e->S.counters + 4, 32, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    if (!nw_ovf[1]) break;
-    // more new IPs than the table had room for: undo both tables' claims, grow, claim again
-    hipLaunchKernelGGL(k_ip_rollback, dim3(grid_for(e->ip_cap)), dim3(kBlock), 0, st, e->ip_cap, e->S, epoch);
-    HIP_OK(hipGetLastError());
-    st_rollback();
-    if (!forced) grow_ip(e, attempt >= 2 ? n_ips + n_el : std::min<uint64_t>(n_ips + n_el, 4 * (e->ip_cap * 3 / 4)));
-  }
-  if (nw_ovf[0]) {
-    hipLaunchKernelGGL(k_ip_commit, dim3(grid_for(nw_ovf[0])), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p,
-                       e->el_new.p, nw_ovf[0], e->coll.p);
-    HIP_OK(hipGetLastError());
-  }
-  uint64_t n_coll = 0;
-  HIP_OK(hipMemcpyAsync(&n_coll, e->S.counters + 3, 8, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
-  if (n_coll) {  // distinct IPs with one 64-bit hash in this batch: resolve exactly, in line order
-    if (n_coll > 1) {
-      uint32_t *ki = e->coll.p, *ko = e->ev_st2.p;
-      cub_call(e, [&](void *tmp, size_t &bytes) {
-        return hipcub::DeviceRadixSort::SortKeys(tmp, bytes, ki, ko, (int)n_coll, 0, 32, st);
-      });
-      HIP_OK(hipMemcpyAsync(e->coll.p, e->ev_st2.p, n_coll * 4, hipMemcpyDeviceToDevice, st));
-    }
-    hipLaunchKernelGGL(k_ip_collide, dim3(1), dim3(64), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p, e->coll.p, n_coll);
-    HIP_OK(hipGetLastError());
-  }
-  // the states: the new IPs' lines (their state shard counts add to the first
-  // launch's), or, after an overflow, every event line again
-  bool all = nw_ovf[3] != 0;
-  for (int attempt = 0;; ++attempt) {
-    uint64_t ovf = 0;
-    if (all) {
-      st_rollback();
-      if (!forced_st || attempt > 0)
-        grow_st(e, attempt >= 2 ? e->host_counters[2] + n_ev
-                                : std::min<uint64_t>(e->host_counters[2] + n_ev, 4 * (e->st_cap * 3 / 4)));
-      forced_st = false;
-      HIP_OK(hipMemsetAsync(e->S.counters + 6, 0, 2 * 8, st));
-      HIP_OK(hipMemsetAsync(e->S.counters + kShardBase, 0, kClaimShards * 128, st));
-      const uint64_t budget = e->st_cap * 3 / 4 - e->host_counters[2];
-      hipLaunchKernelGGL(k_line_st_claim, dim3(grid_for(E.n)), dim3(kBlock), 0, st, B, E, L, offs, e->S,
-                         (const uint32_t *)nullptr, (uint64_t)0, e->el_slot.p, e->el_id.p, e->ev_st.p, e->ev_rec.p,
-                         budget / kClaimShards);
-    } else if (nw_ovf[0]) {
-      const uint64_t budget = e->st_cap * 3 / 4 - e->host_counters[2];
-      hipLaunchKernelGGL(k_line_st_claim, dim3(grid_for(nw_ovf[0])), dim3(kBlock), 0, st, B, E, L, offs, e->S,
-                         e->el_new.p, nw_ovf[0], e->el_slot.p, e->el_id.p, e->ev_st.p, e->ev_rec.p,
-                         (forced_st ? e->dbg_budget : budget) / kClaimShards);
-    }
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(&ovf, e->S.counters + 7, 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    if (!ovf) {
-      hipLaunchKernelGGL(k_fold_claims, dim3(1), dim3(kClaimShards), 0, st, e->S);
-      HIP_OK(hipGetLastError());
-      break;
-    }
-    all = true;  // more new (ip, rule name) states than the table had room for
-  }
-}
-
 // the event sort (state slot keys, records as values) and the Apply kernels,
 // for either record form
 template <typename Rec>
@@ -6441,22 +5675,17 @@ static void rl_sort_apply(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t
   }
 }
 
-// Lp / offs (a local batch): claims per line from the match masks
-// (k_line_claim, k_line_st_claim) instead of per event (ev_el / ev_rule).
 // rec_base (kNoRecBase: none): the events' timestamps are expected within
 // 2^43 ns of it either way, so the sort carries 12-B records (EvRec12).
 constexpr int64_t kNoRecBase = INT64_MIN;
 static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t n_el, uint64_t el_bytes, uint64_t n_ev,
-                             const uint32_t *ev_el, const uint32_t *ev_rule, int64_t rec_base, const Lines *Lp = nullptr,
-                             const uint64_t *offs = nullptr) {
+                             const uint32_t *ev_el, const uint32_t *ev_rule, int64_t rec_base) {
   hipStream_t st = e->stream;
   const bool force16 = getenv("BJX_REC16") != nullptr;  // test hook: the 16-B records throughout
-  bool use12 = !Lp && rec_base != kNoRecBase && B.n_rules < (1u << EvRec12::kRuleBits) && !force16;
+  bool use12 = rec_base != kNoRecBase && B.n_rules < (1u << EvRec12::kRuleBits) && !force16;
   if (use12) rec_base = (int64_t)((uint64_t)rec_base - (EvRec12::kSpan >> 1));
   else rec_base = 0;
   if (E.n >= 0x7FFFFFFFull || n_ev >= 0xFFFFFFFFull) throw BjxError(BJX_ERR_ARG, "batch too large (2^31 lines / 2^32 events)");
-  // the pre-lookup reads the IP table: done before any growth or claim
-  if (e->pre_looked) HIP_OK(hipStreamWaitEvent(st, e->ev_lookup, 0));
   read_counters(e);
   ensure_capacity(e, std::min<uint64_t>(n_el, std::max<uint64_t>(1u << 18, e->host_counters[0] / 8)), el_bytes,
                   std::min<uint64_t>(n_ev, std::max<uint64_t>(1u << 20, e->host_counters[2] / 8)));
@@ -6468,9 +5697,7 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
   e->ev_st.ensure(n_ev); e->ev_st2.ensure(n_ev); e->ev_rec.ensure(n_ev); e->ev_rec2.ensure(n_ev);
   e->ev_out.ensure(n_ev); e->ev_out_s.ensure(n_ev);
   mark(e, 5);
-  if (Lp) {
-    rl_claims_lines(e, B, E, *Lp, offs, n_el, n_ev, epoch);
-  } else {
+  {
     for (int attempt = 0;; ++attempt) {
       const uint64_t n_ips = e->host_counters[0];
       HIP_OK(hipMemsetAsync(e->S.counters + 3, 0, 3 * 8, st));
@@ -6481,7 +5708,7 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
       // a retry after an overflow claims every line again (the rolled-back
       // claims left their lines' el_id set)
       hipLaunchKernelGGL(k_ip_claim, dim3(grid_for(E.n)), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p,
-                         e->el_new.p, budget / kClaimShards, e->pre_looked && attempt == 0 ? 1u : 0u);
+                         e->el_new.p, budget / kClaimShards);
       HIP_OK(hipGetLastError());
       HIP_OK(hipMemcpyAsync(nw_ovf, e->S.counters + 4, 16, hipMemcpyDeviceToHost, st));
       HIP_OK(hipStreamSynchronize(st));
@@ -6622,25 +5849,10 @@ static void run_nfa_jobs(bjx_engine *e, const Bind &B, const uint8_t *buf, uint6
 // consumeLine up to Apply for every line: framing, header, exemption, rule
 // matching, RuleResults and events in reference order (phases 0-4).  Leaves
 // the batch context in e->bc; false if the batch has no complete line.
-// BJX_FUSED_CLAIM=1: claims per line from the match masks (k_line_claim,
-// k_line_st_claim) instead of per event (k_emit, k_ip_claim, k_st_claim).  Off
-// by default: slower at cfg3 (profiles/r04_b: claims 11.6 ms + emit 1.2 against
-// 8.2 + 2.8; the serial per-line event loop's dependent loads)
-static bool fused_claims() {
-  static const bool on = getenv("BJX_FUSED_CLAIM") && atoi(getenv("BJX_FUSED_CLAIM")) == 1;
-  return on;
-}
-
-// need_ev: the per-event line / rule arrays are wanted (the node exchange);
-// a local batch without RuleResult copies claims from the per-line masks
 static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns, uint32_t flags,
-                        bjx_batch_result *out, bool need_ev = true) {
+                        bjx_batch_result *out) {
   e->bc = BatchCtx{};
   HIP_OK(hipSetDevice(e->device));
-  // a previous batch's pre-lookup (side stream) is done before this batch
-  // rewrites the line arrays it read
-  if (e->aux) HIP_OK(hipStreamWaitEvent(e->stream, e->ev_lookup, 0));
-  e->pre_looked = false;
   if (e->bound_uid != rs->uid || e->bound_dec_version != e->decisions_version) {
     // (re)binding: calibrate the gram filter on the head of this batch
     const size_t sn = std::min<size_t>(n, 4u << 20);
@@ -6672,153 +5884,90 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   for (auto &r : e->phase_rec) r = false;
   mark(e, 0);
 
-  // ---- line framing, two-pass by default: pass A counts the '\n' of each
-  // 4 KB wave tile and an exclusive scan gives every tile its first line
-  // index.  With the look-back (bjx_engine_set_scan_lookback, BJX_LOOKBACK=1)
-  // k_scan counts the newlines before each tile itself (group_wait), the
-  // per-line arrays sized from the lines per byte seen so far; a batch with
-  // more lines than that, or a wait that ran too long, is done again
-  // two-pass.
+  // ---- line framing, two passes: pass A counts the '\n' of each 4 KB wave
+  // tile and an exclusive scan gives every tile its first line index
+  // (the two in-kernel line-index designs measured slower)
   const uint64_t n_tiles = (n + kWT - 1) / kWT;
   e->tile_counts.ensure(n_tiles);
   e->tile_base.ensure(n_tiles + 1);
   uint64_t n_lines = 0;
   Lines L;
-  bool scan_hdr = false;
-  for (int pass = 0;; ++pass) {
-    const bool lb = e->scan_lookback && pass == 0;
-    uint64_t cap = 0;
-    if (lb) {
-      cap = (uint64_t)((double)n * e->lines_per_byte * 1.25) + 65536;
-      cap = std::max<uint64_t>(cap, e->nl.n);
-    } else {
-      hipLaunchKernelGGL(k_nl_count_wt, dim3((unsigned)((n_tiles + 3) / 4)), dim3(kBlock), 0, st, buf, (uint64_t)n, n_tiles,
-                         e->tile_counts.p);
-      HIP_OK(hipGetLastError());
-      {
-        uint32_t *in = e->tile_counts.p;
-        uint64_t *o = e->tile_base.p;
-        cub_call(e, [&](void *tmp, size_t &bytes) {
-          return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)n_tiles, st);
-        });
-      }
-      uint64_t last_base = 0;
-      uint32_t last_cnt = 0;
-      HIP_OK(hipMemcpyAsync(&last_base, e->tile_base.p + (n_tiles - 1), 8, hipMemcpyDeviceToHost, st));
-      HIP_OK(hipMemcpyAsync(&last_cnt, e->tile_counts.p + (n_tiles - 1), 4, hipMemcpyDeviceToHost, st));
-      HIP_OK(hipStreamSynchronize(st));
-      n_lines = last_base + last_cnt;
-      out->n_lines = n_lines;
-      if (n_lines == 0) return false;
-      cap = n_lines;
-    }
+  hipLaunchKernelGGL(k_nl_count_wt, dim3((unsigned)((n_tiles + 3) / 4)), dim3(kBlock), 0, st, buf, (uint64_t)n, n_tiles,
+                     e->tile_counts.p);
+  HIP_OK(hipGetLastError());
+  {
+    uint32_t *in = e->tile_counts.p;
+    uint64_t *o = e->tile_base.p;
+    cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)n_tiles, st); });
+  }
+  {
+    uint64_t last_base = 0;
+    uint32_t last_cnt = 0;
+    HIP_OK(hipMemcpyAsync(&last_base, e->tile_base.p + (n_tiles - 1), 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(&last_cnt, e->tile_counts.p + (n_tiles - 1), 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    n_lines = last_base + last_cnt;
+  }
+  out->n_lines = n_lines;
+  if (n_lines == 0) return false;
+  const uint64_t cap = n_lines;
 
-    // ---- per-line arrays
-    e->nl.ensure(cap);
-    e->l_ts.ensure(cap); e->l_iph.ensure(cap); e->l_counts.ensure(cap + 1); e->l_offs.ensure(cap + 1);
-    e->l_masks.ensure(cap * B.mask_words);
-    e->l_ipoff.ensure(cap); e->l_iplen.ensure(cap); e->l_hoff.ensure(cap); e->l_hlen.ensure(cap);
-    e->l_roff.ensure(cap); e->l_hid.ensure(cap); e->l_flags.ensure(cap); e->slow_list.ensure(cap);
-    e->long_list.ensure(cap); e->l_ccnt.ensure(cap); e->l_ip16.ensure(cap);
-    e->l_cand.ensure(B.any_prefilter ? cap * kCandSlots : 1);
-    e->scalars.ensure(16);
-    L.ts = e->l_ts.p; L.ip_hash = e->l_iph.p; L.ip_off = e->l_ipoff.p; L.ip_len = e->l_iplen.p; L.host_off = e->l_hoff.p;
-    L.host_len = e->l_hlen.p; L.rest_off = e->l_roff.p; L.host_id = e->l_hid.p; L.flags = e->l_flags.p;
-    L.counts = e->l_counts.p; L.masks = e->l_masks.p;
-    L.cand_meta = e->l_ccnt.p; L.cand = e->l_cand.p; L.ip16 = e->l_ip16.p;
-    L.cand_first = nullptr;
-    if (B.cfirst) {
-      e->l_cfirst.ensure(cap * kCandFirstLits);
-      L.cand_first = e->l_cfirst.p;
-      HIP_OK(hipMemsetAsync(e->l_cfirst.p, 0xFF, cap * kCandFirstLits * 8, st));
-    }
-    e->jline.ensure(std::max<uint64_t>(e->jline.n, cap + (1u << 20)));
-    e->jkey.ensure(e->jline.n); e->jidx.ensure(e->jline.n); e->jrec.ensure(e->jline.n);
-    HIP_OK(hipMemsetAsync(e->scalars.p, 0, 16 * sizeof(unsigned long long), st));
-    if (B.any_prefilter) HIP_OK(hipMemsetAsync(e->l_ccnt.p, 0, cap * sizeof(CandMeta), st));
-    // BJX_SCAN_HEADER=1: the scan pass parses the header of every line that fits
-    // its window and k_rules decides their rules (the others keep kLineTodo for
-    // k_lines).  Off by default: measured slower at cfg3 (profiles/r02_v2: scan
-    // +19 ms, k_rules 24.8 ms against k_lines 30.4 ms), the rule decisions'
-    // reads of line bytes from HBM outweigh the saved staging.
-    static const bool scan_hdr_env = getenv("BJX_SCAN_HEADER") && atoi(getenv("BJX_SCAN_HEADER")) == 1;
-    scan_hdr = scan_hdr_env;
-    if (scan_hdr) HIP_OK(hipMemsetAsync(e->l_flags.p, kLineTodo, cap, st));
+  // ---- per-line arrays
+  e->nl.ensure(cap);
+  e->l_ts.ensure(cap); e->l_iph.ensure(cap); e->l_counts.ensure(cap + 1); e->l_offs.ensure(cap + 1);
+  e->l_masks.ensure(cap * B.mask_words);
+  e->l_ipoff.ensure(cap); e->l_iplen.ensure(cap); e->l_hoff.ensure(cap); e->l_hlen.ensure(cap);
+  e->l_roff.ensure(cap); e->l_hid.ensure(cap); e->l_flags.ensure(cap); e->slow_list.ensure(cap);
+  e->l_ccnt.ensure(cap); e->l_ip16.ensure(cap);
+  e->l_cand.ensure(B.any_prefilter ? cap * kCandSlots : 1);
+  e->scalars.ensure(16);
+  L.ts = e->l_ts.p; L.ip_hash = e->l_iph.p; L.ip_off = e->l_ipoff.p; L.ip_len = e->l_iplen.p; L.host_off = e->l_hoff.p;
+  L.host_len = e->l_hlen.p; L.rest_off = e->l_roff.p; L.host_id = e->l_hid.p; L.flags = e->l_flags.p;
+  L.counts = e->l_counts.p; L.masks = e->l_masks.p;
+  L.cand_meta = e->l_ccnt.p; L.cand = e->l_cand.p; L.ip16 = e->l_ip16.p;
+  L.cand_first = nullptr;
+  if (B.cfirst) {
+    e->l_cfirst.ensure(cap * kCandFirstLits);
+    L.cand_first = e->l_cfirst.p;
+    HIP_OK(hipMemsetAsync(e->l_cfirst.p, 0xFF, cap * kCandFirstLits * 8, st));
+  }
+  e->jline.ensure(std::max<uint64_t>(e->jline.n, cap + (1u << 20)));
+  e->jkey.ensure(e->jline.n); e->jidx.ensure(e->jline.n); e->jrec.ensure(e->jline.n);
+  HIP_OK(hipMemsetAsync(e->scalars.p, 0, 16 * sizeof(unsigned long long), st));
+  if (B.any_prefilter) HIP_OK(hipMemsetAsync(e->l_ccnt.p, 0, cap * sizeof(CandMeta), st));
+  mark(e, 1);
+
+  // ---- the scan kernel: line framing + literal hits; one block (16 waves)
+  // per CU, grid-stride over the wave tiles
+  {
     int n_cu_scan = 0;
     HIP_OK(hipDeviceGetAttribute(&n_cu_scan, hipDeviceAttributeMultiprocessorCount, e->device));
-    // one block (16 waves) per CU: the whole grid resident, as the in-kernel line index needs
     const unsigned scan_grid = (unsigned)std::min<uint64_t>((n_tiles + kScanWaves - 1) / kScanWaves, (uint64_t)std::max(1, n_cu_scan));
-    if (lb) {
-      e->tstat.ensure((uint64_t)kRing * scan_grid);
-      HIP_OK(hipMemsetAsync(e->tstat.p, 0, (uint64_t)kRing * scan_grid * 8, st));
+    ScanArgs A;
+    A.buf = buf; A.n = n; A.n_tiles = n_tiles; A.n_lines = cap; A.tile_base = e->tile_base.p; A.nl = e->nl.p;
+    A.L = L; A.stats = e->scalars.p + 8;
+    A.debug_skip = getenv("BJX_DEBUG_SKIP") ? (uint32_t)atoi(getenv("BJX_DEBUG_SKIP")) : 0u;
+    // block-shared LDS: gram bitset, the lookup image when it fits, then 16 wave regions
+    const uint32_t fixed = kGramWords * 4 + kScanWaves * kWaveLds;
+    const bool img_lds = fixed + B.img_bytes <= kScanLdsMax;
+    A.shared_bytes = kGramWords * 4 + (img_lds ? B.img_bytes : 0);
+    const uint32_t lds = A.shared_bytes + kScanWaves * kWaveLds;
+    using ScanFn = void (*)(Bind, ScanArgs);
+    const ScanFn kfn = img_lds ? k_scan<true> : k_scan<false>;
+    if (lds != e->scan_lds[img_lds]) {
+      HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      e->scan_lds[img_lds] = lds;
     }
-    mark(e, 1);
-
-    // ---- the scan kernel (the hot, HBM-bound kernel): line framing + literal hits
-    {
-      ScanArgs A;
-      A.buf = buf; A.n = n; A.n_tiles = n_tiles; A.n_lines = cap; A.tile_base = e->tile_base.p; A.nl = e->nl.p;
-      A.L = L; A.stats = e->scalars.p + 8;
-      static const bool lbprof = getenv("BJX_LB_PROF") != nullptr;
-      A.lbprof = nullptr;
-      if (lbprof && lb) {
-        e->lbprof.ensure(4);
-        HIP_OK(hipMemsetAsync(e->lbprof.p, 0, 32, st));
-        A.lbprof = e->lbprof.p;
-      }
-      A.debug_skip = getenv("BJX_DEBUG_SKIP") ? (uint32_t)atoi(getenv("BJX_DEBUG_SKIP")) : 0u;
-      A.hdr = scan_hdr ? 1u : 0u;
-      A.now_ns = now_ns;
-      A.tstat = lb ? e->tstat.p : nullptr;
-      A.lines_out = e->scalars.p + 6;
-      A.lb_abort = e->scalars.p + 7;
-      // block-shared LDS: gram bitset, the lookup image when it fits, then 16 wave regions
-      // (and the block's ScanGroup with the in-kernel line index)
-      const uint32_t grp = lb ? kScanGroupLds : 0u;
-      const uint32_t fixed = kGramWords * 4 + kScanWaves * kWaveLds + grp;
-      const bool img_lds = fixed + B.img_bytes <= kScanLdsMax;
-      A.shared_bytes = kGramWords * 4 + (img_lds ? B.img_bytes : 0);
-      const uint32_t lds = A.shared_bytes + kScanWaves * kWaveLds + grp;
-      using ScanFn = void (*)(Bind, ScanArgs);
-      const ScanFn fns[2][2] = {{k_scan<false, false>, k_scan<false, true>}, {k_scan<true, false>, k_scan<true, true>}};
-      const ScanFn kfn = fns[img_lds][lb];
-      if (lds != e->scan_lds[img_lds][lb]) {
-        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        e->scan_lds[img_lds][lb] = lds;
-      }
-      HIP_OK(hipEventRecord(e->evm0, st));
-      hipLaunchKernelGGL(kfn, dim3(scan_grid), dim3(kScanWaves * 64), lds, st, B, A);
-      HIP_OK(hipGetLastError());
-      HIP_OK(hipEventRecord(e->evm1, st));
-    }
-    if (lb) {
-      unsigned long long r[2] = {0, 0};
-      HIP_OK(hipMemcpyAsync(r, e->scalars.p + 6, 16, hipMemcpyDeviceToHost, st));
-      HIP_OK(hipStreamSynchronize(st));
-      if (e->lbprof.p && getenv("BJX_LB_PROF")) {
-        unsigned long long q[4];
-        HIP_OK(hipMemcpy(q, e->lbprof.p, 32, hipMemcpyDeviceToHost));
-        fprintf(stderr, "lbprof wait %.3f count %.3f publish %.3f loop %.3f (share of wave clocks)\n", (double)q[0] / q[3],
-                (double)q[1] / q[3], (double)q[2] / q[3], 1.0);
-      }
-      if (r[1] || r[0] > cap) {  // the look-back gave up, or more lines than the arrays hold
-        e->lb_fallbacks += 1;
-        if (r[0] > cap && !r[1]) e->lines_per_byte = (double)r[0] / (double)n;
-        continue;
-      }
-      n_lines = r[0];
-      out->n_lines = n_lines;
-      if (n_lines == 0) return false;
-    }
-    const double lpb = (double)n_lines / (double)n;
-    e->lines_per_byte = std::max(e->lines_per_byte * 0.5, lpb);
-    break;
+    HIP_OK(hipEventRecord(e->evm0, st));
+    hipLaunchKernelGGL(kfn, dim3(scan_grid), dim3(kScanWaves * 64), lds, st, B, A);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(e->evm1, st));
   }
   uint64_t last_nl = 0;
   mark(e, 2);
 
-  // ---- rule decisions (k_rules) for the lines the scan parsed; k_lines does
-  // the rest (header past the scan window, exotic timestamps, > 128 rules)
+  // ---- the per-line pass: k_lines2 when the ruleset has its tables, else
+  // k_lines (exotic timestamps go to the per-line fallback either way)
   unsigned long long sc4[5] = {0, 0, 0, 0, 0};
   int n_cu = 0;
   HIP_OK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, e->device));
@@ -6831,8 +5980,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
                           reinterpret_cast<const void *>(&k_lines<false, true, true>),
 #endif
                           reinterpret_cast<const void *>(&k_lines<true, false, true>),
-                          reinterpret_cast<const void *>(&k_lines<false, false, true>),
-                          reinterpret_cast<const void *>(&k_rules<true>), reinterpret_cast<const void *>(&k_rules<false>)})
+                          reinterpret_cast<const void *>(&k_lines<false, false, true>)})
       HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScanLdsMax));
     e->lines_attr = true;
   }
@@ -6855,29 +6003,10 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     A.null_key = 2 * B.n_rules;  // sorts after every job key (windowed r, legacy n_rules + r)
     A.span_bytes = getenv("BJX_SPAN_BYTES") ? (uint32_t)atoi(getenv("BJX_SPAN_BYTES")) & ~15u : kSpanBytes;
     A.list = nullptr; A.n_list = 0; A.prof = nullptr;
-    unsigned long long n_todo = 0;
-    if (scan_hdr) {
-      RulesArgs R;
-      R.buf = buf; R.nl = e->nl.p; R.n_lines = n_lines; R.L = L; R.todo = e->long_list.p; R.todo_count = e->scalars.p + 12;
-      R.jline = A.jline; R.jkey = A.jkey; R.jidx = A.jidx; R.jrec = A.jrec; R.job_count = A.job_count; R.job_cap = A.job_cap;
-      R.job_real = A.job_real; R.null_key = A.null_key;
-      const bool img_lds = B.img_bytes <= kRulesImgMax;
-      const uint32_t lds = ((img_lds ? B.img_bytes : 0) + 15u & ~15u) + (kBlock / 64) * kWaveJobBytes;
-      const void *fn = img_lds ? reinterpret_cast<const void *>(&k_rules<true>) : reinterpret_cast<const void *>(&k_rules<false>);
-      const unsigned grid = resident_grid(fn, lds, n_lines);
-      if (img_lds) hipLaunchKernelGGL(k_rules<true>, dim3(grid), dim3(kBlock), lds, st, B, R);
-      else hipLaunchKernelGGL(k_rules<false>, dim3(grid), dim3(kBlock), lds, st, B, R);
-      HIP_OK(hipGetLastError());
-      HIP_OK(hipMemcpyAsync(&n_todo, e->scalars.p + 12, 8, hipMemcpyDeviceToHost, st));
-      HIP_OK(hipStreamSynchronize(st));
-      A.list = e->long_list.p;
-      A.n_list = n_todo;
-      A.span_bytes = 0;
-    }
     HIP_OK(hipEventRecord(e->evk[0], st));
     // k_lines2 (lines2.h) when the ruleset has its tables; BJX_LINES=1 keeps k_lines
     static const int lines_env = getenv("BJX_LINES") ? atoi(getenv("BJX_LINES")) : 2;
-    const bool use_l2 = !scan_hdr && B.l2_bytes && lines_env != 1 && !getenv("BJX_PROF_LINES") && !A.dbg;
+    const bool use_l2 = B.l2_bytes && lines_env != 1 && !getenv("BJX_PROF_LINES") && !A.dbg;
     if (use_l2) {
       const uint32_t lds = B.l2_bytes + (kL2Block / 64) * kL2WaveLds;
       if (lds != e->lines2_lds) {
@@ -6892,7 +6021,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       if (dbg_img) fprintf(stderr, "[bjx] k_lines2: %u B LDS per block (tables %u), %d blocks per CU, grid %u\n", lds, B.l2_bytes, per_cu, grid);
       hipLaunchKernelGGL(k_lines2, dim3(grid), dim3(kL2Block), lds, st, B, A);
       HIP_OK(hipGetLastError());
-    } else if (!scan_hdr || n_todo) {
+    } else {
       const bool img_lds = B.img_bytes <= kLinesImgMax;
       const bool host_lds = B.hl_bytes != 0;
       const uint32_t fixed = ((img_lds ? B.img_bytes : 0) + 15u & ~15u) + (host_lds ? B.hl_bytes + 15u & ~15u : 0u) +
@@ -6941,7 +6070,6 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       HIP_OK(hipGetLastError());
     }
     HIP_OK(hipEventRecord(e->evk[1], st));
-    e->last_todo = n_todo;
     HIP_OK(hipMemcpyAsync(&last_nl, e->nl.p + (n_lines - 1), 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(sc4, e->scalars.p + 8, 32, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(sc4 + 4, e->scalars.p, 8, hipMemcpyDeviceToHost, st));
@@ -6958,28 +6086,6 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     HIP_OK(hipMemsetAsync(e->scalars.p + 14, 0, 8, st));
   }
   out->consumed_bytes = last_nl + 1;
-  // BJX_IP_PRELOOKUP=1: the IPs of the parsed lines looked up on a side stream
-  // while the DFA jobs run (k_ip_lookup), k_ip_claim then claims only the
-  // unresolved lines; only for this engine's own rate-limit stage, when every
-  // header is parsed by now (no per-line fallback lines) and no test hook
-  // rewrites the IP hashes afterwards.  Off by default: the two did not
-  // overlap (profiles/r04_t8: the lookup's blocks fill the CUs first, the
-  // step 63.5 -> 65.4 ms; a 2-blocks-per-CU lookup grid left it latency-bound,
-  // 13.8 ms, and slowed k_dfa: 69.0 ms)
-  e->pre_looked = false;
-  static const bool pre_env = getenv("BJX_IP_PRELOOKUP") && atoi(getenv("BJX_IP_PRELOOKUP")) == 1;
-  if (pre_env && !need_ev && !scan_hdr && sc4[4] == 0 && !e->dbg_hash_mask && e->ip_cap && e->S.ip && !getenv("BJX_CHECK")) {
-    e->el_id.ensure(n_lines);
-    EvSrc E;
-    E.bytes = buf; E.nl = e->nl.p; E.ip_off = L.ip_off; E.ip_pos = nullptr; E.ip_len = L.ip_len;
-    E.ip_hash = L.ip_hash; E.ts = L.ts; E.counts = L.counts; E.ip16 = L.ip16; E.n = n_lines;
-    HIP_OK(hipEventRecord(e->ev_lines, st));
-    HIP_OK(hipStreamWaitEvent(e->aux, e->ev_lines, 0));
-    hipLaunchKernelGGL(k_ip_lookup, dim3(grid_for(n_lines)), dim3(kBlock), 0, e->aux, E, L.flags, e->S, e->el_id.p);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(e->ev_lookup, e->aux));
-    e->pre_looked = true;
-  }
   // job slots taken (sc4[3]; the chunks' unused ones hold null jobs) and real jobs
   unsigned long long n_jobs = 0;
   HIP_OK(hipMemcpyAsync(&n_jobs, e->scalars.p + 14, 8, hipMemcpyDeviceToHost, st));
@@ -7092,20 +6198,12 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   e->ev_el.ensure(n_ev + 1); e->ev_rule.ensure(n_ev + 1); e->ev_res.ensure(n_ev + 1);
   HIP_OK(hipMemsetAsync(e->scalars.p + 1, 0, 2 * 8, st));
   e->res_written = false;
-  e->ev_arrays = false;
   if (n_res) {
     const bool want_res = (flags & BJX_COPY_RESULTS) != 0;
-    if (!want_res && !need_ev && fused_claims() && !getenv("BJX_CHECK")) {
-      // only the bounds: the claims read the per-line masks (k_line_claim)
-      hipLaunchKernelGGL(k_el_bounds, dim3((unsigned)std::min<uint64_t>(grid_for(n_lines), 4096)), dim3(kBlock), 0, st, n_lines,
-                         L.counts, L.ip_len, e->scalars.p + 1);
-    } else {
-      e->res_written = want_res;
-      e->ev_arrays = true;
-      hipLaunchKernelGGL(k_emit, dim3((unsigned)std::min<uint64_t>(grid_for(n_lines), 4096)), dim3(kBlock), 0, st, B, n_lines, L,
-                         e->l_offs.p, e->res_seq.p, e->res_rule.p, e->ev_el.p, e->ev_rule.p, e->ev_res.p, e->scalars.p + 1,
-                         e->res_written);
-    }
+    e->res_written = want_res;
+    hipLaunchKernelGGL(k_emit, dim3((unsigned)std::min<uint64_t>(grid_for(n_lines), 4096)), dim3(kBlock), 0, st, B, n_lines, L,
+                       e->l_offs.p, e->res_seq.p, e->res_rule.p, e->ev_el.p, e->ev_rule.p, e->ev_res.p, e->scalars.p + 1,
+                       e->res_written);
     HIP_OK(hipGetLastError());
     if (e->res_written) HIP_OK(hipMemsetAsync(e->rl_out.p, 0, n_res, st));
   }
@@ -7285,8 +6383,6 @@ static void emit_bans(bjx_engine *e, uint64_t n, bool records_only) {
 static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, bool sorted) {
   const Bind &B = e->bind;
   hipStream_t st = e->stream;
-  if (e->aux) HIP_OK(hipStreamWaitEvent(st, e->ev_lookup, 0));  // the batch ends after its side-stream work
-  e->pre_looked = false;
   const BatchCtx &c = e->bc;
   const uint64_t n_lines = c.n_lines, n_res = c.n_res, n_ev = c.n_ev;
   const Lines &L = c.L;
@@ -7312,22 +6408,7 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
     if (n_trips) {
       // the selected trips in reference (event) order
       e->trip_ev.ensure(n_trips); e->trip_ev2.ensure(n_trips);
-      if (sorted && !e->ev_arrays) {
-        // no per-event arrays (claims from the line masks): the rule rides with
-        // the event index, the line comes from the lines' event offsets
-        e->trip_evr.ensure(n_trips); e->trip_evr2.ensure(n_trips);
-        hipLaunchKernelGGL(k_trip_events_rules, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_idx.p,
-                           e->ev_rec2.p, e->trip_evr.p);
-        uint64_t *ki = e->trip_evr.p, *ko = e->trip_evr2.p;
-        const int bits = std::max(1, bit_width(n_ev));
-        cub_call(e, [&](void *tmp, size_t &bytes) {
-          return hipcub::DeviceRadixSort::SortKeys(tmp, bytes, ki, ko, (int)n_trips, 32, 32 + bits, st);
-        });
-        e->d_trips.ensure(n_trips);
-        hipLaunchKernelGGL(k_build_trips_offs, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_evr2.p, n_lines,
-                           e->l_offs.p, e->nl.p, L, B.rules, e->d_trips.p);
-        HIP_OK(hipGetLastError());
-      } else {
+      {
       if (sorted)
         hipLaunchKernelGGL(k_trip_events, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_idx.p, ev_words(e),
                            rec_stride(e), e->trip_ev.p);
@@ -7438,14 +6519,10 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
 
 static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns, uint32_t flags,
                       bjx_batch_result *out) {
-  if (!match_phase(e, rs, bytes, n, now_ns, flags, out, false)) return;
+  if (!match_phase(e, rs, bytes, n, now_ns, flags, out)) return;
   if (e->bc.n_ev) {
-    if (fused_claims())
-      rate_limit_stage(e, e->bind, local_evsrc(e), e->bc.n_el, e->bc.el_bytes, e->bc.n_ev, nullptr, nullptr, kNoRecBase, &e->bc.L,
-                       e->l_offs.p);
-    else
-      rate_limit_stage(e, e->bind, local_evsrc(e), e->bc.n_el, e->bc.el_bytes, e->bc.n_ev, e->ev_el.p, e->ev_rule.p,
-                       e->bc.now_ns);
+    rate_limit_stage(e, e->bind, local_evsrc(e), e->bc.n_el, e->bc.el_bytes, e->bc.n_ev, e->ev_el.p, e->ev_rule.p,
+                     e->bc.now_ns);
   }
   finish_phase(e, flags, out, true);
 }
@@ -7507,7 +6584,8 @@ extern "C" int bjx_events_partition(bjx_engine *e, uint32_t n_parts, uint64_t *c
     const uint64_t nl = c.n_lines, n_el = c.n_el;
     e->pk_key.ensure(nl); e->pk_key2.ensure(nl); e->pk_line.ensure(nl); e->pk_line2.ensure(nl);
     e->pk_nev.ensure(n_el + 1); e->pk_ipl.ensure(n_el + 1); e->pk_evoff.ensure(n_el + 1); e->pk_byoff.ensure(n_el + 1);
-    e->pk_start.ensure(n_parts + 1); e->pk_counts.ensure(3 * n_parts); e->pk_bbase.ensure(n_parts);
+    e->pk_start.ensure(n_parts + 1); e->pk_counts.ensure(3 * n_parts + 1); e->pk_bbase.ensure(n_parts);
+    HIP_OK(hipMemsetAsync(e->pk_counts.p + 3 * n_parts, 0, 8, st));
     hipLaunchKernelGGL(k_part_keys, dim3(grid_for(nl)), dim3(kBlock), 0, st, nl, c.L.counts, c.L.ip_hash, n_parts,
                        e->pk_key.p, e->pk_line.p);
     HIP_OK(hipGetLastError());
@@ -7519,7 +6597,7 @@ extern "C" int bjx_events_partition(bjx_engine *e, uint32_t n_parts, uint64_t *c
       });
     }
     hipLaunchKernelGGL(k_pack_prep, dim3(grid_for(n_el + 1)), dim3(kBlock), 0, st, n_el, e->pk_line2.p, c.L.counts,
-                       c.L.ip_len, e->pk_nev.p, e->pk_ipl.p);
+                       c.L.ip_len, e->pk_nev.p, e->pk_ipl.p, reinterpret_cast<unsigned long long *>(e->pk_counts.p + 3 * n_parts));
     HIP_OK(hipGetLastError());
     for (int k = 0; k < 2; ++k) {
       uint64_t *in = k ? e->pk_ipl.p : e->pk_nev.p, *o = k ? e->pk_byoff.p : e->pk_evoff.p;
@@ -7533,7 +6611,13 @@ extern "C" int bjx_events_partition(bjx_engine *e, uint32_t n_parts, uint64_t *c
                        e->pk_byoff.p, e->pk_counts.p, e->pk_bbase.p);
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(counts, e->pk_counts.p, 3 * n_parts * 8, hipMemcpyDeviceToHost, st));
+    uint64_t wide = 0;
+    HIP_OK(hipMemcpyAsync(&wide, e->pk_counts.p + 3 * n_parts, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
+    if (wide) {
+      e->partitioned = false;
+      throw BjxError(BJX_ERR_CAPACITY, "an event line's IP (or event count) exceeds the exchange record's 16-bit field (65535)");
+    }
     uint64_t tl = 0, te = 0;
     for (uint32_t k = 0; k < n_parts; ++k) { tl += counts[3 * k]; te += counts[3 * k + 1]; }
     if (tl != n_el || te != c.n_ev) throw BjxError(BJX_ERR_DEVICE, "internal: partition counts disagree with the batch");
@@ -7916,7 +7000,7 @@ extern "C" size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap)
   if (e->S.counters) read_counters(e);
   const uint64_t v[12] = {e->scan_stats[0], e->scan_stats[1], e->scan_stats[2], e->scan_stats[3], e->scan_stats[4],
                           e->ip_cap, e->host_counters[0], e->st_cap, e->host_counters[2], e->scan_stats[5],
-                          e->last_todo, e->last_long_runs};
+                          0, e->last_long_runs};
   for (size_t k = 0; k < 12 && k < cap; ++k) out[k] = v[k];
   return 12;
 }

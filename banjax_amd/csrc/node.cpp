@@ -571,10 +571,6 @@ extern "C" int bjx_node_create(const int *devices, size_t n_devices, const bjx_e
       rc = BJX_ERR_DEVICE;
     }
   }
-  if (rc == BJX_OK)  // engines sharing a GPU run concurrently: no k_scan look-back for them
-    for (auto &A : n->parts)
-      for (auto &B : n->parts)
-        if (&A != &B && A.dev == B.dev) bjx_engine_set_scan_lookback(A.e, 0);
   if (rc == BJX_OK) {
     // direct xGMI access between every pair of distinct GPUs where the
     // platform offers it (hipMemcpyPeerAsync works either way)

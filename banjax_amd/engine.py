@@ -33,8 +33,14 @@ class BatchOutput:
     @property
     def trips(self):
         if self._trips is None:
+            self._need_full_trips()
             self._trips = [self._res.trips[i] for i in range(self.n_trips)] if self.n_trips else []
         return self._trips
+
+    def _need_full_trips(self):
+        if self.n_trips and not self._res.trips:
+            raise ValueError("this batch was run with compact_trips=True: its trips are in trips_compact(), "
+                             "not in full bjx_trip records")
 
     def trips_compact(self):
         """BJX_TRIPS_COMPACT: numpy uint64 words, line byte offset << 24 | rule index (zero-copy)."""
@@ -48,6 +54,7 @@ class BatchOutput:
         import numpy as np
         if not self.n_trips:
             return np.zeros(0, dtype=np.dtype(_lib.Trip))
+        self._need_full_trips()
         buf = (_lib.Trip * self.n_trips).from_address(C.addressof(self._res.trips.contents))
         return np.ctypeslib.as_array(buf)
 
@@ -263,10 +270,6 @@ class Engine:
     def debug_set_slot_cache(self, on: int):
         """Test hook: state-slot cache on (1), off (0), default (-1), from the next batch."""
         self._check(_lib.lib().bjx_debug_set_slot_cache(self._h, on), "debug_set_slot_cache")
-
-    def set_scan_lookback(self, on: int):
-        """k_scan's newline look-back (on) or the two-pass count (off, the default)."""
-        self._check(_lib.lib().bjx_engine_set_scan_lookback(self._h, on), "set_scan_lookback")
 
     def state_clear(self):
         self._check(_lib.lib().bjx_state_clear(self._h), "state_clear")

@@ -56,11 +56,6 @@ int bjx_debug_set_dfa_state_cap(uint32_t cap);
    block-cooperative NFA (kRuleNfaWide), process-wide; clears the
    compiled-pattern cache. */
 int bjx_debug_force_wide_nfa(int on);
-/* k_scan's newline look-back on, or off (the two-pass count; the default
-   unless BJX_LOOKBACK=1).  Never on for engines sharing a GPU with another
-   engine that may run concurrently (the look-back needs its grid resident as
-   a whole): bjx_node turns it off for them. */
-int bjx_engine_set_scan_lookback(bjx_engine *e, int on);
 #ifdef __cplusplus
 }
 #endif

@@ -158,6 +158,13 @@ def _parse_both(pat):
 
 @pytest.mark.parametrize("name,pat,expect", LIMIT_CASES, ids=[c[0] for c in LIMIT_CASES])
 def test_go_parse_limits(name, pat, expect):
+    """Parity unpinned: the expected boundaries are worked out by hand from
+    Go 1.25's regexp/syntax (parse.go checkSize / checkHeight / maxRunes), and
+    the product (csrc/go_limits.h) and the oracle (oracle/go_limits.c) restate
+    that same reading, so their agreement is not independent evidence.  No
+    reference test and no fixture in /root/reference pins these limits (the
+    image has no Go toolchain to produce one); the rune counts of \\p classes
+    (PL_RUNES) come from the repo's Unicode 15.0 tables."""
     prod, orac = _parse_both(pat)
     # (the two 256-byte buffers truncate a long message differently)
     assert (prod is None) == (orac is None) and (prod or "")[:200] == (orac or "")[:200], (prod, orac)

@@ -139,6 +139,38 @@ def test_node_rejects_chunk_without_newline():
     node.close()
 
 
+def test_node_rejects_oversized_ip_field():
+    """bjx_event_line carries the IP length in 16 bits: a batch with an event
+    line whose IP field is 64 KiB or longer fails with BJX_ERR_CAPACITY rather
+    than keying the owner's state by a truncated IP.  A single engine (no
+    exchange) keys it by every byte, as the oracle does."""
+    from banjax_amd import Engine, Ruleset
+    from banjax_amd._lib import BanjaxGpuError
+    from tests.parity import Pair
+    yml = """
+regexes_with_rates:
+  - rule: "all"
+    regex: ".*"
+    interval: 5
+    hits_per_interval: 1
+    decision: nginx_block
+"""
+    cfg = Config.from_yaml(yml)
+    rs = Ruleset(cfg)
+    big = b"1" * 70_000
+    data = b"1700000000.000 1.2.3.4 GET a.com GET / HTTP/1.1\n1700000000.000 " + big + b" GET a.com GET / HTTP/1.1\n"
+    node = Node([0, 0])
+    with pytest.raises(BanjaxGpuError) as ei:
+        node.process(rs, data, 1700000000 * 10**9)
+    assert ei.value.code == -6 and "65535" in str(ei.value)
+    node.close()
+    eng = Engine(0)
+    pair = Pair(yml, eng)
+    pair.feed(data + data, 1700000000 * 10**9)
+    pair.compare_state(["1.2.3.4", big.decode()])
+    eng.close()
+
+
 def test_node_compact_trips_match_full():
     """A node's BJX_TRIPS_COMPACT words (line offsets rebased to the whole
     batch) equal its full trip records, over three engines."""

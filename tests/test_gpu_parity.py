@@ -646,10 +646,9 @@ def test_dfa_self_loop_acceleration(engine):
 @pytest.mark.parametrize("name,n_lines,batches", [("cfg3", 60_000, 2), ("cfg5", 40_000, 2), ("cfg1", 100_000, 2),
                                                   ("cfg5h", 60_000, 2)])
 def test_workload_trips_only(engine, name, n_lines, batches):
-    """The bench's path: no RuleResult copies, so the state claims read the
-    per-line masks (k_line_claim) and the trips carry their rule from the sorted
-    records (k_build_trips_offs).  States, decisions and the ban log (every trip,
-    in order) against the oracle."""
+    """The bench's path: no RuleResult copies (the events alone feed the
+    claims and the trips).  States, decisions and the ban log (every trip, in
+    order) against the oracle."""
     w = W.scaled(W.ALL[name], n_lines, n_ips=min(W.ALL[name].n_ips, n_lines // 3 + 1))
     pair = Pair(w.rules_yaml, engine)
     per = (n_lines + batches - 1) // batches
@@ -667,7 +666,7 @@ def test_workload_trips_only(engine, name, n_lines, batches):
 
 @pytest.mark.parametrize("budget", [1, 97])
 def test_trips_only_claim_rollback(engine, budget):
-    """k_line_claim's rollback paths (both tables) under the claim-budget hook,
+    """The claims' rollback paths (both tables) under the claim-budget hook,
     on the trip-only path."""
     w = W.scaled(W.CFG5, 24_000, n_ips=8_000)
     engine.debug_set_claim_budget(budget)
@@ -681,30 +680,23 @@ def test_trips_only_claim_rollback(engine, budget):
 
 
 def short_lines(t, n, k):
-    """n lines of ~40 bytes: far more lines per byte than the batches before
-    them, so k_scan's look-back overflows its line arrays and the batch is done
-    again the two-pass way."""
+    """n lines of ~40 bytes: far more lines per byte (and per scan tile) than
+    the batches before them."""
     return b"".join(b"%d 10.%d.0.%d GET s.com GET /%d h\n" % (t, k % 7, i % 50, i % 13) for i in range(n))
 
 
-@pytest.mark.parametrize("lookback", [1, 0])
-def test_scan_lookback_and_two_pass(engine, lookback):
-    """Line framing by k_scan's decoupled look-back and by the two-pass count
-    (default) give the same results: batches of ordinary lines, then a
-    batch of short lines that overflows the look-back's line arrays (redone
-    two-pass), then ordinary lines again."""
+def test_short_line_batches(engine):
+    """Batches of ordinary lines, then a batch of short lines (over 100 lines
+    per 4 KB scan tile), then ordinary lines again: every batch matches the
+    oracle and the per-line arrays follow the line counts."""
     w = W.scaled(W.CFG3, 60_000, n_ips=3_000)
     t = w.now_ns(0, 1) // S
-    engine.set_scan_lookback(lookback)
-    try:
-        pair = Pair(w.rules_yaml, engine)
-        for b in range(2):
-            pair.feed(w.host_lines(b * 20_000, 20_000), w.now_ns(b * 20_000, 20_000))
-        pair.feed(short_lines(t, 30_000, 1), t * S)
-        pair.feed(w.host_lines(40_000, 20_000), w.now_ns(40_000, 20_000))
-        pair.compare_state(["10.1.0.1", "10.1.0.2"])
-    finally:
-        engine.set_scan_lookback(0)
+    pair = Pair(w.rules_yaml, engine)
+    for b in range(2):
+        pair.feed(w.host_lines(b * 20_000, 20_000), w.now_ns(b * 20_000, 20_000))
+    pair.feed(short_lines(t, 30_000, 1), t * S)
+    pair.feed(w.host_lines(40_000, 20_000), w.now_ns(40_000, 20_000))
+    pair.compare_state(["10.1.0.1", "10.1.0.2"])
 
 
 def test_compact_trips_match_full(engine):

@@ -63,8 +63,11 @@ def test_consume_line_hosts_to_skip():
     assert len(st) == 0
     # rest is "GET skiphost.com GET ..." -> "^GET https?://" does not match: no RuleResult at all
     assert res == []
-    # a matching line on a skipped host yields SkipHost and no state
+    # beyond the reference test: "GET skiphost.com GET http://x" still fails
+    # the anchored "^GET https?://" (rest starts at the first method), so no
+    # RuleResult and no state either
     flags, res, _ = st.consume(cfg, line(t0, "1.2.3.4 GET skiphost.com GET http://x HTTP/1.1 x"), int(t0 * 1e9))
+    assert res == [] and flags == [0] and len(st) == 0
     flags, res, _ = st.consume(cfg, line(t0, "1.2.3.4 GET https://a.b GET /x HTTP/1.1 x"), int(t0 * 1e9))
     assert len(res) == 1 and res[0].skip_host == 0 and len(st) == 1
 
