@@ -481,7 +481,8 @@ constexpr int kScanWaves = 16;        // waves per block (one block per CU)
 constexpr uint32_t kTileLds = kWT + kHalo + 16;
 constexpr uint32_t kWaveJobs = 64;   // DFA jobs staged per wave before one global append
 constexpr uint32_t kCandList = 128;   // candidate positions verified per round (one per lane)
-constexpr uint32_t kWaveLds = kTileLds + kLineCap * (2 + 2) + kCandList * 4 + kLineCap * 4;
+constexpr uint32_t kLongList = 64;   // long-line hits listed per round (k_scan flush_long), one per lane
+constexpr uint32_t kWaveLds = kTileLds + kLineCap * (2 + 2) + kCandList * 4 + kLineCap * 4 + kLongList * 8 + 16;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kScanLdsMax = 160 * 1024;  // gfx950 LDS per CU (one scan block per CU)
 constexpr uint32_t kLinesImgMax = 16 * 1024;  // k_lines copies the lookup image to LDS up to this size
@@ -1317,31 +1318,46 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
 
 template <bool IMG_LDS>
 __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_scan(Bind B, ScanArgs A) {
-  // ---- block-shared tables (read-only after this barrier): gram bitset, then
-  // the lookup image when it fits
-  uint32_t *s_bits = reinterpret_cast<uint32_t *>(s_dyn);
-  uint8_t *s_img = s_dyn + kGramWords * 4;
-  for (uint32_t i = threadIdx.x; i < kGramWords / 4; i += blockDim.x)
-    reinterpret_cast<uint4 *>(s_bits)[i] = reinterpret_cast<const uint4 *>(B.gram_bits)[i];
+  // ---- block-shared tables (read-only after this barrier): the gram pair
+  // table, then the scan's lookup image when it fits
+  uint8_t *s_bits = s_dyn;
+  uint8_t *s_img = s_dyn + kPairBytes;
+  for (uint32_t i = threadIdx.x; i < kPairBytes / 16; i += blockDim.x)
+    reinterpret_cast<uint4 *>(s_bits)[i] = reinterpret_cast<const uint4 *>(B.gram_pairs)[i];
   if (IMG_LDS)
-    for (uint32_t i = threadIdx.x; i < B.img_bytes / 16; i += blockDim.x)
-      reinterpret_cast<uint4 *>(s_img)[i] = reinterpret_cast<const uint4 *>(B.img)[i];
+    for (uint32_t i = threadIdx.x; i < B.scan_img_bytes / 16; i += blockDim.x)
+      reinterpret_cast<uint4 *>(s_img)[i] = reinterpret_cast<const uint4 *>(B.scan_img)[i];
   __syncthreads();
-  const Tabs TB = make_tabs(IMG_LDS ? s_img : B.img, B.il);
+  const Tabs TB = make_tabs(IMG_LDS ? s_img : B.scan_img, B.sil);
   const uint32_t *gt = TB.gt, *ge = TB.ge;
 
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint8_t *T = s_dyn + A.shared_bytes + wave * kWaveLds;
   uint16_t *ls = reinterpret_cast<uint16_t *>(T + kTileLds);
   uint16_t *le = ls + kLineCap;
+  uint32_t *clist = reinterpret_cast<uint32_t *>(le + kLineCap);
+  uint32_t *lcnt = clist + kCandList;
+  uint64_t *lh = reinterpret_cast<uint64_t *>(lcnt + kLineCap);  // long-line hits of the round (flush_long)
+  uint32_t *lh_n = reinterpret_cast<uint32_t *>(lh + kLongList);
+  if (lane == 0) *lh_n = 0;
   const Lines &L = A.L;
   uint32_t n_probe = 0, n_hit = 0, n_gram = 0;
 
   const uint64_t nw = (uint64_t)gridDim.x * kScanWaves;
   uint64_t t = (uint64_t)blockIdx.x * kScanWaves + wave;
+  // Everything a tile needs from HBM is loaded one tile ahead, together: its
+  // 64 B per lane, its halo (8 B per lane), and in `qa` the word before the
+  // tile (lane 0) and the tile's first line indices tile_base[t] (lanes 1-2)
+  // and tile_base[t - 1] (lanes 3-4).  Vector memory operations complete in
+  // order (vmcnt), so no load the tile's processing waits for may be issued
+  // after the prefetch: the loop body reads only LDS and registers, and the
+  // long-line hits that need a slot index from HBM wait at the end of a round
+  // (flush_long), when the prefetch has had the whole tile to arrive.
   uint4 q[4];
+  uint2 qh;
+  uint32_t qa;
   auto load_tile = [&](uint64_t tt) {
-    const uint64_t base = tt * kWT + lane * 64u;
+    const uint64_t ts = tt * kWT, base = ts + lane * 64u;
     if (base + 64 <= A.n) {
       const uint4 *src = reinterpret_cast<const uint4 *>(A.buf + base);
 #pragma unroll
@@ -1363,7 +1379,65 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
       for (int k = 0; k < 4; ++k) q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
     }
+    const uint64_t h = ts + kWT + lane * 8u;
+    qh = make_uint2(0, 0);
+    if (h + 8 <= A.n) qh = *reinterpret_cast<const uint2 *>(A.buf + h);
+    else if (h < A.n) {
+      uint32_t a = 0, b = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) {
+        const uint64_t pos = h + k;
+        const uint32_t byte = pos < A.n ? (uint32_t)A.buf[pos < A.n ? pos : A.n - 1] : 0u;
+        if (k < 4) a |= byte << (8 * k); else b |= byte << (8 * (k - 4));
+      }
+      qh = make_uint2(a, b);
+    }
+    qa = 0x0A000000u;  // before the batch: as if after a '\n'
+    if (lane == 0) {
+      if (tt) qa = *reinterpret_cast<const uint32_t *>(A.buf + ts - 4);
+    } else if (lane <= 4 && (lane <= 2 || tt)) {
+      qa = reinterpret_cast<const uint32_t *>(A.tile_base + tt - (lane <= 2 ? 0 : 1))[(lane - 1) & 1];
+    }
   };
+  // The long-line hits listed this round (lh): per line one atomicAdd on its
+  // hit count gives the slot indices, then the slots or the line summary.
+  auto flush_long = [&](uint64_t ts0, uint64_t tb, uint32_t nh) {
+    wave_sync();
+    const uint32_t nlh = min(*lh_n, kLongList);
+    if (nlh == 0) return;
+    const bool act = lane < nlh;
+    const uint64_t e = act ? lh[lane] : 0;
+    const uint32_t lsel = act ? (uint32_t)(e >> 13) & 0x1FFFu : kNone;
+    const uint64_t gline = tb + nh + (uint64_t)lsel - 1u;
+    uint32_t cc = 0;
+    uint64_t pending = __ballot(act);
+    while (pending) {
+      const uint32_t l0 = (uint32_t)__ffsll((unsigned long long)pending) - 1;
+      const uint32_t g = __builtin_amdgcn_readlane(lsel, l0);
+      const uint64_t m = __ballot(act && lsel == g);
+      uint32_t base = 0;
+      if (lane == l0) base = atomicAdd(&L.cand_meta[gline].cnt, (uint32_t)__popcll(m));
+      base = __builtin_amdgcn_readlane(base, l0);
+      if (act && lsel == g) cc = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      pending &= ~m;
+    }
+    if (act) {
+      const uint32_t rel = (uint32_t)e & 0x1FFFu, lit = (uint32_t)(e >> 32) & 0xFFFFu;
+      const uint64_t q0 = ts0 + rel - 256u;
+      const uint64_t ver = ((e >> 26) & 1u) ? kCandVerified : 0ull;
+      if (cc < (uint32_t)kCandSlots) {
+        L.cand[gline * kCandSlots + cc] = (q0 << 24) | ver | lit;
+      } else {
+        const uint64_t bit = 1ull << (lit & 31);
+        atomicOr(reinterpret_cast<unsigned long long *>(&L.cand_meta[gline].bits), ((e >> 27) & 1u) ? bit | (bit << 32) : bit);
+        atomicMax(&L.cand_meta[gline].first_inv, ~(uint32_t)(q0 >> 3));
+      }
+    }
+    wave_sync();
+    if (lane == 0) *lh_n = 0;
+    wave_sync();
+  };
+
   const uint64_t n_iter = (A.n_tiles + nw - 1) / nw;
   if (t < A.n_tiles) load_tile(t);
   for (uint32_t r = 0; r < n_iter; ++r, t += nw) {
@@ -1372,43 +1446,38 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
     uint32_t w[16];
 #pragma unroll
     for (int k = 0; k < 4; ++k) { w[4 * k] = q[k].x; w[4 * k + 1] = q[k].y; w[4 * k + 2] = q[k].z; w[4 * k + 3] = q[k].w; }
+    const uint2 hv = qh;
+    const uint32_t prevb = (uint32_t)__builtin_amdgcn_readlane(qa, 0) >> 24;
+    const uint64_t tb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(qa, 1) | ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(qa, 2) << 32);
+    const uint64_t tbm = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(qa, 3) | ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(qa, 4) << 32);
+    const uint32_t prev_cnt = t ? (uint32_t)(tb - tbm) : 0u;
     if (t + nw < A.n_tiles) load_tile(t + nw);  // prefetch
-    // halo (8 B per lane) and the byte before the tile
-    uint2 hv = make_uint2(0, 0);
-    {
-      const uint64_t h = ts0 + kWT + lane * 8u;
-      if (h + 8 <= A.n) hv = *reinterpret_cast<const uint2 *>(A.buf + h);
-      else if (h < A.n) {
-        uint32_t a = 0, b = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) {
-          const uint64_t pos = h + k;
-          const uint32_t byte = pos < A.n ? (uint32_t)A.buf[pos < A.n ? pos : A.n - 1] : 0u;
-          if (k < 4) a |= byte << (8 * k); else b |= byte << (8 * (k - 4));
-        }
-        hv = make_uint2(a, b);
-      }
-    }
-    const uint32_t prevb = ts0 ? (uint32_t)A.buf[ts0 - 1] : (uint32_t)'\n';
     uint4 *dst = reinterpret_cast<uint4 *>(T + lane * 64u);
 #pragma unroll
     for (int k = 0; k < 4; ++k) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
     *reinterpret_cast<uint2 *>(T + kWT + lane * 8u) = hv;
     if (lane < 4) reinterpret_cast<uint32_t *>(T + kWT + kHalo)[lane] = 0;
 
-    // ---- '\n' bitmask of my 64 bytes (bytes past the batch end are 0)
-    uint64_t nlm = 0;
+    // ---- '\n' bitmask of my 64 bytes (bytes past the batch end are 0): the
+    // 0x80 byte flags of each word (nl_mask_word), 8 bits per two words
+    // gathered by v_dot4_u32_u8 (weights 1, 2, 4, 8 on the first word's flags,
+    // 16 .. 128 on the second's: the sum is 0x80 x the 8-bit mask)
+    uint64_t nlm;
+    {
+      uint32_t nb[8];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const uint32_t hb = nl_mask_word(w[k]);
-      nlm |= (uint64_t)(((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u)) << (4 * k);
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t d = __builtin_amdgcn_udot4(nl_mask_word(w[2 * i]), 0x08040201u, 0u, false);
+        nb[i] = __builtin_amdgcn_udot4(nl_mask_word(w[2 * i + 1]), 0x80402010u, d, false) >> 7;
+      }
+      const uint32_t lo32 = nb[0] | (nb[1] << 8) | (nb[2] << 16) | (nb[3] << 24);
+      const uint32_t hi32 = nb[4] | (nb[5] << 8) | (nb[6] << 16) | (nb[7] << 24);
+      nlm = ((uint64_t)hi32 << 32) | lo32;
     }
     const uint32_t cnt = __popcll(nlm);
     uint32_t pre = wave_incl_sum(cnt);
     const uint32_t tot = __builtin_amdgcn_readlane(pre, 63);
     pre -= cnt;
-    const uint64_t tb = A.tile_base[t];
-    const uint32_t prev_cnt = t ? (uint32_t)(tb - A.tile_base[t - 1]) : 0u;
     const bool head = prevb == '\n';
     const uint32_t nh = head ? 0u : 1u;
     const bool last_nl = (__shfl((uint32_t)(nlm >> 63), 63) & 1u) != 0;
@@ -1437,16 +1506,16 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
     // ---- nl[] and the positions of lines starting in this tile (tile-relative)
     {
       uint64_t x = nlm;
-      uint32_t r = pre;
+      uint32_t rr = pre;
       while (x) {
         const uint32_t b = (uint32_t)__ffsll((unsigned long long)x) - 1;
         x &= x - 1;
         const uint32_t p = lane * 64u + b;
-        if (tb + r < A.n_lines) A.nl[tb + r] = ts0 + p;
-        const int32_t lk = (int32_t)r - (int32_t)nh;  // started line this '\n' ends
+        if (tb + rr < A.n_lines) A.nl[tb + rr] = ts0 + p;
+        const int32_t lk = (int32_t)rr - (int32_t)nh;  // started line this '\n' ends
         if (lk >= 0 && lk < (int32_t)kLineCap) le[lk] = (uint16_t)p;
         if (p + 1 < kWT && lk + 1 < (int32_t)kLineCap) ls[lk + 1] = (uint16_t)(p + 1);
-        ++r;
+        ++rr;
       }
     }
     if (lane == 0 && head) ls[0] = 0;
@@ -1460,36 +1529,39 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
     // the line open at the tile start is long iff it started before the previous
     // tile (that tile has no '\n') or runs past the previous tile's halo
     const bool open_long = !head && (p0 == kNone || p0 >= kHalo || prev_cnt == 0);
+    // window starts in the halo: the last started line's part, before hend
+    const uint32_t hend = last_in_halo ? hfirst : kWT;
 
-    // ---- 4-gram prefilter: positions [64 lane, 64 lane + 64) and the last line's halo part
+    // ---- 4-gram prefilter: positions [64 lane, 64 lane + 64) and the last
+    // line's halo part.  Positions in pairs (k, k + 1), k even: one 8-byte LDS
+    // entry keyed by the 3 bytes the two grams share (gram_pair_index of bytes
+    // k + 1 .. k + 3), its low word holding bit (byte k & 31) for the gram at
+    // k, its high word bit (byte k + 4 & 31) for the gram at k + 1
+    // (engine_types.h gram_pair_*).  Eight entry addresses, then their eight
+    // ds_read_b64 in flight together, then the bits: per pair one or two
+    // alignbytes, a 24-bit mul, a shift and an and (the address), two bfe (the
+    // bfe offsets take the bytes' low 5 bits as they are), a shift, two
+    // shift-ors
     {
       const uint32_t nxt = *reinterpret_cast<const uint32_t *>(T + lane * 64u + 64u);
-      // positions in pairs (k, k + 1), k even: one LDS word keyed by the 3
-      // bytes the two grams share (gram_pair_word), bit (first byte & 15) for
-      // the gram at k and 16 + (last byte & 15) for the gram at k + 1
-      // (engine_types.h gram_pair_*).  Eight word addresses, then their eight
-      // LDS reads in flight together, then the bits: per pair two alignbytes, a
-      // shift, a 24-bit mul_hi, an and, one LDS read, two bfe, two shift-ors
-      const uint8_t *sb = reinterpret_cast<const uint8_t *>(s_bits);
       uint32_t hlo = 0, hhi = 0;
 #pragma unroll
       for (int k0 = 0; k0 < 64; k0 += 16) {
-        uint32_t word[8];
+        uint2 ent[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const int k = k0 + 2 * i;
           const uint32_t lo = w[k >> 2], hi = (k >> 2) < 15 ? w[(k >> 2) + 1] : nxt;
-          const uint32_t g0 = (k & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3)) : lo;  // bytes k .. k + 3
-          word[i] = *reinterpret_cast<const uint32_t *>(sb + gram_pair_byte_off(g0 >> 8));
+          const uint32_t g1 = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3) + 1u);  // bytes k + 1 .. k + 4
+          ent[i] = *reinterpret_cast<const uint2 *>(s_bits + gram_pair_byte_off(g1));
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const int k = k0 + 2 * i;
           const uint32_t lo = w[k >> 2], hi = (k >> 2) < 15 ? w[(k >> 2) + 1] : nxt;
-          const uint32_t g0 = (k & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3)) : lo;
-          const uint32_t g1 = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3) + 1u);  // bytes k + 1 .. k + 4
-          const uint32_t b0 = __builtin_amdgcn_ubfe(word[i], g0 & 15u, 1), b1 = __builtin_amdgcn_ubfe(word[i], (g1 >> 24) | 16u, 1);
-          const uint32_t two = b0 | (b1 << 1);
+          const uint32_t g0 = (k & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3)) : lo;  // bytes k .. k + 3
+          const uint32_t g1 = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3) + 1u);
+          const uint32_t two = __builtin_amdgcn_ubfe(ent[i].x, g0, 1) | (__builtin_amdgcn_ubfe(ent[i].y, g1 >> 24, 1) << 1);
           if (k < 32) hlo |= two << k; else hhi |= two << (k - 32);
         }
       }
@@ -1498,15 +1570,14 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
       // halo positions of the last started line: the lane's 8 halo bytes (hv)
       // and the next lane's first 4, as four pairs with their reads in flight
       uint32_t hh = 0;
-      const uint32_t hend = last_in_halo ? hfirst : kWT;
       if (lane * 8u + kWT < hend) {
         const uint32_t hw[3] = {hv.x, hv.y, *reinterpret_cast<const uint32_t *>(T + kWT + lane * 8u + 8u)};
-        uint32_t word[4];
+        uint2 ent[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int k = 2 * i;
-          const uint32_t g0 = (k & 3) ? __builtin_amdgcn_alignbyte(hw[(k >> 2) + 1], hw[k >> 2], (uint32_t)(k & 3)) : hw[k >> 2];
-          word[i] = *reinterpret_cast<const uint32_t *>(sb + gram_pair_byte_off(g0 >> 8));
+          const uint32_t g1 = __builtin_amdgcn_alignbyte(hw[(k >> 2) + 1], hw[k >> 2], (uint32_t)(k & 3) + 1u);
+          ent[i] = *reinterpret_cast<const uint2 *>(s_bits + gram_pair_byte_off(g1));
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1514,7 +1585,7 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
           const uint32_t lo = hw[k >> 2], hi = hw[(k >> 2) + 1];
           const uint32_t g0 = (k & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3)) : lo;
           const uint32_t g1 = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(k & 3) + 1u);
-          hh |= (__builtin_amdgcn_ubfe(word[i], g0 & 15u, 1) | (__builtin_amdgcn_ubfe(word[i], (g1 >> 24) | 16u, 1) << 1)) << k;
+          hh |= (__builtin_amdgcn_ubfe(ent[i].x, g0, 1) | (__builtin_amdgcn_ubfe(ent[i].y, g1 >> 24, 1) << 1)) << k;
         }
         const uint32_t nv = hend - (kWT + lane * 8u);  // halo positions before hend
         if (nv < 8) hh &= (1u << nv) - 1u;
@@ -1524,17 +1595,15 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
       // ---- candidates, lane-compacted: every lane appends its surviving
       // positions (with the started-line index they belong to) to a wave list,
       // then the list is verified one candidate per lane
-      uint32_t *clist = reinterpret_cast<uint32_t *>(le + kLineCap);
-      uint32_t *lcnt = clist + kCandList;
       for (uint32_t i = lane; i < kLineCap; i += 64) lcnt[i] = 0;
       uint64_t rem = hits;
       uint32_t remh = hh;
       for (;;) {
-        const uint32_t cnt = __popcll(rem) + __popc(remh);
-        uint32_t off = wave_incl_sum(cnt);
+        const uint32_t cn = __popcll(rem) + __popc(remh);
+        uint32_t off = wave_incl_sum(cn);
         const uint32_t total = __builtin_amdgcn_readlane(off, 63);
         if (total == 0) break;
-        off -= cnt;
+        off -= cn;
         // append while the list has room (the rest waits for the next round)
         while ((rem | remh) && off < kCandList) {
           uint32_t pos;
@@ -1555,10 +1624,10 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
         wave_sync();
         const uint32_t nc = total < kCandList ? total : kCandList;
         for (uint32_t c = lane; c < nc; c += 64) {
-          const uint32_t e = clist[c];
-          const uint32_t p = e & 0xFFFF;
-          const int32_t lk = (int32_t)(e >> 16) - 1;
-          const uint32_t g = ld4(T + p);
+          const uint32_t en0 = clist[c];
+          const uint32_t s = en0 & 0xFFFF;
+          const int32_t lk = (int32_t)(en0 >> 16) - 1;
+          const uint32_t g = ld4(T + s);
           if ((g & 0xFF) == '\n' || (A.debug_skip & 8)) continue;
           uint32_t slot = gram_slot(g, B.gt2_cap);
           uint32_t ol;
@@ -1579,45 +1648,59 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
           for (uint32_t ei = 0; ei < (ol & 0xFFFF); ++ei) {
             const uint32_t en = ge[(ol >> 16) + ei];
             const uint32_t lit = en >> 8, goff = en & 0xFF;
-            const int64_t q0 = (int64_t)(ts0 + p) - (int64_t)goff;
+            const int64_t q0 = (int64_t)(ts0 + s) - (int64_t)goff;
             if (q0 < 0) continue;
-            const int32_t s0 = (int32_t)p - (int32_t)goff;
-            uint32_t cc;
-            uint64_t ver = 0;
+            const int32_t s0 = (int32_t)s - (int32_t)goff;
             if (in_window) {
               if (s0 < (int32_t)ls[lk] || (uint32_t)s0 + lit_len_of(TB, lit) > le[lk]) continue;
               if (!literal_at(TB, lit, T + s0)) continue;
-              cc = atomicAdd(&lcnt[lk], 1u);
-              ver = kCandVerified;
+              const uint32_t cc = atomicAdd(&lcnt[lk], 1u);
+              if (B.cfirst) atomicMin(reinterpret_cast<unsigned long long *>(&L.cand_first[gline * kCandFirstLits + lit]),
+                                      (unsigned long long)q0);
+              if (cc < (uint32_t)kCandSlots) {
+                L.cand[gline * kCandSlots + cc] = ((uint64_t)q0 << 24) | kCandVerified | lit;
+              } else {  // past the slots: the line's summary only (CandMeta)
+                // a verified hit kCertainGap bytes past the line start lies in
+                // rest whenever the header is shorter (k_dfa checks rest_off)
+                const bool far = s0 - (int32_t)ls[lk] >= (int32_t)kCertainGap;
+                const uint64_t bit = 1ull << (lit & 31);
+                atomicOr(reinterpret_cast<unsigned long long *>(&L.cand_meta[gline].bits), far ? bit | (bit << 32) : bit);
+                atomicMax(&L.cand_meta[gline].first_inv, ~(uint32_t)((uint64_t)q0 >> 3));
+              }
             } else {
               // the line does not fit the window, the literal usually does:
               // checked here when all its bytes are in the tile + halo (literals
               // hold no '\n', so a match cannot cross into another line)
+              bool ver = false;
               if (s0 >= 0 && !B.lit_nl && (uint64_t)s0 + lit_len_of(TB, lit) <= win_end) {
                 if (!literal_at(TB, lit, T + s0)) continue;
-                ver = kCandVerified;
+                ver = true;
               }
-              cc = atomicAdd(&L.cand_meta[gline].cnt, 1u);
-            }
-            if (B.cfirst) atomicMin(reinterpret_cast<unsigned long long *>(&L.cand_first[gline * kCandFirstLits + lit]),
-                                    (unsigned long long)q0);
-            if (cc < (uint32_t)kCandSlots) {
-              L.cand[gline * kCandSlots + cc] = ((uint64_t)q0 << 24) | ver | lit;
-            } else {  // past the slots: the line's summary only (CandMeta)
-              // a verified hit kCertainGap bytes past the line start lies in
-              // rest whenever the header is shorter (k_dfa checks rest_off).
-              // ls[] holds the first kLineCap line starts only: a later line's
-              // hit is never taken as far (an occurrence bit alone is exact)
+              if (B.cfirst) atomicMin(reinterpret_cast<unsigned long long *>(&L.cand_first[gline * kCandFirstLits + lit]),
+                                      (unsigned long long)q0);
+              // a later line's hit (past the first kLineCap line starts) is
+              // never taken as far (an occurrence bit alone is exact)
               const bool far = lk < 0 ? s0 >= (int32_t)kCertainGap
                                       : lk < (int32_t)kLineCap && s0 - (int32_t)ls[lk] >= (int32_t)kCertainGap;
-              const uint64_t bit = 1ull << (lit & 31);
-              atomicOr(reinterpret_cast<unsigned long long *>(&L.cand_meta[gline].bits), ver && far ? bit | (bit << 32) : bit);
-              atomicMax(&L.cand_meta[gline].first_inv, ~(uint32_t)((uint64_t)q0 >> 3));
+              const uint32_t at = atomicAdd(lh_n, 1u);
+              if (at < kLongList && lk + 1 < 0x1FFF) {  // the slot index at the end of the round (flush_long)
+                lh[at] = (uint64_t)(uint32_t)(s0 + 256) | ((uint64_t)(uint32_t)(lk + 1) << 13) | ((ver ? 1ull : 0ull) << 26) |
+                         ((ver && far ? 1ull : 0ull) << 27) | ((uint64_t)lit << 32);
+              } else {  // list full: the slot index right away
+                const uint32_t cc = atomicAdd(&L.cand_meta[gline].cnt, 1u);
+                if (cc < (uint32_t)kCandSlots) {
+                  L.cand[gline * kCandSlots + cc] = ((uint64_t)q0 << 24) | (ver ? kCandVerified : 0ull) | lit;
+                } else {
+                  const uint64_t bit = 1ull << (lit & 31);
+                  atomicOr(reinterpret_cast<unsigned long long *>(&L.cand_meta[gline].bits), ver && far ? bit | (bit << 32) : bit);
+                  atomicMax(&L.cand_meta[gline].first_inv, ~(uint32_t)((uint64_t)q0 >> 3));
+                }
+              }
             }
             ++n_hit;
           }
-        }
-        wave_sync();
+      }
+        flush_long(ts0, tb, nh);
       }
       // hit counts of the lines decided in this window
       const uint32_t n_win = min(n_st, kLineCap) - ((last_long && n_st <= kLineCap) ? 1u : 0u);
@@ -4568,7 +4651,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   size_t n_gent = 0;
   for (auto &kv : gmap) n_gent += kv.second.size();
   const bool use_pref = n_gent > 0 && n_gent < 65536 && lit_off.size() < 65536;
-  std::vector<uint32_t> gram_bits(kGramWords, 0);
+  std::vector<uint32_t> gram_pairs(2 * kPairEntries, 0);
   const uint32_t gt2_cap = (uint32_t)next_pow2((use_pref ? gmap.size() : 0) * 2 + 16);
   std::vector<uint32_t> gt2(2 * gt2_cap, 0), gt2_ent;
   if (use_pref)
@@ -4576,8 +4659,8 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
       // both roles of the gram (k_scan tests even positions as the left gram
       // of a pair and odd ones as the right gram)
       const uint32_t g = kv.first;
-      gram_bits[gram_pair_word(g >> 8)] |= 1u << (g & 15u);
-      gram_bits[gram_pair_word(g & 0xFFFFFFu)] |= 1u << (16u + ((g >> 24) & 15u));
+      gram_pairs[2 * gram_pair_index(g >> 8)] |= 1u << (g & 31u);
+      gram_pairs[2 * gram_pair_index(g & 0xFFFFFFu) + 1] |= 1u << ((g >> 24) & 31u);
       uint32_t slot = gram_slot(kv.first, gt2_cap);
       while (gt2[2 * slot + 1] & 0xFFFF) slot = (slot + 1) & (gt2_cap - 1);
       gt2[2 * slot] = kv.first;
@@ -5172,6 +5255,37 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   il.lcim = put(cm_al.data(), cm_al.size());
   il.lchk = put(lit_chk.data(), lit_chk.size());
   img.resize((img.size() + 15) & ~size_t(15), 0);
+  // the scan's own image: only what k_scan reads (gram table, gram entries,
+  // the prefilter literals; the gram entries name prefilter literals only),
+  // so it fits LDS beside the pair table whatever the ruleset's other literals
+  std::vector<uint8_t> simg;
+  auto sput = [&](const void *p, size_t nbytes) {
+    const size_t off = (simg.size() + 15) & ~size_t(15);
+    simg.resize(off + nbytes + 4, 0);
+    if (nbytes) memcpy(simg.data() + off, p, nbytes);
+    return (uint32_t)off;
+  };
+  std::vector<uint32_t> slrec(lit_off.size(), 0);
+  std::vector<uint8_t> slb, scm;
+  for (size_t i = 0; i < lit_off.size(); ++i) {
+    if (!lit_pref[i]) continue;
+    slrec[i] = ((uint32_t)slb.size() << 8) | lit_len[i];
+    for (uint32_t k = 0; k < lit_len[i]; ++k) {
+      slb.push_back(lit_bytes[lit_off[i] + k]);
+      scm.push_back(lit_ci[lit_off[i] + k] ? 0x20 : 0);
+    }
+    const size_t padded = ((slb.size() + 3) & ~size_t(3)) + 4;
+    slb.resize(padded, 0);
+    scm.resize(padded, 0);
+  }
+  ImgLayout sil{};
+  sil.gt = sput(gt2.data(), gt2.size() * 4);
+  sil.ge = sput(gt2_ent.data(), gt2_ent.size() * 4);
+  sil.lrec = sput(slrec.data(), slrec.size() * 4);
+  sil.lbytes = sput(slb.data(), slb.size());
+  sil.lcim = sput(scm.data(), scm.size());
+  sil.lchk = sput(lit_chk.data(), lit_chk.size());
+  simg.resize((simg.size() + 15) & ~size_t(15), 0);
   if (getenv("BJX_DEBUG_IMG"))
     fprintf(stderr, "[bjx] image %zu B: gram table %u, gram entries %u, host table %u, literals %zu (recs %u, bytes %zu x2), "
             "plan %zu entries, lit-rule ents %zu, hosts %zu\n", img.size(), il.ge - il.gt, il.ht - il.ge, il.lrec - il.ht,
@@ -5199,8 +5313,8 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
          o_hdlen = bb.add(hd_len), o_hdb = bb.add(hd_bytes), o_hsc = bb.add(host_scope), o_skip = bb.add(skip),
          o_sao = bb.add(sc_addr_off), o_sa = bb.add(sc_addr), o_sso = bb.add(sc_sub_off), o_ss = bb.add(sc_sub),
          o_sto = bb.add(sc_str_off), o_sth = bb.add(sc_str_hash), o_stb = bb.add(sc_str_boff), o_stl = bb.add(sc_str_len),
-         o_stbytes = bb.add(sc_str_bytes), o_gbits = bb.add(gram_bits),
-         o_rl = bb.add(rule_lits), o_img = bb.add(img), o_lro = bb.add(lr_off), o_lrg = bb.add(lr_gend),
+         o_stbytes = bb.add(sc_str_bytes), o_gbits = bb.add(gram_pairs),
+         o_rl = bb.add(rule_lits), o_img = bb.add(img), o_simg = bb.add(simg), o_lro = bb.add(lr_off), o_lrg = bb.add(lr_gend),
          o_lre = bb.add(lr_ent), o_lrh = bb.add(lr_host), o_sca = bb.add(sc_always), o_scs = bb.add(sc_skipm),
          o_dso = bb.add(dfa_site_off), o_ds = bb.add(dfa_site), o_dg = bb.add(dfa_glob), o_pso = bb.add(pref_site_off),
          o_dsq = bb.add(dfa_site_q), o_dgq = bb.add(dfa_glob_q),
@@ -5247,7 +5361,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.n_scopes = n_scopes;
   B.any_allow = any_allow ? 1 : 0;
   B.mask_words = std::max<uint32_t>(1, (max_app + 63) / 64);
-  B.gram_bits = reinterpret_cast<const uint32_t *>(base + o_gbits);
+  B.gram_pairs = reinterpret_cast<const uint2 *>(base + o_gbits);
   B.rule_lits = reinterpret_cast<const uint32_t *>(base + o_rl);
   B.n_lits = n_lit;
   B.any_anchored = any_anchored ? 1 : 0;
@@ -5258,6 +5372,9 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.img = base + o_img;
   B.img_bytes = (uint32_t)img.size();
   B.il = il;
+  B.scan_img = base + o_simg;
+  B.scan_img_bytes = (uint32_t)simg.size();
+  B.sil = sil;
   B.gt2_cap = gt2_cap;
   B.gt2_nent = (uint32_t)gt2_ent.size();
   B.ht_cap = ht_cap;
@@ -5947,10 +6064,10 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     A.buf = buf; A.n = n; A.n_tiles = n_tiles; A.n_lines = cap; A.tile_base = e->tile_base.p; A.nl = e->nl.p;
     A.L = L; A.stats = e->scalars.p + 8;
     A.debug_skip = getenv("BJX_DEBUG_SKIP") ? (uint32_t)atoi(getenv("BJX_DEBUG_SKIP")) : 0u;
-    // block-shared LDS: gram bitset, the lookup image when it fits, then 16 wave regions
-    const uint32_t fixed = kGramWords * 4 + kScanWaves * kWaveLds;
-    const bool img_lds = fixed + B.img_bytes <= kScanLdsMax;
-    A.shared_bytes = kGramWords * 4 + (img_lds ? B.img_bytes : 0);
+    // block-shared LDS: the gram pair table, the scan's lookup image when it fits, then 16 wave regions
+    const uint32_t fixed = kPairBytes + kScanWaves * kWaveLds;
+    const bool img_lds = fixed + B.scan_img_bytes <= kScanLdsMax;
+    A.shared_bytes = kPairBytes + (img_lds ? B.scan_img_bytes : 0);
     const uint32_t lds = A.shared_bytes + kScanWaves * kWaveLds;
     using ScanFn = void (*)(Bind, ScanArgs);
     const ScanFn kfn = img_lds ? k_scan<true> : k_scan<false>;
@@ -6092,7 +6209,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   HIP_OK(hipStreamSynchronize(st));
   const unsigned long long n_slow = sc4[4], n_slots = sc4[3];
   e->last_jobs = n_jobs;
-  e->scan_stats[0] = sc4[0]; e->scan_stats[1] = sc4[1]; e->scan_stats[2] = n_slow; e->scan_stats[3] = B.img_bytes;
+  e->scan_stats[0] = sc4[0]; e->scan_stats[1] = sc4[1]; e->scan_stats[2] = n_slow; e->scan_stats[3] = B.scan_img_bytes;
   e->scan_stats[4] = n_jobs; e->scan_stats[5] = sc4[2];
   HIP_OK(hipEventRecord(e->evk[2], st));
   if (n_jobs) {

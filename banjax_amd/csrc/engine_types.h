@@ -40,13 +40,19 @@ struct DevRule {
 // Bind::jinfo flags (word y; lead_dist in bits 16-31)
 constexpr uint32_t kJiNfa = 1, kJiEquiv = 2, kJiBigLit = 16;  // bits 2-3: lead & 3
 
-// Prefilter gram bitset (LDS resident, 64K bits = 2048 words), tested two
-// positions per word (gram_pair_* below).  gram_mix: the low 32 bits of a
-// 24 x 24-bit product (one full-rate v_mul_u32_u24 on the device when the key
-// is visibly 24-bit); its bits 13..23 pick the word.  (Bits 34..44 of the
-// full product spread cfg2's similar host literals worse: k_scan 17.5 -> 32 ms.)
-constexpr uint32_t kGramLog2 = 16;
-constexpr uint32_t kGramWords = (1u << kGramLog2) / 32;
+// Prefilter gram pair table (k_scan, LDS resident): 2048 entries of 8 B.
+// The scan tests byte positions in pairs: positions k (even) and k + 1 share
+// the 3 bytes k + 1 .. k + 3, which pick one entry (gram_pair_index); the gram
+// at k is bit (its first byte & 31) of the entry's low word, the gram at
+// k + 1 bit (its last byte & 31) of the high word.  A registered gram sets its
+// bit in both roles (the entry of its last three bytes, low word; the entry of
+// its first three bytes, high word), so no occurrence is missed at either
+// parity.  gram_mix: the low 32 bits of a 24 x 24-bit product (one full-rate
+// v_mul_u32_u24 on the device; only the key's low 24 bits count); its bits
+// 13..23 pick the entry.  (Bits 34..44 of the full product spread cfg2's
+// similar host literals worse: k_scan 17.5 -> 32 ms, round 4.)
+constexpr uint32_t kPairEntries = 2048;
+constexpr uint32_t kPairBytes = kPairEntries * 8;
 constexpr uint32_t kGramMul = 0x2C1B3Bu;
 __host__ __device__ inline uint32_t gram_mix(uint32_t x) {
 #ifdef __HIP_DEVICE_COMPILE__
@@ -55,14 +61,8 @@ __host__ __device__ inline uint32_t gram_mix(uint32_t x) {
   return (x & 0xFFFFFFu) * kGramMul;
 #endif
 }
-// The scan pass tests grams in pairs: positions k (even) and k + 1 share the
-// 3 bytes k + 1 .. k + 3, which pick one 32-bit word of the bitset; the gram
-// at k is bit (its first byte & 15), the gram at k + 1 bit 16 + (its last byte
-// & 15).  A registered gram sets its bit in both roles (word of its last three
-// bytes, low half; word of its first three bytes, high half), so no occurrence
-// is missed at either parity.  key = 3 bytes (24 bits).
-__host__ __device__ inline uint32_t gram_pair_word(uint32_t key) { return (gram_mix(key) >> 13) & (kGramWords - 1); }
-__host__ __device__ inline uint32_t gram_pair_byte_off(uint32_t key) { return (gram_mix(key) >> 11) & ((kGramWords - 1) << 2); }
+__host__ __device__ inline uint32_t gram_pair_index(uint32_t key) { return (gram_mix(key) >> 13) & (kPairEntries - 1); }
+__host__ __device__ inline uint32_t gram_pair_byte_off(uint32_t key) { return (gram_mix(key) >> 10) & ((kPairEntries - 1) << 3); }
 // home slot of a gram in the exact gram table (cap a power of two <= 2^18):
 // Fibonacci hashing, high product bits
 __host__ __device__ inline uint32_t gram_slot(uint32_t g, uint32_t cap) { return ((g * 0x9E3779B1u) >> 14) & (cap - 1); }
@@ -133,7 +133,7 @@ struct Bind {
   uint32_t any_allow;
   uint32_t mask_words;         // ceil(max applicable rules per line / 64)
   // prefilter
-  const uint32_t *gram_bits;   // kGramWords
+  const uint2 *gram_pairs;     // kPairEntries: the prefilter's pair table (gram_pair_*)
   const uint32_t *rule_lits;
   uint32_t n_lits;
   uint32_t any_anchored;
@@ -152,6 +152,11 @@ struct Bind {
   //               ASCII-case-insensitive), 4-byte aligned; check-window offsets
   const uint8_t *img;
   uint32_t img_bytes;
+  // k_scan's own image (same layout, the ImgLayout sil): the gram table and
+  // entries and the prefilter literals only (host fields unused)
+  const uint8_t *scan_img;
+  uint32_t scan_img_bytes;
+  ImgLayout sil;
   uint32_t gt2_cap, gt2_nent;
   uint32_t ht_cap;
   uint32_t max_app;            // most rules applicable to one line (<= 128 on the scan path)

@@ -228,7 +228,7 @@ class Engine:
     def scan_stats(self):
         out = (C.c_uint64 * 12)()
         _lib.lib().bjx_debug_scan_stats(self._h, out, 12)
-        return {"gram_bitset_hits": out[0], "literal_hits": out[1], "fallback_lines": out[2], "lookup_image_bytes": out[3],
+        return {"pair_filter_hits": out[0], "literal_hits": out[1], "fallback_lines": out[2], "scan_image_bytes": out[3],
                 "dfa_jobs": out[4], "ip_table_slots": out[5], "ips": out[6], "state_table_slots": out[7], "states": out[8],
                 "gram_table_hits": out[9], "per_line_kernel_lines": out[10], "long_runs": out[11]}
 
