@@ -748,6 +748,35 @@ __device__ __forceinline__ bool literal_at(const Tabs &T, uint32_t lit, const ui
   return true;
 }
 
+// literal_at for the scan pass (text and tables in LDS): a literal of at most
+// 16 bytes is compared from five text words, four literal words and four
+// case-mask words loaded up front (one LDS round trip, no chain of dependent
+// word compares); longer ones go word by word.  The literal tables are padded
+// (image slack), and the text is read at most 20 bytes past p - 3, inside the
+// wave's tile + halo region for any hit the scan verifies.
+__device__ __forceinline__ bool literal_at16(const Tabs &T, uint32_t lit, const uint8_t *p) {
+  const uint32_t rec = T.lrec[lit];
+  const uint32_t off = rec >> 8, len = rec & 0xFF;
+  if (len > 16) return literal_at(T, lit, p);
+  const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+  const uint32_t *tw = reinterpret_cast<const uint32_t *>(p - sh);
+  const uint32_t *lw = reinterpret_cast<const uint32_t *>(T.lbytes + off);
+  const uint32_t *mw = reinterpret_cast<const uint32_t *>(T.lcim + off);
+  uint32_t t[5], l[4], m[4];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) t[k] = tw[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { l[k] = lw[k]; m[k] = mw[k]; }
+  uint32_t diff = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t x = __builtin_amdgcn_alignbyte(t[k + 1], t[k], sh);
+    const int32_t rest = (int32_t)len - 4 * k;
+    const uint32_t valid = rest >= 4 ? ~0u : rest > 0 ? (1u << (8 * rest)) - 1u : 0u;
+    diff |= ((x | m[k]) ^ l[k]) & valid;
+  }
+  return diff == 0;
+}
 
 __device__ __forceinline__ void set_pos(uint64_t &m0, uint64_t &m1, uint32_t pos) {
   if (pos < 64) m0 |= 1ull << pos; else m1 |= 1ull << (pos - 64);
@@ -1653,7 +1682,7 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
             const int32_t s0 = (int32_t)s - (int32_t)goff;
             if (in_window) {
               if (s0 < (int32_t)ls[lk] || (uint32_t)s0 + lit_len_of(TB, lit) > le[lk]) continue;
-              if (!literal_at(TB, lit, T + s0)) continue;
+              if (!literal_at16(TB, lit, T + s0)) continue;
               const uint32_t cc = atomicAdd(&lcnt[lk], 1u);
               if (B.cfirst) atomicMin(reinterpret_cast<unsigned long long *>(&L.cand_first[gline * kCandFirstLits + lit]),
                                       (unsigned long long)q0);
@@ -1673,7 +1702,7 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
               // hold no '\n', so a match cannot cross into another line)
               bool ver = false;
               if (s0 >= 0 && !B.lit_nl && (uint64_t)s0 + lit_len_of(TB, lit) <= win_end) {
-                if (!literal_at(TB, lit, T + s0)) continue;
+                if (!literal_at16(TB, lit, T + s0)) continue;
                 ver = true;
               }
               if (B.cfirst) atomicMin(reinterpret_cast<unsigned long long *>(&L.cand_first[gline * kCandFirstLits + lit]),
@@ -2791,15 +2820,17 @@ __device__ __forceinline__ bool ip_claim_line(const EvSrc &E, const State &S, ui
                                               uint64_t shard_budget) {
   const uint64_t h = E.ip_hash[i];
   const uint32_t len = E.ip_len[i];
-  const uint8_t *ip = ev_ip(E, i);
   const bool inl = len <= 15;
-  const uint4 k16 = !inl ? make_uint4(0, 0, 0, 0) : E.ip16 ? E.ip16[i] : ip_key16_bytes(ip, len);
+  const uint4 k16 = !inl ? make_uint4(0, 0, 0, 0) : E.ip16 ? E.ip16[i] : ip_key16_bytes(ev_ip(E, i), len);
   uint64_t s = h & S.ip_mask;
   bool claimed = false;
   for (;;) {
-    // the whole 32 B slot in one round trip: hash, id, born, key16.  Fields
-    // changed in this launch (hash, born) are re-read by the CAS paths below;
-    // id and key16 of IPs from earlier batches are settled.
+    // the whole 32 B slot in one round trip: hash, id, born, key16.  A slot
+    // claimed in this launch may read stale (hash 0 or born 0): the CAS below
+    // decides the hash, and born 0 means claimed in this launch.  id and key16
+    // of IPs from earlier batches are settled.  (Device-coherent sc1 loads of
+    // hash and born, which spare a new IP's later lines their CAS, measured
+    // slower: the cold cfg3 claim 46 -> 52 ms, the steady one 4.3 -> 5.5 ms.)
     const uint4 *sp = reinterpret_cast<const uint4 *>(&S.ip[s]);
     const uint4 q0 = sp[0], q1 = sp[1];
     uint64_t cur = ((uint64_t)q0.y << 32) | q0.x;
@@ -2810,23 +2841,30 @@ __device__ __forceinline__ bool ip_claim_line(const EvSrc &E, const State &S, ui
         return false;
       }
       cur = atomicCAS((unsigned long long *)&S.ip[s].hash, 0ull, (unsigned long long)h);
-      if (cur == 0) { cur = h; claimed = true; }
+      if (cur == 0) {
+        cur = h;
+        claimed = true;
+        __hip_atomic_store(&S.ip[s].born, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     if (cur == h) {
-      uint32_t b = q0.w;  // 0 (stale) when the hash came from the CAS: the CAS below decides
-      if (b == 0) b = atomicCAS(&S.ip[s].born, 0u, epoch);
+      // born: an earlier batch's epoch (stored before this launch, so every
+      // lane sees it), or 0 / this epoch for a slot claimed in this launch (its
+      // claimer stores the epoch after winning the hash): no atomic per line
+      const uint32_t b = claimed ? epoch : q0.w;
       if (b == 0 || b == epoch) {  // created in this batch: identity checked by k_ip_commit
         // a hot new IP has every one of its lines here: read before the atomic,
         // so only lines that can still lower the first index contend for it
-        if (__hip_atomic_load(&S.ip_first[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > (uint32_t)i)
-          atomicMin(&S.ip_first[s], (uint32_t)i);
+        // (a plain load: the index only falls, so a stale value at or below i
+        // means the atomic would change nothing)
+        if (S.ip_first[s] > (uint32_t)i) atomicMin(&S.ip_first[s], (uint32_t)i);
         el_slot[i] = (uint32_t)s;
         el_id[i] = kNewIp;
         return claimed;
       }
       // created by an earlier batch: short IPs compare inline, long ones in the arena
       const uint32_t id = q0.z;
-      if (inl ? key16_eq(q1, k16) : (S.ip_len[id] == len && bytes_eq(S.arena + S.ip_off[id], ip, len))) {
+      if (inl ? key16_eq(q1, k16) : (S.ip_len[id] == len && bytes_eq(S.arena + S.ip_off[id], ev_ip(E, i), len))) {
         el_slot[i] = (uint32_t)s;
         el_id[i] = id;
         return claimed;
@@ -2836,9 +2874,36 @@ __device__ __forceinline__ bool ip_claim_line(const EvSrc &E, const State &S, ui
   }
 }
 
-// exclusive prefix of v over the wave and one atomicAdd of the wave's total
-// on ctr; returns ctr's old value + the prefix (every lane of the wave calls it)
-__device__ __forceinline__ uint64_t wave_alloc(unsigned long long *ctr, uint32_t v);
+// exclusive prefix of v over the block and one atomicAdd of the block's total
+// on ctr; returns ctr's old value + the prefix (every thread of the block
+// calls it).  One atomic per block, not per wave: a single counter address
+// takes about 88 atomics per microsecond, which made the per-wave form cost
+// 3.5 ms (k_ip_claim's new-line list) and 7 ms (k_ip_commit's two counters)
+// on a cold batch of 20M new IPs.
+__device__ __forceinline__ uint64_t block_alloc(unsigned long long *ctr, uint64_t v) {
+  __shared__ unsigned long long s_w[kBlock / 64 + 1];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  __syncthreads();  // a previous call's readers are done with s_w
+  if (lane == 63) s_w[wave] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long tot = 0;
+    for (int w = 0; w < kBlock / 64; ++w) {
+      const unsigned long long t = s_w[w];
+      s_w[w] = tot;
+      tot += t;
+    }
+    s_w[kBlock / 64] = tot ? atomicAdd(ctr, tot) : 0ull;
+  }
+  __syncthreads();
+  return s_w[kBlock / 64] + s_w[wave] + (x - v);
+}
 
 // el_new / counters[4]: the event lines whose IP is new to the table (created
 // in this batch), listed for k_ip_commit
@@ -2853,22 +2918,8 @@ __global__ __launch_bounds__(kBlock) void k_ip_claim(EvSrc E, State S, uint32_t 
     isnew = el_id[i] == kNewIp;
   }
   count_claims(S, 0, 5, claimed, shard_budget);
-  const uint64_t at = wave_alloc((unsigned long long *)&S.counters[4], isnew ? 1u : 0u);
+  const uint64_t at = block_alloc((unsigned long long *)&S.counters[4], isnew ? 1u : 0u);
   if (isnew) el_new[at] = (uint32_t)i;
-}
-
-__device__ __forceinline__ uint64_t wave_alloc(unsigned long long *ctr, uint32_t v) {
-  const uint32_t lane = threadIdx.x & 63;
-  uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d);
-    if (lane >= (uint32_t)d) x += y;
-  }
-  unsigned long long base = 0;
-  if (lane == 63 && x) base = atomicAdd(ctr, (unsigned long long)x);
-  base = __shfl(base, 63);
-  return base + (x - v);
 }
 
 // over the event lines k_ip_claim listed (el_new, n_new of them): IPs of
@@ -2880,27 +2931,32 @@ __global__ __launch_bounds__(kBlock) void k_ip_commit(EvSrc E, State S, uint32_t
   const bool act = t < n_new;
   const uint64_t i = act ? el_new[t] : 0;
   uint32_t s = 0, f = 0, len = 0;
-  const uint8_t *ip = nullptr;
   if (act) {
     s = el_slot[i];
     f = S.ip_first[s];
     len = E.ip_len[i];
-    ip = ev_ip(E, i);
   }
   const bool first = act && f == (uint32_t)i;
-  // ids and arena bytes: one atomic per wave
-  const uint32_t id = (uint32_t)wave_alloc((unsigned long long *)&S.counters[0], first ? 1u : 0u);
-  const uint64_t off = wave_alloc((unsigned long long *)&S.counters[1], first ? len : 0u);
+  // ids and arena bytes: one atomic per block
+  const uint32_t id = (uint32_t)block_alloc((unsigned long long *)&S.counters[0], first ? 1u : 0u);
+  const uint64_t off = block_alloc((unsigned long long *)&S.counters[1], first ? len : 0u);
   if (first) {
+    const uint8_t *ip = ev_ip(E, i);
     for (uint32_t k = 0; k < len; ++k) S.arena[off + k] = ip[k];
     S.ip_off[id] = off;
     S.ip_len[id] = len;
     S.ip[s].id = id;
     S.ip[s].key16 = E.ip16 ? E.ip16[i] : ip_key16_bytes(ip, len);
     el_id[i] = id | kFirstIp;
-  } else if (act && (E.ip_len[f] != len || !bytes_eq(ev_ip(E, f), ip, len))) {
-    const uint64_t k = atomicAdd((unsigned long long *)&S.counters[3], 1ull);
-    coll[k] = (uint32_t)i;
+  } else if (act) {
+    // the same IP as its slot's first line?  IPs of up to 15 bytes by their
+    // inline keys (bytes and length: exact), longer ones byte by byte
+    const uint32_t lf = E.ip_len[f];
+    const bool same = lf == len && (len <= 15 && E.ip16 ? key16_eq(E.ip16[f], E.ip16[i]) : bytes_eq(ev_ip(E, f), ev_ip(E, i), len));
+    if (!same) {
+      const uint64_t k = atomicAdd((unsigned long long *)&S.counters[3], 1ull);
+      coll[k] = (uint32_t)i;
+    }
   }
 }
 
@@ -4112,6 +4168,7 @@ struct bjx_engine {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evm0 = nullptr, evm1 = nullptr;
   hipEvent_t evk[4] = {};      // k_lines launch, DFA-job sort + k_dfa / k_nfa (bench: per-kernel roofline)
   double kernel_ms[3] = {};   // last batch: k_scan, k_lines, DFA jobs
+  uint32_t last_line_kernel = 0;  // last batch's per-line kernel: 2 = k_lines2, 1 = k_lines
   static constexpr int kPhases = 8;
   hipEvent_t ph[kPhases + 1] = {};
   double phase_ms[kPhases] = {};
@@ -4139,6 +4196,7 @@ struct bjx_engine {
   State S{};
   uint64_t ip_cap = 0, st_cap = 0;
   uint64_t rehashes = 0;
+  uint64_t last_new_ips = 0, last_new_states = 0;  // entries the last batch created (capacity prediction)
   uint32_t epoch = 0;  // batch counter (IpSlot.born)
   uint64_t dbg_hash_mask = 0;  // bjx_debug_set_ip_hash_mask
   uint64_t dbg_budget = 0;     // bjx_debug_set_claim_budget (0 = off)
@@ -5804,8 +5862,13 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
   else rec_base = 0;
   if (E.n >= 0x7FFFFFFFull || n_ev >= 0xFFFFFFFFull) throw BjxError(BJX_ERR_ARG, "batch too large (2^31 lines / 2^32 events)");
   read_counters(e);
-  ensure_capacity(e, std::min<uint64_t>(n_el, std::max<uint64_t>(1u << 18, e->host_counters[0] / 8)), el_bytes,
-                  std::min<uint64_t>(n_ev, std::max<uint64_t>(1u << 20, e->host_counters[2] / 8)));
+  // room for the new entries expected: an eighth of the table's entries, or
+  // 1.25 x the previous batch's new entries (a stream of new IPs), whichever
+  // is more, at most the batch's worst case
+  const uint64_t ips0 = e->host_counters[0], st0 = e->host_counters[2];
+  ensure_capacity(e, std::min<uint64_t>(n_el, std::max<uint64_t>(std::max<uint64_t>(1u << 18, ips0 / 8), e->last_new_ips * 5 / 4)),
+                  el_bytes,
+                  std::min<uint64_t>(n_ev, std::max<uint64_t>(std::max<uint64_t>(1u << 20, st0 / 8), e->last_new_states * 5 / 4)));
   if (e->host_counters[0] + n_el >= 0x7FFFFFFFull) throw BjxError(BJX_ERR_CAPACITY, "more than 2^31 distinct IPs");
   if (++e->epoch == 0) ++e->epoch;  // 0 marks a slot being claimed
   const uint32_t epoch = e->epoch;
@@ -5833,7 +5896,9 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
       // more new IPs than the table had room for: undo, grow, claim again
       hipLaunchKernelGGL(k_ip_rollback, dim3(grid_for(e->ip_cap)), dim3(kBlock), 0, st, e->ip_cap, e->S, epoch);
       HIP_OK(hipGetLastError());
-      if (!forced) grow_ip(e, attempt >= 2 ? n_ips + n_el : std::min<uint64_t>(n_ips + n_el, 4 * (e->ip_cap * 3 / 4)));
+      // straight to the batch's worst case (every event line a new IP): one
+      // rollback at most (stepwise growth redid the whole claim pass per step)
+      if (!forced) grow_ip(e, n_ips + n_el);
     }
     if (nw_ovf[0]) {
       hipLaunchKernelGGL(k_ip_commit, dim3(grid_for(nw_ovf[0])), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p,
@@ -5894,12 +5959,13 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
       HIP_OK(hipGetLastError());
       HIP_OK(hipMemsetAsync(e->S.ip_st, 0xFF, e->S.ip_st_cap * 4, st));  // may name rolled-back slots
       read_counters(e);
-      if (!forced)
-        grow_st(e, attempt >= 2 ? e->host_counters[2] + n_ev
-                                : std::min<uint64_t>(e->host_counters[2] + n_ev, 4 * (e->st_cap * 3 / 4)));
+      if (!forced) grow_st(e, e->host_counters[2] + n_ev);  // the batch's worst case, as for the IP table
     }
   }
   mark(e, 6);
+  read_counters(e);
+  e->last_new_ips = e->host_counters[0] - ips0;
+  e->last_new_states = e->host_counters[2] - st0;
   e->rec12 = use12;
   e->rec_base = rec_base;
   if (use12) rl_sort_apply<EvRec12>(e, B, E, n_ev, ev_el, ev_rule, rec_base);
@@ -6124,6 +6190,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     // k_lines2 (lines2.h) when the ruleset has its tables; BJX_LINES=1 keeps k_lines
     static const int lines_env = getenv("BJX_LINES") ? atoi(getenv("BJX_LINES")) : 2;
     const bool use_l2 = B.l2_bytes && lines_env != 1 && !getenv("BJX_PROF_LINES") && !A.dbg;
+    e->last_line_kernel = use_l2 ? 2u : 1u;
     if (use_l2) {
       const uint32_t lds = B.l2_bytes + (kL2Block / 64) * kL2WaveLds;
       if (lds != e->lines2_lds) {
@@ -7108,8 +7175,11 @@ extern "C" size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap) {
 }
 extern "C" size_t bjx_debug_kernel_ms(bjx_engine *e, double *out, size_t cap) {
   if (!e) return 0;
-  for (size_t k = 0; k < cap && k < 3; ++k) out[k] = e->kernel_ms[k];
-  return 3;
+  // [3]: which per-line kernel ran (2 = k_lines2, 1 = k_lines), [4]: its line window / staging bytes
+  const double v[5] = {e->kernel_ms[0], e->kernel_ms[1], e->kernel_ms[2], (double)e->last_line_kernel,
+                       e->last_line_kernel == 2 ? (double)kL2Win : (double)kSpanBytes};
+  for (size_t k = 0; k < cap && k < 5; ++k) out[k] = v[k];
+  return 5;
 }
 extern "C" size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap) {
   if (!e) return 0;

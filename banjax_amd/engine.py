@@ -244,10 +244,16 @@ class Engine:
         return {k: round(out[i], 3) for i, k in enumerate(self.PHASES)}
 
     def kernel_ms(self):
-        """Device ms of the last batch's k_scan, k_lines and DFA-job resolve (HIP events)."""
-        out = (C.c_double * 3)()
-        _lib.lib().bjx_debug_kernel_ms(self._h, out, 3)
+        """Device ms of the last batch's k_scan, per-line kernel and DFA-job resolve (HIP events)."""
+        out = (C.c_double * 5)()
+        _lib.lib().bjx_debug_kernel_ms(self._h, out, 5)
         return {"k_scan": out[0], "k_lines": out[1], "dfa_jobs": out[2]}
+
+    def line_kernel(self):
+        """The last batch's per-line kernel: ("k_lines2", window bytes per line) or ("k_lines", staging bytes per wave)."""
+        out = (C.c_double * 5)()
+        _lib.lib().bjx_debug_kernel_ms(self._h, out, 5)
+        return ("k_lines2" if out[3] == 2 else "k_lines" if out[3] == 1 else None), int(out[4])
 
     def state_get(self, ip, name):
         hits, start = C.c_int64(), C.c_int64()

@@ -105,13 +105,22 @@ def pmc_traffic(kernel):
 
 KERNELS = {
     "k_scan": "k_scan (framing + line index + literal prefilter over every byte of the batch)",
-    "k_lines": "k_lines2 (one lane per line: header from a 64 B window, host, CheckIsAllowed, rule decisions "
-               "from the literal hits; undecided pairs emitted as DFA-job windows)",
+    "k_lines2": "k_lines2 (one lane per line: header from a %d B window of the line, host, CheckIsAllowed, rule "
+                "decisions from the literal hits; undecided pairs emitted as DFA-job windows)",
+    "k_lines": "k_lines (the per-line fallback for rulesets past k_lines2's tables: each wave's lines staged in "
+               "%d B of LDS, the host's rules walked entry by entry; undecided pairs emitted as DFA jobs)",
     "dfa_jobs": "DFA-job sort + k_dfa / k_nfa (the (line, rule) pairs the literals cannot decide)",
 }
 
 
-def roofline(kms, nbytes, args):
+def kernel_desc(dom, line_kernel):
+    if dom != "k_lines":
+        return KERNELS[dom]
+    name, nb = line_kernel
+    return KERNELS[name or "k_lines2"] % nb
+
+
+def roofline(kms, nbytes, args, line_kernel=("k_lines2", 112)):
     """The dominant kernel of the timed steps (HIP events on the engine stream,
     averaged over the timed steps): algorithmic bytes = the batch's log bytes
     (every line read once) / its average time."""
@@ -122,7 +131,7 @@ def roofline(kms, nbytes, args):
     traffic, src = pmc_traffic(dom) if default else (None, None)
     r = {
         "bound": "hbm",
-        "kernel": KERNELS[dom],
+        "kernel": kernel_desc(dom, line_kernel),
         "achieved": round(achieved, 1),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
@@ -281,8 +290,22 @@ def main():
         else:
             torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        step()
+    # the first step goes into empty IP / state tables (every IP and (ip, rule
+    # name) state of the batch is new): timed on its own, with its phases
+    cold = None
+    for wi in range(args.warmup):
+        if wi == 0:
+            sync_all()
+            tc0 = time.perf_counter()
+            step()
+            sync_all()
+            cold = {"ms": round((time.perf_counter() - tc0) * 1000.0, 3)}
+            if drives:
+                cold["phase_ms"] = eng.phase_ms()
+                st0 = node.state_stats() if node else eng.state_stats()
+                cold["new_ips"], cold["new_states"] = st0.get("ips"), st0.get("states")
+        else:
+            step()
     kacc = {"k_scan": 0.0, "k_lines": 0.0, "dfa_jobs": 0.0}
 
     def timed_step():
@@ -354,6 +377,19 @@ def main():
                "ms_per_step": round(el3 * 1000.0 / args.bans_steps, 3), "steps": args.bans_steps,
                "what": "each step also builds the per-IP DynamicDecisionLists updates on the device and copies them "
                        "to pinned host memory, without the LogRegexBan lines (BJX_EMIT_BANS | BJX_BAN_RECORDS_ONLY)"}
+    # empty tables again, workspace warm: one step that creates every IP and
+    # state of the batch (the new-IP path without the engine's first
+    # allocations), single-engine runs
+    cold_clear = None
+    if not node_mode and not dist and ex is None:
+        eng.state_clear()
+        sync_all()
+        tcc = time.perf_counter()
+        step()
+        sync_all()
+        cold_clear = {"ms": round((time.perf_counter() - tcc) * 1000.0, 3), "phase_ms": eng.phase_ms(),
+                      "what": "one step right after bjx_state_clear: empty IP / state tables (their capacity kept), "
+                              "the per-line workspace already allocated; every IP and state of the batch is created"}
     total_lines = n_lines * n_parts
     value = total_lines / (elapsed / args.steps)
     kms = {k: v / args.steps for k, v in kacc.items()}
@@ -398,8 +434,15 @@ def main():
                         else "device copies (engines sharing a GPU)") if node_mode else "RCCL all-to-all of the event records"))
                 if n_parts > 1 else "dp1",
             },
-            "roofline": roofline(kms, nbytes, args),
+            "roofline": roofline(kms, nbytes, args, eng.line_kernel()),
         }
+        if cold:
+            cold["what"] = ("wall time of the first warm-up step, into empty IP / state tables: every IP and "
+                            "(ip, rule name) state of the batch is created (rate_limit.go:45-51); phases of "
+                            "engine 0")
+            line["cold_first_step"] = cold
+        if cold_clear:
+            line["cold_step_after_clear"] = cold_clear
         mp_ms = phases["count"] + phases["scan"] + phases["resolve"]
         line["roofline"]["match_pass"] = {
             "kernels": "k_nl_count_wt + k_scan + k_lines + DFA-job sort + k_dfa / k_nfa (phases count+scan+resolve)",

@@ -30,8 +30,9 @@ int bjx_debug_regex_parse(const char *pattern, size_t len, char *err, size_t err
    (returns the phase count) */
 size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap);
 /* device ms of the last batch's dominant kernels, from HIP events on the
-   engine stream: k_scan, k_lines (0 when the scan-header path left it no
-   lines), DFA-job sort + k_dfa / k_nfa (returns the count, 3) */
+   engine stream: k_scan, the per-line kernel, DFA-job sort + k_dfa / k_nfa;
+   then which per-line kernel ran (2 = k_lines2, 1 = k_lines) and its window
+   bytes per line (k_lines2) or staging bytes per wave (k_lines) (returns 5) */
 size_t bjx_debug_kernel_ms(bjx_engine *e, double *out, size_t cap);
 /* last batch: gram bitset hits, recorded literal hits, lines sent to the per-line
    fallback, lines decided by the long-line pass, DFA jobs; then the state
