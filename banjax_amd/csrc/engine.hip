@@ -4783,7 +4783,9 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
       nbytes += ((host_by_id[h].size() + 3) & ~size_t(3)) + 4;
     }
     const size_t words = 2 + 2 * (size_t)ht_cap + n_hosts + nbytes / 4;
-    if (ok && n_hosts && words * 4 <= kLinesHostLdsMax && !getenv("BJX_NO_HOST_LDS")) {
+    // (a ruleset without hosts keeps the empty dictionary: every lookup
+    // returns -1, and k_lines2 runs the global rules' decision class)
+    if (ok && words * 4 <= kLinesHostLdsMax && !getenv("BJX_NO_HOST_LDS")) {
       hl.assign(words, 0);
       hl[0] = ht_cap;
       hl[1] = n_hosts;
@@ -4991,7 +4993,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   // dictionary blob when both fit kLinesTabLdsMax
   uint32_t lt_hinfo = 0, lt_cls = 0, lt_trec = 0, lt_pool = 0;
   uint32_t l2_hdc = 0, l2_dcls = 0, l2_none = 0, l2_bytes = 0;  // k_lines2 tables (0 bytes: not eligible)
-  if (use_plan && hl_bytes && n_hosts && !getenv("BJX_NO_PLAN_LDS")) {
+  if (use_plan && hl_bytes && !getenv("BJX_NO_PLAN_LDS")) {
     std::vector<uint2> hinfo(n_hosts, make_uint2(0, 0));
     std::vector<uint4> cls, trec;
     std::vector<uint8_t> pool;
