@@ -2905,42 +2905,108 @@ __device__ __forceinline__ uint64_t block_alloc(unsigned long long *ctr, uint64_
   return s_w[kBlock / 64] + s_w[wave] + (x - v);
 }
 
-// el_new / counters[4]: the event lines whose IP is new to the table (created
-// in this batch), listed for k_ip_commit
+// counters[4]: the event lines whose IP is new to the table (created in this
+// batch), counted per block shard (claim_shard 2) and summed by k_fold_new.
+// el_id of a line without events is 0 (k_ip_commit passes over every line).
 __global__ __launch_bounds__(kBlock) void k_ip_claim(EvSrc E, State S, uint32_t epoch, uint32_t *__restrict__ el_slot,
-                                                     uint32_t *__restrict__ el_id, uint32_t *__restrict__ el_new,
-                                                     uint64_t shard_budget) {
+                                                     uint32_t *__restrict__ el_id, uint64_t shard_budget) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool claimed = false, isnew = false;
-  if (i < E.n && ev_has(E, i) && !flag_set(S, 5)) {
-    el_id[i] = 0;
-    claimed = ip_claim_line(E, S, epoch, i, el_slot, el_id, shard_budget);
-    isnew = el_id[i] == kNewIp;
+  if (i < E.n && !flag_set(S, 5)) {
+    if (ev_has(E, i)) {
+      el_id[i] = 0;
+      claimed = ip_claim_line(E, S, epoch, i, el_slot, el_id, shard_budget);
+      isnew = el_id[i] == kNewIp;
+    } else {
+      el_id[i] = 0;
+    }
   }
   count_claims(S, 0, 5, claimed, shard_budget);
-  const uint64_t at = block_alloc((unsigned long long *)&S.counters[4], isnew ? 1u : 0u);
-  if (isnew) el_new[at] = (uint32_t)i;
+  const uint64_t nn = __ballot(isnew);
+  if (nn && (threadIdx.x & 63) == (uint32_t)(__ffsll((unsigned long long)nn) - 1))
+    atomicAdd(claim_shard(S, 2), (unsigned long long)__popcll(nn));
 }
 
-// over the event lines k_ip_claim listed (el_new, n_new of them): IPs of
-// earlier batches were settled there
-__global__ __launch_bounds__(kBlock) void k_ip_commit(EvSrc E, State S, uint32_t epoch, const uint32_t *__restrict__ el_slot,
-                                                      uint32_t *__restrict__ el_id, const uint32_t *__restrict__ el_new,
-                                                      uint64_t n_new, uint32_t *__restrict__ coll) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool act = t < n_new;
-  const uint64_t i = act ? el_new[t] : 0;
-  uint32_t s = 0, f = 0, len = 0;
-  if (act) {
-    s = el_slot[i];
-    f = S.ip_first[s];
-    len = E.ip_len[i];
+// the shards' new-line counts -> counters[4] (one wave: lane = shard)
+__global__ void k_fold_new(State S) {
+  const uint32_t t = threadIdx.x;
+  unsigned long long v = S.counters[kShardBase + 16 * t + 2];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+  if (t == 0) S.counters[4] = v;
+}
+
+// A new IP's first event line (ip_first of its slot) gets its id and arena
+// bytes.  Ids and byte offsets come from a scan, not from atomics on one
+// counter (a single address takes about 88 atomics per microsecond: a cold
+// batch of 125M lines paid about 11 ms for one per block): k_ip_firsts counts
+// each block's first lines and their bytes, an exclusive scan over the blocks
+// gives each block its base, and k_ip_commit adds the in-block prefix.
+__device__ __forceinline__ bool ip_first_line(const EvSrc &E, const State &S, const uint32_t *el_slot, const uint32_t *el_id,
+                                              uint64_t i, uint32_t &len) {
+  len = 0;
+  if (i >= E.n || el_id[i] != kNewIp) return false;
+  if (S.ip_first[el_slot[i]] != (uint32_t)i) return false;
+  len = E.ip_len[i];
+  return true;
+}
+
+// block sums of (a, b); valid in thread 0
+__device__ __forceinline__ void block_sum2(uint64_t &a, uint64_t &b) {
+  __shared__ unsigned long long s_a[kBlock / 64], s_b[kBlock / 64];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) { a += __shfl_xor(a, d); b += __shfl_xor(b, d); }
+  if ((threadIdx.x & 63) == 0) { s_a[threadIdx.x >> 6] = a; s_b[threadIdx.x >> 6] = b; }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int w = 1; w < kBlock / 64; ++w) { a += s_a[w]; b += s_b[w]; }
+}
+
+__global__ __launch_bounds__(kBlock) void k_ip_firsts(EvSrc E, State S, const uint32_t *__restrict__ el_slot,
+                                                      const uint32_t *__restrict__ el_id, uint32_t *__restrict__ blk_n,
+                                                      uint64_t *__restrict__ blk_b) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t len;
+  const bool first = ip_first_line(E, S, el_slot, el_id, i, len);
+  uint64_t a = first ? 1 : 0, b = len;
+  block_sum2(a, b);
+  if (threadIdx.x == 0) { blk_n[blockIdx.x] = (uint32_t)a; blk_b[blockIdx.x] = b; }
+}
+
+// exclusive prefix of v over the block (every thread calls it)
+__device__ __forceinline__ uint64_t block_excl(uint64_t v) {
+  __shared__ unsigned long long s_w[kBlock / 64];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d);
+    if (lane >= (uint32_t)d) x += y;
   }
-  const bool first = act && f == (uint32_t)i;
-  // ids and arena bytes: one atomic per block
-  const uint32_t id = (uint32_t)block_alloc((unsigned long long *)&S.counters[0], first ? 1u : 0u);
-  const uint64_t off = block_alloc((unsigned long long *)&S.counters[1], first ? len : 0u);
+  __syncthreads();  // a previous call's readers are done with s_w
+  if (lane == 63) s_w[wave] = x;
+  __syncthreads();
+  uint64_t before = 0;
+  for (uint32_t w = 0; w < wave; ++w) before += s_w[w];
+  return before + x - v;
+}
+
+// every event line whose IP is new in this batch (el_id kNewIp): the first
+// line of the IP writes its bytes, id and key; the others check theirs
+// against it (a 64-bit hash collision inside the batch -> k_ip_collide, serial)
+__global__ __launch_bounds__(kBlock) void k_ip_commit(EvSrc E, State S, const uint32_t *__restrict__ el_slot,
+                                                      uint32_t *__restrict__ el_id, const uint32_t *__restrict__ blk_noff,
+                                                      const uint64_t *__restrict__ blk_boff, uint32_t *__restrict__ coll) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t len;
+  const bool first = ip_first_line(E, S, el_slot, el_id, i, len);
+  const uint64_t id_in = block_excl(first ? 1 : 0);
+  const uint64_t off_in = block_excl(len);
+  const bool act = i < E.n && el_id[i] == kNewIp;
   if (first) {
+    const uint32_t s = el_slot[i];
+    const uint32_t id = (uint32_t)(S.counters[0] + blk_noff[blockIdx.x] + id_in);
+    const uint64_t off = S.counters[1] + blk_boff[blockIdx.x] + off_in;
     const uint8_t *ip = ev_ip(E, i);
     for (uint32_t k = 0; k < len; ++k) S.arena[off + k] = ip[k];
     S.ip_off[id] = off;
@@ -2951,13 +3017,22 @@ __global__ __launch_bounds__(kBlock) void k_ip_commit(EvSrc E, State S, uint32_t
   } else if (act) {
     // the same IP as its slot's first line?  IPs of up to 15 bytes by their
     // inline keys (bytes and length: exact), longer ones byte by byte
-    const uint32_t lf = E.ip_len[f];
-    const bool same = lf == len && (len <= 15 && E.ip16 ? key16_eq(E.ip16[f], E.ip16[i]) : bytes_eq(ev_ip(E, f), ev_ip(E, i), len));
+    const uint32_t f = S.ip_first[el_slot[i]];
+    const uint32_t ln = E.ip_len[i], lf = E.ip_len[f];
+    const bool same = lf == ln && (ln <= 15 && E.ip16 ? key16_eq(E.ip16[f], E.ip16[i]) : bytes_eq(ev_ip(E, f), ev_ip(E, i), ln));
     if (!same) {
       const uint64_t k = atomicAdd((unsigned long long *)&S.counters[3], 1ull);
       coll[k] = (uint32_t)i;
     }
   }
+}
+
+// counters[0] / [1] += this batch's new IPs and their bytes (after k_ip_commit)
+__global__ void k_ip_commit_total(State S, uint64_t nb, const uint32_t *__restrict__ blk_n, const uint32_t *__restrict__ blk_noff,
+                                  const uint64_t *__restrict__ blk_b, const uint64_t *__restrict__ blk_boff) {
+  if (blockIdx.x || threadIdx.x) return;
+  S.counters[0] += (uint64_t)blk_noff[nb - 1] + blk_n[nb - 1];
+  S.counters[1] += blk_boff[nb - 1] + blk_b[nb - 1];
 }
 
 // Lines whose IP differs from the first line of its slot (equal 64-bit hash):
@@ -4242,7 +4317,8 @@ struct bjx_engine {
   bool rec12 = false;
   int64_t rec_base = 0;
   DevBuf<uint32_t> el_id;
-  DevBuf<uint32_t> el_new;  // event lines with a new IP (k_ip_claim -> k_ip_commit)
+  DevBuf<uint32_t> blk_n;   // k_ip_firsts: first lines per block, then their exclusive scan
+  DevBuf<uint64_t> blk_b;   // ... and their IP bytes
   DevBuf<uint8_t> rl_out, ev_out, ev_out_s, trip_flag;
   DevBuf<uint32_t> trip_ev, trip_ev2;
   DevBuf<bjx_trip> d_trips;
@@ -5698,7 +5774,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   e->scalars.release(); e->res_seq.release(); e->res_rule.release(); e->ev_el.release(); e->ev_rule.release();
 
   e->ev_res.release(); e->ev_st.release(); e->ev_st2.release(); e->ev_idx.release(); e->ev_idx2.release();
-  e->el_slot.release(); e->coll.release(); e->el_new.release(); e->ev_rec.release(); e->ev_rec2.release(); e->el_id.release();
+  e->el_slot.release(); e->coll.release(); e->blk_n.release(); e->blk_b.release(); e->ev_rec.release(); e->ev_rec2.release(); e->el_id.release();
 
   for (auto *b : {&e->pk_key, &e->pk_key2, &e->pk_line, &e->pk_line2, &e->pack_src, &e->rx_len, &e->rx_ev_el}) b->release();
   for (auto *b : {&e->pk_nev, &e->pk_ipl, &e->pk_evoff, &e->pk_byoff, &e->pk_start, &e->pk_counts, &e->pk_bbase,
@@ -5874,7 +5950,7 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
   if (e->host_counters[0] + n_el >= 0x7FFFFFFFull) throw BjxError(BJX_ERR_CAPACITY, "more than 2^31 distinct IPs");
   if (++e->epoch == 0) ++e->epoch;  // 0 marks a slot being claimed
   const uint32_t epoch = e->epoch;
-  e->el_slot.ensure(E.n); e->el_id.ensure(E.n); e->coll.ensure(E.n); e->el_new.ensure(E.n);
+  e->el_slot.ensure(E.n); e->el_id.ensure(E.n); e->coll.ensure(E.n);
   uint64_t nw_ovf[2] = {0, 0};  // new-IP event lines (k_ip_claim's list), IP table overflow flag
   e->ev_st.ensure(n_ev); e->ev_st2.ensure(n_ev); e->ev_rec.ensure(n_ev); e->ev_rec2.ensure(n_ev);
   e->ev_out.ensure(n_ev); e->ev_out_s.ensure(n_ev);
@@ -5890,7 +5966,8 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
       // a retry after an overflow claims every line again (the rolled-back
       // claims left their lines' el_id set)
       hipLaunchKernelGGL(k_ip_claim, dim3(grid_for(E.n)), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p,
-                         e->el_new.p, budget / kClaimShards);
+                         budget / kClaimShards);
+      hipLaunchKernelGGL(k_fold_new, dim3(1), dim3(kClaimShards), 0, st, e->S);
       HIP_OK(hipGetLastError());
       HIP_OK(hipMemcpyAsync(nw_ovf, e->S.counters + 4, 16, hipMemcpyDeviceToHost, st));
       HIP_OK(hipStreamSynchronize(st));
@@ -5903,8 +5980,15 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
       if (!forced) grow_ip(e, n_ips + n_el);
     }
     if (nw_ovf[0]) {
-      hipLaunchKernelGGL(k_ip_commit, dim3(grid_for(nw_ovf[0])), dim3(kBlock), 0, st, E, e->S, epoch, e->el_slot.p, e->el_id.p,
-                         e->el_new.p, nw_ovf[0], e->coll.p);
+      const uint64_t nb = grid_for(E.n);
+      e->blk_n.ensure(2 * nb); e->blk_b.ensure(2 * nb);
+      uint32_t *bn = e->blk_n.p, *bno = e->blk_n.p + nb;
+      uint64_t *bb = e->blk_b.p, *bbo = e->blk_b.p + nb;
+      hipLaunchKernelGGL(k_ip_firsts, dim3(nb), dim3(kBlock), 0, st, E, e->S, e->el_slot.p, e->el_id.p, bn, bb);
+      cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, bn, bno, (int)nb, st); });
+      cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, bb, bbo, (int)nb, st); });
+      hipLaunchKernelGGL(k_ip_commit, dim3(nb), dim3(kBlock), 0, st, E, e->S, e->el_slot.p, e->el_id.p, bno, bbo, e->coll.p);
+      hipLaunchKernelGGL(k_ip_commit_total, dim3(1), dim3(64), 0, st, e->S, nb, bn, bno, bb, bbo);
       HIP_OK(hipGetLastError());
     }
     uint64_t n_coll = 0;
