@@ -5292,6 +5292,66 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
         rec[8] = w_rows; rec[9] = w_pr; rec[10] = w_anc; rec[11] = (uint32_t)(D.anc.size() / kL2AncWords);
       }
       al4();
+      // inline DFAs (l2_inline): a position whose rule is anchored at the
+      // start of rest (its automaton decides within a few dozen bytes, inside
+      // the window; rules that look for a literal anywhere mostly decide past
+      // it: at cfg3 inlining those cost k_lines2 2.9 ms and saved 1 % of the
+      // jobs) and whose automaton is small (< 256 states, no NFA) gets its
+      // next-state table over ASCII bytes
+      // (u8 [state][128]) and its accept-at-end flags in the blob, so a job of
+      // that rule is run in k_lines2 over the line's window when the window
+      // holds the decision; kPlanOwn positions (a different rule per host) and
+      // tables past kL2TabMax keep their jobs
+      {
+        // the inline tables may not cost k_lines2 a block per CU: they fit
+        // what two blocks (8 waves and their windows each) leave of the CU's
+        // LDS, when the tables before them did
+        const size_t two_blocks = kScanLdsMax / 2 - (size_t)(kL2Block / 64) * kL2WaveLds;
+        const size_t inl_max = t.size() * 4 <= two_blocks ? std::min<size_t>(kL2TabMax, two_blocks) : (size_t)kL2TabMax;
+        std::map<uint32_t, uint32_t> inl_of;  // rule -> entry word offset (0: not inline)
+        for (uint32_t d = 0; d < dcs.size() && ok; ++d) {
+          Dc &D = dcs[d];
+          uint32_t pin[64] = {};
+          bool any = false;
+          for (uint32_t p = 0; p < 64; ++p) {
+            const uint32_t w = D.prule[p];
+            if (!w || (w & kPlanOwn)) continue;
+            const uint32_t r = w & 0xFFFFFu;
+            if (r >= drules.size()) continue;
+            auto it = inl_of.find(r);
+            if (it == inl_of.end()) {
+              const DevRule &dr = drules[r];
+              const CompiledRegex &rx = rs->rules[r].rx;
+              uint32_t at = 0;
+              const size_t need = 16 + (size_t)dr.n_states * 128 + ((dr.n_states + 3) & ~3u) + 16;
+              if (dr.mode == kModeAnchored && !(dr.flags & (kRuleNfa | kRuleNfaWide | kRuleAlways | kRuleNever)) &&
+                  dr.n_states >= 2 && dr.n_states < 256 &&
+                  rx.trans.size() >= (size_t)dr.n_states * dr.ncls && (t.size() + 4) * 4 + need + 256 <= inl_max) {
+                at = al4();
+                t.resize(t.size() + 4, 0);
+                const uint32_t w_tr = al4();
+                t.resize(t.size() + (size_t)dr.n_states * 32, 0);
+                uint8_t *tb = reinterpret_cast<uint8_t *>(t.data() + w_tr);
+                for (uint32_t st = 0; st < dr.n_states; ++st)
+                  for (uint32_t b = 0; b < 128; ++b) tb[st * 128 + b] = (uint8_t)rx.trans[(size_t)st * dr.ncls + rx.ascii_cls[b]];
+                const uint32_t w_ae = al4();
+                t.resize(t.size() + (dr.n_states + 3) / 4, 0);
+                uint8_t *ab = reinterpret_cast<uint8_t *>(t.data() + w_ae);
+                for (uint32_t st = 0; st < dr.n_states; ++st) ab[st] = rx.accept_end[st] ? 1 : 0;
+                t[at] = w_tr * 4; t[at + 1] = w_ae * 4; t[at + 2] = dr.start; t[at + 3] = dr.skip_len ? dr.skip_state : dr.start;
+              }
+              it = inl_of.emplace(r, at).first;
+            }
+            pin[p] = it->second;
+            any = any || it->second != 0;
+          }
+          if (!any || (t.size() + 68) * 4 > inl_max) continue;
+          const uint32_t w_pin = al4();
+          t.insert(t.end(), pin, pin + 64);
+          t[w_dc + kL2DclsWords * d + 12] = w_pin;
+        }
+        al4();
+      }
       if (ok && t.size() * 4 <= kL2TabMax) {
         l2_hdc = w_hdc; l2_dcls = w_dc; l2_none = none;
         l2_bytes = (uint32_t)(t.size() * 4);

@@ -227,6 +227,30 @@ __device__ __forceinline__ uint64_t l2_job_rec(const Bind &B, uint32_t r, const 
 
 __device__ __forceinline__ uint4 l2_ld4w(const uint32_t *hl, uint32_t w) { return *reinterpret_cast<const uint4 *>(hl + w); }
 
+// A job's automaton run here, over the line's window, for a rule with an
+// inline table (entry word `ent` of the blob: {next-state table byte offset,
+// accept-at-end byte offset, start state, skip state}; u8 next states over
+// ASCII bytes): 1 matched, 0 no match, 2 undecided (the decision lies past
+// the window, or a non-ASCII byte needs rune decoding: the job goes to k_dfa).
+// The same steps as dfa_line from the job's start: stop at the dead or accept
+// state, or at the line's end with the accept-at-end flag.
+__device__ __forceinline__ uint32_t l2_inline(const uint32_t *hl, uint32_t ent, const L2Line &X, uint64_t s, uint64_t rec) {
+  const uint4 e = l2_ld4w(hl, ent);
+  const uint8_t *tr = reinterpret_cast<const uint8_t *>(hl) + e.x;
+  const uint8_t *ae = reinterpret_cast<const uint8_t *>(hl) + e.y;
+  uint32_t st = (rec & kJobSkipState) ? e.w : e.z;
+  uint32_t o = (uint32_t)((rec & kJobOffMask) - s);
+  const uint32_t lim = X.n < X.lim ? X.n : X.lim;
+  for (; o < lim; ++o) {
+    const uint32_t b = X.wp[o];
+    if (b >= 0x80) return 2;
+    st = tr[st * 128u + b];
+    if (st <= 1) return st == kAccept ? 1u : 0u;
+  }
+  if (o < X.n) return 2;
+  return ae[st] ? 1u : 0u;
+}
+
 __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
   uint32_t *s_hl = reinterpret_cast<uint32_t *>(s_dyn);
   for (uint32_t i = threadIdx.x; i < B.l2_bytes / 16; i += blockDim.x)
@@ -337,7 +361,7 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
         const uint64_t anyhit = ((uint64_t)d1.y << 32) | d1.x, anyovf = ((uint64_t)d1.w << 32) | d1.z;
         const uint32_t rows = d2.x, prule = d2.y, anc = d2.z, n_anc = d2.w;
         const uint32_t first_rule = hid >= 0 ? LT.hinfo[hid].y : 0u;
-        (void)d3;
+        const uint32_t pinl = d3.x;  // the class's inline-DFA entries per position (0: none)
         const bool exempt = B.any_allow && check_is_allowed(B, hid, X.gp + ip_off, ip_len);
         const int64_t tsn = ns_from_seconds(f);
         uint8_t fl = 0;
@@ -444,8 +468,14 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
             const uint32_t w = s_hl[prule + p];
             const uint32_t r = (w & kPlanOwn) ? first_rule + p : (w & 0xFFFFFu);
             const uint64_t rec = l2_job_rec(B, r, cm, cv, rs, rest_len, rest_off);
-            if (rec == kJobDecided) m |= l2_bit(p);
-            else emit_job(S, j, r, p, rec | (((skp >> p) & 1) ? kJobNoCount : 0ull));
+            uint32_t res = 2;
+            if (rec == kJobDecided) res = 1;
+            else if (pinl && !(rec & kJobLegacy)) {
+              const uint32_t ent = s_hl[pinl + p];
+              if (ent) res = l2_inline(s_hl, ent, X, s, rec);
+            }
+            if (res == 1) m |= l2_bit(p);
+            else if (res == 2) emit_job(S, j, r, p, rec | (((skp >> p) & 1) ? kJobNoCount : 0ull));
           }
           L.masks[j * B.mask_words] = m;
           if (B.mask_words > 1) L.masks[j * B.mask_words + 1] = 0;
