@@ -102,7 +102,7 @@ EXPORTS = [
     "bjx_ruleset_rule_info", "bjx_engine_create", "bjx_engine_destroy", "bjx_engine_set_decision_lists",
     "bjx_process_batch", "bjx_state_get", "bjx_state_len", "bjx_state_clear", "bjx_state_dump",
     "bjx_engine_last_error", "bjx_match_batch", "bjx_events_partition", "bjx_events_pack", "bjx_apply_events",
-    "bjx_finish_batch", "bjx_tailer_open", "bjx_tailer_next", "bjx_tailer_release", "bjx_tailer_stats",
+    "bjx_finish_batch", "bjx_apply_events_trips", "bjx_finish_batch_trips", "bjx_tailer_open", "bjx_tailer_next", "bjx_tailer_release", "bjx_tailer_stats",
     "bjx_tailer_close", "bjx_engine_set_ban_options", "bjx_batch_bans", "bjx_state_stats_get",
     "bjx_node_create", "bjx_node_destroy", "bjx_node_size", "bjx_node_engine", "bjx_node_last_error", "bjx_node_set_decision_lists",
     "bjx_node_set_ban_options", "bjx_node_process_batch", "bjx_node_process_chunks", "bjx_node_batch_bans",
@@ -166,6 +166,11 @@ def lib():
     L.bjx_apply_events.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, C.POINTER(C.c_uint64), vp]
     L.bjx_finish_batch.restype = C.c_int
     L.bjx_finish_batch.argtypes = [vp, vp, C.c_uint32, C.POINTER(BatchResult)]
+    L.bjx_apply_events_trips.restype = C.c_int
+    L.bjx_apply_events_trips.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), vp,
+                                         C.POINTER(C.c_uint64)]
+    L.bjx_finish_batch_trips.restype = C.c_int
+    L.bjx_finish_batch_trips.argtypes = [vp, vp, C.c_uint64, C.c_uint32, C.POINTER(BatchResult)]
     L.bjx_state_get.restype = C.c_int
     L.bjx_state_get.argtypes = [vp, C.c_char_p, sz, C.c_char_p, sz, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.bjx_state_len.restype = C.c_int64

@@ -74,6 +74,8 @@ __device__ __forceinline__ uint32_t ld4(const uint8_t *p) {
 
 BJX_HD uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 
+BJX_HD uint64_t hash_finish(uint32_t a, uint32_t b, uint32_t t);
+
 // 64-bit hash of a byte string (engine-internal: host dictionary, IP state
 // keys); 4 bytes per step in two 32-bit lanes, murmur3-style finalizer.
 // Never returns 0 or ~0 (table sentinels).
@@ -87,6 +89,12 @@ BJX_HD uint64_t hash_bytes(const uint8_t *p, uint32_t n) {
   }
   uint32_t t = 0;
   for (uint32_t k = 0; i + k < n; ++k) t |= (uint32_t)p[i + k] << (8 * k);
+  return hash_finish(a, b, t);
+}
+
+// hash_bytes' last step: the tail word t (the 0-3 bytes after the last full
+// word, zero padded) and the finalizer
+BJX_HD uint64_t hash_finish(uint32_t a, uint32_t b, uint32_t t) {
   a = rotl32(a ^ t ^ 0xA5A5A5A5u, 7) * 0x27D4EB2Du;
   b = rotl32(b + t, 13) * 0x165667B1u;
   a ^= b >> 16; a *= 0x85EBCA6Bu; a ^= a >> 13; a *= 0xC2B2AE35u; a ^= a >> 16;

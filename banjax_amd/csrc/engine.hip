@@ -112,8 +112,57 @@ __device__ __forceinline__ uint4 ip_key16_bytes(const uint8_t *ip, uint32_t len)
   w[3] |= (len < 255 ? len : 255u) << 24;
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
+constexpr uint32_t kIpWords = 12;  // IPs of < 48 bytes (IPv4 and IPv6 text) are handled as words in registers
+
+// bytes [p, p + n), n <= 4 * NW, as NW zero-padded little-endian words,
+// every load issued at once; loads only the aligned words holding at least
+// one of the bytes (an exchanged IP pool may end at p + n)
+template <uint32_t NW>
+__device__ __forceinline__ void ip_words(const uint8_t *p, uint32_t n, uint32_t (&w)[NW]) {
+  const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+  const uint32_t *a = reinterpret_cast<const uint32_t *>(p - sh);
+  const uint32_t nw = n ? (sh + n + 3) >> 2 : 0u;
+  uint32_t r[NW + 1];
+#pragma unroll
+  for (uint32_t k = 0; k <= NW; ++k) r[k] = k < nw ? a[k] : 0u;
+#pragma unroll
+  for (uint32_t k = 0; k < NW; ++k) {
+    const uint32_t lo = 4u * k;
+    const uint32_t m = n <= lo ? 0u : (n >= lo + 4 ? 0xFFFFFFFFu : (1u << (8 * (n - lo))) - 1u);
+    w[k] = __builtin_amdgcn_alignbyte(r[k + 1], r[k], sh) & m;
+  }
+}
+// hash_bytes of n < 4 * NW bytes given as ip_words
+template <uint32_t NW>
+__device__ __forceinline__ uint64_t hash_words(const uint32_t (&w)[NW], uint32_t n) {
+  uint32_t a = 0x9E3779B9u ^ n, b = 0x7F4A7C15u + n * 0x85EBCA6Bu;
+  const uint32_t full = n >> 2;
+  uint32_t t = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < NW; ++k) {
+    if (k < full) {
+      a = rotl32(a ^ w[k], 7) * 0x27D4EB2Du;
+      b = rotl32(b + w[k], 13) * 0x165667B1u;
+    } else if (k == full) {
+      t = w[k];
+    }
+  }
+  return hash_finish(a, b, t);
+}
 __device__ __forceinline__ bool key16_eq(const uint4 &a, const uint4 &b) {
   return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+}
+// equal byte strings of length n: below 4 * kIpWords bytes by word loads all
+// issued at once (bytes_eq's loop waits for each word pair in turn)
+__device__ __forceinline__ bool ip_eq(const uint8_t *a, const uint8_t *b, uint32_t n) {
+  if (n >= 4 * kIpWords) return bytes_eq(a, b, n);
+  uint32_t wa[kIpWords], wb[kIpWords];
+  ip_words(a, n, wa);
+  ip_words(b, n, wb);
+  bool eq = true;
+#pragma unroll
+  for (uint32_t k = 0; k < kIpWords; ++k) eq = eq && wa[k] == wb[k];
+  return eq;
 }
 
 // host string -> host id (per_site_regexes_with_rates key / skip host / allow-list site)
@@ -2821,7 +2870,10 @@ __device__ __forceinline__ bool ip_claim_line(const EvSrc &E, const State &S, ui
   const uint64_t h = E.ip_hash[i];
   const uint32_t len = E.ip_len[i];
   const bool inl = len <= 15;
-  const uint4 k16 = !inl ? make_uint4(0, 0, 0, 0) : E.ip16 ? E.ip16[i] : ip_key16_bytes(ev_ip(E, i), len);
+  // the inline key: the whole IP up to 15 bytes, else its first 15 bytes and
+  // length (a slot whose key differs holds another IP; an equal one compares
+  // the arena bytes)
+  const uint4 k16 = E.ip16 ? E.ip16[i] : ip_key16_bytes(ev_ip(E, i), len);
   uint64_t s = h & S.ip_mask;
   bool claimed = false;
   for (;;) {
@@ -2864,7 +2916,8 @@ __device__ __forceinline__ bool ip_claim_line(const EvSrc &E, const State &S, ui
       }
       // created by an earlier batch: short IPs compare inline, long ones in the arena
       const uint32_t id = q0.z;
-      if (inl ? key16_eq(q1, k16) : (S.ip_len[id] == len && bytes_eq(S.arena + S.ip_off[id], ev_ip(E, i), len))) {
+      if (key16_eq(q1, k16) &&
+          (inl || ((len < 255 || S.ip_len[id] == len) && ip_eq(S.arena + S.ip_off[id], ev_ip(E, i), len)))) {
         el_slot[i] = (uint32_t)s;
         el_id[i] = id;
         return claimed;
@@ -3019,7 +3072,7 @@ __global__ __launch_bounds__(kBlock) void k_ip_commit(EvSrc E, State S, const ui
     // inline keys (bytes and length: exact), longer ones byte by byte
     const uint32_t f = S.ip_first[el_slot[i]];
     const uint32_t ln = E.ip_len[i], lf = E.ip_len[f];
-    const bool same = lf == ln && (ln <= 15 && E.ip16 ? key16_eq(E.ip16[f], E.ip16[i]) : bytes_eq(ev_ip(E, f), ev_ip(E, i), ln));
+    const bool same = lf == ln && (ln <= 15 && E.ip16 ? key16_eq(E.ip16[f], E.ip16[i]) : ip_eq(ev_ip(E, f), ev_ip(E, i), ln));
     if (!same) {
       const uint64_t k = atomicAdd((unsigned long long *)&S.counters[3], 1ull);
       coll[k] = (uint32_t)i;
@@ -3825,114 +3878,237 @@ __global__ void k_rehash_st(uint64_t old_cap, const StSlot *__restrict__ o, StSl
 }
 
 // --------------------------------------------------------------- multi-GPU exchange
-// owner of each event line: (ip_hash >> 32) % n_parts; lines without events sort last
-__global__ void k_part_keys(uint64_t n_lines, const uint64_t *__restrict__ counts, const uint64_t *__restrict__ ip_hash,
-                            uint32_t n_parts, uint32_t *__restrict__ key, uint32_t *__restrict__ val) {
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n_lines) return;
-  key[j] = (counts[j] & 0xFFFFFFFFull) ? (uint32_t)((ip_hash[j] >> 32) % n_parts) : n_parts;
-  val[j] = (uint32_t)j;
+// The partition runs over the lines in tiles of `steps` x kBlock lines (one
+// block each, one line per lane per step), in line order: k_part_count sums
+// each tile's (event lines, events, IP bytes) per owner; one exclusive scan
+// per quantity over [owner][tile] gives every (owner, tile) its first packed
+// position, owner-major (the order of a stable sort by owner); k_pack re-reads
+// the tile and writes each event line's record, rule indices and IP bytes
+// there.  Inside a tile, lanes of one owner are ranked by ballot (one pass per
+// distinct owner in the wave) and the four waves by their per-owner totals, so
+// a line's place follows line order.  Each IP takes a 4-byte aligned slot of
+// the byte pool (its length rounded up), so a lane stores its IP as whole
+// words with no neighbour sharing them.
+constexpr uint32_t kMaxParts = 256;       // owners of one partition
+__host__ __device__ __forceinline__ uint32_t ip_slot_bytes(uint32_t len) { return (len + 3u) & ~3u; }
+
+struct PartLine {
+  bool ev;           // an event line
+  uint32_t o, ne, len;
+};
+__device__ __forceinline__ PartLine part_line(uint64_t j, uint64_t n_lines, const Lines &L, uint32_t n_parts) {
+  PartLine r{false, 0, 0, 0};
+  if (j < n_lines) {
+    r.ne = (uint32_t)(L.counts[j] & 0xFFFFFFFFull);
+    if (r.ne) {
+      r.ev = true;
+      r.o = (uint32_t)((L.ip_hash[j] >> 32) % n_parts);
+      r.len = L.ip_len[j];
+    }
+  }
+  return r;
+}
+// (events | IP slot bytes << 32) of one line; clamped to the 16-bit wire
+// fields so a tile's sums stay in 32 bits (a wider line fails the batch: *wide)
+__device__ __forceinline__ uint64_t part_eb(const PartLine &x) {
+  return (uint64_t)min(x.ne, 0xFFFFu) | ((uint64_t)ip_slot_bytes(min(x.len, 0xFFFFu)) << 32);
+}
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, uint32_t lane) {
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t x = __shfl_up(v, d, 64);
+    if (lane >= d) v += x;
+  }
+  return v;
 }
 
-// scan inputs per packed line (index n_el: 0, so the exclusive scans end in
-// totals).  *wide is raised for a line whose IP length or event count does
-// not fit bjx_event_line's 16-bit fields (the batch then fails with
-// BJX_ERR_CAPACITY instead of packing a truncated key)
-__global__ void k_pack_prep(uint64_t n_el, const uint32_t *__restrict__ line, const uint64_t *__restrict__ counts,
-                            const uint32_t *__restrict__ ip_len, uint64_t *__restrict__ nev, uint64_t *__restrict__ ipl,
-                            unsigned long long *__restrict__ wide) {
-  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p > n_el) return;
-  if (p == n_el) { nev[p] = 0; ipl[p] = 0; return; }
-  const uint32_t j = line[p];
-  nev[p] = counts[j] & 0xFFFFFFFFull;
-  ipl[p] = ip_len[j];
-  if (nev[p] > 0xFFFFu || ip_len[j] > 0xFFFFu) atomicOr(wide, 1ull);
+// hist: three arrays of S = n_parts * n_tiles + 1 entries (event lines,
+// events, IP bytes), entry o * n_tiles + tile; the last entry of each is left
+// zero (the scans then end in the totals).  *wide: a line whose event count or
+// IP length does not fit bjx_event_line's 16-bit fields (the batch then fails
+// with BJX_ERR_CAPACITY instead of packing a truncated key)
+__global__ __launch_bounds__(kBlock) void k_part_count(uint64_t n_lines, uint32_t n_tiles, uint32_t steps, Lines L,
+                                                       uint32_t n_parts, uint64_t *__restrict__ hist,
+                                                       unsigned long long *__restrict__ wide) {
+  __shared__ unsigned long long s_n[kMaxParts], s_eb[kMaxParts];
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t o = threadIdx.x; o < n_parts; o += kBlock) s_n[o] = 0, s_eb[o] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * steps * kBlock;
+  bool w = false;
+  for (uint32_t s = 0; s < steps; ++s) {
+    const PartLine x = part_line(base + s * kBlock + threadIdx.x, n_lines, L, n_parts);
+    w |= x.ev && (x.ne > 0xFFFFu || x.len > 0xFFFFu);
+    for (uint64_t todo = __ballot(x.ev); todo;) {  // each owner present in the wave once
+      const uint32_t lead = (uint32_t)__ffsll((unsigned long long)todo) - 1;
+      const uint32_t o = __shfl(x.o, lead, 64);
+      const bool mine = x.ev && x.o == o;
+      const uint64_t m = __ballot(mine);
+      todo &= ~m;
+      uint64_t v = mine ? part_eb(x) : 0;
+#pragma unroll
+      for (uint32_t d = 32; d; d >>= 1) v += __shfl_xor(v, d, 64);
+      if (lane == lead) {
+        atomicAdd(&s_n[o], (unsigned long long)__popcll(m));
+        atomicAdd(&s_eb[o], (unsigned long long)v);
+      }
+    }
+  }
+  if (__ballot(w) && lane == 0) atomicOr(wide, 1ull);
+  __syncthreads();
+  const uint64_t S = (uint64_t)n_parts * n_tiles + 1;
+  for (uint32_t o = threadIdx.x; o < n_parts; o += kBlock) {
+    const uint64_t i = (uint64_t)o * n_tiles + blockIdx.x;
+    hist[i] = s_n[o];
+    hist[S + i] = s_eb[o] & 0xFFFFFFFFull;
+    hist[2 * S + i] = s_eb[o] >> 32;
+  }
 }
 
-// first packed index of each owner (keys sorted); start[] preset to n_el
-__global__ void k_part_bounds(uint64_t n_el, const uint32_t *__restrict__ key, uint64_t *__restrict__ start) {
-  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < n_el && (p == 0 || key[p] != key[p - 1])) start[key[p]] = p;
-}
-
-// per owner: (lines, events, bytes) and the owner's first byte; one thread
-__global__ void k_part_counts(uint32_t n_parts, uint64_t n_el, uint64_t *__restrict__ start,
-                              const uint64_t *__restrict__ ev_off, const uint64_t *__restrict__ by_off,
+// per owner: (lines, events, bytes) and the owner's first byte (off: the
+// exclusive scans of k_part_count's arrays); one thread
+__global__ void k_part_counts(uint32_t n_parts, uint32_t n_tiles, const uint64_t *__restrict__ off,
                               uint64_t *__restrict__ counts, uint64_t *__restrict__ byte_base) {
   if (blockIdx.x || threadIdx.x) return;
-  uint64_t nxt = n_el;
-  for (int k = (int)n_parts - 1; k >= 0; --k) {  // owners without lines start where the next one does
-    if (start[k] > nxt) start[k] = nxt;
-    nxt = start[k];
-  }
+  const uint64_t S = (uint64_t)n_parts * n_tiles + 1;
   for (uint32_t k = 0; k < n_parts; ++k) {
-    const uint64_t b = start[k], e = k + 1 < n_parts ? start[k + 1] : n_el;
-    counts[3 * k + 0] = e - b;
-    counts[3 * k + 1] = ev_off[e] - ev_off[b];
-    counts[3 * k + 2] = by_off[e] - by_off[b];
-    byte_base[k] = by_off[b];
+    const uint64_t b = (uint64_t)k * n_tiles, e = b + n_tiles;
+    for (int c = 0; c < 3; ++c) counts[3 * k + c] = off[c * S + e] - off[c * S + b];
+    byte_base[k] = off[2 * S + b];
   }
 }
 
-constexpr uint32_t kPackWaveBytes = 2048;  // a wave's IP bytes staged in LDS for 16 B stores
-__global__ __launch_bounds__(kBlock) void k_pack(uint64_t n_el, const uint32_t *__restrict__ key, const uint32_t *__restrict__ line,
-                       const uint64_t *__restrict__ ev_off, const uint64_t *__restrict__ by_off,
-                       const uint64_t *__restrict__ part_byte_base, const uint8_t *__restrict__ buf,
-                       const uint64_t *__restrict__ nl, Lines L, const uint64_t *__restrict__ offs,
-                       const uint32_t *__restrict__ ev_rule, bjx_event_line *__restrict__ d_lines,
-                       uint32_t *__restrict__ d_events, uint8_t *__restrict__ d_bytes, uint32_t *__restrict__ pack_src) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_ip[kBlock / 64][kPackWaveBytes + 32];
-  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t lane = threadIdx.x & 63;
-  uint8_t *sw = s_ip[threadIdx.x >> 6];
-  // the wave's packed IP bytes are one contiguous range [b0, b1) of d_bytes
-  const uint64_t p0 = p - lane, pl = min<uint64_t>(p0 + 64, n_el);
-  const uint64_t b0 = p0 < n_el ? by_off[p0] : 0, b1 = p0 < n_el ? by_off[pl] : 0;
-  const bool staged = p0 < n_el && b1 - b0 <= kPackWaveBytes;
-  const uint32_t head = (uint32_t)(b0 & 15);  // LDS byte of d_bytes[b0]: 16 B stores stay aligned
-  if (p < n_el) {
-    const uint32_t j = line[p];
-    const uint32_t ne = (uint32_t)(L.counts[j] & 0xFFFFFFFFull);
-    const uint32_t len = L.ip_len[j];
-    bjx_event_line r;
-    r.ts_ns = L.ts[j];
-    r.ip_off = (uint32_t)(by_off[p] - part_byte_base[key[p]]);
-    r.ip_len = (uint16_t)len;
-    r.n_events = (uint16_t)ne;
-    d_lines[p] = r;
-    const uint64_t eo = offs[j] & 0xFFFFFFFFull, pe = ev_off[p];
-    for (uint32_t t = 0; t < ne; ++t) {
-      d_events[pe + t] = ev_rule[eo + t];
-      pack_src[pe + t] = (uint32_t)(eo + t);
-    }
-    // the IP bytes, byte stores into the wave's LDS stage (or the packed
-    // pool): an IP of <= 15 bytes from its inline key (L.ip16, k_lines2 wrote
-    // it beside the line's other fields), a longer one by word loads from the
-    // line (a log line continues past its IP; a random 128 B fetch per line)
-    const bool inl = len <= 15;
-    const uint4 k16 = inl ? L.ip16[j] : make_uint4(0, 0, 0, 0);
-    const uint8_t *ip = inl ? nullptr : buf + line_start(nl, j) + L.ip_off[j];
-    uint8_t *dst = staged ? sw + head + (by_off[p] - b0) : d_bytes + by_off[p];
-    for (uint32_t k = 0; k < len; k += 4) {
-      const uint32_t w = inl ? (k < 4 ? k16.x : k < 8 ? k16.y : k < 12 ? k16.z : k16.w) : ld4(ip + k);
-#pragma unroll
-      for (uint32_t b = 0; b < 4; ++b)
-        if (k + b < len) dst[k + b] = (uint8_t)(w >> (8 * b));
-    }
+struct PackArgs {
+  uint64_t n_lines;
+  uint32_t n_tiles, n_parts, steps;
+  const uint64_t *off;        // k_part_count's arrays, exclusive-scanned
+  const uint64_t *byte_base;  // each owner's first byte
+  const uint8_t *buf;
+  const uint64_t *nl;
+  Lines L;
+  const uint64_t *offs;       // line -> first event (low 32 bits)
+  const uint32_t *ev_rule;
+  bjx_event_line *d_lines;
+  uint32_t *d_events;
+  uint8_t *d_bytes;
+  uint32_t *pack_src;         // packed event -> local event
+};
+
+// dynamic LDS: s_run[3][n_parts] (the tile's next positions per owner) and
+// s_wt[2][4][n_parts] x 2 words (per step parity and wave: an owner's lines and
+// events | bytes << 32)
+__host__ __device__ constexpr uint32_t pack_lds_bytes(uint32_t n_parts) {
+  return 3 * n_parts * 8 + 2 * (kBlock / 64) * n_parts * 16;
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack(PackArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+  const uint32_t N = A.n_parts, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t *s_run = reinterpret_cast<uint64_t *>(s_dyn);
+  uint64_t *s_wt = s_run + 3 * N;  // [parity][wave][owner][2]
+  const uint64_t S = (uint64_t)N * A.n_tiles + 1;
+  for (uint32_t o = threadIdx.x; o < N; o += kBlock) {
+    const uint64_t i = (uint64_t)o * A.n_tiles + blockIdx.x;
+    s_run[o] = A.off[i];
+    s_run[N + o] = A.off[S + i];
+    s_run[2 * N + o] = A.off[2 * S + i];
   }
-  if (!staged) return;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // the range out with 16 B stores, the partial first and last pieces bytewise
-  const uint64_t a = b0 & ~15ull;
-  for (uint64_t q = a + 16ull * lane; q < b1; q += 16ull * 64) {
-    const uint32_t o = (uint32_t)(q - a);
-    if (q >= b0 && q + 16 <= b1) *reinterpret_cast<uint4 *>(d_bytes + q) = *reinterpret_cast<const uint4 *>(sw + o);
-    else
-      for (uint32_t k = 0; k < 16; ++k)
-        if (q + k >= b0 && q + k < b1) d_bytes[q + k] = sw[o + k];
+  const uint64_t base = (uint64_t)blockIdx.x * A.steps * kBlock;
+  for (uint32_t s = 0; s < A.steps; ++s) {
+    const uint64_t j = base + s * kBlock + threadIdx.x;
+    const PartLine x = part_line(j, A.n_lines, A.L, N);
+    uint64_t *wt = s_wt + (size_t)(s & 1) * (kBlock / 64) * N * 2;
+    uint64_t *mine_wt = wt + (size_t)wv * N * 2;
+    // this wave's row: zero, then each present owner's totals
+    for (uint32_t o = lane; o < N; o += 64) mine_wt[2 * o] = 0, mine_wt[2 * o + 1] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t rank = 0;
+    uint64_t pre = 0;  // events | bytes << 32 of the wave's earlier lanes of this owner
+    for (uint64_t todo = __ballot(x.ev); todo;) {
+      const uint32_t lead = (uint32_t)__ffsll((unsigned long long)todo) - 1;
+      const uint32_t o = __shfl(x.o, lead, 64);
+      const bool mine = x.ev && x.o == o;
+      const uint64_t m = __ballot(mine);
+      todo &= ~m;
+      const uint64_t v = mine ? part_eb(x) : 0;
+      const uint64_t inc = wave_incl_scan64(v, lane);
+      if (mine) {
+        rank = (uint32_t)__popcll(m & ((1ull << lane) - 1));
+        pre = inc - v;
+      }
+      const uint64_t tot = __shfl(inc, 63, 64);
+      if (lane == lead) mine_wt[2 * o] = (uint64_t)__popcll(m), mine_wt[2 * o + 1] = tot;
+    }
+    __syncthreads();
+    uint64_t pl = 0, pe = 0, pb = 0;
+    if (x.ev) {
+      uint64_t cl = 0, ceb = 0;
+      for (uint32_t w2 = 0; w2 < wv; ++w2) {
+        cl += wt[((size_t)w2 * N + x.o) * 2];
+        ceb += wt[((size_t)w2 * N + x.o) * 2 + 1];
+      }
+      pl = s_run[x.o] + cl + rank;
+      pe = s_run[N + x.o] + (ceb & 0xFFFFFFFFull) + (pre & 0xFFFFFFFFull);
+      pb = s_run[2 * N + x.o] + (ceb >> 32) + (pre >> 32);
+    }
+    __syncthreads();
+    for (uint32_t o = threadIdx.x; o < N; o += kBlock) {  // the tile's positions after this step
+      uint64_t cl = 0, ceb = 0;
+      for (uint32_t w2 = 0; w2 < kBlock / 64; ++w2) {
+        cl += wt[((size_t)w2 * N + o) * 2];
+        ceb += wt[((size_t)w2 * N + o) * 2 + 1];
+      }
+      s_run[o] += cl;
+      s_run[N + o] += ceb & 0xFFFFFFFFull;
+      s_run[2 * N + o] += ceb >> 32;
+    }
+    // the line's record and rule indices
+    const uint32_t jj = (uint32_t)j;
+    if (x.ev) {
+      bjx_event_line r;
+      r.ts_ns = A.L.ts[jj];
+      r.ip_off = (uint32_t)(pb - A.byte_base[x.o]);
+      r.ip_len = (uint16_t)x.len;
+      r.n_events = (uint16_t)x.ne;
+      A.d_lines[pl] = r;
+      const uint64_t eo = A.offs[jj] & 0xFFFFFFFFull;
+      for (uint32_t t = 0; t < x.ne; ++t) {
+        A.d_events[pe + t] = A.ev_rule[eo + t];
+        A.pack_src[pe + t] = (uint32_t)(eo + t);
+      }
+    }
+    // the IP bytes as whole words into the line's aligned slot: an IP of <= 15
+    // bytes from its inline key, a longer one by aligned word loads from the
+    // line, all issued at once (a chain of dependent loads cost a round trip
+    // per word), one of 48 bytes or more word by word
+    if (x.ev) {
+      uint32_t *dst = reinterpret_cast<uint32_t *>(A.d_bytes + pb);
+      const uint32_t nw = (x.len + 3) >> 2;
+      if (x.len <= 15) {
+        const uint4 k16 = A.L.ip16[jj];
+        const uint32_t kw[4] = {k16.x, k16.y, k16.z, k16.w & 0x00FFFFFFu};  // byte 15 is the length
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+          if (k < nw) dst[k] = kw[k];
+      } else {
+        const uint8_t *ip = A.buf + line_start(A.nl, jj) + A.L.ip_off[jj];
+        if (x.len < 4 * kIpWords) {
+          uint32_t iw[kIpWords];
+          ip_words(ip, x.len, iw);
+#pragma unroll
+          for (uint32_t k = 0; k < kIpWords; ++k)
+            if (k < nw) dst[k] = iw[k];
+        } else {
+          for (uint32_t k = 0; k < nw; ++k) {
+            const uint32_t w = ld4(ip + 4 * k);
+            const uint32_t left = x.len - 4 * k;
+            dst[k] = left >= 4 ? w : w & ((1u << (8 * left)) - 1u);
+          }
+        }
+      }
+    }
   }
 }
 
@@ -3948,13 +4124,25 @@ __global__ void k_unpack_lines(uint64_t n, uint64_t first, uint64_t byte_base, c
   if (i >= n) return;
   const bjx_event_line r = rec[first + i];
   ts[first + i] = r.ts_ns;
-  // the IP's hash from its bytes (the source's hash_bytes; not on the wire)
-  const uint64_t h = hash_bytes(bytes + byte_base + r.ip_off, r.ip_len);
+  // the IP's hash (the source's hash_bytes; not on the wire) and inline key,
+  // an IP of <= 15 bytes from one set of word loads
+  const uint8_t *ip = bytes + byte_base + r.ip_off;
+  uint64_t h;
+  uint4 k16;
+  if (r.ip_len < 4 * kIpWords) {  // IPv4 and IPv6 text: one set of word loads
+    uint32_t w[kIpWords];
+    ip_words(ip, r.ip_len, w);
+    h = hash_words(w, r.ip_len);
+    k16 = make_uint4(w[0], w[1], w[2], (r.ip_len <= 15 ? w[3] : w[3] & 0x00FFFFFFu) | (min((uint32_t)r.ip_len, 255u) << 24));
+  } else {
+    h = hash_bytes(ip, r.ip_len);
+    k16 = ip_key16_bytes(ip, r.ip_len);
+  }
   hash[first + i] = dbg_mask ? (h & dbg_mask) | 1 : h;
   pos[first + i] = byte_base + r.ip_off;
   len[first + i] = r.ip_len;
   nev[first + i] = r.n_events;
-  ip16[first + i] = ip_key16_bytes(bytes + byte_base + r.ip_off, r.ip_len);
+  ip16[first + i] = k16;
 }
 
 // event -> its line (events of line i are [off[i], off[i] + nev[i])); flags bad rule ids
@@ -3968,6 +4156,39 @@ __global__ void k_expand_events(uint64_t n, const uint64_t *__restrict__ off, co
   for (uint64_t k = b; k < e; ++k) {
     if (ev_rule[k] >= n_rules) atomicAdd(bad, 1ull);
     ev_el[k] = (uint32_t)i;
+  }
+}
+
+// owner side of bjx_apply_events_trips: the ascending received indices of
+// the tripping events -> base[k] + index inside source k's segment (ev_base:
+// the segments' first received event, n_src + 1 entries); start[k] = source
+// k's first trip (untouched when it has none)
+__global__ void k_trip_rebase(uint64_t n, const uint32_t *__restrict__ u, uint32_t n_src, const uint64_t *__restrict__ ev_base,
+                              const uint64_t *__restrict__ base, uint32_t *__restrict__ out, uint64_t *__restrict__ start) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint64_t x = u[t];
+  uint32_t lo = 0, hi = n_src;  // the last source whose segment starts at or before x
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (ev_base[mid] <= x) lo = mid;
+    else hi = mid;
+  }
+  out[t] = (uint32_t)(base[lo] + (x - ev_base[lo]));
+  if (t == 0 || u[t - 1] < ev_base[lo]) start[lo] = t;
+}
+
+// source side of bjx_finish_batch_trips: packed event index -> local event
+// index (out-of-range indices counted in bad)
+__global__ void k_map_trips(uint64_t n, const uint32_t *__restrict__ packed, uint64_t n_ev, const uint32_t *__restrict__ src,
+                            uint32_t *__restrict__ out, unsigned long long *__restrict__ bad) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint32_t q = packed[t];
+  if (q < n_ev) out[t] = src[q];
+  else {
+    out[t] = 0;
+    atomicAdd(bad, 1ull);
   }
 }
 
@@ -4247,6 +4468,11 @@ struct bjx_engine {
   static constexpr int kPhases = 8;
   hipEvent_t ph[kPhases + 1] = {};
   double phase_ms[kPhases] = {};
+  // node batches: from bjx_events_partition to the start of the owner's
+  // rate-limit stage (partition, pack, the copies' wait, unpack)
+  hipEvent_t xev[2] = {};
+  bool xev_rec = false;
+  double exchange_ms = 0;
   bool phase_rec[kPhases + 1] = {};
 
   // decision lists (config order)
@@ -4321,6 +4547,7 @@ struct bjx_engine {
   DevBuf<uint64_t> blk_b;   // ... and their IP bytes
   DevBuf<uint8_t> rl_out, ev_out, ev_out_s, trip_flag;
   DevBuf<uint32_t> trip_ev, trip_ev2;
+  DevBuf<uint64_t> tr_base;  // bjx_apply_events_trips: segment bases, trip bases, first trips
   DevBuf<bjx_trip> d_trips;
   DevBuf<bjx_rule_result> d_results;
   DevBuf<uint8_t> cub_tmp;
@@ -4330,11 +4557,11 @@ struct bjx_engine {
   // the batch between its match phase and its finish (bjx_match_batch / bjx_finish_batch)
   BatchCtx bc;
   // multi-GPU exchange workspace
-  DevBuf<uint32_t> pk_key, pk_key2, pk_line, pk_line2, pack_src, rx_len, rx_ev_el;
-  DevBuf<uint64_t> pk_nev, pk_ipl, pk_evoff, pk_byoff, pk_start, pk_counts, pk_bbase, rx_hash, rx_pos, rx_nev, rx_evoff;
+  DevBuf<uint32_t> pack_src, rx_len, rx_ev_el;
+  DevBuf<uint64_t> pk_hist, pk_off, pk_counts, pk_bbase, rx_hash, rx_pos, rx_nev, rx_evoff;
   DevBuf<int64_t> rx_ts;
   DevBuf<uint4> rx_ip16;  // received event lines: IpSlot.key16 of each IP (k_unpack_lines)
-  uint32_t pk_parts = 0;
+  uint32_t pk_parts = 0, pk_tiles = 0, pk_steps = 1;
   uint64_t pk_n_ev = 0;
   bool partitioned = false;
 
@@ -5804,6 +6031,7 @@ extern "C" int bjx_engine_create(int device, const bjx_engine_options *opts, bjx
     HIP_OK(hipEventCreate(&e->evm1));
     for (auto &x : e->evk) HIP_OK(hipEventCreate(&x));
     for (auto &x : e->ph) HIP_OK(hipEventCreate(&x));
+    for (auto &x : e->xev) HIP_OK(hipEventCreate(&x));
     // >= 4M slots: a quarter of the table stays free for the claims in flight
     // when a launch spends its budget (see k_ip_claim)
     uint64_t ipc = std::max<uint64_t>(opts && opts->ip_capacity ? next_pow2(opts->ip_capacity) : 0, 1ull << 22);
@@ -5836,11 +6064,10 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   e->ev_res.release(); e->ev_st.release(); e->ev_st2.release(); e->ev_idx.release(); e->ev_idx2.release();
   e->el_slot.release(); e->coll.release(); e->blk_n.release(); e->blk_b.release(); e->ev_rec.release(); e->ev_rec2.release(); e->el_id.release();
 
-  for (auto *b : {&e->pk_key, &e->pk_key2, &e->pk_line, &e->pk_line2, &e->pack_src, &e->rx_len, &e->rx_ev_el}) b->release();
-  for (auto *b : {&e->pk_nev, &e->pk_ipl, &e->pk_evoff, &e->pk_byoff, &e->pk_start, &e->pk_counts, &e->pk_bbase,
-                  &e->rx_hash, &e->rx_pos, &e->rx_nev, &e->rx_evoff})
+  for (auto *b : {&e->pack_src, &e->rx_len, &e->rx_ev_el}) b->release();
+  for (auto *b : {&e->pk_hist, &e->pk_off, &e->pk_counts, &e->pk_bbase, &e->rx_hash, &e->rx_pos, &e->rx_nev, &e->rx_evoff})
     b->release();
-  e->rx_ts.release(); e->rx_ip16.release(); e->trip_idx.release(); e->d_trips.release();
+  e->rx_ts.release(); e->rx_ip16.release(); e->trip_idx.release(); e->d_trips.release(); e->tr_base.release();
   for (auto *b : {&e->bn_key, &e->bn_key2, &e->bn_len, &e->bn_off, &e->dl_hash}) b->release();
   for (auto *b : {&e->bn_val, &e->bn_val2, &e->bn_head, &e->bn_seg, &e->bn_first, &e->bn_cnt, &e->bn_ipt, &e->bn_coll,
                   &e->dl_off, &e->dl_len, &e->nm_off})
@@ -5857,6 +6084,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   (void)hipEventDestroy(e->ev0); (void)hipEventDestroy(e->ev1); (void)hipEventDestroy(e->evm0); (void)hipEventDestroy(e->evm1);
   for (auto &x : e->evk) (void)hipEventDestroy(x);
   for (auto &x : e->ph) (void)hipEventDestroy(x);
+  for (auto &x : e->xev) (void)hipEventDestroy(x);
   (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -6708,9 +6936,43 @@ static void emit_bans(bjx_engine *e, uint64_t n, bool records_only) {
   e->ban_n_trips = n;
 }
 
+// Where finish_phase finds the trips: Apply outcomes in state-slot order (this
+// engine's rate-limit stage), outcomes in event order (a node's
+// bjx_finish_batch), or a list of the tripping events (bjx_finish_batch_trips)
+enum FinishFrom { kFinSorted, kFinEvents, kFinList };
+
+// Exceeded events -> their event indices, ascending, in e->trip_ev2 (count
+// returned).  kFinList: the n_list indices are already in e->trip_idx.
+static uint64_t trip_events(bjx_engine *e, uint64_t n_ev, FinishFrom from, uint64_t n_list) {
+  hipStream_t st = e->stream;
+  uint64_t n_trips = n_list;
+  if (from != kFinList) {
+    e->trip_idx.ensure(n_ev + 1);
+    HIP_OK(hipMemsetAsync(e->scalars.p + 4, 0, 8, st));
+    hipLaunchKernelGGL(k_select_trips, dim3(grid_for((n_ev + kSelPer - 1) / kSelPer)), dim3(kBlock), 0, st, n_ev,
+                       from == kFinSorted ? e->ev_out_s.p : e->ev_out.p, e->trip_idx.p, e->scalars.p + 4);
+    HIP_OK(hipGetLastError());
+    unsigned long long nt = 0;
+    HIP_OK(hipMemcpyAsync(&nt, e->scalars.p + 4, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    n_trips = nt;
+  }
+  if (!n_trips) return 0;
+  e->trip_ev.ensure(n_trips); e->trip_ev2.ensure(n_trips);
+  if (from == kFinSorted)
+    hipLaunchKernelGGL(k_trip_events, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_idx.p, ev_words(e),
+                       rec_stride(e), e->trip_ev.p);
+  uint32_t *ki = from == kFinSorted ? e->trip_ev.p : e->trip_idx.p, *ko = e->trip_ev2.p;
+  const int bits = std::max(1, bit_width(n_ev));
+  cub_call(e, [&](void *tmp, size_t &bytes) {
+    return hipcub::DeviceRadixSort::SortKeys(tmp, bytes, ki, ko, (int)n_trips, 0, bits, st);
+  });
+  return n_trips;
+}
+
 // Trips (reference order) and the optional per-line / RuleResult copies, once
-// e->ev_out holds every local event's Apply outcome (phases 7-8).
-static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, bool sorted) {
+// the local events' Apply outcomes are known (phases 7-8).
+static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, FinishFrom from, uint64_t n_list = 0) {
   const Bind &B = e->bind;
   hipStream_t st = e->stream;
   const BatchCtx &c = e->bc;
@@ -6723,36 +6985,13 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
   e->ban_ipb.resize(0); e->ban_ipo.resize(1); e->ban_ipo.data()[0] = 0;
   if (n_ev) {
     mark(e, 7);
-    // trips: Exceeded outcomes.  sorted: outcomes in state-slot order (this
-    // engine's rate-limit stage), selected there and put back in reference
-    // order; otherwise outcomes already in event (= reference) order
-    e->trip_idx.ensure(n_ev + 1);
-    HIP_OK(hipMemsetAsync(e->scalars.p + 4, 0, 8, st));
-    hipLaunchKernelGGL(k_select_trips, dim3(grid_for((n_ev + kSelPer - 1) / kSelPer)), dim3(kBlock), 0, st, n_ev,
-                       sorted ? e->ev_out_s.p : e->ev_out.p, e->trip_idx.p, e->scalars.p + 4);
-    HIP_OK(hipGetLastError());
-    unsigned long long nt = 0;
-    HIP_OK(hipMemcpyAsync(&nt, e->scalars.p + 4, 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    n_trips = nt;
+    // the trips in reference (event) order
+    n_trips = trip_events(e, n_ev, from, n_list);
     if (n_trips) {
-      // the selected trips in reference (event) order
-      e->trip_ev.ensure(n_trips); e->trip_ev2.ensure(n_trips);
-      {
-      if (sorted)
-        hipLaunchKernelGGL(k_trip_events, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_idx.p, ev_words(e),
-                           rec_stride(e), e->trip_ev.p);
-      uint32_t *ki = sorted ? e->trip_ev.p : e->trip_idx.p, *ko = e->trip_ev2.p;
-      const int bits = std::max(1, bit_width(n_ev));
-      cub_call(e, [&](void *tmp, size_t &bytes) {
-        return hipcub::DeviceRadixSort::SortKeys(tmp, bytes, ki, ko, (int)n_trips, 0, bits, st);
-      });
-      const uint32_t *trip_ev = e->trip_ev2.p;
       e->d_trips.ensure(n_trips);
-      hipLaunchKernelGGL(k_build_trips, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, trip_ev, e->ev_el.p,
+      hipLaunchKernelGGL(k_build_trips, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_ev2.p, e->ev_el.p,
                          e->ev_rule.p, e->nl.p, L, B.rules, e->d_trips.p);
       HIP_OK(hipGetLastError());
-      }
       if (flags & BJX_TRIPS_COMPACT) {
         e->d_trips_c.ensure(n_trips);
         hipLaunchKernelGGL(k_pack_trips, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->d_trips.p, e->d_trips_c.p);
@@ -6777,7 +7016,7 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, b
       e->res_written = true;
     }
     if (flags & BJX_COPY_RESULTS) {
-      if (sorted)
+      if (from == kFinSorted)
         hipLaunchKernelGGL(k_unsort, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, ev_words(e), rec_stride(e), e->ev_out_s.p,
                            e->ev_out.p);
       hipLaunchKernelGGL(k_scatter_rl, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, e->ev_res.p, e->ev_out.p, e->rl_out.p);
@@ -6854,7 +7093,7 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
     rate_limit_stage(e, e->bind, local_evsrc(e), e->bc.n_el, e->bc.el_bytes, e->bc.n_ev, e->ev_el.p, e->ev_rule.p,
                      e->bc.now_ns);
   }
-  finish_phase(e, flags, out, true);
+  finish_phase(e, flags, out, kFinSorted);
 }
 
 extern "C" int bjx_process_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns,
@@ -6902,7 +7141,7 @@ extern "C" int bjx_match_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8
 }
 
 extern "C" int bjx_events_partition(bjx_engine *e, uint32_t n_parts, uint64_t *counts) {
-  if (!counts || n_parts == 0 || n_parts > 4096) return BJX_ERR_ARG;
+  if (!counts || n_parts == 0 || n_parts > kMaxParts) return BJX_ERR_ARG;
   return guarded(e, [&]() -> int {
     const BatchCtx &c = e->bc;
     memset(counts, 0, sizeof(uint64_t) * 3 * n_parts);
@@ -6911,34 +7150,29 @@ extern "C" int bjx_events_partition(bjx_engine *e, uint32_t n_parts, uint64_t *c
     e->partitioned = true;
     if (!c.live || c.n_ev == 0) return BJX_OK;
     hipStream_t st = e->stream;
-    const uint64_t nl = c.n_lines, n_el = c.n_el;
-    e->pk_key.ensure(nl); e->pk_key2.ensure(nl); e->pk_line.ensure(nl); e->pk_line2.ensure(nl);
-    e->pk_nev.ensure(n_el + 1); e->pk_ipl.ensure(n_el + 1); e->pk_evoff.ensure(n_el + 1); e->pk_byoff.ensure(n_el + 1);
-    e->pk_start.ensure(n_parts + 1); e->pk_counts.ensure(3 * n_parts + 1); e->pk_bbase.ensure(n_parts);
+    HIP_OK(hipEventRecord(e->xev[0], st));
+    e->xev_rec = true;
+    const uint64_t nl = c.n_lines;
+    // one step per tile (the most blocks in flight) unless the [owner][tile]
+    // arrays would pass 4M entries
+    const uint64_t rows = (nl + kBlock - 1) / kBlock;
+    const uint32_t steps = (uint32_t)std::max<uint64_t>(1, (rows * n_parts + (1u << 22) - 1) >> 22);
+    const uint32_t n_tiles = (uint32_t)((rows + steps - 1) / steps);
+    const uint64_t S = (uint64_t)n_parts * n_tiles + 1;
+    e->pk_hist.ensure(3 * S); e->pk_off.ensure(3 * S);
+    e->pk_counts.ensure(3 * n_parts + 1); e->pk_bbase.ensure(n_parts);
+    e->pk_tiles = n_tiles;
+    e->pk_steps = steps;
     HIP_OK(hipMemsetAsync(e->pk_counts.p + 3 * n_parts, 0, 8, st));
-    hipLaunchKernelGGL(k_part_keys, dim3(grid_for(nl)), dim3(kBlock), 0, st, nl, c.L.counts, c.L.ip_hash, n_parts,
-                       e->pk_key.p, e->pk_line.p);
+    for (int k = 0; k < 3; ++k) HIP_OK(hipMemsetAsync(e->pk_hist.p + k * S + S - 1, 0, 8, st));
+    hipLaunchKernelGGL(k_part_count, dim3(n_tiles), dim3(kBlock), 0, st, nl, n_tiles, steps, c.L, n_parts, e->pk_hist.p,
+                       reinterpret_cast<unsigned long long *>(e->pk_counts.p + 3 * n_parts));
     HIP_OK(hipGetLastError());
-    {
-      uint32_t *ki = e->pk_key.p, *ko = e->pk_key2.p, *vi = e->pk_line.p, *vo = e->pk_line2.p;
-      const int bits = std::max(1, bit_width(n_parts));
-      cub_call(e, [&](void *tmp, size_t &bytes) {
-        return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)nl, 0, bits, st);
-      });
+    for (int k = 0; k < 3; ++k) {
+      uint64_t *in = e->pk_hist.p + k * S, *o = e->pk_off.p + k * S;
+      cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)S, st); });
     }
-    hipLaunchKernelGGL(k_pack_prep, dim3(grid_for(n_el + 1)), dim3(kBlock), 0, st, n_el, e->pk_line2.p, c.L.counts,
-                       c.L.ip_len, e->pk_nev.p, e->pk_ipl.p, reinterpret_cast<unsigned long long *>(e->pk_counts.p + 3 * n_parts));
-    HIP_OK(hipGetLastError());
-    for (int k = 0; k < 2; ++k) {
-      uint64_t *in = k ? e->pk_ipl.p : e->pk_nev.p, *o = k ? e->pk_byoff.p : e->pk_evoff.p;
-      cub_call(e, [&](void *tmp, size_t &bytes) {
-        return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)(n_el + 1), st);
-      });
-    }
-    HIP_OK(hipMemsetAsync(e->pk_start.p, 0xFF, (n_parts + 1) * 8, st));
-    hipLaunchKernelGGL(k_part_bounds, dim3(grid_for(n_el)), dim3(kBlock), 0, st, n_el, e->pk_key2.p, e->pk_start.p);
-    hipLaunchKernelGGL(k_part_counts, dim3(1), dim3(64), 0, st, n_parts, n_el, e->pk_start.p, e->pk_evoff.p,
-                       e->pk_byoff.p, e->pk_counts.p, e->pk_bbase.p);
+    hipLaunchKernelGGL(k_part_counts, dim3(1), dim3(64), 0, st, n_parts, n_tiles, e->pk_off.p, e->pk_counts.p, e->pk_bbase.p);
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(counts, e->pk_counts.p, 3 * n_parts * 8, hipMemcpyDeviceToHost, st));
     uint64_t wide = 0;
@@ -6950,7 +7184,7 @@ extern "C" int bjx_events_partition(bjx_engine *e, uint32_t n_parts, uint64_t *c
     }
     uint64_t tl = 0, te = 0;
     for (uint32_t k = 0; k < n_parts; ++k) { tl += counts[3 * k]; te += counts[3 * k + 1]; }
-    if (tl != n_el || te != c.n_ev) throw BjxError(BJX_ERR_DEVICE, "internal: partition counts disagree with the batch");
+    if (tl != c.n_el || te != c.n_ev) throw BjxError(BJX_ERR_DEVICE, "internal: partition counts disagree with the batch");
     e->pk_n_ev = te;
     return BJX_OK;
   });
@@ -6964,70 +7198,95 @@ extern "C" int bjx_events_pack(bjx_engine *e, bjx_event_line *d_lines, uint32_t 
     if (!d_lines || !d_events || (c.el_bytes && !d_bytes)) return BJX_ERR_ARG;
     hipStream_t st = e->stream;
     e->pack_src.ensure(c.n_ev);
-    hipLaunchKernelGGL(k_pack, dim3(grid_for(c.n_el)), dim3(kBlock), 0, st, c.n_el, e->pk_key2.p, e->pk_line2.p,
-                       e->pk_evoff.p, e->pk_byoff.p, e->pk_bbase.p, c.buf, e->nl.p, c.L, e->l_offs.p, e->ev_rule.p, d_lines,
-                       d_events, d_bytes, e->pack_src.p);
+    PackArgs A;
+    A.n_lines = c.n_lines; A.n_tiles = e->pk_tiles; A.n_parts = e->pk_parts; A.steps = e->pk_steps; A.off = e->pk_off.p; A.byte_base = e->pk_bbase.p;
+    A.buf = c.buf; A.nl = e->nl.p; A.L = c.L; A.offs = e->l_offs.p; A.ev_rule = e->ev_rule.p;
+    A.d_lines = d_lines; A.d_events = d_events; A.d_bytes = d_bytes; A.pack_src = e->pack_src.p;
+    const uint32_t lds = pack_lds_bytes(A.n_parts);
+    if (lds > 64 * 1024)
+      HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pack), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_pack, dim3(A.n_tiles), dim3(kBlock), lds, st, A);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(st));
     return BJX_OK;
   });
 }
 
-extern "C" int bjx_apply_events(bjx_engine *e, const bjx_ruleset *rs, const bjx_event_line *d_lines, const uint32_t *d_events,
-                                const uint8_t *d_bytes, uint32_t n_src, const uint64_t *src_counts, uint8_t *d_out) {
-  if (!rs || (n_src && !src_counts)) return BJX_ERR_ARG;
-  return guarded(e, [&]() -> int {
-    uint64_t n_lines = 0, n_ev = 0, n_bytes = 0;
-    for (uint32_t k = 0; k < n_src; ++k) {
-      n_lines += src_counts[3 * k];
-      n_ev += src_counts[3 * k + 1];
-      n_bytes += src_counts[3 * k + 2];
-    }
-    if (n_ev == 0) return BJX_OK;
-    if (!d_lines || !d_events || !d_out || (n_bytes && !d_bytes)) return BJX_ERR_ARG;
-    if (e->bound_uid != rs->uid || e->bound_dec_version != e->decisions_version) bind_ruleset(e, rs, nullptr, 0);
-    const Bind &B = e->bind;
-    hipStream_t st = e->stream;
-    e->rx_ts.ensure(n_lines); e->rx_hash.ensure(n_lines); e->rx_pos.ensure(n_lines); e->rx_len.ensure(n_lines);
-    e->rx_nev.ensure(n_lines + 1); e->rx_evoff.ensure(n_lines + 1); e->rx_ev_el.ensure(n_ev); e->rx_ip16.ensure(n_lines);
-    uint64_t first = 0, bbase = 0;
-    for (uint32_t k = 0; k < n_src; ++k) {
-      const uint64_t nk = src_counts[3 * k];
-      if (nk)
-        hipLaunchKernelGGL(k_unpack_lines, dim3(grid_for(nk)), dim3(kBlock), 0, st, nk, first, bbase, d_lines, d_bytes,
-                           e->rx_ts.p, e->rx_hash.p, e->rx_pos.p, e->rx_len.p, e->rx_nev.p, e->rx_ip16.p, e->dbg_hash_mask);
-      first += nk;
-      bbase += src_counts[3 * k + 2];
-    }
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipMemsetAsync(e->rx_nev.p + n_lines, 0, 8, st));
-    {
-      uint64_t *in = e->rx_nev.p, *o = e->rx_evoff.p;
-      cub_call(e, [&](void *tmp, size_t &bytes) {
-        return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)(n_lines + 1), st);
-      });
-    }
-    HIP_OK(hipMemsetAsync(e->scalars.p + 6, 0, 8, st));
-    hipLaunchKernelGGL(k_expand_events, dim3(grid_for(n_lines)), dim3(kBlock), 0, st, n_lines, e->rx_evoff.p, e->rx_nev.p,
-                       n_ev, d_events, B.n_rules, e->rx_ev_el.p, e->scalars.p + 6);
-    HIP_OK(hipGetLastError());
-    uint64_t chk[2] = {0, 0};
-    HIP_OK(hipMemcpyAsync(&chk[0], e->rx_evoff.p + n_lines, 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(&chk[1], e->scalars.p + 6, 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    if (chk[0] != n_ev || chk[1]) throw BjxError(BJX_ERR_ARG, "received event records are inconsistent");
-    EvSrc E;
-    E.bytes = d_bytes; E.nl = nullptr; E.ip_off = nullptr; E.ip_pos = e->rx_pos.p; E.ip_len = e->rx_len.p;
-    E.ip_hash = e->rx_hash.p; E.ts = e->rx_ts.p; E.counts = nullptr; E.ip16 = e->rx_ip16.p; E.n = n_lines;
-    // the clock of this engine's last match phase (the node's batch) as the
-    // 12-B records' base; a stale or foreign one only costs the 16-B re-claim
-    rate_limit_stage(e, B, E, n_lines, n_bytes, n_ev, e->rx_ev_el.p, d_events, e->bc.now_ns ? e->bc.now_ns : kNoRecBase);
+// the received records of n_src sources through the rate-limit stage;
+// d_out: each event's outcome byte in received order (nullptr: left in
+// state-slot order, e->ev_out_s)
+static int apply_received(bjx_engine *e, const bjx_ruleset *rs, const bjx_event_line *d_lines, const uint32_t *d_events,
+                          const uint8_t *d_bytes, uint32_t n_src, const uint64_t *src_counts, uint8_t *d_out) {
+  uint64_t n_lines = 0, n_ev = 0, n_bytes = 0;
+  for (uint32_t k = 0; k < n_src; ++k) {
+    n_lines += src_counts[3 * k];
+    n_ev += src_counts[3 * k + 1];
+    n_bytes += src_counts[3 * k + 2];
+  }
+  if (n_ev == 0) return BJX_OK;
+  if (!d_lines || !d_events || (n_bytes && !d_bytes)) return BJX_ERR_ARG;
+  if (e->bound_uid != rs->uid || e->bound_dec_version != e->decisions_version) bind_ruleset(e, rs, nullptr, 0);
+  const Bind &B = e->bind;
+  hipStream_t st = e->stream;
+  e->rx_ts.ensure(n_lines); e->rx_hash.ensure(n_lines); e->rx_pos.ensure(n_lines); e->rx_len.ensure(n_lines);
+  e->rx_nev.ensure(n_lines + 1); e->rx_evoff.ensure(n_lines + 1); e->rx_ev_el.ensure(n_ev); e->rx_ip16.ensure(n_lines);
+  uint64_t first = 0, bbase = 0;
+  for (uint32_t k = 0; k < n_src; ++k) {
+    const uint64_t nk = src_counts[3 * k];
+    if (nk)
+      hipLaunchKernelGGL(k_unpack_lines, dim3(grid_for(nk)), dim3(kBlock), 0, st, nk, first, bbase, d_lines, d_bytes,
+                         e->rx_ts.p, e->rx_hash.p, e->rx_pos.p, e->rx_len.p, e->rx_nev.p, e->rx_ip16.p, e->dbg_hash_mask);
+    first += nk;
+    bbase += src_counts[3 * k + 2];
+  }
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemsetAsync(e->rx_nev.p + n_lines, 0, 8, st));
+  {
+    uint64_t *in = e->rx_nev.p, *o = e->rx_evoff.p;
+    cub_call(e, [&](void *tmp, size_t &bytes) {
+      return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)(n_lines + 1), st);
+    });
+  }
+  HIP_OK(hipMemsetAsync(e->scalars.p + 6, 0, 8, st));
+  hipLaunchKernelGGL(k_expand_events, dim3(grid_for(n_lines)), dim3(kBlock), 0, st, n_lines, e->rx_evoff.p, e->rx_nev.p,
+                     n_ev, d_events, B.n_rules, e->rx_ev_el.p, e->scalars.p + 6);
+  HIP_OK(hipGetLastError());
+  uint64_t chk[2] = {0, 0};
+  HIP_OK(hipMemcpyAsync(&chk[0], e->rx_evoff.p + n_lines, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(&chk[1], e->scalars.p + 6, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  if (chk[0] != n_ev || chk[1]) throw BjxError(BJX_ERR_ARG, "received event records are inconsistent");
+  EvSrc E;
+  E.bytes = d_bytes; E.nl = nullptr; E.ip_off = nullptr; E.ip_pos = e->rx_pos.p; E.ip_len = e->rx_len.p;
+  E.ip_hash = e->rx_hash.p; E.ts = e->rx_ts.p; E.counts = nullptr; E.ip16 = e->rx_ip16.p; E.n = n_lines;
+  // the clock of this engine's last match phase (the node's batch) as the
+  // 12-B records' base; a stale or foreign one only costs the 16-B re-claim
+  const bool timed = e->xev_rec;
+  if (timed) HIP_OK(hipEventRecord(e->xev[1], st));
+  e->xev_rec = false;
+  rate_limit_stage(e, B, E, n_lines, n_bytes, n_ev, e->rx_ev_el.p, d_events, e->bc.now_ns ? e->bc.now_ns : kNoRecBase);
+  e->exchange_ms = 0;
+  if (timed) {
+    float x = 0;
+    HIP_OK(hipEventElapsedTime(&x, e->xev[0], e->xev[1]));
+    e->exchange_ms = x;
+  }
+  if (d_out) {
     hipLaunchKernelGGL(k_unsort, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, n_ev, ev_words(e), rec_stride(e), e->ev_out_s.p,
                        d_out);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(st));
-    return BJX_OK;
-  });
+  }
+  return BJX_OK;
+}
+
+extern "C" int bjx_apply_events(bjx_engine *e, const bjx_ruleset *rs, const bjx_event_line *d_lines, const uint32_t *d_events,
+                                const uint8_t *d_bytes, uint32_t n_src, const uint64_t *src_counts, uint8_t *d_out) {
+  if (!rs || (n_src && !src_counts)) return BJX_ERR_ARG;
+  uint64_t n_ev = 0;
+  for (uint32_t k = 0; k < n_src; ++k) n_ev += src_counts[3 * k + 1];
+  if (n_ev && !d_out) return BJX_ERR_ARG;
+  return guarded(e, [&]() -> int { return apply_received(e, rs, d_lines, d_events, d_bytes, n_src, src_counts, d_out); });
 }
 
 extern "C" int bjx_finish_batch(bjx_engine *e, const uint8_t *d_outcomes, uint32_t flags, bjx_batch_result *out) {
@@ -7047,7 +7306,86 @@ extern "C" int bjx_finish_batch(bjx_engine *e, const uint8_t *d_outcomes, uint32
     out->consumed_bytes = c.consumed;
     out->n_results = c.n_res;
     out->n_events = c.n_ev;
-    finish_phase(e, flags, out, false);
+    finish_phase(e, flags, out, kFinEvents);
+    e->partitioned = false;
+    return BJX_OK;
+  });
+}
+
+extern "C" int bjx_apply_events_trips(bjx_engine *e, const bjx_ruleset *rs, const bjx_event_line *d_lines,
+                                      const uint32_t *d_events, const uint8_t *d_bytes, uint32_t n_src,
+                                      const uint64_t *src_counts, const uint64_t *trip_base, uint32_t *d_trips,
+                                      uint64_t *trip_counts) {
+  if (!rs || (n_src && (!src_counts || !trip_base || !trip_counts)) || n_src > kMaxParts) return BJX_ERR_ARG;
+  return guarded(e, [&]() -> int {
+    for (uint32_t k = 0; k < n_src; ++k) trip_counts[k] = 0;
+    uint64_t n_ev = 0;
+    std::vector<uint64_t> host(2 * (size_t)n_src + 1);
+    for (uint32_t k = 0; k < n_src; ++k) {
+      host[k] = n_ev;
+      n_ev += src_counts[3 * k + 1];
+    }
+    host[n_src] = n_ev;
+    if (n_ev == 0) return BJX_OK;
+    if (!d_trips) return BJX_ERR_ARG;
+    for (uint32_t k = 0; k < n_src; ++k) host[n_src + 1 + k] = trip_base[k];
+    // the rate-limit stage on the received records, outcomes left in
+    // state-slot order (no event-order copy)
+    const int rc = apply_received(e, rs, d_lines, d_events, d_bytes, n_src, src_counts, nullptr);
+    if (rc != BJX_OK) return rc;
+    hipStream_t st = e->stream;
+    const uint64_t n_trips = trip_events(e, n_ev, kFinSorted, 0);
+    if (!n_trips) return BJX_OK;
+    e->tr_base.ensure(host.size() + n_src);
+    uint64_t *ev_base = e->tr_base.p, *base = ev_base + n_src + 1, *start = base + n_src;
+    HIP_OK(hipMemcpyAsync(ev_base, host.data(), host.size() * 8, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetAsync(start, 0xFF, n_src * 8ull, st));
+    hipLaunchKernelGGL(k_trip_rebase, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_ev2.p, n_src, ev_base, base,
+                       d_trips, start);
+    HIP_OK(hipGetLastError());
+    std::vector<uint64_t> first(n_src);
+    HIP_OK(hipMemcpyAsync(first.data(), start, n_src * 8ull, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    uint64_t nxt = n_trips;
+    for (int k = (int)n_src - 1; k >= 0; --k) {
+      if (first[k] > nxt) first[k] = nxt;  // no trips: empty at the next source's start
+      trip_counts[k] = nxt - first[k];
+      nxt = first[k];
+    }
+    return BJX_OK;
+  });
+}
+
+extern "C" int bjx_finish_batch_trips(bjx_engine *e, const uint32_t *d_trips, uint64_t n, uint32_t flags, bjx_batch_result *out) {
+  if (!out || (n && !d_trips)) return BJX_ERR_ARG;
+  if (flags & BJX_COPY_RESULTS) return BJX_ERR_ARG;  // per-event outcomes: bjx_finish_batch
+  return guarded(e, [&]() -> int {
+    const BatchCtx &c = e->bc;
+    memset(out, 0, sizeof *out);
+    if (!c.live) return BJX_OK;
+    if (c.n_ev) {
+      if (!e->partitioned || e->pk_n_ev != c.n_ev) throw BjxError(BJX_ERR_ARG, "bjx_finish_batch_trips without a packed batch");
+      if (n > c.n_ev) throw BjxError(BJX_ERR_ARG, "bjx_finish_batch_trips: more trips than packed events");
+    } else if (n) {
+      throw BjxError(BJX_ERR_ARG, "bjx_finish_batch_trips: trips for a batch without events");
+    }
+    if (n) {
+      hipStream_t st = e->stream;
+      e->trip_idx.ensure(n + 1);
+      HIP_OK(hipMemsetAsync(e->scalars.p + 6, 0, 8, st));
+      hipLaunchKernelGGL(k_map_trips, dim3(grid_for(n)), dim3(kBlock), 0, st, n, d_trips, c.n_ev, e->pack_src.p, e->trip_idx.p,
+                         e->scalars.p + 6);
+      HIP_OK(hipGetLastError());
+      unsigned long long bad = 0;
+      HIP_OK(hipMemcpyAsync(&bad, e->scalars.p + 6, 8, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      if (bad) throw BjxError(BJX_ERR_ARG, "bjx_finish_batch_trips: packed event index out of range");
+    }
+    out->n_lines = c.n_lines;
+    out->consumed_bytes = c.consumed;
+    out->n_results = c.n_res;
+    out->n_events = c.n_ev;
+    finish_phase(e, flags, out, kFinList, n);
     e->partitioned = false;
     return BJX_OK;
   });
@@ -7317,7 +7655,8 @@ extern "C" int bjx_debug_set_slot_cache(bjx_engine *e, int on) {
 extern "C" size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap) {
   if (!e) return 0;
   for (size_t k = 0; k < cap && k < (size_t)bjx_engine::kPhases; ++k) out[k] = e->phase_ms[k];
-  return bjx_engine::kPhases;
+  if (cap > (size_t)bjx_engine::kPhases) out[bjx_engine::kPhases] = e->exchange_ms;
+  return bjx_engine::kPhases + 1;
 }
 extern "C" size_t bjx_debug_kernel_ms(bjx_engine *e, double *out, size_t cap) {
   if (!e) return 0;

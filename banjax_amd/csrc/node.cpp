@@ -19,7 +19,9 @@
 //      order, so every (ip, rule name) state sees its events in the
 //      reference's order;
 //   5. the outcome bytes go back the same way, and each engine selects its
-//      trips (bjx_finish_batch);
+//      trips (bjx_finish_batch); a batch that wants trips only (no
+//      BJX_COPY_RESULTS) sends back just the packed indices of the tripping
+//      events instead (bjx_apply_events_trips / bjx_finish_batch_trips);
 //   6. the node concatenates the engines' trips (global line order) and
 //      merges their per-IP decision records (highest decision, first trip).
 // Phases 1, 2, 4 and 5 run on one host thread per engine, so the GPUs work
@@ -89,6 +91,8 @@ struct Part {
   std::vector<uint64_t> send;          // 3 * n: lines / events / bytes to each owner
   DevMem s_lines, s_ev, s_bytes, s_out;  // packed outgoing records, outcomes coming back
   DevMem r_lines, r_ev, r_bytes, r_out;  // received records, their outcomes
+  DevMem r_trips, s_trips;             // trips-only batches: owner's trip lists out, the source's back
+  std::vector<uint64_t> tr_counts;     // owner side: trips per source
   bjx_batch_result res{};
 };
 
@@ -453,11 +457,11 @@ void run_batch(bjx_node *n, const bjx_ruleset *rs, const uint8_t *const *chunks,
     P.s_lines.ensure(s_tot[3 * k] * kLineRec + 1);
     P.s_ev.ensure(s_tot[3 * k + 1] * 4 + 1);
     P.s_bytes.ensure(s_tot[3 * k + 2] + 1);
-    P.s_out.ensure(s_tot[3 * k + 1] + 1);
+    if (flags & BJX_COPY_RESULTS) P.s_out.ensure(s_tot[3 * k + 1] + 1);
     P.r_lines.ensure(r_tot[3 * k] * kLineRec + 1);
     P.r_ev.ensure(r_tot[3 * k + 1] * 4 + 1);
     P.r_bytes.ensure(r_tot[3 * k + 2] + 1);
-    P.r_out.ensure(r_tot[3 * k + 1] + 1);
+    if (flags & BJX_COPY_RESULTS) P.r_out.ensure(r_tot[3 * k + 1] + 1);
     return bjx_events_pack(P.e, reinterpret_cast<bjx_event_line *>(P.s_lines.p), reinterpret_cast<uint32_t *>(P.s_ev.p),
                            P.s_bytes.p);
   });
@@ -471,21 +475,62 @@ void run_batch(bjx_node *n, const bjx_ruleset *rs, const uint8_t *const *chunks,
       *b = recv_counts[(p * N + k) * 3 + c] * unit[c];
     });
   sync_copies(n);
-  // 4. owners apply their events in source order
-  each(n, [&](size_t p) {
-    Part &P = n->parts[p];
-    return bjx_apply_events(P.e, rs, reinterpret_cast<const bjx_event_line *>(P.r_lines.p),
-                            reinterpret_cast<const uint32_t *>(P.r_ev.p), P.r_bytes.p, (uint32_t)N, &recv_counts[p * N * 3],
-                            P.r_out.p);
-  });
-  // 5. outcomes back to the sources (owner-major, the pack order)
-  exchange(n, [&](size_t k, size_t p, void **d, const void **s, size_t *b) {
-    *d = n->parts[k].s_out.p + s_off[(k * N + p) * 3 + 1];
-    *s = n->parts[p].r_out.p + r_off[(p * N + k) * 3 + 1];
-    *b = recv_counts[(p * N + k) * 3 + 1];
-  });
-  sync_copies(n);
-  each(n, [&](size_t k) { return bjx_finish_batch(n->parts[k].e, n->parts[k].s_out.p, flags, &n->parts[k].res); });
+  if (!(flags & BJX_COPY_RESULTS)) {
+    // 4. owners apply their events in source order and list, per source, the
+    // packed indices of the events that tripped
+    each(n, [&](size_t p) {
+      Part &P = n->parts[p];
+      std::vector<uint64_t> base(N);
+      for (size_t k = 0; k < N; ++k) base[k] = s_off[(k * N + p) * 3 + 1];
+      P.tr_counts.assign(N, 0);
+      P.r_trips.ensure(r_tot[3 * p + 1] * 4 + 4);
+      return bjx_apply_events_trips(P.e, rs, reinterpret_cast<const bjx_event_line *>(P.r_lines.p),
+                                    reinterpret_cast<const uint32_t *>(P.r_ev.p), P.r_bytes.p, (uint32_t)N,
+                                    &recv_counts[p * N * 3], base.data(), reinterpret_cast<uint32_t *>(P.r_trips.p),
+                                    P.tr_counts.data());
+    });
+    // 5. the trip lists back to their sources (owner order)
+    std::vector<uint64_t> o_off(N * N), t_off(N * N), t_tot(N, 0);
+    for (size_t p = 0; p < N; ++p) {
+      uint64_t o = 0;
+      for (size_t k = 0; k < N; ++k) {
+        o_off[p * N + k] = o;
+        o += n->parts[p].tr_counts[k];
+      }
+    }
+    for (size_t k = 0; k < N; ++k)
+      for (size_t p = 0; p < N; ++p) {
+        t_off[k * N + p] = t_tot[k];
+        t_tot[k] += n->parts[p].tr_counts[k];
+      }
+    for (size_t k = 0; k < N; ++k) n->parts[k].s_trips.ensure(t_tot[k] * 4 + 4);
+    exchange(n, [&](size_t k, size_t p, void **d, const void **s, size_t *b) {
+      *d = n->parts[k].s_trips.p + t_off[k * N + p] * 4;
+      *s = n->parts[p].r_trips.p + o_off[p * N + k] * 4;
+      *b = n->parts[p].tr_counts[k] * 4;
+    });
+    sync_copies(n);
+    each(n, [&](size_t k) {
+      return bjx_finish_batch_trips(n->parts[k].e, reinterpret_cast<const uint32_t *>(n->parts[k].s_trips.p), t_tot[k], flags,
+                                    &n->parts[k].res);
+    });
+  } else {
+    // 4. owners apply their events in source order
+    each(n, [&](size_t p) {
+      Part &P = n->parts[p];
+      return bjx_apply_events(P.e, rs, reinterpret_cast<const bjx_event_line *>(P.r_lines.p),
+                              reinterpret_cast<const uint32_t *>(P.r_ev.p), P.r_bytes.p, (uint32_t)N, &recv_counts[p * N * 3],
+                              P.r_out.p);
+    });
+    // 5. outcomes back to the sources (owner-major, the pack order)
+    exchange(n, [&](size_t k, size_t p, void **d, const void **s, size_t *b) {
+      *d = n->parts[k].s_out.p + s_off[(k * N + p) * 3 + 1];
+      *s = n->parts[p].r_out.p + r_off[(p * N + k) * 3 + 1];
+      *b = recv_counts[(p * N + k) * 3 + 1];
+    });
+    sync_copies(n);
+    each(n, [&](size_t k) { return bjx_finish_batch(n->parts[k].e, n->parts[k].s_out.p, flags, &n->parts[k].res); });
+  }
   // 6. merge in chunk (= stream) order
   bjx_batch_result r{};
   n->trips.clear(); n->trips_c.clear(); n->results.clear(); n->line_flags.clear();
@@ -548,8 +593,8 @@ extern "C" int bjx_node_create(const int *devices, size_t n_devices, const bjx_e
       err[err_len - 1] = 0;
     }
   };
-  if (!devices || !out || n_devices == 0 || n_devices > 4096) {
-    say("bjx_node_create: need 1..4096 devices and an out pointer");
+  if (!devices || !out || n_devices == 0 || n_devices > 256) {
+    say("bjx_node_create: need 1..256 devices and an out pointer");
     return BJX_ERR_ARG;
   }
   *out = nullptr;
@@ -625,7 +670,8 @@ extern "C" void bjx_node_destroy(bjx_node *n) {
   for (ncclComm_t c : n->comms)
     if (c) (void)ncclCommDestroy(c);
   for (auto &P : n->parts) {
-    for (DevMem *m : {&P.s_lines, &P.s_ev, &P.s_bytes, &P.s_out, &P.r_lines, &P.r_ev, &P.r_bytes, &P.r_out}) m->release();
+    for (DevMem *m : {&P.s_lines, &P.s_ev, &P.s_bytes, &P.s_out, &P.r_lines, &P.r_ev, &P.r_bytes, &P.r_out, &P.r_trips,
+                      &P.s_trips}) m->release();
     if (P.copy) {
       (void)hipSetDevice(P.dev);
       (void)hipStreamDestroy(P.copy);

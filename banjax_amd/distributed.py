@@ -3,7 +3,8 @@
 One engine per GPU.  Rank r holds the r-th contiguous chunk of the log and
 runs consumeLine up to Apply on it.  The events of each line go to the engine
 that owns the line's IP, (ip_hash >> 32) % world.  The owner applies them with
-its HBM state and sends one outcome byte per event back.  Exchange volume is
+its HBM state and sends one outcome byte per event back, or, when the batch
+wants trips only, the packed indices of the events that tripped.  Exchange volume is
 one 32 B record per event line, 4 B per event and the IP bytes; it crosses
 xGMI once each way as an RCCL all-to-all.
 
@@ -124,6 +125,22 @@ def sharded_batch(engine, rs: Ruleset, now_ns: int, device_ptr: int, nbytes: int
     r_lines = ex.exchange(lines, [c[0] * LINE_REC for c in send], [c[0] * LINE_REC for c in recv])
     r_events = ex.exchange(events, [c[1] * 4 for c in send], [c[1] * 4 for c in recv])
     r_ipb = ex.exchange(ipb, [c[2] for c in send], [c[2] for c in recv])
+    if not copy_results:
+        # trips only: each owner returns the packed indices of the tripping
+        # events (4 B per trip instead of 1 B per event)
+        offs, acc = [], 0
+        for c in send:
+            offs.append(acc)
+            acc += c[1]
+        base = [b[0] for b in ex.counts([(o, 0, 0) for o in offs])]
+        tr = torch.empty(max(1, sum(c[1] for c in recv)) * 4, dtype=torch.uint8, device=dev)
+        tcnt = engine.apply_events_trips(rs, r_lines.data_ptr(), r_events.data_ptr(), r_ipb.data_ptr(), recv, base,
+                                         tr.data_ptr())
+        mine = [c[0] for c in ex.counts([(c, 0, 0) for c in tcnt])]
+        back = ex.exchange(tr, [c * 4 for c in tcnt], [c * 4 for c in mine])
+        if emit_bans:
+            return engine.finish_trips(back.data_ptr(), sum(mine), emit_bans=True)
+        return engine.finish_trips(back.data_ptr(), sum(mine))
     out = torch.empty(max(1, sum(c[1] for c in recv)), dtype=torch.uint8, device=dev)
     engine.apply_events(rs, r_lines.data_ptr(), r_events.data_ptr(), r_ipb.data_ptr(), recv, out.data_ptr())
     back = ex.exchange(out, [c[1] for c in recv], [c[1] for c in send])

@@ -216,6 +216,29 @@ class Engine:
                                                 C.c_void_p(bytes_ptr), len(src_counts), arr, C.c_void_p(out_ptr)),
                     "apply_events")
 
+    def apply_events_trips(self, rs: Ruleset, lines_ptr: int, events_ptr: int, bytes_ptr: int,
+                           src_counts: List[Tuple[int, int, int]], trip_base: List[int], trips_ptr: int) -> List[int]:
+        """Trips-only Apply: per source, its tripping events' packed indices
+        (trip_base[k] + index in source k's segment) into trips_ptr, source
+        order; returns the per-source counts."""
+        n = len(src_counts)
+        arr = (C.c_uint64 * max(1, 3 * n))()
+        for k, (a, b, c) in enumerate(src_counts):
+            arr[3 * k], arr[3 * k + 1], arr[3 * k + 2] = a, b, c
+        base = (C.c_uint64 * max(1, n))(*trip_base)
+        cnt = (C.c_uint64 * max(1, n))()
+        self._check(_lib.lib().bjx_apply_events_trips(self._h, rs.handle, C.c_void_p(lines_ptr), C.c_void_p(events_ptr),
+                                                      C.c_void_p(bytes_ptr), n, arr, base, C.c_void_p(trips_ptr), cnt),
+                    "apply_events_trips")
+        return [cnt[k] for k in range(n)]
+
+    def finish_trips(self, trips_ptr: int, n: int, emit_bans: bool = False) -> BatchOutput:
+        res = _lib.BatchResult()
+        flags = _lib.EMIT_BANS if emit_bans else 0
+        self._check(_lib.lib().bjx_finish_batch_trips(self._h, C.c_void_p(trips_ptr), n, flags, C.byref(res)),
+                    "finish_batch_trips")
+        return BatchOutput(res, False)
+
     def finish(self, outcomes_ptr: int, copy_results: bool = False, emit_bans: bool = False) -> BatchOutput:
         res = _lib.BatchResult()
         flags = (_lib.COPY_RESULTS if copy_results else 0) | (_lib.EMIT_BANS if emit_bans else 0)
@@ -223,7 +246,7 @@ class Engine:
                     "finish_batch")
         return BatchOutput(res, copy_results)
 
-    PHASES = ("count", "scan", "resolve", "emit", "capacity", "ip_state_claim", "sort_apply", "trips")
+    PHASES = ("count", "scan", "resolve", "emit", "capacity", "ip_state_claim", "sort_apply", "trips", "exchange")
 
     def scan_stats(self):
         out = (C.c_uint64 * 12)()
@@ -239,9 +262,16 @@ class Engine:
         return {k: getattr(st, k) for k, _ in _lib.StateStats._fields_}
 
     def phase_ms(self):
-        out = (C.c_double * 8)()
-        _lib.lib().bjx_debug_phase_ms(self._h, out, 8)
-        return {k: round(out[i], 3) for i, k in enumerate(self.PHASES)}
+        """Device ms of the last batch's phases; "exchange" (a node batch only)
+        is the part of "capacity" spent partitioning, packing, moving and
+        unpacking the event records."""
+        n = len(self.PHASES)
+        out = (C.c_double * n)()
+        _lib.lib().bjx_debug_phase_ms(self._h, out, n)
+        d = {k: round(out[i], 3) for i, k in enumerate(self.PHASES)}
+        if not d["exchange"]:
+            del d["exchange"]
+        return d
 
     def kernel_ms(self):
         """Device ms of the last batch's k_scan, per-line kernel and DFA-job resolve (HIP events)."""

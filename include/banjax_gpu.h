@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define BJX_ABI_VERSION 4
+#define BJX_ABI_VERSION 5  /* 5: IP slots of the exchange byte pool 4-byte aligned; trips-only node return */
 
 enum bjx_status {
   BJX_OK = 0,
@@ -198,19 +198,22 @@ int bjx_process_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
      bjx_apply_events                    Apply for the received records, in source order
      -- caller: all-to-all of the outcome bytes back --
      bjx_finish_batch                    trips / RuleResults of the local lines
+   (trips only: bjx_apply_events_trips, the trip lists back, bjx_finish_batch_trips)
    Source order must be stream order (rank r holds the r-th chunk), which makes
    the owner's event order the reference's.  All buffers are device pointers
    allocated by the caller; the engine never retains them. */
 typedef struct bjx_event_line {  /* 16 B (ABI 4; the owner hashes the IP bytes itself) */
   int64_t ts_ns;     /* parsed line timestamp */
-  uint32_t ip_off;   /* offset of the IP bytes in this owner's part of the byte buffer */
+  uint32_t ip_off;   /* offset of the IP bytes in this owner's part of the byte buffer: each IP
+                        starts a 4-byte aligned slot of (ip_len + 3) & ~3 bytes, zero padded (ABI 5) */
   uint16_t ip_len;
   uint16_t n_events; /* events of the line; their rule indices follow in the event buffer */
 } bjx_event_line;
 
 int bjx_match_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns, uint32_t flags,
                     bjx_batch_result *out);
-/* counts[3*p + 0/1/2] = event lines / events / IP bytes going to owner p (host array) */
+/* counts[3*p + 0/1/2] = event lines / events / IP slot bytes going to owner p
+   (host array); 1 <= n_parts <= 256.  The byte buffers are 4-byte aligned. */
 int bjx_events_partition(bjx_engine *e, uint32_t n_parts, uint64_t *counts);
 int bjx_events_pack(bjx_engine *e, bjx_event_line *d_lines, uint32_t *d_events, uint8_t *d_bytes);
 /* received records of n_src sources, concatenated in source order; src_counts as
@@ -220,6 +223,20 @@ int bjx_apply_events(bjx_engine *e, const bjx_ruleset *rs, const bjx_event_line 
                      const uint8_t *d_bytes, uint32_t n_src, const uint64_t *src_counts, uint8_t *d_out);
 /* d_outcomes: one byte per packed event, in bjx_events_pack order */
 int bjx_finish_batch(bjx_engine *e, const uint8_t *d_outcomes, uint32_t flags, bjx_batch_result *out);
+/* Trips-only round trip (a batch without BJX_COPY_RESULTS needs no per-event
+   outcome): the owner hands back, per source, the packed indices of that
+   source's events that came out Exceeded.  trip_base[k] is added to each index
+   inside source k's received segment (the caller passes that segment's offset
+   in source k's bjx_events_pack order); d_trips (device, room for every
+   received event) gets the sources' lists concatenated in source order, each
+   ascending; trip_counts[k] (host) their lengths.  Replaces the outcome bytes
+   + bjx_finish_batch when the batch needs trips (and bans) only. */
+int bjx_apply_events_trips(bjx_engine *e, const bjx_ruleset *rs, const bjx_event_line *d_lines, const uint32_t *d_events,
+                           const uint8_t *d_bytes, uint32_t n_src, const uint64_t *src_counts, const uint64_t *trip_base,
+                           uint32_t *d_trips, uint64_t *trip_counts);
+/* d_trips: n packed event indices (bjx_events_pack order) that came out Exceeded,
+   in any order; flags without BJX_COPY_RESULTS */
+int bjx_finish_batch_trips(bjx_engine *e, const uint32_t *d_trips, uint64_t n, uint32_t flags, bjx_batch_result *out);
 
 /* RegexRateLimitStates.Get(ip)[name]: 1 found (num_hits, start_ns set), 0 not found, <0 error. */
 int bjx_state_get(bjx_engine *e, const char *ip, size_t ip_len, const char *name, size_t name_len,

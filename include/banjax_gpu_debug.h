@@ -26,8 +26,11 @@ int bjx_debug_rule_lead(const bjx_ruleset *rs, size_t rule_idx);
    Go's error text, e.g. the "expression too large" limits), no automaton. */
 int bjx_debug_regex_parse(const char *pattern, size_t len, char *err, size_t err_len);
 /* device ms of the last batch's phases: framing count, scan, per-line resolve,
-   emit, capacity check, IP/state slot claim, sort + automaton, trips
-   (returns the phase count) */
+   emit, capacity check, IP/state slot claim, sort + automaton, trips; then the
+   node exchange as this engine saw it (bjx_events_partition to the start of
+   its owner's rate-limit stage: partition, pack, the wait for the copies,
+   unpack; 0 for a batch without one), which the capacity phase of a node
+   batch contains (returns 9) */
 size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap);
 /* device ms of the last batch's dominant kernels, from HIP events on the
    engine stream: k_scan, the per-line kernel, DFA-job sort + k_dfa / k_nfa;

@@ -1,6 +1,7 @@
 """CPU stand-in for the engine's multi-GPU entry points (test infrastructure).
 
-Implements match / events_partition / events_pack / apply_events / finish with
+Implements match / events_partition / events_pack / apply_events / finish (and
+the trips-only apply_events_trips / finish_trips) with
 the same wire format as include/banjax_gpu.h (bjx_event_line records, u32
 rule indices, IP bytes), so banjax_amd.distributed.sharded_batch can run over
 real torch.distributed collectives (gloo) on CPU tensors.  Matching comes from
@@ -70,7 +71,8 @@ class MockEngine:
         self.parts = [[] for _ in range(world)]
         for j in sorted(by_line):
             self.parts[(ip_hash(self.line_ip[j]) >> 32) % world].append((j, by_line[j]))
-        return [(len(p), sum(len(ev) for _, ev in p), sum(len(self.line_ip[j]) for j, _ in p)) for p in self.parts]
+        return [(len(p), sum(len(ev) for _, ev in p), sum((len(self.line_ip[j]) + 3) & ~3 for j, _ in p))
+                for p in self.parts]
 
     # ---- bjx_events_pack
     def events_pack(self, lines_ptr, events_ptr, bytes_ptr):
@@ -80,7 +82,7 @@ class MockEngine:
             for j, ev in part:
                 ip = self.line_ip[j]
                 recs += REC.pack(self.line_ts[j], len(ipb) - base, len(ip), len(ev))
-                ipb += ip
+                ipb += ip + b"\0" * (-len(ip) % 4)  # 4-byte aligned IP slots (ABI 5)
                 for e in ev:
                     evs += struct.pack("<I", self.results[self.events[e]][1])
                     self.pack_src.append(e)
@@ -139,3 +141,25 @@ class MockEngine:
             if r[6]:
                 trips.append(Trip(r[0], r[1]))
         return Out(self.n_lines, self.results, trips)
+
+    # ---- bjx_apply_events_trips: per source, base + index of its Exceeded events
+    def apply_events_trips(self, rs, lines_ptr, events_ptr, bytes_ptr, src_counts, trip_base, trips_ptr):
+        ne = sum(c[1] for c in src_counts)
+        buf = (C.c_uint8 * max(1, ne))()
+        self.apply_events(rs, lines_ptr, events_ptr, bytes_ptr, src_counts, C.addressof(buf))
+        out, counts, e0 = [], [], 0
+        for k, (_, ce, _) in enumerate(src_counts):
+            mine = [trip_base[k] + i for i in range(ce) if buf[e0 + i] & 8]
+            out += mine
+            counts.append(len(mine))
+            e0 += ce
+        if out:
+            C.memmove(trips_ptr, struct.pack("<%dI" % len(out), *out), 4 * len(out))
+        return counts
+
+    # ---- bjx_finish_batch_trips
+    def finish_trips(self, trips_ptr, n, emit_bans=False):
+        o = bytearray(max(1, len(self.pack_src)))
+        for q in (struct.unpack("<%dI" % n, C.string_at(trips_ptr, 4 * n)) if n else ()):
+            o[q] = 8
+        return self.finish(C.addressof((C.c_uint8 * len(o)).from_buffer(o)))

@@ -21,7 +21,7 @@ def test_library_exports_every_declared_symbol():
     assert declared == set(_lib.EXPORTS), declared ^ set(_lib.EXPORTS)
     for name in declared:
         assert hasattr(L, name), name
-    assert L.bjx_abi_version() == 4
+    assert L.bjx_abi_version() == 5
 
 
 def test_regex_with_rate_unmarshal():

@@ -447,12 +447,15 @@ def test_ip_hash_collisions(engine, mask):
         engine.debug_set_ip_hash_mask(0)
 
 
-@pytest.mark.parametrize("wl,world", [(("cfg5", 3000), 2), (("cfg3", 2000), 3)])
-def test_sharded_engines_match_single_process(wl, world):
+@pytest.mark.parametrize("wl,world,copy", [(("cfg5", 3000), 2, True), (("cfg3", 2000), 3, True), (("cfg3", 2000), 3, False),
+                                           (("cfg5", 3000), 2, False)])
+def test_sharded_engines_match_single_process(wl, world, copy):
     """The multi-GPU path on one GPU: `world` engines as threads (ThreadMesh),
     each matching its chunk, rate limits sharded by IP hash with the real
-    bjx_events_pack / bjx_apply_events / bjx_finish_batch.  Bit-exact against
-    one oracle over the stream, and each IP's state lives on exactly one engine."""
+    bjx_events_pack / bjx_apply_events / bjx_finish_batch (copy=False: the
+    trips-only return, bjx_apply_events_trips / bjx_finish_batch_trips).
+    Bit-exact against one oracle over the stream, and each IP's state lives on
+    exactly one engine."""
     import threading
 
     import torch
@@ -481,12 +484,13 @@ def test_sharded_engines_match_single_process(wl, world):
                 k = step * world + r
                 t = torch.frombuffer(bytearray(chunks[k]), dtype=torch.uint8).to(dev)
                 out = sharded_batch(engines[r], rs, w.now_ns(0, per), t.data_ptr(), len(chunks[k]), ex,
-                                    copy_results=True, emit_bans=True)
+                                    copy_results=copy, emit_bans=True)
                 trips = [SimpleNamespace(line_offset=x.line_offset, line_len=x.line_len, ip_off=x.ip_off,
                                          ip_len=x.ip_len, host_off=x.host_off, host_len=x.host_len) for x in out.trips]
                 bans[k] = (engines[r].bans(), trips, chunks[k])
                 got[k] = ([[x.line_idx, x.rule_idx, x.rule_pos, x.skip_host, x.seen_ip, x.match_type, x.exceeded]
-                           for x in out.results], [(x.line_idx, x.rule_idx) for x in out.trips], bytes(out.line_flags))
+                           for x in out.results] if copy else None, [(x.line_idx, x.rule_idx) for x in out.trips],
+                          bytes(out.line_flags) if copy else None)
         except BaseException as e:  # noqa: BLE001
             errs.append(e)
             mesh.barrier.abort()
@@ -504,9 +508,10 @@ def test_sharded_engines_match_single_process(wl, world):
         oflags, ores, _ = st.consume(oc, data, w.now_ns(0, per), cap=(data.count(b"\n") + 1) * (len(cfg.all_rules()) + 1))
         exp = [[r.line_idx, r.rule_id, r.rule_pos, r.skip_host, r.seen_ip, r.match_type, r.exceeded] for r in ores]
         results, trips, flags = got[k]
-        assert list(flags) == oflags
-        assert results == exp, "chunk %d" % k
-        assert trips == [(r[0], r[1]) for r in exp if r[6]]
+        if copy:
+            assert list(flags) == oflags
+            assert results == exp, "chunk %d" % k
+        assert trips == [(r[0], r[1]) for r in exp if r[6]], "chunk %d" % k
         n_trips += len(trips)
     assert n_trips > 0
     # device decision emission, merged over the ranks of each step
@@ -530,6 +535,59 @@ def test_sharded_engines_match_single_process(wl, world):
             assert [h for h in have if h is not None] == ([exp] if exp is not None else [])
     for e in engines:
         e.close()
+
+
+@pytest.mark.parametrize("n_parts,trips_only", [(256, False), (7, True), (1, False)])
+def test_partition_many_owners_one_engine(n_parts, trips_only):
+    """bjx_events_partition / bjx_events_pack with up to 256 owners (many
+    distinct owners in every wave of k_pack), the packed records fed straight
+    back into the same engine as n_parts "sources": every IP lives in exactly
+    one owner segment, in line order, so Apply over the segments in owner
+    order gives the reference's outcomes.  Bit-exact against the oracle, over
+    the outcome-byte and the trip-list returns."""
+    import torch
+
+    w = W.scaled(W.CFG3, 6000, n_ips=3000)
+    cfg = Config.from_yaml(w.rules_yaml)
+    rs = Ruleset(cfg)
+    eng = Engine(0)
+    eng.set_decision_lists(cfg.decision_entries)
+    oc = oracle_config(cfg)
+    st = O.State()
+    dev = torch.device("cuda", 0)
+    for b in range(2):
+        data = w.host_lines(b * 3000, 3000)
+        now = w.now_ns(b * 3000, 3000)
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+        eng.match(rs, now, t.data_ptr(), len(data), copy_results=not trips_only)
+        send = eng.events_partition(n_parts)
+        assert sum(c[0] > 0 for c in send) > min(n_parts, 100) // 2
+        tl, te, tb = (sum(c[i] for c in send) for i in range(3))
+        lines = torch.empty(max(1, tl * 16), dtype=torch.uint8, device=dev)
+        events = torch.empty(max(1, te * 4), dtype=torch.uint8, device=dev)
+        ipb = torch.empty(max(1, tb), dtype=torch.uint8, device=dev)
+        eng.events_pack(lines.data_ptr(), events.data_ptr(), ipb.data_ptr())
+        if trips_only:
+            base, acc = [], 0
+            for c in send:
+                base.append(acc)
+                acc += c[1]
+            tr = torch.empty(max(1, te) * 4, dtype=torch.uint8, device=dev)
+            cnt = eng.apply_events_trips(rs, lines.data_ptr(), events.data_ptr(), ipb.data_ptr(), send, base, tr.data_ptr())
+            out = eng.finish_trips(tr.data_ptr(), sum(cnt))
+        else:
+            o = torch.empty(max(1, te), dtype=torch.uint8, device=dev)
+            eng.apply_events(rs, lines.data_ptr(), events.data_ptr(), ipb.data_ptr(), send, o.data_ptr())
+            out = eng.finish(o.data_ptr(), copy_results=True)
+        _, ores, _ = st.consume(oc, data, now, cap=(data.count(b"\n") + 1) * (len(cfg.all_rules()) + 1))
+        exp = [[r.line_idx, r.rule_id, r.rule_pos, r.skip_host, r.seen_ip, r.match_type, r.exceeded] for r in ores]
+        if not trips_only:
+            assert [[x.line_idx, x.rule_idx, x.rule_pos, x.skip_host, x.seen_ip, x.match_type, x.exceeded]
+                    for x in out.results] == exp
+        assert [(x.line_idx, x.rule_idx) for x in out.trips] == [(r[0], r[1]) for r in exp if r[6]]
+    assert sum(r[6] for r in exp) > 0
+    assert eng.state_len() == len(st)
+    eng.close()
 
 
 @pytest.mark.parametrize("budget,slot_cache", [(1, 1), (97, 1), (5000, 1), (1, 0), (97, 0)])
