@@ -188,6 +188,22 @@ def timed_region(dist, step, sync_all, steps, clock_device):
     return elapsed, outs
 
 
+def tail_inclusive(workload):
+    """The committed tail-inclusive measurement for this workload (file ->
+    pinned -> HBM -> engine, tools/tail_bench.py on the box), reported beside
+    the HBM-resident value, never as it."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05_tail", "tail_inclusive.json")
+    if workload != "cfg3" or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        t = json.load(f)
+    st = t["steady"]
+    return {"lines_per_s": st["lines_per_s_tail_inclusive"], "file_to_HBM_GBps": st["file_to_HBM_GBps"],
+            "lines": st["lines"], "batch_MiB": st["batch_MiB"], "engine_only_lines_per_s": st["lines_per_s_engine_only"],
+            "bound": t["parts"]["reading"], "source": "profiles/r05_tail/tail_inclusive.json (%s)" % t["command"],
+            "what": "not measured in this run: the committed tools/tail_bench.py result on the same workload"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -452,6 +468,9 @@ def main():
             line["with_decision_emission"] = dec
         if rec:
             line["with_decision_records_only"] = rec
+        tail = tail_inclusive(w0.name) if n_parts == 1 else None
+        if tail:
+            line["tail_inclusive"] = tail
         if not args.no_cpu_baseline and n_parts == 1:
             line["cpu_baseline"] = cpu_baseline(w, args.cpu_sample)
         print(json.dumps(line), flush=True)

@@ -177,3 +177,21 @@ def test_gpu_tail_to_engine_parity(tmp_path):
     assert sum(seen) == len(blob) and len(seen) > 1
     pair.compare_state()
     eng.close()
+
+
+def test_large_backlog_parallel_reads(tmp_path):
+    """A backlog of 96 MB read from offset 0 in 40 MB slots: each fill is
+    split over several pread threads; the batches still concatenate to the
+    file's complete lines, in order, and the partial tail waits."""
+    p = str(tmp_path / "big.log")
+    rnd = random.Random(5)
+    lines = [b"%d %s x\n" % (i, b"y" * rnd.randrange(0, 300)) for i in range(400_000)]
+    body = b"".join(lines)
+    while len(body) < 96 << 20:
+        body += body[:len(body) // 2]
+        body = body[:body.rindex(b"\n") + 1]
+    append(p, body + b"no newline yet")
+    with LogTailer(p, device=-1, from_start=True, batch_bytes=40 << 20, poll_ms=POLL) as t:
+        got, _ = drain(t, len(body), timeout_s=60)
+        assert got == body
+        assert t.next(timeout_ms=60) is None

@@ -3,7 +3,7 @@ lines is followed from offset 0 by the native tailer (pinned slots, HBM copy
 on its own stream) and every batch runs through bjx_process_batch on its HBM
 copy.  Prints one JSON line: file bytes, lines, wall time, lines/s, and the
 engine-only device time of the same batches (Banner replay not included).
-usage: python tools/tail_bench.py [cfg] [lines] [batch_MiB] [dir]"""
+usage: python tools/tail_bench.py [cfg] [lines] [batch_MiB] [dir] [slots]"""
 import json
 import os
 import sys
@@ -24,6 +24,7 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 20_000_000
     batch_mib = int(sys.argv[3]) if len(sys.argv) > 3 else 256
     d = sys.argv[4] if len(sys.argv) > 4 else os.environ.get("TMPDIR", "/tmp")
+    slots = int(sys.argv[5]) if len(sys.argv) > 5 else 3
     w = W.scaled(getattr(W, cfg.upper()), n)
     t, nb = w.device_lines(0)
     path = os.path.join(d, "bjx_tail_bench.log")
@@ -45,7 +46,7 @@ def main():
         lines = 0
         batches = 0
         t0 = time.perf_counter()
-        with LogTailer(path, device=0, from_start=True, batch_bytes=batch_mib << 20, poll_ms=1) as tl:
+        with LogTailer(path, device=0, from_start=True, batch_bytes=batch_mib << 20, poll_ms=1, slots=slots) as tl:
             got = 0
             while got < nb:
                 b = tl.next(timeout_ms=1000)
@@ -59,7 +60,7 @@ def main():
                 batches += 1
                 tl.release(b)
         wall = time.perf_counter() - t0
-        res = {"workload": cfg, "file_bytes": nb, "lines": lines, "batches": batches, "batch_MiB": batch_mib,
+        res = {"workload": cfg, "file_bytes": nb, "lines": lines, "batches": batches, "batch_MiB": batch_mib, "slots": slots,
                "wall_s": round(wall, 3), "lines_per_s_tail_inclusive": round(lines / wall, 1),
                "file_to_HBM_GBps": round(nb / wall / 1e9, 2), "engine_device_s": round(dev_ms / 1e3, 3),
                "lines_per_s_engine_only": round(lines / (dev_ms / 1e3), 1), "rep": rep,
