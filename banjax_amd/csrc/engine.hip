@@ -4502,6 +4502,7 @@ struct bjx_engine {
   uint64_t dbg_hash_mask = 0;  // bjx_debug_set_ip_hash_mask
   uint64_t dbg_budget = 0;     // bjx_debug_set_claim_budget (0 = off)
   uint32_t lines2_lds = 0;     // dynamic LDS k_lines2 was last configured for
+  uint32_t lines2_w = 0;       // ... and the instance (mask width) it was set on
   int dbg_slot_cache = -1;     // bjx_debug_set_slot_cache: -1 = BJX_SLOT_CACHE / default on, 0 off, 1 on
   uint64_t host_counters[3] = {0, 0, 0};
 
@@ -5296,6 +5297,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   // dictionary blob when both fit kLinesTabLdsMax
   uint32_t lt_hinfo = 0, lt_cls = 0, lt_trec = 0, lt_pool = 0;
   uint32_t l2_hdc = 0, l2_dcls = 0, l2_none = 0, l2_bytes = 0;  // k_lines2 tables (0 bytes: not eligible)
+  uint32_t l2_w = 1;  // their mask width in 64-bit words
   if (use_plan && hl_bytes && !getenv("BJX_NO_PLAN_LDS")) {
     std::vector<uint2> hinfo(n_hosts, make_uint2(0, 0));
     std::vector<uint4> cls, trec;
@@ -5405,39 +5407,47 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
     // k_lines reads: per decision class (site plan class, site rules, ALWAYS
     // and hosts_to_skip masks) the per-literal rows, their checks, the rule of
     // each position and the anchored / no-literal entries
-    // the literals a hit can carry (the scan pass's gram-table literals) must have
-    // ids below kL2Lits: they index the rows, and the overflow bits (id & 31) name
-    // them exactly
-    uint32_t pref_ids_ok = 1;
+    // W 64-bit words of position bits cover the ruleset's widest scope (at
+    // most 128 positions: the plan entries hold a 7-bit position); one row per
+    // prefilter literal id (the literals a hit can carry)
+    const uint32_t l2w = max_app <= 64 ? 1u : 2u;
+    uint32_t n_lrows = 0;  // rows for literal ids up to the largest prefilter one
     for (uint32_t id = 0; id < lit_pref.size(); ++id)
-      if (lit_pref[id] && id >= kL2Lits) pref_ids_ok = 0;
-    if (lt_cls && pref_ids_ok && max_app <= 64 && !getenv("BJX_NO_LINES2")) {
+      if (lit_pref[id]) n_lrows = id + 1;
+    if (lt_cls && max_app <= 128 && !getenv("BJX_NO_LINES2")) {
+      const uint32_t DW = l2_dcls_words(l2w), RW = l2_row_words(l2w), NP = 64 * l2w;
+      using Mask = std::array<uint64_t, 2>;
       struct Dc {
-        uint64_t eq[kL2Lits] = {}, job[kL2Lits] = {}, lm[kL2Lits] = {};
-        std::vector<uint4> chk[kL2Lits];
-        uint32_t prule[64] = {};
+        std::vector<Mask> eq, job, lm;
+        std::vector<std::vector<uint4>> chk;
+        std::vector<uint32_t> prule;
         std::vector<uint32_t> anc;  // kL2AncWords per entry
-        uint64_t alw = 0, skp = 0, anyhit = 0, anyovf = 0;
+        Mask alw{}, skp{}, anyhit{}, anyovf{}, lmbig{};
       };
       std::vector<Dc> dcs;
-      std::map<std::tuple<uint32_t, uint32_t, uint64_t, uint64_t>, uint32_t> dc_ids;
+      std::map<std::tuple<uint32_t, uint32_t, uint64_t, uint64_t, uint64_t, uint64_t>, uint32_t> dc_ids;
       const uint32_t n_glob_ent = (uint32_t)(plan_glob.size() / 2);
       bool ok = true;
+      auto set = [](Mask &m, uint32_t p) { m[p >> 6] |= 1ull << (p & 63); };
       auto add_entry = [&](Dc &D, uint4 a, const uint4 b, uint32_t p) {
         const uint32_t kind = (a.x >> 27) & 7u, eq = (a.x >> 30) & 1u;
-        const uint64_t bit = 1ull << p;
+        if (p >= NP) { ok = false; return; }
         a.x = (a.x & ~(0x7Fu << 20)) | (p << 20);
         D.prule[p] = a.x;
         auto ids = [&](auto fn) {
           const uint32_t l4[4] = {a.y & 0xFFFFu, a.y >> 16, a.z & 0xFFFFu, a.z >> 16};
           for (uint32_t l : l4)
-            if (l != 0xFFFFu) fn(l);
+            if (l != 0xFFFFu) {
+              if (l >= n_lrows) { ok = false; continue; }
+              fn(l);
+            }
         };
         if (kind == kPlanLit) {
           ids([&](uint32_t l) {
-            D.lm[l] |= bit;
-            if (a.w == kNone) (eq ? D.eq[l] : D.job[l]) |= bit;
-            else if (!eq) D.job[l] |= bit;
+            set(D.lm[l], p);
+            if (l >= 32) set(D.lmbig, p);
+            if (a.w == kNone) set(eq ? D.eq[l] : D.job[l], p);
+            else if (!eq) set(D.job[l], p);
             else {
               const uint32_t off = a.w & 0xFFu, flen = b.y;
               D.chk[l].push_back(make_uint4(p | (kL2ChkFull << 8) | (1u << 10), a.w, flen, flen > off ? flen - off : 0u));
@@ -5447,13 +5457,14 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
           const uint4 rec = trec[a.w];
           const uint32_t la = rec.x & 0xFF, lc = (rec.x >> 8) & 0xFF, side = (rec.x >> 16) & 1u;
           ids([&](uint32_t l) {
-            D.lm[l] |= bit;
+            set(D.lm[l], p);
+            if (l >= 32) set(D.lmbig, p);
             D.chk[l].push_back(make_uint4(p | (kL2ChkTmpl << 8) | (eq << 10) | ((side ? 0u : 1u) << 11), a.w, 0u,
                                           side ? lc : la + lc));
           });
         } else if (kind == kPlanLitAny) {
-          D.anyhit |= bit;
-          D.anyovf |= bit;
+          set(D.anyhit, p);
+          set(D.anyovf, p);
         } else {  // kPlanAnchor, kPlanAnchorT, kPlanScan: the bytes of rest each may read
           uint32_t ext = 0;
           if (kind == kPlanAnchorT) {
@@ -5469,11 +5480,15 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
           D.anc.insert(D.anc.end(), w, w + kL2AncWords);
         }
       };
-      auto dc_of = [&](uint32_t ci, uint32_t n_ent, uint32_t nsite, uint64_t alw, uint64_t skp) {
-        const auto key = std::make_tuple(ci | (n_ent << 16), nsite, alw, skp);
+      auto dc_of = [&](uint32_t ci, uint32_t n_ent, uint32_t nsite, uint32_t sc) {
+        const Mask alw{sc_always[2 * sc], sc_always[2 * sc + 1]}, skp{sc_skipm[2 * sc], sc_skipm[2 * sc + 1]};
+        const auto key = std::make_tuple(ci | (n_ent << 16), nsite, alw[0], alw[1], skp[0], skp[1]);
         auto it = dc_ids.find(key);
         if (it != dc_ids.end()) return it->second;
         Dc D;
+        D.eq.assign(n_lrows, Mask{}); D.job.assign(n_lrows, Mask{}); D.lm.assign(n_lrows, Mask{});
+        D.chk.assign(n_lrows, {});
+        D.prule.assign(NP, 0);
         D.alw = alw;
         D.skp = skp;
         for (uint32_t e = 0; e < n_ent; ++e) add_entry(D, cls[2 * (ci + e)], cls[2 * (ci + e) + 1], (cls[2 * (ci + e)].x >> 20) & 0x7Fu);
@@ -5486,37 +5501,40 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
       };
       std::vector<uint32_t> hdc(n_hosts, 0);
       for (uint32_t h = 0; h < n_hosts; ++h)
-        hdc[h] = dc_of(hinfo[h].x & 0xFFFFu, hinfo[h].x >> 16, (uint32_t)per_host[h].size(), sc_always[2 * h], sc_skipm[2 * h]);
-      const uint32_t none = dc_of(0xFFFFu, 0, 0, sc_always[2 * n_hosts], sc_skipm[2 * n_hosts]);
+        hdc[h] = dc_of(hinfo[h].x & 0xFFFFu, hinfo[h].x >> 16, (uint32_t)per_host[h].size(), h);
+      const uint32_t none = dc_of(0xFFFFu, 0, 0, n_hosts);
       // layout (words, 16 B aligned pieces)
       std::vector<uint32_t> t(((hl.size() + 3) & ~size_t(3)), 0);
       std::copy(hl.begin(), hl.end(), t.begin());
       auto al4 = [&]() { t.resize((t.size() + 3) & ~size_t(3), 0); return (uint32_t)t.size(); };
+      auto put = [&](uint32_t at, const Mask &m) {
+        for (uint32_t k = 0; k < l2w; ++k) { t[at + 2 * k] = (uint32_t)m[k]; t[at + 2 * k + 1] = (uint32_t)(m[k] >> 32); }
+      };
       const uint32_t w_hdc = al4();
       t.insert(t.end(), hdc.begin(), hdc.end());
       const uint32_t w_dc = al4();
-      t.resize(t.size() + kL2DclsWords * dcs.size(), 0);
-      for (uint32_t d = 0; d < dcs.size(); ++d) {
+      t.resize(t.size() + (size_t)DW * dcs.size(), 0);
+      for (uint32_t d = 0; d < dcs.size() && ok; ++d) {
         Dc &D = dcs[d];
         const uint32_t w_rows = al4();
-        t.resize(t.size() + kL2RowWords * kL2Lits, 0);
-        for (uint32_t l = 0; l < kL2Lits; ++l) {
+        t.resize(t.size() + (size_t)RW * n_lrows, 0);
+        for (uint32_t l = 0; l < n_lrows; ++l) {
           const uint32_t w_ck = al4();
           for (const uint4 &c : D.chk[l]) { t.push_back(c.x); t.push_back(c.y); t.push_back(c.z); t.push_back(c.w); }
-          uint32_t *r = t.data() + w_rows + kL2RowWords * l;
-          r[0] = (uint32_t)D.eq[l]; r[1] = (uint32_t)(D.eq[l] >> 32);
-          r[2] = (uint32_t)D.job[l]; r[3] = (uint32_t)(D.job[l] >> 32);
-          r[4] = (uint32_t)D.lm[l]; r[5] = (uint32_t)(D.lm[l] >> 32);
-          r[6] = w_ck; r[7] = (uint32_t)D.chk[l].size();
+          const uint32_t r = w_rows + RW * l;
+          put(r, D.eq[l]); put(r + 2 * l2w, D.job[l]); put(r + 4 * l2w, D.lm[l]);
+          t[r + 6 * l2w] = w_ck; t[r + 6 * l2w + 1] = (uint32_t)D.chk[l].size();
         }
         const uint32_t w_pr = al4();
-        t.insert(t.end(), D.prule, D.prule + 64);
+        t.insert(t.end(), D.prule.begin(), D.prule.end());
         const uint32_t w_anc = al4();
         t.insert(t.end(), D.anc.begin(), D.anc.end());
-        uint32_t *rec = t.data() + w_dc + kL2DclsWords * d;
-        const uint64_t v[4] = {D.alw, D.skp, D.anyhit, D.anyovf};
-        for (int k = 0; k < 4; ++k) { rec[2 * k] = (uint32_t)v[k]; rec[2 * k + 1] = (uint32_t)(v[k] >> 32); }
-        rec[8] = w_rows; rec[9] = w_pr; rec[10] = w_anc; rec[11] = (uint32_t)(D.anc.size() / kL2AncWords);
+        const uint32_t rec = w_dc + DW * d;
+        put(rec, D.alw); put(rec + 2 * l2w, D.skp); put(rec + 4 * l2w, D.anyhit); put(rec + 6 * l2w, D.anyovf);
+        put(rec + 8 * l2w, D.lmbig);
+        t[rec + 10 * l2w] = w_rows; t[rec + 10 * l2w + 1] = w_pr; t[rec + 10 * l2w + 2] = w_anc;
+        t[rec + 10 * l2w + 3] = (uint32_t)(D.anc.size() / kL2AncWords);
+        if ((size_t)t.size() * 4 > kL2TabMax) ok = false;  // stop laying out tables that cannot be used
       }
       al4();
       // inline DFAs (l2_inline): a position whose rule is anchored at the
@@ -5538,9 +5556,9 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
         std::map<uint32_t, uint32_t> inl_of;  // rule -> entry word offset (0: not inline)
         for (uint32_t d = 0; d < dcs.size() && ok; ++d) {
           Dc &D = dcs[d];
-          uint32_t pin[64] = {};
+          std::vector<uint32_t> pin(NP, 0);
           bool any = false;
-          for (uint32_t p = 0; p < 64; ++p) {
+          for (uint32_t p = 0; p < NP; ++p) {
             const uint32_t w = D.prule[p];
             if (!w || (w & kPlanOwn)) continue;
             const uint32_t r = w & 0xFFFFFu;
@@ -5572,20 +5590,21 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
             pin[p] = it->second;
             any = any || it->second != 0;
           }
-          if (!any || (t.size() + 68) * 4 > inl_max) continue;
+          if (!any || (t.size() + NP + 4) * 4 > inl_max) continue;
           const uint32_t w_pin = al4();
-          t.insert(t.end(), pin, pin + 64);
-          t[w_dc + kL2DclsWords * d + 12] = w_pin;
+          t.insert(t.end(), pin.begin(), pin.end());
+          t[w_dc + DW * d + 10 * l2w + 4] = w_pin;
         }
         al4();
       }
       if (ok && t.size() * 4 <= kL2TabMax) {
         l2_hdc = w_hdc; l2_dcls = w_dc; l2_none = none;
         l2_bytes = (uint32_t)(t.size() * 4);
+        l2_w = l2w;
         hl.swap(t);
       }
       if (getenv("BJX_DEBUG_IMG"))
-        fprintf(stderr, "[bjx] k_lines2 tables: %zu decision classes, %zu B (%s)\n", dcs.size(),
+        fprintf(stderr, "[bjx] k_lines2 tables (%u-word masks): %zu decision classes, %zu B (%s)\n", l2w, dcs.size(),
                 (l2_bytes ? hl.size() : t.size()) * 4, l2_bytes ? "on" : "off");
     }
     if (getenv("BJX_DEBUG_IMG"))
@@ -5812,7 +5831,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.hl = reinterpret_cast<const uint32_t *>(base + o_hl);
   B.hl_bytes = hl_bytes;
   B.lt_hinfo = lt_hinfo; B.lt_cls = lt_cls; B.lt_trec = lt_trec; B.lt_pool = lt_pool;
-  B.l2_hdc = l2_hdc; B.l2_dcls = l2_dcls; B.l2_none = l2_none; B.l2_bytes = l2_bytes;
+  B.l2_hdc = l2_hdc; B.l2_dcls = l2_dcls; B.l2_none = l2_none; B.l2_bytes = l2_bytes; B.l2_w = l2_w;
   {
     // k_dfa stages the block's rule in LDS when it fits: size that LDS by the
     // ruleset's largest DFA, not the cap, so smaller rulesets run more blocks
@@ -6567,17 +6586,20 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     e->last_line_kernel = use_l2 ? 2u : 1u;
     if (use_l2) {
       const uint32_t lds = B.l2_bytes + (kL2Block / 64) * kL2WaveLds;
-      if (lds != e->lines2_lds) {
-        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_lines2), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      const void *fn = B.l2_w == 2 ? reinterpret_cast<const void *>(&k_lines2<2>) : reinterpret_cast<const void *>(&k_lines2<1>);
+      if (lds != e->lines2_lds || B.l2_w != e->lines2_w) {
+        HIP_OK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         e->lines2_lds = lds;
+        e->lines2_w = B.l2_w;
       }
       int per_cu = 0;
-      HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&k_lines2), kL2Block, lds));
+      HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kL2Block, lds));
       const uint64_t resident = (uint64_t)std::max(1, per_cu) * (uint64_t)std::max(1, n_cu);
       const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n_lines + kL2Block - 1) / kL2Block, resident));
       static const bool dbg_img = getenv("BJX_DEBUG_IMG") != nullptr;
       if (dbg_img) fprintf(stderr, "[bjx] k_lines2: %u B LDS per block (tables %u), %d blocks per CU, grid %u\n", lds, B.l2_bytes, per_cu, grid);
-      hipLaunchKernelGGL(k_lines2, dim3(grid), dim3(kL2Block), lds, st, B, A);
+      if (B.l2_w == 2) hipLaunchKernelGGL(k_lines2<2>, dim3(grid), dim3(kL2Block), lds, st, B, A);
+      else hipLaunchKernelGGL(k_lines2<1>, dim3(grid), dim3(kL2Block), lds, st, B, A);
       HIP_OK(hipGetLastError());
     } else {
       const bool img_lds = B.img_bytes <= kLinesImgMax;

@@ -210,6 +210,7 @@ struct Bind {
   // offsets; lines2.h): per-host decision class, class records, the class of
   // lines without a host; l2_bytes = the blob with them (0: k_lines2 off)
   uint32_t l2_hdc, l2_dcls, l2_none, l2_bytes;
+  uint32_t l2_w;  // mask width of k_lines2's tables: 64-bit words of positions (1 or 2; k_lines2<W>)
   // k_dfa's LDS: transition entries / accel words staged per block (the
   // ruleset's largest DFA within kDfaLdsEntries / kDfaAccelLds), dynamic bytes
   uint32_t dfa_tr, dfa_acc, dfa_lds;

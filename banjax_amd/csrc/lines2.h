@@ -13,8 +13,9 @@
 //
 // Decisions.  A decision class is one (site plan class, number of site rules,
 // ALWAYS mask, hosts_to_skip mask) of the line's scope; its positions are the
-// host's site rules then the global rules (<= 64 in all).  Per class and
-// literal id (rulesets of <= 32 interned literals) one row holds:
+// host's site rules then the global rules, at most 64 W (W = 1 or 2 words of
+// position bits, the ruleset's widest scope; k_lines2<W>).  Per class and
+// prefilter literal id one row holds:
 //   eq   positions a hit of the literal matches outright (equivalent literal
 //        rules, literal not host-split),
 //   job  positions a hit sends to the automaton (non-equivalent literal rules),
@@ -35,10 +36,49 @@ constexpr int kL2Block = 512;     // 8 waves; two blocks per CU
 constexpr uint32_t kL2WaveLds = 64 * kL2Win + kWaveJobBytes;
 constexpr uint32_t kL2TabMax = 20 * 1024;  // hl blob with the k_lines2 tables (LDS, per block)
 constexpr uint32_t kL2ChkTmpl = 1, kL2ChkFull = 2;
-constexpr uint32_t kL2DclsWords = 16, kL2RowWords = 8, kL2Lits = 32, kL2AncWords = 12;
+constexpr uint32_t kL2AncWords = 12;
+// class record (u32 words): ALWAYS, hosts_to_skip, any-hit jobs, overflow
+// jobs, overflow jobs of literals with ids >= 32 (W 64-bit words each), then
+// the rows, position -> rule, anchored entries (offset, count) and inline-DFA
+// offsets; a literal's row: eq, job, lm (W 64-bit words each), checks
+// (offset, count)
+__host__ __device__ constexpr uint32_t l2_dcls_words(uint32_t w) { return (10 * w + 5 + 3) & ~3u; }
+__host__ __device__ constexpr uint32_t l2_row_words(uint32_t w) { return (6 * w + 2 + 3) & ~3u; }
 
-// positions <-> bits
-__device__ __forceinline__ uint64_t l2_bit(uint32_t p) { return 1ull << p; }
+// W-word position masks
+template <int W>
+struct L2Mask {
+  uint64_t w[W];
+};
+template <int W>
+__device__ __forceinline__ L2Mask<W> l2_ld_mask(const uint32_t *hl, uint32_t at) {
+  L2Mask<W> m;
+#pragma unroll
+  for (int k = 0; k < W; ++k) {
+    const uint2 v = *reinterpret_cast<const uint2 *>(hl + at + 2 * k);
+    m.w[k] = ((uint64_t)v.y << 32) | v.x;
+  }
+  return m;
+}
+template <int W>
+__device__ __forceinline__ void l2_or(L2Mask<W> &a, const L2Mask<W> &b) {
+#pragma unroll
+  for (int k = 0; k < W; ++k) a.w[k] |= b.w[k];
+}
+template <int W>
+__device__ __forceinline__ void l2_set(L2Mask<W> &a, uint32_t p) {
+#pragma unroll
+  for (int k = 0; k < W; ++k)
+    if ((p >> 6) == (uint32_t)k) a.w[k] |= 1ull << (p & 63);
+}
+template <int W>
+__device__ __forceinline__ bool l2_has(const L2Mask<W> &a, uint32_t p) {
+  bool r = false;
+#pragma unroll
+  for (int k = 0; k < W; ++k)
+    if ((p >> 6) == (uint32_t)k) r = (a.w[k] >> (p & 63)) & 1;
+  return r;
+}
 
 // up to four spaces of mask m (bit i = line byte base + i) appended to sp0..sp3
 __device__ __forceinline__ void l2_take_spaces(uint64_t m, int32_t base, uint32_t &ns, uint32_t &sp0, uint32_t &sp1,
@@ -251,7 +291,9 @@ __device__ __forceinline__ uint32_t l2_inline(const uint32_t *hl, uint32_t ent, 
   return ae[st] ? 1u : 0u;
 }
 
+template <int W>
 __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
+  constexpr uint32_t DW = l2_dcls_words(W), RW = l2_row_words(W);
   uint32_t *s_hl = reinterpret_cast<uint32_t *>(s_dyn);
   for (uint32_t i = threadIdx.x; i < B.l2_bytes / 16; i += blockDim.x)
     reinterpret_cast<uint4 *>(s_hl)[i] = reinterpret_cast<const uint4 *>(B.hl)[i];
@@ -355,20 +397,20 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
         const int32_t hid = hostw ? host_lookup_lds(s_hl, X.wp + host_off, host_len)
                                   : host_lookup_lds(s_hl, X.gp + host_off, host_len);
         const uint32_t dc = hid >= 0 ? s_hl[B.l2_hdc + (uint32_t)hid] : B.l2_none;
-        const uint32_t dw = B.l2_dcls + dc * kL2DclsWords;
-        const uint4 d0 = l2_ld4w(s_hl, dw), d1 = l2_ld4w(s_hl, dw + 4), d2 = l2_ld4w(s_hl, dw + 8), d3 = l2_ld4w(s_hl, dw + 12);
-        const uint64_t alw = ((uint64_t)d0.y << 32) | d0.x, skp = ((uint64_t)d0.w << 32) | d0.z;
-        const uint64_t anyhit = ((uint64_t)d1.y << 32) | d1.x, anyovf = ((uint64_t)d1.w << 32) | d1.z;
-        const uint32_t rows = d2.x, prule = d2.y, anc = d2.z, n_anc = d2.w;
+        const uint32_t dw = B.l2_dcls + dc * DW;
+        const uint32_t rows = s_hl[dw + 10 * W], prule = s_hl[dw + 10 * W + 1], anc = s_hl[dw + 10 * W + 2],
+                       n_anc = s_hl[dw + 10 * W + 3];
         const uint32_t first_rule = hid >= 0 ? LT.hinfo[hid].y : 0u;
-        const uint32_t pinl = d3.x;  // the class's inline-DFA entries per position (0: none)
+        const uint32_t pinl = s_hl[dw + 10 * W + 4];  // the class's inline-DFA entries per position (0: none)
         const bool exempt = B.any_allow && check_is_allowed(B, hid, X.gp + ip_off, ip_len);
         const int64_t tsn = ns_from_seconds(f);
         uint8_t fl = 0;
         if (go_sub(A.now_ns, tsn) > 10000000000LL) fl = kLineOld;
         else if (exempt) fl = kLineExempt;
         const uint32_t rest_len = n - rest_off, host_rel = host_off - rest_off;
-        uint64_t m = alw, J = 0;
+        L2Mask<W> m = l2_ld_mask<W>(s_hl, dw), J;  // ALWAYS
+#pragma unroll
+        for (int k = 0; k < W; ++k) J.w[k] = 0;
         bool evl = false;  // the line has or may get (through its jobs) a rate-limit event
         if (fl) {
           L.counts[j] = 0;
@@ -377,7 +419,10 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
           const uint32_t cc = cm.cnt;
           const bool ovf = cc > (uint32_t)kCandSlots;
           const uint64_t rs = s + rest_off;
-          uint64_t ovbits = 0, done = 0;
+          uint32_t ovbits = 0;  // literal ids < 32 among the verified hits
+          L2Mask<W> done;
+#pragma unroll
+          for (int k = 0; k < W; ++k) done.w[k] = 0;
           uint32_t nlit = 0;
 #pragma unroll
           for (uint32_t c = 0; c < (uint32_t)kCandSlots; ++c) {
@@ -391,18 +436,18 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
               if (o + ll > n) continue;
               if (!(l2_in(X, o, ll) ? literal_at(TB, lit, X.wp + o) : literal_at(TB, lit, X.gp + o))) continue;
             }
-            ovbits |= 1ull << (lit & 31);
+            if (lit < 32) ovbits |= 1u << lit;
             ++nlit;
             if (ovf) continue;
             const uint32_t hp = q - rs < 0xFFFF ? (uint32_t)(q - rs) : 0xFFFFu;
-            const uint32_t rw = rows + (lit & 31) * kL2RowWords;
-            const uint4 ra = l2_ld4w(s_hl, rw), rb = l2_ld4w(s_hl, rw + 4);
-            m |= ((uint64_t)ra.y << 32) | ra.x;
-            J |= ((uint64_t)ra.w << 32) | ra.z;
-            for (uint32_t k = 0; k < rb.w; ++k) {
-              const uint4 ck = l2_ld4w(s_hl, rb.z + 4 * k);
-              const uint64_t bit = l2_bit(ck.x & 0xFFu);
-              if (done & bit) continue;
+            const uint32_t rw = rows + lit * RW;
+            l2_or(m, l2_ld_mask<W>(s_hl, rw));
+            l2_or(J, l2_ld_mask<W>(s_hl, rw + 2 * W));
+            const uint32_t ck_off = s_hl[rw + 6 * W], n_ck = s_hl[rw + 6 * W + 1];
+            for (uint32_t k = 0; k < n_ck; ++k) {
+              const uint4 ck = l2_ld4w(s_hl, ck_off + 4 * k);
+              const uint32_t bit = ck.x & 0xFFu;
+              if (l2_has(done, bit)) continue;
               uint32_t out;
               if (hp == 0xFFFFu) out = 2;  // hit offset unknown: the automaton decides
               else {
@@ -414,26 +459,28 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
                           : l2_check<false>(TB, LT, ck, X.gp + rest_off, rest_len, host_rel, host_len, hp);
               }
               if (out) {
-                done |= bit;
-                if (out == 1) m |= bit;
-                else J |= bit;
+                l2_set(done, bit);
+                if (out == 1) l2_set(m, bit);
+                else l2_set(J, bit);
               }
             }
           }
           if (ovf) {
             // more hits than slots: a literal rule none of whose literals occurred
             // cannot match; the others go to their automaton
-            ovbits |= cm.bits & 0xFFFFFFFFull;
-            uint64_t ob = ovbits;
+            // (literal ids >= 32: which occurred is not recorded, so every
+            // rule needing one of them goes to its automaton)
+            ovbits |= (uint32_t)(cm.bits & 0xFFFFFFFFull);
+            uint32_t ob = ovbits;
             while (ob) {
-              const uint32_t l = (uint32_t)__ffsll((unsigned long long)ob) - 1;
+              const uint32_t l = (uint32_t)__ffs(ob) - 1;
               ob &= ob - 1;
-              const uint4 rb = l2_ld4w(s_hl, rows + l * kL2RowWords + 4);
-              J |= ((uint64_t)rb.y << 32) | rb.x;
+              l2_or(J, l2_ld_mask<W>(s_hl, rows + l * RW + 4 * W));
             }
-            J |= anyovf;
+            l2_or(J, l2_ld_mask<W>(s_hl, dw + 6 * W));
+            l2_or(J, l2_ld_mask<W>(s_hl, dw + 8 * W));
           } else if (nlit) {
-            J |= anyhit;
+            l2_or(J, l2_ld_mask<W>(s_hl, dw + 4 * W));
           }
           // anchored and no-literal entries of the class, wave-uniform per class
           uint32_t todo_anc = n_anc ? 1u : 0u;
@@ -455,31 +502,45 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
                 const bool inw = hostw && rest_off + need + 8 <= X.lim;
                 const uint32_t out = inw ? l2_anchored<true>(B, TB, LT, a, bq, r, X.wp + rest_off, rest_len, host_rel, host_len)
                                          : l2_anchored<false>(B, TB, LT, a, bq, r, X.gp + rest_off, rest_len, host_rel, host_len);
-                if (out == 1) m |= l2_bit(pos);
-                else if (out == 2) J |= l2_bit(pos);
+                if (out == 1) l2_set(m, pos);
+                else if (out == 2) l2_set(J, pos);
               }
             }
           }
-          J &= ~m;
-          evl = ((m | J) & ~skp) != 0;
-          while (J) {
-            const uint32_t p = (uint32_t)__ffsll((unsigned long long)J) - 1;
-            J &= J - 1;
-            const uint32_t w = s_hl[prule + p];
-            const uint32_t r = (w & kPlanOwn) ? first_rule + p : (w & 0xFFFFFu);
-            const uint64_t rec = l2_job_rec(B, r, cm, cv, rs, rest_len, rest_off);
-            uint32_t res = 2;
-            if (rec == kJobDecided) res = 1;
-            else if (pinl && !(rec & kJobLegacy)) {
-              const uint32_t ent = s_hl[pinl + p];
-              if (ent) res = l2_inline(s_hl, ent, X, s, rec);
-            }
-            if (res == 1) m |= l2_bit(p);
-            else if (res == 2) emit_job(S, j, r, p, rec | (((skp >> p) & 1) ? kJobNoCount : 0ull));
+          const L2Mask<W> skp = l2_ld_mask<W>(s_hl, dw + 2 * W);
+#pragma unroll
+          for (int k = 0; k < W; ++k) {
+            J.w[k] &= ~m.w[k];
+            evl = evl || ((m.w[k] | J.w[k]) & ~skp.w[k]) != 0;
           }
-          L.masks[j * B.mask_words] = m;
-          if (B.mask_words > 1) L.masks[j * B.mask_words + 1] = 0;
-          L.counts[j] = ((uint64_t)__popcll(m) << 32) | (uint64_t)__popcll(m & ~skp);
+#pragma unroll
+          for (int k = 0; k < W; ++k) {
+            uint64_t Jk = J.w[k];
+            while (Jk) {
+              const uint32_t p = 64u * k + (uint32_t)__ffsll((unsigned long long)Jk) - 1;
+              Jk &= Jk - 1;
+              const uint32_t w = s_hl[prule + p];
+              const uint32_t r = (w & kPlanOwn) ? first_rule + p : (w & 0xFFFFFu);
+              const uint64_t rec = l2_job_rec(B, r, cm, cv, rs, rest_len, rest_off);
+              uint32_t res = 2;
+              if (rec == kJobDecided) res = 1;
+              else if (pinl && !(rec & kJobLegacy)) {
+                const uint32_t ent = s_hl[pinl + p];
+                if (ent) res = l2_inline(s_hl, ent, X, s, rec);
+              }
+              if (res == 1) m.w[k] |= 1ull << (p & 63);
+              else if (res == 2) emit_job(S, j, r, p, rec | (((skp.w[k] >> (p & 63)) & 1) ? kJobNoCount : 0ull));
+            }
+          }
+          uint32_t n_m = 0, n_ev = 0;
+#pragma unroll
+          for (int k = 0; k < W; ++k) {
+            L.masks[j * B.mask_words + k] = m.w[k];
+            n_m += __popcll(m.w[k]);
+            n_ev += __popcll(m.w[k] & ~skp.w[k]);
+          }
+          if (W == 1 && B.mask_words > 1) L.masks[j * B.mask_words + 1] = 0;
+          L.counts[j] = ((uint64_t)n_m << 32) | (uint64_t)n_ev;
         }
         L.rest_off[j] = rest_off;
         L.host_id[j] = hid;

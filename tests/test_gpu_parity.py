@@ -129,7 +129,7 @@ def test_per_site_regex_stress(engine):
     ("cfg1", 200_000, 3), ("cfg2", 40_000, 2), ("cfg3", 100_000, 3), ("cfg4", 1_500, 2), ("cfg5", 60_000, 2)])
 def test_workload_parity(engine, name, n_lines, batches):
     """Every BASELINE.json config shape, oracle-sized, split into batches so the
-    HBM state carries across bjx_process_batch calls."""
+    HBM state carries across bjx_process_batch calls; each through k_lines2."""
     w = W.scaled(W.ALL[name], n_lines, n_ips=min(W.ALL[name].n_ips, n_lines // 3 + 1))
     pair = Pair(w.rules_yaml, engine)
     per = (n_lines + batches - 1) // batches
@@ -142,6 +142,9 @@ def test_workload_parity(engine, name, n_lines, batches):
             if len(parts) > 2:
                 ips.add(parts[1].decode())
         pair.feed(data, w.now_ns(first, cnt))
+        # every BASELINE config runs the window kernel (cfg2: 100 positions,
+        # 2-word masks, literal ids past 32)
+        assert pair.engine.line_kernel()[0] == "k_lines2", name
     pair.compare_state(sorted(ips)[:100])
 
 
@@ -795,3 +798,47 @@ def test_event_record_forms(engine, rec16, monkeypatch):
     pair.feed(w.host_lines(20_000, 10_000), w.now_ns(20_000, 10_000), want_results=False)
     pair.feed(w.host_lines(30_000, 10_000), w.now_ns(30_000, 10_000) - 3 * 3600 * S, want_results=False)
     pair.compare_state()
+
+
+def test_lines2_wide_masks(engine):
+    """k_lines2 with 2-word position masks and literal ids past 32: a host of
+    12 site rules plus 110 global rules (positions up to 121), with ALWAYS,
+    anchored, no-literal and hosts_to_skip rules past position 64 and lines
+    whose literal hits overflow the scan's 4 slots.  Bit-exact against the
+    oracle, and the window kernel is the one that ran."""
+    rnd = random.Random(41)
+    decs = ["challenge", "nginx_block", "iptables_block"]
+    out = ["regexes_with_rates:"]
+    for k in range(110):
+        if k in (3, 70, 101):
+            p = r".*"
+        elif k % 17 == 5:
+            p = r"^GET \S+ GET \/q%d\/" % k
+        elif k % 23 == 7:
+            p = r"(GET|POST) \S+ (GET|POST) \/[a-z]%d[0-9]+" % k
+        else:
+            p = r"\/p%03d\/[a-z]+" % k if k % 2 else r"tok%03dx" % k
+        skip = "\n    hosts_to_skip:\n      s.example.com: true" if k in (66, 90, 101) else ""
+        out.append("  - rule: 'g%d'\n    regex: '%s'\n    interval: %d\n    hits_per_interval: %d\n    decision: %s%s"
+                   % (k, p, 1 + k % 3, k % 4, decs[k % 3], skip))
+    out.append("per_site_regexes_with_rates:")
+    out.append("  s.example.com:")
+    for k in range(12):
+        out.append("    - rule: 's%d'\n      regex: '%s'\n      interval: 2\n      hits_per_interval: 1\n      decision: %s"
+                   % (k, r"\/site%d\/" % k, decs[k % 3]))
+    pair = Pair("\n".join(out) + "\n", engine)
+    hosts = ["s.example.com", "o.example.com"]
+    frags = ["/p%03d/ab" % k for k in range(1, 110, 2)] + ["tok%03dx" % k for k in range(0, 110, 2)] + \
+            ["/q%d/" % k for k in range(5, 110, 17)] + ["/b%d77" % k for k in range(7, 110, 23)] + \
+            ["/site%d/" % k for k in range(12)] + ["/none", "zz"]
+    base = 1700000000
+    for b in range(2):
+        lines = []
+        for j in range(5000):
+            n_frag = rnd.choice([0, 1, 1, 2, 3, 6, 9])
+            uri = "".join(rnd.choice(frags) for _ in range(n_frag)) or "/"
+            lines.append("%.3f 10.1.%d.%d GET %s GET %s HTTP/1.1 UA\n" % (
+                base + b * 2 + j * 0.0003, rnd.randrange(4), rnd.randrange(16), rnd.choice(hosts), uri))
+        pair.feed("".join(lines).encode(), (base + b * 2 + 2) * S)
+        assert pair.engine.line_kernel()[0] == "k_lines2"
+    pair.compare_state(["10.1.%d.%d" % (a, c) for a in range(4) for c in range(16)])
