@@ -5554,13 +5554,89 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
         const size_t two_blocks = kScanLdsMax / 2 - (size_t)(kL2Block / 64) * kL2WaveLds;
         const size_t inl_max = t.size() * 4 <= two_blocks ? std::min<size_t>(kL2TabMax, two_blocks) : (size_t)kL2TabMax;
         std::map<uint32_t, uint32_t> inl_of;  // rule -> entry word offset (0: not inline)
+        // The automaton of rule r from its skip state (past its anchored
+        // literal prefix) over ASCII, renumbered canonically (dead 0, accept
+        // 1, the others in breadth-first order from the skip state, which is
+        // 2): rules that differ only in their prefix give equal tables.
+        // Empty when r does not qualify or the sub-automaton has 256 states.
+        auto suffix_dfa = [&](uint32_t r, std::vector<uint8_t> &tab, std::vector<uint8_t> &ae) {
+          tab.clear();
+          ae.clear();
+          if (r >= drules.size()) return;
+          const DevRule &dr = drules[r];
+          const CompiledRegex &rx = rs->rules[r].rx;
+          if (dr.mode != kModeAnchored || !dr.skip_len || (dr.flags & (kRuleNfa | kRuleNfaWide | kRuleAlways | kRuleNever)) ||
+              dr.skip_state <= kAccept || rx.trans.size() < (size_t)dr.n_states * dr.ncls)
+            return;
+          std::unordered_map<uint32_t, uint32_t> id{{kDead, kDead}, {kAccept, kAccept}};
+          std::vector<uint32_t> order{kDead, kAccept, dr.skip_state};
+          id[dr.skip_state] = 2;
+          for (size_t k = 2; k < order.size(); ++k) {
+            if (order.size() > 255) { tab.clear(); ae.clear(); return; }
+            const uint32_t st = order[k];
+            for (uint32_t b = 0; b < 128; ++b) {
+              const uint32_t nx = rx.trans[(size_t)st * dr.ncls + rx.ascii_cls[b]];
+              if (!id.count(nx)) { id[nx] = (uint32_t)order.size(); order.push_back(nx); }
+            }
+          }
+          if (order.size() > 255) return;
+          tab.assign(order.size() * 128, 0);
+          ae.assign(order.size(), 0);
+          for (size_t k = 2; k < order.size(); ++k) {
+            for (uint32_t b = 0; b < 128; ++b) tab[k * 128 + b] = (uint8_t)id[rx.trans[(size_t)order[k] * dr.ncls + rx.ascii_cls[b]]];
+            ae[k] = rx.accept_end[order[k]] ? 1 : 0;
+          }
+          ae[kAccept] = 1;
+        };
+        std::map<std::vector<uint8_t>, uint32_t> own_of;  // canonical suffix table (+ flags) -> entry word offset
+        auto own_suffix = [&](uint32_t d, uint32_t p) -> uint32_t {
+          std::vector<uint8_t> key, tab, ae;
+          for (uint32_t h = 0; h < n_hosts; ++h) {
+            if (hdc[h] != d) continue;
+            suffix_dfa(hinfo[h].y + p, tab, ae);
+            if (tab.empty()) return 0;
+            std::vector<uint8_t> k2 = tab;
+            k2.insert(k2.end(), ae.begin(), ae.end());
+            if (key.empty()) key.swap(k2);
+            else if (k2 != key) return 0;
+          }
+          if (key.empty()) return 0;
+          auto it = own_of.find(key);
+          if (it != own_of.end()) return it->second;
+          const uint32_t ns = (uint32_t)(tab.size() / 128);
+          const size_t need = 16 + (size_t)ns * 128 + ((ns + 3) & ~3u) + 16;
+          uint32_t at = 0;
+          if ((t.size() + 4) * 4 + need + 256 <= inl_max) {
+            at = al4();
+            t.resize(t.size() + 4, 0);
+            const uint32_t w_tr = al4();
+            t.resize(t.size() + (size_t)ns * 32, 0);
+            memcpy(reinterpret_cast<uint8_t *>(t.data() + w_tr), tab.data(), tab.size());
+            const uint32_t w_ae = al4();
+            t.resize(t.size() + (ns + 3) / 4, 0);
+            memcpy(reinterpret_cast<uint8_t *>(t.data() + w_ae), ae.data(), ae.size());
+            // no start state: only jobs that begin past the prefix run here
+            t[at] = w_tr * 4; t[at + 1] = w_ae * 4; t[at + 2] = kL2NoStart; t[at + 3] = 2;
+          }
+          own_of.emplace(key, at);
+          return at;
+        };
         for (uint32_t d = 0; d < dcs.size() && ok; ++d) {
           Dc &D = dcs[d];
           std::vector<uint32_t> pin(NP, 0);
           bool any = false;
           for (uint32_t p = 0; p < NP; ++p) {
             const uint32_t w = D.prule[p];
-            if (!w || (w & kPlanOwn)) continue;
+            if (!w) continue;
+            if (w & kPlanOwn) {
+              // a different rule per host (its own host spelled in an anchored
+              // prefix): inline when every host of the class has the same
+              // automaton past its prefix, for the jobs that start there
+              const uint32_t e = own_suffix(d, p);
+              pin[p] = e;
+              any = any || e != 0;
+              continue;
+            }
             const uint32_t r = w & 0xFFFFFu;
             if (r >= drules.size()) continue;
             auto it = inl_of.find(r);

@@ -37,6 +37,7 @@ constexpr uint32_t kL2WaveLds = 64 * kL2Win + kWaveJobBytes;
 constexpr uint32_t kL2TabMax = 20 * 1024;  // hl blob with the k_lines2 tables (LDS, per block)
 constexpr uint32_t kL2ChkTmpl = 1, kL2ChkFull = 2;
 constexpr uint32_t kL2AncWords = 12;
+constexpr uint32_t kL2NoStart = 0xFFFFFFFFu;  // inline entry without a start state (per-host rules: from the skip state only)
 // class record (u32 words): ALWAYS, hosts_to_skip, any-hit jobs, overflow
 // jobs, overflow jobs of literals with ids >= 32 (W 64-bit words each), then
 // the rows, position -> rule, anchored entries (offset, count) and inline-DFA
@@ -272,12 +273,16 @@ __device__ __forceinline__ uint4 l2_ld4w(const uint32_t *hl, uint32_t w) { retur
 // accept-at-end byte offset, start state, skip state}; u8 next states over
 // ASCII bytes): 1 matched, 0 no match, 2 undecided (the decision lies past
 // the window, or a non-ASCII byte needs rune decoding: the job goes to k_dfa).
+// A table shared by per-host rules holds only the automaton past their
+// anchored prefix (start kL2NoStart): a job that does not begin there stays a
+// job.
 // The same steps as dfa_line from the job's start: stop at the dead or accept
 // state, or at the line's end with the accept-at-end flag.
 __device__ __forceinline__ uint32_t l2_inline(const uint32_t *hl, uint32_t ent, const L2Line &X, uint64_t s, uint64_t rec) {
   const uint4 e = l2_ld4w(hl, ent);
   const uint8_t *tr = reinterpret_cast<const uint8_t *>(hl) + e.x;
   const uint8_t *ae = reinterpret_cast<const uint8_t *>(hl) + e.y;
+  if (!(rec & kJobSkipState) && e.z == kL2NoStart) return 2;  // a table from the skip state only
   uint32_t st = (rec & kJobSkipState) ? e.w : e.z;
   uint32_t o = (uint32_t)((rec & kJobOffMask) - s);
   const uint32_t lim = X.n < X.lim ? X.n : X.lim;
