@@ -842,3 +842,22 @@ def test_lines2_wide_masks(engine):
         pair.feed("".join(lines).encode(), (base + b * 2 + 2) * S)
         assert pair.engine.line_kernel()[0] == "k_lines2"
     pair.compare_state(["10.1.%d.%d" % (a, c) for a in range(4) for c in range(16)])
+
+
+@pytest.mark.parametrize("switch,name", [("BJX_NO_LINES2", "cfg3"), ("BJX_NO_PLAN_LDS", "cfg3"), ("BJX_NO_HOST_LDS", "cfg3"),
+                                         ("BJX_NO_PLAN", "cfg2"), ("BJX_NO_DFA_SKIP", "cfg5")])
+def test_fallback_paths(switch, name, monkeypatch):
+    """The bind-time switches that force a fallback path (the per-line
+    kernel k_lines, plan tables in HBM, the host dictionary in HBM, the rule
+    walk without plans, DFA jobs from rest[0]): the paths a ruleset too large
+    for the fast tables takes, bit-exact against the oracle."""
+    monkeypatch.setenv(switch, "1")
+    eng = Engine(0)
+    w = W.scaled(W.ALL[name], 20_000, n_ips=4_000)
+    pair = Pair(w.rules_yaml, eng)
+    for b in range(2):
+        pair.feed(w.host_lines(b * 10_000, 10_000), w.now_ns(b * 10_000, 10_000))
+    if switch == "BJX_NO_LINES2":
+        assert eng.line_kernel()[0] == "k_lines"
+    pair.compare_state([ln.split(b" ")[1].decode() for ln in w.host_lines(0, 50).split(b"\n")[:50] if ln])
+    eng.close()

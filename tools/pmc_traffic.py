@@ -12,7 +12,7 @@ import json
 import os
 import sys
 
-KERNELS = {"k_scan": ("k_scan<",), "k_lines": ("k_lines2(", "k_lines<"), "dfa_jobs": ("k_dfa(",)}
+KERNELS = {"k_scan": ("k_scan<",), "k_lines": ("k_lines2<", "k_lines<"), "dfa_jobs": ("k_dfa(",)}
 
 
 def last_value(d, counter, prefix):
