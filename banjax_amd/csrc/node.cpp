@@ -604,7 +604,8 @@ extern "C" int bjx_node_create(const int *devices, size_t n_devices, const bjx_e
   for (size_t k = 0; k < n_devices && rc == BJX_OK; ++k) {
     Part &P = n->parts[k];
     P.dev = devices[k];
-    for (DevMem *m : {&P.s_lines, &P.s_ev, &P.s_bytes, &P.s_out, &P.r_lines, &P.r_ev, &P.r_bytes, &P.r_out}) m->dev = P.dev;
+    for (DevMem *m : {&P.s_lines, &P.s_ev, &P.s_bytes, &P.s_out, &P.r_lines, &P.r_ev, &P.r_bytes, &P.r_out, &P.r_trips, &P.s_trips})
+      m->dev = P.dev;
     char e2[512] = {0};
     rc = bjx_engine_create(P.dev, opts, &P.e, e2, sizeof e2);
     if (rc != BJX_OK) {
