@@ -1801,6 +1801,7 @@ __global__ __launch_bounds__(kScanWaves * 64) __attribute__((amdgpu_waves_per_eu
 
 struct LinesArgs {
   uint32_t dbg;  // timing experiments only (BJX_DEBUG_LINES): 1 no anchored checks, 2 no literal hits, 4 unstaged, 8 no host lookup
+  uint32_t dbg2; // timing experiments only (BJX_DEBUG_L2, k_lines2; results wrong): 1 no anchored entries, 2 no hit rows, 4 no jobs, 8 no IP fields
   const uint8_t *buf;
   uint64_t n;  // batch bytes
   const uint64_t *nl;
@@ -6648,6 +6649,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     LinesArgs A;
     A.buf = buf; A.n = n; A.nl = e->nl.p; A.n_lines = n_lines; A.L = L; A.now_ns = now_ns;
     A.dbg = getenv("BJX_DEBUG_LINES") ? (uint32_t)atoi(getenv("BJX_DEBUG_LINES")) : 0u;
+    A.dbg2 = getenv("BJX_DEBUG_L2") ? (uint32_t)atoi(getenv("BJX_DEBUG_L2")) : 0u;
     A.slow_list = e->slow_list.p; A.slow_count = e->scalars.p;
     A.jline = e->jline.p; A.jkey = e->jkey.p; A.jidx = e->jidx.p; A.jrec = e->jrec.p; A.job_count = e->scalars.p + 11;
     A.job_cap = std::min(std::min(e->jline.n, e->jkey.n), std::min(e->jidx.n, e->jrec.n));

@@ -431,7 +431,7 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
           uint32_t nlit = 0;
 #pragma unroll
           for (uint32_t c = 0; c < (uint32_t)kCandSlots; ++c) {
-            if (c >= cc) break;
+            if (c >= cc || (A.dbg2 & 2)) break;
             const uint64_t v = cv[c];
             const uint32_t lit = (uint32_t)(v & 0x7FFFFF);
             const uint64_t q = v >> 24;
@@ -487,30 +487,24 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
           } else if (nlit) {
             l2_or(J, l2_ld_mask<W>(s_hl, dw + 4 * W));
           }
-          // anchored and no-literal entries of the class, wave-uniform per class
-          uint32_t todo_anc = n_anc ? 1u : 0u;
-          while (__ballot(todo_anc) != 0) {
-            const uint32_t f0 = (uint32_t)__ffsll((unsigned long long)__ballot(todo_anc)) - 1;
-            const uint32_t cur = __builtin_amdgcn_readlane(dc, f0);
-            if (todo_anc && dc == cur) {
-              todo_anc = 0;
-              const uint32_t na = __builtin_amdgcn_readlane(n_anc, f0), ab = __builtin_amdgcn_readlane(anc, f0);
-              for (uint32_t i = 0; i < na; ++i) {
-                const uint32_t ew = ab + kL2AncWords * i;
-                const uint4 a = l2_ld4w(s_hl, ew), bq = l2_ld4w(s_hl, ew + 4);
-                const uint32_t ext = s_hl[ew + 8];
-                const uint32_t pos = (a.x >> 20) & 0x7Fu;
-                const uint32_t r = (a.x & kPlanOwn) ? first_rule + pos : (a.x & 0xFFFFFu);
-                // in the window: the bytes of rest the entry may read (ext, plus the
-                // host for a template) and the host field
-                const uint32_t need = (ext & 0x7FFFFFFFu) + ((ext >> 31) ? host_len : 0u);
-                const bool inw = hostw && rest_off + need + 8 <= X.lim;
-                const uint32_t out = inw ? l2_anchored<true>(B, TB, LT, a, bq, r, X.wp + rest_off, rest_len, host_rel, host_len)
-                                         : l2_anchored<false>(B, TB, LT, a, bq, r, X.gp + rest_off, rest_len, host_rel, host_len);
-                if (out == 1) l2_set(m, pos);
-                else if (out == 2) l2_set(J, pos);
-              }
-            }
+          // anchored and no-literal entries of the class, each lane its own
+          // class's list (a wave-uniform walk per class serialised the classes
+          // of a wave's lines)
+          const uint32_t na = (A.dbg2 & 1) ? 0u : n_anc;
+          for (uint32_t i = 0; i < na; ++i) {
+            const uint32_t ew = anc + kL2AncWords * i;
+            const uint4 a = l2_ld4w(s_hl, ew), bq = l2_ld4w(s_hl, ew + 4);
+            const uint32_t ext = s_hl[ew + 8];
+            const uint32_t pos = (a.x >> 20) & 0x7Fu;
+            const uint32_t r = (a.x & kPlanOwn) ? first_rule + pos : (a.x & 0xFFFFFu);
+            // in the window: the bytes of rest the entry may read (ext, plus the
+            // host for a template) and the host field
+            const uint32_t need = (ext & 0x7FFFFFFFu) + ((ext >> 31) ? host_len : 0u);
+            const bool inw = hostw && rest_off + need + 8 <= X.lim;
+            const uint32_t out = inw ? l2_anchored<true>(B, TB, LT, a, bq, r, X.wp + rest_off, rest_len, host_rel, host_len)
+                                     : l2_anchored<false>(B, TB, LT, a, bq, r, X.gp + rest_off, rest_len, host_rel, host_len);
+            if (out == 1) l2_set(m, pos);
+            else if (out == 2) l2_set(J, pos);
           }
           const L2Mask<W> skp = l2_ld_mask<W>(s_hl, dw + 2 * W);
 #pragma unroll
@@ -520,7 +514,7 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
           }
 #pragma unroll
           for (int k = 0; k < W; ++k) {
-            uint64_t Jk = J.w[k];
+            uint64_t Jk = (A.dbg2 & 4) ? 0ull : J.w[k];
             while (Jk) {
               const uint32_t p = 64u * k + (uint32_t)__ffsll((unsigned long long)Jk) - 1;
               Jk &= Jk - 1;
@@ -553,7 +547,7 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
         // exchange, trips, bans): the others get ip_len 0 (k_ip_lookup skips
         // them) and 36 B fewer stores
         L.ip_len[j] = evl ? ip_len : 0u;
-        if (evl) {
+        if (evl && !(A.dbg2 & 8)) {
           L.ip_off[j] = ip_off;
           L.host_off[j] = host_off;
           L.host_len[j] = host_len;

@@ -25,4 +25,4 @@ for i in range(reps):
     print(json.dumps({"workload": name, "lines": o.n_lines, "bytes": nb, "results": o.n_results,
                       "events": o.n_events, "trips": o.n_trips, "device_ms": round(o.device_ms, 3),
                       "scan_ms": round(o.match_kernel_ms, 3), "scan_GBps": round(nb / o.match_kernel_ms / 1e6, 1),
-                      "phases": e.phase_ms(), "stats": e.scan_stats()}), flush=True)
+                      "phases": e.phase_ms(), "kernel_ms": e.kernel_ms(), "stats": e.scan_stats()}), flush=True)
