@@ -5646,7 +5646,21 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
               const CompiledRegex &rx = rs->rules[r].rx;
               uint32_t at = 0;
               const size_t need = 16 + (size_t)dr.n_states * 128 + ((dr.n_states + 3) & ~3u) + 16;
-              if (dr.mode == kModeAnchored && !(dr.flags & (kRuleNfa | kRuleNfaWide | kRuleAlways | kRuleNever)) &&
+              // anchored rules, and lead rules (jobs start at a literal's first
+              // hit) whose automaton has no state past the start that waits on
+              // most bytes (a .* after the literal: a failing run would walk on)
+              auto scans_on = [&]() {
+                if (rx.trans.size() < (size_t)dr.n_states * dr.ncls) return true;
+                for (uint32_t st = 2; st < dr.n_states; ++st) {
+                  if (st == dr.start) continue;
+                  uint32_t self = 0;
+                  for (uint32_t b = 0; b < 128; ++b) self += rx.trans[(size_t)st * dr.ncls + rx.ascii_cls[b]] == st;
+                  if (self >= 64) return true;
+                }
+                return false;
+              };
+              if ((dr.mode == kModeAnchored || ((dr.lead & 3u) == 3u && !scans_on())) &&
+                  !(dr.flags & (kRuleNfa | kRuleNfaWide | kRuleAlways | kRuleNever)) &&
                   dr.n_states >= 2 && dr.n_states < 256 &&
                   rx.trans.size() >= (size_t)dr.n_states * dr.ncls && (t.size() + 4) * 4 + need + 256 <= inl_max) {
                 at = al4();

@@ -37,6 +37,7 @@ constexpr uint32_t kL2WaveLds = 64 * kL2Win + kWaveJobBytes;
 constexpr uint32_t kL2TabMax = 20 * 1024;  // hl blob with the k_lines2 tables (LDS, per block)
 constexpr uint32_t kL2ChkTmpl = 1, kL2ChkFull = 2;
 constexpr uint32_t kL2AncWords = 12;
+constexpr uint32_t kL2InlineSteps = 64;      // bytes an inline automaton steps from its job's start
 constexpr uint32_t kL2NoStart = 0xFFFFFFFFu;  // inline entry without a start state (per-host rules: from the skip state only)
 // class record (u32 words): ALWAYS, hosts_to_skip, any-hit jobs, overflow
 // jobs, overflow jobs of literals with ids >= 32 (W 64-bit words each), then
@@ -204,12 +205,13 @@ __device__ __forceinline__ uint32_t l2_check(const Tabs &T, const LdsTabs &LT, c
 
 // The window record of a DFA job (engine.hip kJob*), or kJobDecided when the
 // pair is decided here: k_dfa's eq_certain, skip and lead_start steps on the
-// line's hit slots in registers.  Lead seeks past overflowed slots, rules with
-// literal ids >= 32, NFA rules and first-hit tables (cfirst) stay with k_dfa
+// line's hit slots in registers (or, for rulesets with first-hit tables,
+// cfirst, from the line's first candidate of each literal).  Lead seeks past
+// overflowed slots, rules with literal ids >= 32 and NFA rules stay with k_dfa
 // (kJobLegacy).
 constexpr uint64_t kJobDecided = ~0ull;
 __device__ __forceinline__ uint64_t l2_job_rec(const Bind &B, uint32_t r, const CandMeta &cm, const uint64_t (&cv)[kCandSlots],
-                                               uint64_t rs, uint32_t rl, uint32_t rest_off) {
+                                               uint64_t rs, uint32_t rl, uint32_t rest_off, const uint64_t *cfirst) {
   // one 16 B load: Bind::jinfo[r] (a class entry naming another rule names one
   // with the same pattern, so its literals and flags are the line's own)
   const uint4 ji = B.jinfo[r];
@@ -233,8 +235,22 @@ __device__ __forceinline__ uint64_t l2_job_rec(const Bind &B, uint32_t r, const 
   const uint32_t skl = ji.z & 0xFFFFu;
   const uint32_t sk = skl && skl <= rl ? skl : 0u;
   uint32_t st0 = 0;
-  if (lead == 3u) {  // lead_start (lead & 1 gates it, lead & 3 == 3 runs it)
-    if (B.cfirst) return kJobLegacy;
+  if (lead == 3u && B.cfirst) {
+    // lead_start from the line's first candidate of each of the rule's
+    // literals (rulesets of <= kCandFirstLits literals: exact, overflow or not)
+    const uint32_t ld = fl >> 16, back = ld ? ld + 3u : 0u;
+    uint64_t f = ~0ull;
+    for (uint32_t m = lm; m; m &= m - 1) {
+      const uint64_t q = cfirst[(uint32_t)__ffs(m) - 1];
+      f = q < f ? q : f;
+    }
+    if (f == ~0ull) st0 = rl;  // none of its literals occurs: no match
+    else {
+      // a first candidate in the header still bounds the first one in rest from below
+      const uint32_t o = f <= rs ? 0u : (uint32_t)min<uint64_t>(f - rs, rl);
+      st0 = o > back ? o - back : 0u;
+    }
+  } else if (lead == 3u) {  // lead_start (lead & 1 gates it, lead & 3 == 3 runs it)
     const uint32_t ld = fl >> 16, back = ld ? ld + 3u : 0u;
     uint64_t f = ~0ull;
 #pragma unroll
@@ -285,12 +301,39 @@ __device__ __forceinline__ uint32_t l2_inline(const uint32_t *hl, uint32_t ent, 
   if (!(rec & kJobSkipState) && e.z == kL2NoStart) return 2;  // a table from the skip state only
   uint32_t st = (rec & kJobSkipState) ? e.w : e.z;
   uint32_t o = (uint32_t)((rec & kJobOffMask) - s);
-  const uint32_t lim = X.n < X.lim ? X.n : X.lim;
+  // at most kL2InlineSteps bytes from the job's start: a rule that decides
+  // near its literal does so within them; one scanning on (a .* after its
+  // literal, no match) stays a job instead of walking the line here
+  const uint32_t stop = min(X.n, o + kL2InlineSteps);
+  const uint32_t lim = min(stop, X.lim);
   for (; o < lim; ++o) {
     const uint32_t b = X.wp[o];
     if (b >= 0x80) return 2;
     st = tr[st * 128u + b];
     if (st <= 1) return st == kAccept ? 1u : 0u;
+  }
+  // past the window (a lead rule's job starts at its literal's first hit,
+  // often far into a long line): from HBM, 16 B aligned loads stepped from
+  // registers
+  const uint32_t end = stop;
+  while (o < end) {
+    const uint32_t al = (uint32_t)(reinterpret_cast<uintptr_t>(X.gp + o) & 15);
+    // the aligned 16 B are read whole only while they end at or before the
+    // line's '\n' (every line of a batch has one): no read past the batch
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (16 - al <= X.n + 1 - o) v = *reinterpret_cast<const uint4 *>(X.gp + o - al);
+    else {
+      uint32_t t[4] = {0, 0, 0, 0};
+      for (uint32_t k = al; k < 16 && o + (k - al) <= X.n; ++k) t[k >> 2] |= (uint32_t)X.gp[o + (k - al)] << (8 * (k & 3));
+      v = make_uint4(t[0], t[1], t[2], t[3]);
+    }
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (uint32_t k = al; k < 16 && o < end; ++k, ++o) {
+      const uint32_t b = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+      if (b >= 0x80) return 2;
+      st = tr[st * 128u + b];
+      if (st <= 1) return st == kAccept ? 1u : 0u;
+    }
   }
   if (o < X.n) return 2;
   return ae[st] ? 1u : 0u;
@@ -520,7 +563,8 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
               Jk &= Jk - 1;
               const uint32_t w = s_hl[prule + p];
               const uint32_t r = (w & kPlanOwn) ? first_rule + p : (w & 0xFFFFFu);
-              const uint64_t rec = l2_job_rec(B, r, cm, cv, rs, rest_len, rest_off);
+              const uint64_t rec = l2_job_rec(B, r, cm, cv, rs, rest_len, rest_off,
+                                              B.cfirst ? L.cand_first + j * kCandFirstLits : nullptr);
               uint32_t res = 2;
               if (rec == kJobDecided) res = 1;
               else if (pinl && !(rec & kJobLegacy)) {
