@@ -3320,6 +3320,177 @@ __global__ __launch_bounds__(kBlock) void k_apply(uint64_t n_ev, const uint32_t 
   }
 }
 
+// ---- Two-level grouping (round 5).  The global radix sort orders the events
+// by the state slot's high kBucketBits bits only (two onesweep passes instead of
+// four for a 2^28-slot table); each bucket of 2^L slots then goes to one block
+// (k_bucket_apply), which ranks its events by the slot's low L bits in LDS with
+// a stable block radix sort and runs Apply over each slot's events as k_apply
+// does.  A slot's events never leave its bucket, so no run crosses blocks (no
+// k_long_* pass).  Buckets of more than kBucketCap events (hot keys) are listed;
+// their events alone go through the full sort + k_apply + k_long_* path.
+// out_sorted stays indexed by the position in the (bucket-)sorted array, as
+// k_apply's is, so the trip and outcome kernels after it are unchanged.
+constexpr int kBucketBits = 16;
+constexpr uint32_t kBucketItems = 16;
+constexpr uint32_t kBucketCap = kBlock * kBucketItems;  // 4096 events
+
+// bstart[b] = first sorted position whose bucket (key >> L) is >= b, b <= nb
+__global__ __launch_bounds__(kBlock) void k_bucket_bounds(uint64_t n_ev, const uint32_t *__restrict__ key, uint32_t L,
+                                                          uint32_t nb, uint32_t *__restrict__ bstart) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n_ev) return;
+  const uint32_t b = i < n_ev ? key[i] >> L : nb;
+  const uint32_t lo = i ? (key[i - 1] >> L) + 1 : 0u;
+  for (uint32_t x = lo; x <= b; ++x) bstart[x] = (uint32_t)i;
+}
+
+// One bucket per block.  The low key bits are ranked by a stable block radix
+// sort of the bucket's (low bits, position) pairs; padding ranks take the
+// largest low key and come last (they sit after every real record in the
+// sort's input order, which it keeps for equal keys).  Run heads are compacted
+// in rank order and taken longest first, as in k_apply; a lane walks its run
+// through the rank -> position table, loading each record from the bucket's
+// few KB of HBM / L2, the next one in flight while the current one is applied.
+// (Gathering the records into LDS in rank order first, 16 independent loads
+// per thread, measured slower: 6.8 against 6.1 ms per cfg3 batch, at two blocks
+// per CU instead of four.)
+template <typename R>
+__global__ __launch_bounds__(kBlock) void k_bucket_apply(const uint32_t *__restrict__ key, const R *__restrict__ rec,
+                                                         const uint32_t *__restrict__ bstart, uint32_t L, int64_t tbase,
+                                                         const DevRule *__restrict__ rules, StSlot *__restrict__ st,
+                                                         uint8_t *__restrict__ out_sorted, uint32_t *__restrict__ big,
+                                                         unsigned long long *__restrict__ n_big) {
+  using Sort = hipcub::BlockRadixSort<uint32_t, kBlock, kBucketItems, uint16_t>;
+  constexpr uint32_t kLongRun = 8;
+  __shared__ union {
+    typename Sort::TempStorage sort;
+    uint32_t lk[kBucketCap];  // low key bits in position order (before the sort)
+    uint16_t ho[2 * kBucketCap];  // run heads in rank order, run order (after the sort)
+  } s_u;
+  __shared__ uint16_t s_lk[kBucketCap];    // low key bits in rank order
+  __shared__ uint16_t s_perm[kBucketCap];  // rank -> position
+  uint16_t *const s_head = s_u.ho;
+  uint16_t *const s_ord = s_u.ho + kBucketCap;  // run indices, long runs first
+  __shared__ uint8_t s_out[kBucketCap];                     // by position
+  __shared__ uint32_t s_wsum[kBlock / 64], s_front, s_back;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t bk = blockIdx.x, u0 = bstart[bk], n = bstart[bk + 1] - u0;
+  if (n == 0) return;
+  if (n > kBucketCap) {
+    if (tid == 0) big[atomicAdd(n_big, 1ull)] = bk;
+    return;
+  }
+  const uint32_t mask = (1u << L) - 1u;
+  for (uint32_t i = tid; i < n; i += kBlock) s_u.lk[i] = key[u0 + i] & mask;
+  if (tid == 0) { s_front = 0; s_back = 0; }
+  __syncthreads();
+  uint32_t k[kBucketItems];
+  uint16_t v[kBucketItems];
+#pragma unroll
+  for (uint32_t j = 0; j < kBucketItems; ++j) {
+    const uint32_t i = tid * kBucketItems + j;  // blocked: the sort is stable in this order
+    k[j] = i < n ? s_u.lk[i] : mask;
+    v[j] = (uint16_t)i;
+  }
+  __syncthreads();
+  Sort(s_u.sort).SortBlockedToStriped(k, v, 0, (int)L);
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < kBucketItems; ++j) {
+    const uint32_t r = j * kBlock + tid;
+    s_lk[r] = (uint16_t)k[j];
+    s_perm[r] = v[j];
+  }
+  __syncthreads();
+  // run heads, compacted in rank order (block scan of per-thread counts)
+  uint32_t fl = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kBucketItems; ++j) {
+    const uint32_t i = tid * kBucketItems + j;
+    if (i < n && (i == 0 || s_lk[i] != s_lk[i - 1])) fl |= 1u << j;
+  }
+  const uint32_t cnt = __popc(fl);
+  uint32_t x = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) s_wsum[wave] = x;
+  __syncthreads();
+  uint32_t base = x - cnt, nh = 0;
+  for (uint32_t w = 0; w < kBlock / 64; ++w) {
+    if (w < wave) base += s_wsum[w];
+    nh += s_wsum[w];
+  }
+  for (uint32_t j = 0; fl; ++j, fl >>= 1)
+    if (fl & 1) s_head[base++] = (uint16_t)(tid * kBucketItems + j);
+  __syncthreads();
+  for (uint32_t h = tid; h < nh; h += kBlock) {
+    const uint32_t len = (h + 1 < nh ? s_head[h + 1] : n) - s_head[h];
+    if (len >= kLongRun) s_ord[atomicAdd(&s_front, 1u)] = (uint16_t)h;
+    else s_ord[nh - 1 - atomicAdd(&s_back, 1u)] = (uint16_t)h;
+  }
+  __syncthreads();
+  const uint32_t qb = bk << L;
+  for (uint32_t t = tid; t < nh; t += kBlock) {
+    const uint32_t h = s_ord[t];
+    const uint32_t b = s_head[h], e = h + 1 < nh ? s_head[h + 1] : n;
+    const uint32_t q = qb | s_lk[b];
+    const StSlot cur = st[q];
+    bool valid = cur.valid != 0;
+    int64_t hits = cur.hits, start = cur.start, interval = 0, limit = 0;
+    uint32_t pr = 0xFFFFFFFFu;
+    uint32_t p = s_perm[b];
+    R rv = rec[u0 + p];
+    for (uint32_t u = b; u < e; ++u) {
+      R nx;
+      uint32_t pn = 0;
+      if (u + 1 < e) { pn = s_perm[u + 1]; nx = rec[u0 + pn]; }  // next record in flight while this one is applied
+      s_out[p] = apply_step(rv, tbase, rules, pr, interval, limit, valid, hits, start);
+      rv = nx;
+      p = pn;
+    }
+    st[q].hits = hits;
+    st[q].start = start;
+    st[q].valid = 1;
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += kBlock) out_sorted[u0 + i] = s_out[i];
+}
+
+// the events of the oversized buckets: keys and sorted positions; one thread
+// per event, its segment ({source position, events, destination}) by bisection
+__global__ __launch_bounds__(kBlock) void k_big_gather(const uint4 *__restrict__ seg, uint32_t n_seg, uint64_t total,
+                                                       const uint32_t *__restrict__ key, uint32_t *__restrict__ ko,
+                                                       uint32_t *__restrict__ po) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  uint32_t lo = 0, hi = n_seg - 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (seg[mid].z <= i) lo = mid;
+    else hi = mid - 1;
+  }
+  const uint4 s = seg[lo];
+  const uint32_t src = s.x + (uint32_t)(i - s.z);
+  ko[i] = key[src];
+  po[i] = src;
+}
+
+template <typename R>
+__global__ __launch_bounds__(kBlock) void k_big_recs(uint64_t n, const uint32_t *__restrict__ pos, const R *__restrict__ rec,
+                                                     R *__restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = rec[pos[i]];
+}
+
+__global__ __launch_bounds__(kBlock) void k_big_outs(uint64_t n, const uint32_t *__restrict__ pos, const uint8_t *__restrict__ o,
+                                                     uint8_t *__restrict__ out_sorted) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out_sorted[pos[i]] = o[i];
+}
+
 // One (ip, rule name) state whose sorted run crosses a k_apply chunk (hot
 // keys: a DDoS IP's run can hold a large share of the batch).
 // One block per run, from its head:
@@ -4530,6 +4701,15 @@ struct bjx_engine {
   DevBuf<int64_t> lr_t0, lr_h0;
   DevBuf<uint32_t> lr_flags, lr_nwin;
   DevBuf<unsigned long long> long_count;
+  // two-level grouping (k_bucket_apply): bucket bounds, oversized buckets, their events
+  DevBuf<uint32_t> bk_start, bk_big, bk_key, bk_pos;
+  DevBuf<unsigned long long> bk_nbig;
+  DevBuf<uint4> bk_seg;
+  DevBuf<EvRec> bk_rec;
+  DevBuf<uint8_t> bk_out;
+  uint64_t last_big_events = 0;
+  uint32_t sort2_hold = 0;
+  uint64_t last_grouping = 0;  // 0: full sort; else 1 + the events of oversized buckets (bjx_debug_scan_stats[10])  // batches left on the full sort after one with many hot-key events
   uint32_t scan_lds[2] = {0, 0};
   bool lines_attr = false;
   DevBuf<CandMeta> l_ccnt;
@@ -6187,6 +6367,8 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   e->rb_first.release(); e->rb_last.release(); e->long_heads.release(); e->long_count.release();
   e->lr_end.release(); e->lr_len.release(); e->lr_off.release(); e->lr_win.release(); e->lr_t0.release(); e->lr_h0.release();
   e->lr_flags.release(); e->lr_nwin.release(); e->chk.release();
+  for (auto *b : {&e->bk_start, &e->bk_big, &e->bk_key, &e->bk_pos}) b->release();
+  e->bk_nbig.release(); e->bk_seg.release(); e->bk_rec.release(); e->bk_out.release();
   e->d_results.release(); e->q_out.release();
   e->ban_ips.release(); e->ban_log.release(); e->ban_off.release(); e->ban_kind.release(); e->ban_ipb.release();
   e->ban_ipo.release();
@@ -6240,38 +6422,22 @@ static void mark(bjx_engine *e, int k) {
 // Phases 5 (IP + state slots), 6 (sort), 7 (automaton).
 // the event sort (state slot keys, records as values) and the Apply kernels,
 // for either record form
+// k_apply + k_long_* over n events sorted by their full state slot (key, rec),
+// outcomes to out in that order
 template <typename Rec>
-static void rl_sort_apply(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t n_ev, const uint32_t *ev_el,
-                          const uint32_t *ev_rule, int64_t base) {
+static uint64_t rl_apply_sorted(bjx_engine *e, const Bind &B, uint64_t n_ev, const uint32_t *key, const Rec *rec2,
+                                int64_t base, uint8_t *out, uint32_t *wcnt) {
   hipStream_t st = e->stream;
-  const Rec *rec2 = reinterpret_cast<const Rec *>(e->ev_rec2.p);
-  {
-    uint32_t *ki = e->ev_st.p, *ko = e->ev_st2.p;
-    Rec *vi = reinterpret_cast<Rec *>(e->ev_rec.p), *vo = reinterpret_cast<Rec *>(e->ev_rec2.p);
-    const int bits = std::max(1, bit_width(e->st_cap - 1));
-    cub_call(e, [&](void *tmp, size_t &bytes) {
-      return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)n_ev, 0, bits, st);
-    });
-  }
   const uint64_t n_chunks = (n_ev + kApplyChunk - 1) / kApplyChunk;
-  const bool check = getenv("BJX_CHECK") != nullptr;
-  uint32_t *wcnt = nullptr;
-  if (check) {
-    HIP_OK(hipMemsetAsync(e->ev_out_s.p, 0, n_ev, st));
-    e->chk_w.ensure(2 * n_ev);
-    wcnt = e->chk_w.p;
-    HIP_OK(hipMemsetAsync(wcnt, 0, 2 * n_ev * 4, st));
-  }
   e->long_heads.ensure(n_chunks + 1);
   e->long_count.ensure(1);
   HIP_OK(hipMemsetAsync(e->long_count.p, 0, 8, st));
-  hipLaunchKernelGGL(k_apply<Rec>, dim3((unsigned)n_chunks), dim3(kBlock), 0, st, n_ev, e->ev_st2.p, rec2, base, B.rules, e->S.st,
-                     e->ev_out_s.p, e->long_heads.p, e->long_count.p, wcnt);
+  hipLaunchKernelGGL(k_apply<Rec>, dim3((unsigned)n_chunks), dim3(kBlock), 0, st, n_ev, key, rec2, base, B.rules, e->S.st,
+                     out, e->long_heads.p, e->long_count.p, wcnt);
   HIP_OK(hipGetLastError());
   unsigned long long n_long = 0;
   HIP_OK(hipMemcpyAsync(&n_long, e->long_count.p, 8, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
-  e->last_long_runs = n_long;
   if (n_long) {
     // runs crossing a k_apply chunk (hot keys): ends, a parallel regularity
     // check, the window starts per run, then every record in parallel
@@ -6281,7 +6447,7 @@ static void rl_sort_apply(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t
     R.head = e->long_heads.p; R.end = e->lr_end.p; R.off = e->lr_off.p; R.t0 = e->lr_t0.p; R.h0 = e->lr_h0.p;
     R.flags = e->lr_flags.p; R.nwin = e->lr_nwin.p; R.n = n_long; R.win = nullptr; R.wcnt = wcnt;
     HIP_OK(hipMemsetAsync(e->lr_len.p + n_long, 0, 8, st));
-    hipLaunchKernelGGL(k_long_ends<Rec>, dim3((unsigned)n_long), dim3(kBlock), 0, st, n_ev, e->ev_st2.p, rec2, base, e->S.st,
+    hipLaunchKernelGGL(k_long_ends<Rec>, dim3((unsigned)n_long), dim3(kBlock), 0, st, n_ev, key, rec2, base, e->S.st,
                        B.rules, R, e->lr_len.p);
     HIP_OK(hipGetLastError());
     {
@@ -6294,11 +6460,117 @@ static void rl_sort_apply(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t
     e->lr_win.ensure(total + 1);
     R.win = e->lr_win.p;
     hipLaunchKernelGGL(k_long_check<Rec>, dim3(grid_for(total)), dim3(kBlock), 0, st, total, rec2, base, B.rules, R);
-    hipLaunchKernelGGL(k_long_windows<Rec>, dim3((unsigned)n_long), dim3(kBlock), 0, st, e->ev_st2.p, rec2, base, B.rules,
-                       e->S.st, e->ev_out_s.p, R);
-    hipLaunchKernelGGL(k_long_fill<Rec>, dim3(grid_for(total)), dim3(kBlock), 0, st, total, rec2, B.rules, e->ev_out_s.p, R);
+    hipLaunchKernelGGL(k_long_windows<Rec>, dim3((unsigned)n_long), dim3(kBlock), 0, st, key, rec2, base, B.rules,
+                       e->S.st, out, R);
+    hipLaunchKernelGGL(k_long_fill<Rec>, dim3(grid_for(total)), dim3(kBlock), 0, st, total, rec2, B.rules, out, R);
     HIP_OK(hipGetLastError());
   }
+  return n_long;
+}
+
+// RegexRateLimitStates.Apply for n_ev events (reference order) whose lines are
+// E; writes e->ev_out[k].  n_el / el_bytes bound the new IPs / arena bytes.
+// Phases 5 (IP + state slots), 6 (sort), 7 (automaton).
+// the event sort (state slot keys, records as values) and the Apply kernels,
+// for either record form
+template <typename Rec>
+static void rl_sort_apply(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t n_ev, const uint32_t *ev_el,
+                          const uint32_t *ev_rule, int64_t base) {
+  hipStream_t st = e->stream;
+  const Rec *rec2 = reinterpret_cast<const Rec *>(e->ev_rec2.p);
+  const bool check = getenv("BJX_CHECK") != nullptr;
+  const int bits = std::max(1, bit_width(e->st_cap - 1));
+  const int L = bits - kBucketBits;
+  // BJX_SORT2 (test / timing hook, read per batch): 0 the full sort always,
+  // 2 two-level whenever the table allows it (no batch-size gate, no hold)
+  const char *s2 = getenv("BJX_SORT2");
+  const int sort2 = s2 ? atoi(s2) : 1;
+  // two-level grouping (k_bucket_apply) unless the buckets would be too full on
+  // average (then most of them would take the full path anyway); BJX_CHECK's
+  // write accounting follows the full path
+  const uint32_t nb = 1u << kBucketBits;
+  // a batch whose oversized buckets held more than 1/32 of its events (a hot
+  // key) is followed by kSort2Hold batches on the full sort: the events of those
+  // buckets pay for a gather and a sort of their own on top of the two passes
+  constexpr uint32_t kSort2Hold = 32;
+  // small batches (fewer than 512 events per bucket on average) keep the full
+  // sort: 2^16 mostly empty blocks cost more than the two passes they save
+  // (cfg4, 2M lines: 0.6 -> 1.5 ms)
+  bool two = !check && sort2 != 0 && L > 0 && L <= 15 &&
+             (sort2 == 2 || (n_ev >= (uint64_t)nb * 512 && n_ev <= (uint64_t)nb * (kBucketCap * 3 / 4)));
+  if (two && sort2 != 2 && e->sort2_hold) {
+    --e->sort2_hold;
+    two = false;
+  }
+  {
+    uint32_t *ki = e->ev_st.p, *ko = e->ev_st2.p;
+    Rec *vi = reinterpret_cast<Rec *>(e->ev_rec.p), *vo = reinterpret_cast<Rec *>(e->ev_rec2.p);
+    const int lo = two ? L : 0;
+    cub_call(e, [&](void *tmp, size_t &bytes) {
+      return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, (int)n_ev, lo, bits, st);
+    });
+  }
+  uint32_t *wcnt = nullptr;
+  if (check) {
+    HIP_OK(hipMemsetAsync(e->ev_out_s.p, 0, n_ev, st));
+    e->chk_w.ensure(2 * n_ev);
+    wcnt = e->chk_w.p;
+    HIP_OK(hipMemsetAsync(wcnt, 0, 2 * n_ev * 4, st));
+  }
+  unsigned long long n_long = 0;
+  e->last_big_events = 0;
+  e->last_grouping = two ? 1 : 0;
+  if (!two) {
+    n_long = rl_apply_sorted<Rec>(e, B, n_ev, e->ev_st2.p, rec2, base, e->ev_out_s.p, wcnt);
+  } else {
+    e->bk_start.ensure(nb + 1); e->bk_big.ensure(nb); e->bk_nbig.ensure(1);
+    HIP_OK(hipMemsetAsync(e->bk_nbig.p, 0, 8, st));
+    hipLaunchKernelGGL(k_bucket_bounds, dim3(grid_for(n_ev + 1)), dim3(kBlock), 0, st, n_ev, e->ev_st2.p, (uint32_t)L, nb,
+                       e->bk_start.p);
+    hipLaunchKernelGGL(k_bucket_apply<Rec>, dim3(nb), dim3(kBlock), 0, st, e->ev_st2.p, rec2, e->bk_start.p, (uint32_t)L, base,
+                       B.rules, e->S.st, e->ev_out_s.p, e->bk_big.p, e->bk_nbig.p);
+    HIP_OK(hipGetLastError());
+    unsigned long long n_big = 0;
+    HIP_OK(hipMemcpyAsync(&n_big, e->bk_nbig.p, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (n_big) {
+      // oversized buckets (hot keys): their events, in bucket order, through
+      // the full sort and k_apply + k_long_*, outcomes back to their positions
+      std::vector<uint32_t> big(n_big), bs(nb + 1);
+      HIP_OK(hipMemcpyAsync(big.data(), e->bk_big.p, n_big * 4, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(bs.data(), e->bk_start.p, (nb + 1) * 4ull, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      std::sort(big.begin(), big.end());
+      std::vector<uint4> seg(n_big);
+      uint64_t total = 0;
+      for (size_t k = 0; k < n_big; ++k) {
+        const uint32_t b = big[k];
+        seg[k] = make_uint4(bs[b], bs[b + 1] - bs[b], (uint32_t)total, 0u);
+        total += bs[b + 1] - bs[b];
+      }
+      e->bk_seg.ensure(n_big); e->bk_key.ensure(2 * total); e->bk_pos.ensure(2 * total);
+      e->bk_rec.ensure(total); e->bk_out.ensure(total);
+      HIP_OK(hipMemcpyAsync(e->bk_seg.p, seg.data(), n_big * sizeof(uint4), hipMemcpyHostToDevice, st));
+      uint32_t *k0 = e->bk_key.p, *k1 = e->bk_key.p + total, *p0 = e->bk_pos.p, *p1 = e->bk_pos.p + total;
+      hipLaunchKernelGGL(k_big_gather, dim3(grid_for(total)), dim3(kBlock), 0, st, e->bk_seg.p, (uint32_t)n_big, total,
+                         e->ev_st2.p, k0, p0);
+      HIP_OK(hipGetLastError());
+      cub_call(e, [&](void *tmp, size_t &bytes) {
+        return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, k0, k1, p0, p1, (int)total, 0, bits, st);
+      });
+      Rec *r3 = reinterpret_cast<Rec *>(e->bk_rec.p);
+      hipLaunchKernelGGL(k_big_recs<Rec>, dim3(grid_for(total)), dim3(kBlock), 0, st, total, p1, rec2, r3);
+      HIP_OK(hipGetLastError());
+      n_long = rl_apply_sorted<Rec>(e, B, total, k1, r3, base, e->bk_out.p, nullptr);
+      hipLaunchKernelGGL(k_big_outs, dim3(grid_for(total)), dim3(kBlock), 0, st, total, p1, e->bk_out.p, e->ev_out_s.p);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipStreamSynchronize(st));  // seg (host memory) stays alive until its copy is done
+      e->last_big_events = total;
+      e->last_grouping = 1 + total;
+      if (total > n_ev / 32) e->sort2_hold = kSort2Hold;
+    }
+  }
+  e->last_long_runs = n_long;
   if (check) {
     e->chk.ensure(16);
     HIP_OK(hipMemsetAsync(e->chk.p, 0, 128, st));
@@ -7652,6 +7924,7 @@ extern "C" int bjx_state_clear(bjx_engine *e) {
   try {
     HIP_OK(hipSetDevice(e->device));
     HIP_OK(hipDeviceSynchronize());  // nothing of an earlier batch may land after the clear
+    e->sort2_hold = 0;
     HIP_OK(hipMemsetAsync(e->S.ip, 0, e->ip_cap * sizeof(IpSlot), e->stream));
     HIP_OK(hipMemsetAsync(e->S.ip_first, 0xFF, e->ip_cap * 4, e->stream));
     HIP_OK(hipMemsetAsync(e->S.st, 0, e->st_cap * sizeof(StSlot), e->stream));
@@ -7786,7 +8059,7 @@ extern "C" size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap)
   if (e->S.counters) read_counters(e);
   const uint64_t v[12] = {e->scan_stats[0], e->scan_stats[1], e->scan_stats[2], e->scan_stats[3], e->scan_stats[4],
                           e->ip_cap, e->host_counters[0], e->st_cap, e->host_counters[2], e->scan_stats[5],
-                          0, e->last_long_runs};
+                          e->last_grouping, e->last_long_runs};
   for (size_t k = 0; k < 12 && k < cap; ++k) out[k] = v[k];
   return 12;
 }

@@ -253,7 +253,7 @@ class Engine:
         _lib.lib().bjx_debug_scan_stats(self._h, out, 12)
         return {"pair_filter_hits": out[0], "literal_hits": out[1], "fallback_lines": out[2], "scan_image_bytes": out[3],
                 "dfa_jobs": out[4], "ip_table_slots": out[5], "ips": out[6], "state_table_slots": out[7], "states": out[8],
-                "gram_table_hits": out[9], "per_line_kernel_lines": out[10], "long_runs": out[11]}
+                "gram_table_hits": out[9], "grouping": out[10], "long_runs": out[11]}
 
     def state_stats(self):
         """Occupancy of the HBM rate-limit tables (bjx_state_stats_get)."""

@@ -39,9 +39,10 @@ size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap);
 size_t bjx_debug_kernel_ms(bjx_engine *e, double *out, size_t cap);
 /* last batch: gram bitset hits, recorded literal hits, lines sent to the per-line
    fallback, lines decided by the long-line pass, DFA jobs; then the state
-   tables: IP slots, IPs, state slots, states; then gram table hits, lines
-   the per-line kernel took from the scan-header path, rate-limit runs that
-   crossed a k_apply chunk (k_long_runs) (returns the count, 12) */
+   tables: IP slots, IPs, state slots, states; then gram table hits, the
+   rate-limit grouping (0: full sort by state slot; else two-level, 1 + the
+   events of its oversized buckets), rate-limit runs that crossed a k_apply
+   chunk (k_long_runs) (returns the count, 12) */
 size_t bjx_debug_scan_stats(bjx_engine *e, uint64_t *out, size_t cap);
 /* Test hook: IP hashes become (hash & mask) | 1 (0 = off), so distinct IPs
    share 64-bit hashes and the exact collision path of the IP table runs. */

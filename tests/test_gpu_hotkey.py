@@ -21,10 +21,13 @@ def engine():
     e.close()
 
 
-@pytest.mark.parametrize("slot_cache", [1, 0])
-def test_hot_key_workload(engine, slot_cache):
+@pytest.mark.parametrize("slot_cache,sort2", [(1, "1"), (0, "1"), (1, "2")])
+def test_hot_key_workload(engine, slot_cache, sort2, monkeypatch):
     """cfg5h shape (one IP sends 25% of the lines), oracle-sized, two batches;
-    with the state-slot cache of k_st_claim on and off (bit-exact both ways)."""
+    with the state-slot cache of k_st_claim on and off (bit-exact both ways),
+    and through the two-level grouping (BJX_SORT2=2: the hot IP's buckets
+    overflow and take the full sort on their own)."""
+    monkeypatch.setenv("BJX_SORT2", sort2)
     w = W.scaled(W.CFG5H, 160_000, n_ips=20_000)
     engine.debug_set_slot_cache(slot_cache)
     try:
@@ -77,8 +80,9 @@ def _hot_lines(t0_ms, n, step_ms=1, backwards_every=0, post_every=7):
     ("2", 37, "2", 5, 0),       # rules sharing the name with different limits: serial
     ("2", 37, "2", 37, 97),     # timestamps going backwards: serial
 ])
-@pytest.mark.parametrize("slot_cache", [1, 0])
-def test_hot_key_runs(engine, iv1, lim1, iv2, lim2, back, slot_cache):
+@pytest.mark.parametrize("slot_cache,sort2", [(1, "1"), (0, "1"), (1, "2")])
+def test_hot_key_runs(engine, iv1, lim1, iv2, lim2, back, slot_cache, sort2, monkeypatch):
+    monkeypatch.setenv("BJX_SORT2", sort2)
     engine.debug_set_slot_cache(slot_cache)
     try:
         engine.state_clear()

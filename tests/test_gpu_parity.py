@@ -861,3 +861,23 @@ def test_fallback_paths(switch, name, monkeypatch):
         assert eng.line_kernel()[0] == "k_lines"
     pair.compare_state([ln.split(b" ")[1].decode() for ln in w.host_lines(0, 50).split(b"\n")[:50] if ln])
     eng.close()
+
+
+@pytest.mark.parametrize("name,rec16", [("cfg3", 0), ("cfg5", 0), ("cfg1", 0), ("cfg3", 1)])
+def test_two_level_grouping(engine, name, rec16, monkeypatch):
+    """The rate-limit stage's two-level grouping (engine.hip k_bucket_apply:
+    the event sort on the state slot's high 16 bits, then each bucket ranked by
+    its low bits in LDS) forced on test-sized batches with BJX_SORT2=2, for both
+    record forms; cfg1's Zipf IPs overflow buckets, whose events take the full
+    sort on their own.  Bit-exact against the oracle's sequential Apply
+    (rate_limit.go:37-78) through state carried across the batches."""
+    monkeypatch.setenv("BJX_SORT2", "2")
+    if rec16:
+        monkeypatch.setenv("BJX_REC16", "1")
+    engine.state_clear()
+    w = W.scaled(W.ALL[name], 60_000, n_ips=3_000)
+    pair = Pair(w.rules_yaml, engine)
+    for b in range(3):
+        pair.feed(w.host_lines(b * 20_000, 20_000), w.now_ns(b * 20_000, 20_000))
+        assert engine.scan_stats()["grouping"] >= 1
+    pair.compare_state([ln.split(b" ")[1].decode() for ln in w.host_lines(0, 50).split(b"\n")[:50] if ln])
