@@ -6497,7 +6497,7 @@ static void rl_sort_apply(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t
   // sort: 2^16 mostly empty blocks cost more than the two passes they save
   // (cfg4, 2M lines: 0.6 -> 1.5 ms)
   bool two = !check && sort2 != 0 && L > 0 && L <= 15 &&
-             (sort2 == 2 || (n_ev >= (uint64_t)nb * 512 && n_ev <= (uint64_t)nb * (kBucketCap * 3 / 4)));
+             (sort2 == 2 || (n_ev >= (uint64_t)nb * 512 && n_ev <= (uint64_t)nb * (kBucketCap * 7 / 8)));
   if (two && sort2 != 2 && e->sort2_hold) {
     --e->sort2_hold;
     two = false;
