@@ -6489,9 +6489,11 @@ static void rl_sort_apply(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t
   // average (then most of them would take the full path anyway); BJX_CHECK's
   // write accounting follows the full path
   const uint32_t nb = 1u << kBucketBits;
-  // a batch whose oversized buckets held more than 1/32 of its events (a hot
+  // a batch whose oversized buckets held more than 1/8 of its events (a hot
   // key) is followed by kSort2Hold batches on the full sort: the events of those
   // buckets pay for a gather and a sort of their own on top of the two passes
+  // (cfg5h, 25 %: 16.6 ms against 10.0; the node rehearsal's owners, 8 %: 28.4
+  // against 30.6 ms for both engines)
   constexpr uint32_t kSort2Hold = 32;
   // small batches (fewer than 512 events per bucket on average) keep the full
   // sort: 2^16 mostly empty blocks cost more than the two passes they save
@@ -6567,7 +6569,7 @@ static void rl_sort_apply(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t
       HIP_OK(hipStreamSynchronize(st));  // seg (host memory) stays alive until its copy is done
       e->last_big_events = total;
       e->last_grouping = 1 + total;
-      if (total > n_ev / 32) e->sort2_hold = kSort2Hold;
+      if (total > n_ev / 8) e->sort2_hold = kSort2Hold;
     }
   }
   e->last_long_runs = n_long;
