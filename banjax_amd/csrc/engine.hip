@@ -3359,7 +3359,7 @@ __global__ __launch_bounds__(kBlock) void k_bucket_apply(const uint32_t *__restr
                                                          const uint32_t *__restrict__ bstart, uint32_t L, int64_t tbase,
                                                          const DevRule *__restrict__ rules, StSlot *__restrict__ st,
                                                          uint8_t *__restrict__ out_sorted, uint32_t *__restrict__ big,
-                                                         unsigned long long *__restrict__ n_big) {
+                                                         unsigned long long *__restrict__ n_big, uint32_t *__restrict__ wcnt) {
   using Sort = hipcub::BlockRadixSort<uint32_t, kBlock, kBucketItems, uint16_t>;
   constexpr uint32_t kLongRun = 8;
   __shared__ union {
@@ -3448,6 +3448,7 @@ __global__ __launch_bounds__(kBlock) void k_bucket_apply(const uint32_t *__restr
       uint32_t pn = 0;
       if (u + 1 < e) { pn = s_perm[u + 1]; nx = rec[u0 + pn]; }  // next record in flight while this one is applied
       s_out[p] = apply_step(rv, tbase, rules, pr, interval, limit, valid, hits, start);
+      if (wcnt) atomicAdd(&wcnt[u0 + p], 1u);  // BJX_CHECK: writes per sorted position
       rv = nx;
       p = pn;
     }
@@ -3485,10 +3486,16 @@ __global__ __launch_bounds__(kBlock) void k_big_recs(uint64_t n, const uint32_t 
   if (i < n) out[i] = rec[pos[i]];
 }
 
+// (BJX_CHECK: wsrc[i] = writes of o[i] by the full-sort apply, carried to the
+// sorted position it lands on, so a position counts exactly once only when its
+// outcome was written once there and copied once here)
 __global__ __launch_bounds__(kBlock) void k_big_outs(uint64_t n, const uint32_t *__restrict__ pos, const uint8_t *__restrict__ o,
-                                                     uint8_t *__restrict__ out_sorted) {
+                                                     uint8_t *__restrict__ out_sorted, const uint32_t *__restrict__ wsrc,
+                                                     uint32_t *__restrict__ wcnt) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out_sorted[pos[i]] = o[i];
+  if (i >= n) return;
+  out_sorted[pos[i]] = o[i];
+  if (wcnt) atomicAdd(&wcnt[pos[i]], wsrc[i]);
 }
 
 // One (ip, rule name) state whose sorted run crosses a k_apply chunk (hot
@@ -4364,6 +4371,13 @@ __global__ void k_map_trips(uint64_t n, const uint32_t *__restrict__ packed, uin
   }
 }
 
+// sorted event indices: count adjacent equal pairs (a trip list that names one
+// event twice)
+__global__ void k_count_dups(uint64_t n, const uint32_t *__restrict__ sorted, unsigned long long *__restrict__ dups) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (t < n && sorted[t] == sorted[t - 1]) atomicAdd(dups, 1ull);
+}
+
 __global__ void k_scatter_outcomes(uint64_t n, const uint32_t *__restrict__ src, const uint8_t *__restrict__ in,
                                    uint8_t *__restrict__ out) {
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -4698,6 +4712,7 @@ struct bjx_engine {
   DevBuf<uint32_t> wl_line, wl_rule, wl_pos;  // the per-line fallback's wide-NFA jobs
   uint32_t wide_max_w = 0, wide_max_g = 0, n_wide = 0;
   DevBuf<uint32_t> chk_w;  // BJX_CHECK: per-outcome write counts, event-index counts
+  DevBuf<uint32_t> chk_wb;  // BJX_CHECK: write counts of the oversized buckets' full-sort outcomes
   DevBuf<int64_t> lr_t0, lr_h0;
   DevBuf<uint32_t> lr_flags, lr_nwin;
   DevBuf<unsigned long long> long_count;
@@ -6366,7 +6381,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   e->bn_best.release(); e->bn_rep.release(); e->bn_sel.release(); e->bn_ipb.release(); e->tz_at.release(); e->tz_off.release();
   e->rb_first.release(); e->rb_last.release(); e->long_heads.release(); e->long_count.release();
   e->lr_end.release(); e->lr_len.release(); e->lr_off.release(); e->lr_win.release(); e->lr_t0.release(); e->lr_h0.release();
-  e->lr_flags.release(); e->lr_nwin.release(); e->chk.release();
+  e->lr_flags.release(); e->lr_nwin.release(); e->chk.release(); e->chk_w.release(); e->chk_wb.release();
   for (auto *b : {&e->bk_start, &e->bk_big, &e->bk_key, &e->bk_pos}) b->release();
   e->bk_nbig.release(); e->bk_seg.release(); e->bk_rec.release(); e->bk_out.release();
   e->d_results.release(); e->q_out.release();
@@ -6487,19 +6502,23 @@ static void rl_sort_apply(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t
   const int sort2 = s2 ? atoi(s2) : 1;
   // two-level grouping (k_bucket_apply) unless the buckets would be too full on
   // average (then most of them would take the full path anyway); BJX_CHECK's
-  // write accounting follows the full path
+  // write accounting covers both paths
   const uint32_t nb = 1u << kBucketBits;
   // a batch whose oversized buckets held more than 1/8 of its events (a hot
   // key) is followed by kSort2Hold batches on the full sort: the events of those
   // buckets pay for a gather and a sort of their own on top of the two passes
   // (cfg5h, 25 %: 16.6 ms against 10.0; the node rehearsal's owners, 8 %: 28.4
   // against 30.6 ms for both engines)
-  constexpr uint32_t kSort2Hold = 32;
+  // (BJX_SORT2_HOLD / BJX_SORT2_MIN: test hooks that shorten the hold and lower
+  // the batch-size gate, so test-sized batches exercise the default policy)
+  const char *hold_env = getenv("BJX_SORT2_HOLD"), *min_env = getenv("BJX_SORT2_MIN");
+  const uint32_t kSort2Hold = hold_env ? (uint32_t)atoi(hold_env) : 32u;
   // small batches (fewer than 512 events per bucket on average) keep the full
   // sort: 2^16 mostly empty blocks cost more than the two passes they save
   // (cfg4, 2M lines: 0.6 -> 1.5 ms)
-  bool two = !check && sort2 != 0 && L > 0 && L <= 15 &&
-             (sort2 == 2 || (n_ev >= (uint64_t)nb * 512 && n_ev <= (uint64_t)nb * (kBucketCap * 7 / 8)));
+  const uint64_t per_bucket_min = min_env ? (uint64_t)atoll(min_env) : 512ull;
+  bool two = sort2 != 0 && L > 0 && L <= 15 &&
+             (sort2 == 2 || (n_ev >= (uint64_t)nb * per_bucket_min && n_ev <= (uint64_t)nb * (kBucketCap * 7 / 8)));
   if (two && sort2 != 2 && e->sort2_hold) {
     --e->sort2_hold;
     two = false;
@@ -6530,7 +6549,7 @@ static void rl_sort_apply(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t
     hipLaunchKernelGGL(k_bucket_bounds, dim3(grid_for(n_ev + 1)), dim3(kBlock), 0, st, n_ev, e->ev_st2.p, (uint32_t)L, nb,
                        e->bk_start.p);
     hipLaunchKernelGGL(k_bucket_apply<Rec>, dim3(nb), dim3(kBlock), 0, st, e->ev_st2.p, rec2, e->bk_start.p, (uint32_t)L, base,
-                       B.rules, e->S.st, e->ev_out_s.p, e->bk_big.p, e->bk_nbig.p);
+                       B.rules, e->S.st, e->ev_out_s.p, e->bk_big.p, e->bk_nbig.p, wcnt);
     HIP_OK(hipGetLastError());
     unsigned long long n_big = 0;
     HIP_OK(hipMemcpyAsync(&n_big, e->bk_nbig.p, 8, hipMemcpyDeviceToHost, st));
@@ -6563,8 +6582,15 @@ static void rl_sort_apply(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t
       Rec *r3 = reinterpret_cast<Rec *>(e->bk_rec.p);
       hipLaunchKernelGGL(k_big_recs<Rec>, dim3(grid_for(total)), dim3(kBlock), 0, st, total, p1, rec2, r3);
       HIP_OK(hipGetLastError());
-      n_long = rl_apply_sorted<Rec>(e, B, total, k1, r3, base, e->bk_out.p, nullptr);
-      hipLaunchKernelGGL(k_big_outs, dim3(grid_for(total)), dim3(kBlock), 0, st, total, p1, e->bk_out.p, e->ev_out_s.p);
+      uint32_t *wbig = nullptr;
+      if (check) {
+        e->chk_wb.ensure(total);
+        wbig = e->chk_wb.p;
+        HIP_OK(hipMemsetAsync(wbig, 0, total * 4, st));
+      }
+      n_long = rl_apply_sorted<Rec>(e, B, total, k1, r3, base, e->bk_out.p, wbig);
+      hipLaunchKernelGGL(k_big_outs, dim3(grid_for(total)), dim3(kBlock), 0, st, total, p1, e->bk_out.p, e->ev_out_s.p, wbig,
+                         wcnt);
       HIP_OK(hipGetLastError());
       HIP_OK(hipStreamSynchronize(st));  // seg (host memory) stays alive until its copy is done
       e->last_big_events = total;
@@ -7355,6 +7381,17 @@ static uint64_t trip_events(bjx_engine *e, uint64_t n_ev, FinishFrom from, uint6
   cub_call(e, [&](void *tmp, size_t &bytes) {
     return hipcub::DeviceRadixSort::SortKeys(tmp, bytes, ki, ko, (int)n_trips, 0, bits, st);
   });
+  if (from == kFinList && n_trips > 1) {
+    // the owners' lists are sets of distinct events: a repeated index would
+    // duplicate a trip (and its ban count) silently
+    HIP_OK(hipMemsetAsync(e->scalars.p + 6, 0, 8, st));
+    hipLaunchKernelGGL(k_count_dups, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, ko, e->scalars.p + 6);
+    HIP_OK(hipGetLastError());
+    unsigned long long dups = 0;
+    HIP_OK(hipMemcpyAsync(&dups, e->scalars.p + 6, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (dups) throw BjxError(BJX_ERR_ARG, "bjx_finish_batch_trips: an event index appears more than once");
+  }
   return n_trips;
 }
 
@@ -7476,6 +7513,9 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, F
 
 static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes, size_t n, int64_t now_ns, uint32_t flags,
                       bjx_batch_result *out) {
+  // a standalone batch has no exchange: no node batch's figure carries over
+  e->exchange_ms = 0;
+  e->xev_rec = false;
   if (!match_phase(e, rs, bytes, n, now_ns, flags, out)) return;
   if (e->bc.n_ev) {
     rate_limit_stage(e, e->bind, local_evsrc(e), e->bc.n_el, e->bc.el_bytes, e->bc.n_ev, e->ev_el.p, e->ev_rule.p,
@@ -7523,6 +7563,8 @@ extern "C" int bjx_match_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8
   if (!rs || !out || (n && !bytes)) return BJX_ERR_ARG;
   return guarded(e, [&]() -> int {
     e->partitioned = false;
+    e->exchange_ms = 0;  // set by this batch's bjx_events_partition .. apply, if any
+    e->xev_rec = false;
     match_phase(e, rs, bytes, n, now_ns, flags, out);
     return BJX_OK;
   });

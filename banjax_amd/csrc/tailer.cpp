@@ -276,6 +276,12 @@ void reader_main(bjx_tailer *t) {
       // no complete line: keep the bytes, give the slot back
       carry.assign(s.host, s.host + n);
       carry_off = start_off;
+      // the parallel reads may have queued copies out of this slot's pinned
+      // bytes: they finish before the slot is refilled or freed
+      if (copied && hipStreamSynchronize(t->copy_stream) != hipSuccess) {
+        finish(t, BJX_ERR_DEVICE, "tailer host-to-device copy failed");
+        return;
+      }
       {
         std::lock_guard<std::mutex> g(t->mu);
         t->free_q.push_front(si);

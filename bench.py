@@ -148,14 +148,23 @@ def roofline(kms, nbytes, args, line_kernel=("k_lines2", 112)):
     return r
 
 
-def rank_plan(world, rank, local, node_engines, exchange, n_devices, n_lines):
+def rank_plan(world, rank, local, node_engines, exchange, n_devices, n_lines, gpus=1):
     """Which engines this rank drives and which lines each engine holds.
 
-    node mode (N>1 with --exchange node, or --node-engines > 1): rank 0 drives
-    every engine through one bjx_node, engine k on device k % n_devices holding
-    lines [k n_lines, (k + 1) n_lines); the other ranks drive nothing and only
-    join the barriers.  Otherwise each rank drives one engine on its local GPU
-    over lines [rank n_lines, (rank + 1) n_lines) (weak scaling)."""
+    node mode (N>1 with --exchange node, or --node-engines > 1, or a single
+    process started as `bench.py --gpus N` with N > 1 and no WORLD_SIZE): rank
+    0 drives every engine through one bjx_node, engine k on device k %
+    n_devices holding lines [k n_lines, (k + 1) n_lines); the other ranks drive
+    nothing and only join the barriers.  Otherwise each rank drives one engine
+    on its local GPU over lines [rank n_lines, (rank + 1) n_lines) (weak
+    scaling).  A single process asked for more GPUs than it sees fails (the
+    line would otherwise report fewer GPUs than were asked for)."""
+    if world == 1 and gpus > 1:
+        if n_devices < gpus:
+            raise SystemExit("bench.py --gpus %d: only %d device(s) visible" % (gpus, n_devices))
+        if node_engines and node_engines != gpus:
+            raise SystemExit("bench.py: --gpus %d and --node-engines %d disagree" % (gpus, node_engines))
+        node_engines = gpus
     node_mode = (world > 1 and exchange == "node") or node_engines > 1
     drives = not node_mode or rank == 0
     n_parts = world if world > 1 else max(1, node_engines)
@@ -246,7 +255,9 @@ def main():
     w0 = W.ALL[args.config]
     n_lines = args.lines or w0.n_lines
     w = W.scaled(w0, n_lines, n_ips=w0.n_ips) if args.lines else w0
-    P = rank_plan(world, rank, local, args.node_engines, args.exchange, torch.cuda.device_count(), n_lines)
+    if world > 1 and args.gpus not in (1, world):
+        raise SystemExit("bench.py --gpus %d under %d launched ranks" % (args.gpus, world))
+    P = rank_plan(world, rank, local, args.node_engines, args.exchange, torch.cuda.device_count(), n_lines, args.gpus)
     node_mode, drives, n_parts, devices = P["node_mode"], P["drives"], P["n_parts"], P["devices"]
     first = rank * n_lines
     chunks, keep = [], []

@@ -47,6 +47,27 @@ def test_rank_plan_rccl_and_single_process():
     assert not p["node_mode"] and p["chunks"] == [(0, 0, n)]
 
 
+def test_rank_plan_single_process_gpus8():
+    """`python3 bench.py --gpus 8` with no launcher (WORLD_SIZE unset): one
+    process drives 8 engines on 8 distinct devices through one bjx_node."""
+    n = 700
+    p = bench.rank_plan(1, 0, 0, 0, "node", 8, n, gpus=8)
+    assert p["node_mode"] and p["drives"] and p["n_parts"] == 8
+    assert p["devices"] == list(range(8)) and len(set(p["devices"])) == 8
+    assert p["chunks"] == [(k, k * n, n) for k in range(8)]
+    # --gpus 1 is the plain single-engine run
+    p = bench.rank_plan(1, 0, 0, 0, "node", 8, n, gpus=1)
+    assert not p["node_mode"] and p["chunks"] == [(0, 0, n)]
+    # fewer devices than asked for: refuse instead of timing fewer GPUs
+    with pytest.raises(SystemExit):
+        bench.rank_plan(1, 0, 0, 0, "node", 4, n, gpus=8)
+    with pytest.raises(SystemExit):
+        bench.rank_plan(1, 0, 0, 2, "node", 8, n, gpus=8)
+    # under a launcher every rank sees WORLD_SIZE and the node of rank 0 is unchanged
+    p = bench.rank_plan(8, 0, 0, 0, "node", 8, n, gpus=8)
+    assert p["devices"] == list(range(8)) and p["drives"]
+
+
 class _Counted:
     """torch.distributed with its collectives counted (in call order)."""
 

@@ -24,6 +24,15 @@ def test_library_exports_every_declared_symbol():
     assert L.bjx_abi_version() == 5
 
 
+def test_build_entry_abi_check_matches_header():
+    """__graft_entry__.build() ends with this check: the library's ABI against
+    the version include/banjax_gpu.h declares (round 5 left it asserting a
+    stale version for most of the round with no test noticing)."""
+    import __graft_entry__ as G
+    want = int(re.search(r"#define BJX_ABI_VERSION (\d+)", open(HEADER).read()).group(1))
+    assert G.check_abi() == want
+
+
 def test_regex_with_rate_unmarshal():
     """config_test.go:47-72 TestRegexWithRate."""
     cfg = Config.from_yaml("""

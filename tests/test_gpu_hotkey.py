@@ -109,3 +109,41 @@ def test_hot_key_reload_lowers_limit(engine):
     pair.lim.reload(pair.cfg)
     pair.feed(_hot_lines(t0 + 3_000, 20_000), (t0 + 3_000) * 1_000_000)
     pair.compare_state(["6.6.6.6"])
+
+
+def _spread_lines(t0_ms, n, n_ips=3000):
+    out = []
+    for k in range(n):
+        t = t0_ms + k
+        m = "POST" if k % 7 == 0 else "GET"
+        out.append("%d.%03d 10.%d.%d.%d %s h.com %s /x HTTP/1.1 ua" % (t // 1000, t % 1000, (k % n_ips) >> 16,
+                                                                   ((k % n_ips) >> 8) & 255, k % 256, m, m))
+    return ("\n".join(out) + "\n").encode()
+
+
+def test_two_level_hot_key_hold(engine, monkeypatch):
+    """The default grouping policy (no BJX_SORT2), with its batch-size gate
+    lowered (BJX_SORT2_MIN=0) and the hold shortened to 2 batches: a batch with
+    more than 1/8 of its events in oversized buckets runs two-level (those
+    buckets through the full sort), the next 2 batches keep the full sort
+    (grouping 0), and the one after returns to two-level grouping.  BJX_CHECK=1
+    verifies every sorted outcome is written exactly once on both paths
+    (k_bucket_apply, and k_apply + k_big_outs for the oversized buckets).
+    Bit-exact against the oracle throughout."""
+    monkeypatch.delenv("BJX_SORT2", raising=False)
+    monkeypatch.setenv("BJX_SORT2_MIN", "0")
+    monkeypatch.setenv("BJX_SORT2_HOLD", "2")
+    monkeypatch.setenv("BJX_CHECK", "1")
+    engine.state_clear()
+    pair = Pair(HOT_CFG % ("2", 37, "2", 37), engine)
+    t0 = 1700000000_000
+    out = pair.feed(_hot_lines(t0, 30_000), t0 * 1_000_000)
+    g = engine.scan_stats()["grouping"]
+    assert g - 1 > out.n_events // 8, (g, out.n_events)  # two-level, the hot buckets fully sorted
+    seen = []
+    for b in range(3):
+        t = t0 + 30_000 * (b + 1)
+        pair.feed(_spread_lines(t, 20_000), t * 1_000_000)
+        seen.append(engine.scan_stats()["grouping"])
+    assert seen[0] == 0 and seen[1] == 0 and seen[2] == 1, seen
+    pair.compare_state(["6.6.6.6", "7.7.7.1", "10.0.1.1"])

@@ -577,7 +577,13 @@ def test_partition_many_owners_one_engine(n_parts, trips_only):
                 acc += c[1]
             tr = torch.empty(max(1, te) * 4, dtype=torch.uint8, device=dev)
             cnt = eng.apply_events_trips(rs, lines.data_ptr(), events.data_ptr(), ipb.data_ptr(), send, base, tr.data_ptr())
-            out = eng.finish_trips(tr.data_ptr(), sum(cnt))
+            nt = sum(cnt)
+            if nt:
+                # a list naming one event twice is refused (it would duplicate a trip)
+                dup = torch.cat([tr[:nt * 4], tr[:4]])
+                with pytest.raises(RuntimeError, match="more than once"):
+                    eng.finish_trips(dup.data_ptr(), nt + 1)
+            out = eng.finish_trips(tr.data_ptr(), nt)
         else:
             o = torch.empty(max(1, te), dtype=torch.uint8, device=dev)
             eng.apply_events(rs, lines.data_ptr(), events.data_ptr(), ipb.data_ptr(), send, o.data_ptr())
@@ -863,15 +869,20 @@ def test_fallback_paths(switch, name, monkeypatch):
     eng.close()
 
 
-@pytest.mark.parametrize("name,rec16", [("cfg3", 0), ("cfg5", 0), ("cfg1", 0), ("cfg3", 1)])
-def test_two_level_grouping(engine, name, rec16, monkeypatch):
+@pytest.mark.parametrize("name,rec16,check", [("cfg3", 0, 0), ("cfg5", 0, 0), ("cfg1", 0, 0), ("cfg3", 1, 0), ("cfg1", 0, 1)])
+def test_two_level_grouping(engine, name, rec16, check, monkeypatch):
     """The rate-limit stage's two-level grouping (engine.hip k_bucket_apply:
     the event sort on the state slot's high 16 bits, then each bucket ranked by
     its low bits in LDS) forced on test-sized batches with BJX_SORT2=2, for both
     record forms; cfg1's Zipf IPs overflow buckets, whose events take the full
     sort on their own.  Bit-exact against the oracle's sequential Apply
-    (rate_limit.go:37-78) through state carried across the batches."""
+    (rate_limit.go:37-78) through state carried across the batches.  With
+    BJX_CHECK=1 the engine also verifies, per batch, that every bucket-sorted
+    outcome is written exactly once (k_bucket_apply, and k_apply + k_big_outs
+    for the overflowing buckets) and that the sorted records are a permutation."""
     monkeypatch.setenv("BJX_SORT2", "2")
+    if check:
+        monkeypatch.setenv("BJX_CHECK", "1")
     if rec16:
         monkeypatch.setenv("BJX_REC16", "1")
     engine.state_clear()

@@ -1,4 +1,4 @@
-"""Kernels of the last cold batch in a tools/r05_cold.sh trace (time order,
+"""Kernels of the last cold batch in a tools/sessions/r05_cold.sh trace (time order,
 kernels of at least 0.2 ms), and the total per kernel name over that batch.
 
     python tools/cold_summary.py gpurun_out/cold/cfg3

@@ -1,4 +1,4 @@
-"""Per-kernel PMC table for tools/r05_pmc_scan.sh output (last dispatch of each
+"""Per-kernel PMC table for tools/sessions/r05_pmc_scan.sh output (last dispatch of each
 kernel per pass: the second scan_stats batch, warm).
 
     python tools/pmc_scan_summary.py gpurun_out/pmc_<tag> [cfg3|cfg4 ...]
