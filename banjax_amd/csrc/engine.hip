@@ -149,6 +149,31 @@ __device__ __forceinline__ uint64_t hash_words(const uint32_t (&w)[NW], uint32_t
   }
   return hash_finish(a, b, t);
 }
+// hash_bytes of an IP of n <= 15 bytes from its inline key (ip_key16: the
+// bytes zero padded, the length in byte 15)
+__device__ __forceinline__ uint64_t key16_hash(const uint4 &k, uint32_t n) {
+  const uint32_t w[4] = {k.x, k.y, k.z, k.w & 0x00FFFFFFu};
+  return hash_words<4>(w, n);
+}
+// an IP's inline key and (past 15 bytes) its hash from word loads issued
+// together (p + n + 3 readable): no dependent byte loop
+__device__ __forceinline__ void ip_key_hash(const uint8_t *p, uint32_t n, uint4 &k16, uint64_t &h) {
+  if (n <= 15) {  // the key alone: the hash of so short an IP comes from it where it is needed (key16_hash)
+    uint32_t w[4];
+    ip_words(p, n, w);
+    k16 = make_uint4(w[0], w[1], w[2], w[3] | (n << 24));
+    h = 0;
+  } else if (n < 4 * kIpWords) {
+    uint32_t w[kIpWords];
+    ip_words(p, n, w);
+    h = hash_words(w, n);
+    const uint32_t m3 = n >= 15 ? 0x00FFFFFFu : n <= 12 ? 0u : (1u << (8 * (n - 12))) - 1u;
+    k16 = make_uint4(w[0], w[1], w[2], (w[3] & m3) | ((n < 255 ? n : 255u) << 24));
+  } else {
+    h = hash_bytes(p, n);
+    k16 = ip_key16(p, n);
+  }
+}
 __device__ __forceinline__ bool key16_eq(const uint4 &a, const uint4 &b) {
   return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
 }
@@ -437,11 +462,16 @@ __device__ void parse_and_match(const Bind &B, const uint8_t *__restrict__ p, ui
   double f;
   hid = host_lookup(B, p + host_off, host_len);
   exempt = B.any_allow && check_is_allowed(B, hid, p + ip_off, ip_len);
-  L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
-  L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
+  L.ip_len[j] = ip_len;
+  L.rest_off[j] = rest_off;
   L.host_id[j] = hid;
-  L.ip_hash[j] = hash_bytes(p + ip_off, ip_len);
-  L.ip16[j] = ip_key16(p + ip_off, ip_len);
+  {
+    uint4 k16;
+    uint64_t h;
+    ip_key_hash(p + ip_off, ip_len, k16, h);
+    if (ip_len > 15) L.ip_hash[j] = h;
+    L.ip16[j] = k16;
+  }
   if (!SLOW) {
     if (parse_float_fast(p, sp1, &f) != 0) {
       // rare: exotic timestamp token -> general ParseFloat kernel
@@ -741,7 +771,23 @@ __device__ __forceinline__ int32_t host_lookup_lds(const uint32_t *hl, const uin
   const uint2 *slots = reinterpret_cast<const uint2 *>(hl + 2);
   const uint32_t *offs = hl + 2 + 2 * cap;
   const uint8_t *bytes = reinterpret_cast<const uint8_t *>(hl + 2 + 2 * cap + nh);
-  const uint64_t hh = hash_bytes(h, n);
+  // a host of < 32 bytes (every usual one) as words in registers: its loads
+  // issued at once, hashed and compared from there (hash_bytes' loop waits on
+  // each word in turn)
+  constexpr uint32_t NW = 8;
+  uint32_t w[NW];
+#ifdef BJX_HOST_LOOP
+  const bool short_host = false;  // timing builds: the byte-loop lookup
+#else
+  const bool short_host = n < 4 * NW;
+#endif
+  uint64_t hh;
+  if (short_host) {
+    ip_words(h, n, w);
+    hh = hash_words(w, n);
+  } else {
+    hh = hash_bytes(h, n);
+  }
   const uint32_t tag = (uint32_t)(hh >> 32) | 1u;
   uint32_t s = (uint32_t)hh & (cap - 1);
   for (;;) {
@@ -750,9 +796,18 @@ __device__ __forceinline__ int32_t host_lookup_lds(const uint32_t *hl, const uin
     if (e.x == tag && (e.y & 0xFFFFu) == n) {
       const uint32_t hid = e.y >> 16;
       const uint8_t *q = bytes + offs[hid];
-      uint32_t diff = 0, i = 0;
-      for (; i + 4 <= n; i += 4) diff |= ld4(h + i) ^ ld4(q + i);
-      if (i < n) diff |= (ld4(h + i) ^ ld4(q + i)) & ((1u << (8 * (n - i))) - 1u);
+      uint32_t diff = 0;
+      if (short_host) {
+        // dictionary hosts are word aligned and zero padded to a whole word
+        const uint32_t *qw = reinterpret_cast<const uint32_t *>(q);
+#pragma unroll
+        for (uint32_t k = 0; k < NW; ++k)
+          if (4 * k < n) diff |= qw[k] ^ w[k];
+      } else {
+        uint32_t i = 0;
+        for (; i + 4 <= n; i += 4) diff |= ld4(h + i) ^ ld4(q + i);
+        if (i < n) diff |= (ld4(h + i) ^ ld4(q + i)) & ((1u << (8 * (n - i))) - 1u);
+      }
       if (!diff) return (int32_t)hid;
     }
     s = (s + 1) & (cap - 1);
@@ -1914,11 +1969,16 @@ __device__ __forceinline__ void line_body(const Bind &B, const Tabs &TB, const L
     }
     if (PROF) { __builtin_amdgcn_s_waitcnt(0); P.mark(4); }
     if (A.dbg & 64) return;  // timing experiment: no per-line stores
-    L.ip_off[j] = ip_off; L.ip_len[j] = ip_len;
-    L.rest_off[j] = rest_off; L.host_off[j] = host_off; L.host_len[j] = host_len;
+    L.ip_len[j] = ip_len;
+    L.rest_off[j] = rest_off;
     L.host_id[j] = hid;
-    L.ip_hash[j] = hash_bytes(p + ip_off, ip_len);
-    L.ip16[j] = ip_key16(p + ip_off, ip_len);
+    {
+      uint4 k16;
+      uint64_t h;
+      ip_key_hash(p + ip_off, ip_len, k16, h);
+      if (ip_len > 15) L.ip_hash[j] = h;
+      L.ip16[j] = k16;
+    }
     L.ts[j] = tsn;
     L.flags[j] = fl;
     if (PROF) { __builtin_amdgcn_s_waitcnt(0); P.mark(5); }
@@ -2827,7 +2887,13 @@ __global__ __launch_bounds__(kBlock) void k_emit(Bind B, uint64_t n_lines, Lines
 __device__ __forceinline__ uint64_t line_start(const uint64_t *nl, uint64_t line) { return line ? nl[line - 1] + 1 : 0; }
 
 __device__ __forceinline__ const uint8_t *ev_ip(const EvSrc &E, uint64_t i) {
-  return E.bytes + (E.nl ? line_start(E.nl, i) + E.ip_off[i] : E.ip_pos[i]);
+  return E.bytes + (E.nl ? line_start(E.nl, i) + E.rest_off[i] - E.ip_len[i] - 1 : E.ip_pos[i]);
+}
+// hash_bytes of event line i's IP: a local line's IP of <= 15 bytes from its
+// inline key (no hash is stored for it), else the stored hash
+__device__ __forceinline__ uint64_t ev_hash(const EvSrc &E, uint64_t i, const uint4 &k16, uint32_t len) {
+  const uint64_t h = E.nl && len <= 15 ? key16_hash(k16, len) : E.ip_hash[i];
+  return E.hmask ? (h & E.hmask) | 1ull : h;
 }
 __device__ __forceinline__ bool ev_has(const EvSrc &E, uint64_t i) {
   return !E.counts || (E.counts[i] & 0xFFFFFFFFull) != 0;
@@ -2868,13 +2934,13 @@ __device__ __forceinline__ void count_claims(const State &S, uint32_t which, uin
 __device__ __forceinline__ bool ip_claim_line(const EvSrc &E, const State &S, uint32_t epoch, uint64_t i,
                                               uint32_t *__restrict__ el_slot, uint32_t *__restrict__ el_id,
                                               uint64_t shard_budget) {
-  const uint64_t h = E.ip_hash[i];
   const uint32_t len = E.ip_len[i];
   const bool inl = len <= 15;
   // the inline key: the whole IP up to 15 bytes, else its first 15 bytes and
   // length (a slot whose key differs holds another IP; an equal one compares
   // the arena bytes)
   const uint4 k16 = E.ip16 ? E.ip16[i] : ip_key16_bytes(ev_ip(E, i), len);
+  const uint64_t h = ev_hash(E, i, k16, len);
   uint64_t s = h & S.ip_mask;
   bool claimed = false;
   for (;;) {
@@ -3097,9 +3163,10 @@ __global__ void k_ip_collide(EvSrc E, State S, uint32_t epoch, uint32_t *__restr
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   for (uint64_t c = 0; c < n_coll; ++c) {
     const uint32_t i = coll[c];
-    const uint64_t h = E.ip_hash[i];
     const uint32_t len = E.ip_len[i];
     const uint8_t *ip = ev_ip(E, i);
+    const uint4 k16 = E.ip16 ? E.ip16[i] : ip_key16_bytes(ip, len);
+    const uint64_t h = ev_hash(E, i, k16, len);
     uint64_t s = h & S.ip_mask;
     for (;;) {
       const uint64_t cur = S.ip[s].hash;
@@ -3113,7 +3180,7 @@ __global__ void k_ip_collide(EvSrc E, State S, uint32_t epoch, uint32_t *__restr
         S.ip[s].hash = h;
         S.ip[s].id = id;
         S.ip[s].born = epoch;
-        S.ip[s].key16 = E.ip16 ? E.ip16[i] : ip_key16_bytes(ip, len);
+        S.ip[s].key16 = k16;
         S.ip_first[s] = i;
         el_slot[i] = (uint32_t)s;
         el_id[i] = id | kFirstIp;
@@ -3767,11 +3834,6 @@ __global__ void k_check_most(uint64_t n, const uint32_t *__restrict__ cnt, uint3
   if (t < n && cnt[t] > most && atomicAdd(&chk[1], 1ull) == 0) chk[2] = t;
 }
 
-__global__ void k_dbg_mask_hash(uint64_t n, uint64_t *__restrict__ h, uint64_t mask) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) h[i] = (h[i] & mask) | 1;
-}
-
 // sorted outcomes -> event order (evw: the sorted records' event index words,
 // `stride` words apart: either record form)
 __global__ void k_unsort(uint64_t n, const uint32_t *__restrict__ evw, uint32_t stride, const uint8_t *__restrict__ in,
@@ -3848,9 +3910,12 @@ __global__ void k_flag_trips(uint64_t n, const uint8_t *__restrict__ ev_out, uin
   if (i < n) f[i] = (ev_out[i] & 8) ? 1 : 0;
 }
 
+// (the host field is found again in the line: the per-line pass stores no
+// host offsets, and only about 1 % of lines trip)
 __global__ void k_build_trips(uint64_t n_trips, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ ev_el,
-                              const uint32_t *__restrict__ ev_rule, const uint64_t *__restrict__ nl, Lines L,
-                              const DevRule *__restrict__ rules, bjx_trip *__restrict__ out) {
+                              const uint32_t *__restrict__ ev_rule, const uint8_t *__restrict__ buf,
+                              const uint64_t *__restrict__ nl, Lines L, const DevRule *__restrict__ rules,
+                              bjx_trip *__restrict__ out) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_trips) return;
   const uint32_t k = idx[t];
@@ -3861,11 +3926,13 @@ __global__ void k_build_trips(uint64_t n_trips, const uint32_t *__restrict__ idx
   tr.line_len = (uint32_t)(nl[line] - tr.line_offset);
   tr.rule_idx = ev_rule[k];
   tr.ts_ns = L.ts[line];
-  tr.ip_off = L.ip_off[line];
   tr.ip_len = L.ip_len[line];
-  tr.host_off = L.host_off[line];
-  tr.host_len = L.host_len[line];
   tr.rest_off = L.rest_off[line];
+  tr.ip_off = tr.rest_off - tr.ip_len - 1;
+  uint32_t sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
+  find_spaces(buf + tr.line_offset, tr.line_len, sp0, sp1, sp2, sp3);  // an event line has four
+  tr.host_off = sp2 + 1;
+  tr.host_len = sp3 - sp2 - 1;
   tr.decision = rules[tr.rule_idx].decision;
   out[t] = tr;
 }
@@ -4081,8 +4148,9 @@ __device__ __forceinline__ PartLine part_line(uint64_t j, uint64_t n_lines, cons
     r.ne = (uint32_t)(L.counts[j] & 0xFFFFFFFFull);
     if (r.ne) {
       r.ev = true;
-      r.o = (uint32_t)((L.ip_hash[j] >> 32) % n_parts);
       r.len = L.ip_len[j];
+      // the owner: a function of the IP bytes (hash_bytes), as every source computes it
+      r.o = (uint32_t)(((r.len <= 15 ? key16_hash(L.ip16[j], r.len) : L.ip_hash[j]) >> 32) % n_parts);
     }
   }
   return r;
@@ -4272,7 +4340,7 @@ __global__ __launch_bounds__(kBlock) void k_pack(PackArgs A) {
         for (uint32_t k = 0; k < 4; ++k)
           if (k < nw) dst[k] = kw[k];
       } else {
-        const uint8_t *ip = A.buf + line_start(A.nl, jj) + A.L.ip_off[jj];
+        const uint8_t *ip = A.buf + line_start(A.nl, jj) + A.L.rest_off[jj] - x.len - 1;
         if (x.len < 4 * kIpWords) {
           uint32_t iw[kIpWords];
           ip_words(ip, x.len, iw);
@@ -4698,7 +4766,7 @@ struct bjx_engine {
   DevBuf<uint64_t> tile_base, nl;
   DevBuf<int64_t> l_ts;
   DevBuf<uint64_t> l_iph, l_counts, l_offs, l_masks;
-  DevBuf<uint32_t> l_ipoff, l_iplen, l_hoff, l_hlen, l_roff, slow_list;
+  DevBuf<uint32_t> l_iplen, l_roff, slow_list;
   DevBuf<int32_t> l_hid;
   DevBuf<uint64_t> l_cand;
   DevBuf<uint4> l_ip16;
@@ -6362,8 +6430,8 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
                   &e->cub_tmp, &e->q_ip})
     b->release();
   e->tile_counts.release(); e->tile_base.release(); e->nl.release(); e->l_ts.release(); e->l_iph.release();
-  e->l_counts.release(); e->l_offs.release(); e->l_masks.release(); e->l_ipoff.release(); e->l_iplen.release();
-  e->l_hoff.release(); e->l_hlen.release(); e->l_roff.release(); e->slow_list.release(); e->l_hid.release();
+  e->l_counts.release(); e->l_offs.release(); e->l_masks.release(); e->l_iplen.release();
+  e->l_roff.release(); e->slow_list.release(); e->l_hid.release();
   e->scalars.release(); e->res_seq.release(); e->res_rule.release(); e->ev_el.release(); e->ev_rule.release();
 
   e->ev_res.release(); e->ev_st.release(); e->ev_st2.release(); e->ev_idx.release(); e->ev_idx2.release();
@@ -6883,13 +6951,13 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   e->nl.ensure(cap);
   e->l_ts.ensure(cap); e->l_iph.ensure(cap); e->l_counts.ensure(cap + 1); e->l_offs.ensure(cap + 1);
   e->l_masks.ensure(cap * B.mask_words);
-  e->l_ipoff.ensure(cap); e->l_iplen.ensure(cap); e->l_hoff.ensure(cap); e->l_hlen.ensure(cap);
+  e->l_iplen.ensure(cap);
   e->l_roff.ensure(cap); e->l_hid.ensure(cap); e->l_flags.ensure(cap); e->slow_list.ensure(cap);
   e->l_ccnt.ensure(cap); e->l_ip16.ensure(cap);
   e->l_cand.ensure(B.any_prefilter ? cap * kCandSlots : 1);
   e->scalars.ensure(16);
-  L.ts = e->l_ts.p; L.ip_hash = e->l_iph.p; L.ip_off = e->l_ipoff.p; L.ip_len = e->l_iplen.p; L.host_off = e->l_hoff.p;
-  L.host_len = e->l_hlen.p; L.rest_off = e->l_roff.p; L.host_id = e->l_hid.p; L.flags = e->l_flags.p;
+  L.ts = e->l_ts.p; L.ip_hash = e->l_iph.p; L.ip_len = e->l_iplen.p;
+  L.rest_off = e->l_roff.p; L.host_id = e->l_hid.p; L.flags = e->l_flags.p;
   L.counts = e->l_counts.p; L.masks = e->l_masks.p;
   L.cand_meta = e->l_ccnt.p; L.cand = e->l_cand.p; L.ip16 = e->l_ip16.p;
   L.cand_first = nullptr;
@@ -6990,9 +7058,26 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n_lines + kL2Block - 1) / kL2Block, resident));
       static const bool dbg_img = getenv("BJX_DEBUG_IMG") != nullptr;
       if (dbg_img) fprintf(stderr, "[bjx] k_lines2: %u B LDS per block (tables %u), %d blocks per CU, grid %u\n", lds, B.l2_bytes, per_cu, grid);
+#ifdef BJX_PROF_L2
+      e->chk.ensure(16);
+      HIP_OK(hipMemsetAsync(e->chk.p, 0, 128, st));
+      A.prof = e->chk.p;
+#endif
       if (B.l2_w == 2) hipLaunchKernelGGL(k_lines2<2>, dim3(grid), dim3(kL2Block), lds, st, B, A);
       else hipLaunchKernelGGL(k_lines2<1>, dim3(grid), dim3(kL2Block), lds, st, B, A);
       HIP_OK(hipGetLastError());
+#ifdef BJX_PROF_L2
+      {
+        unsigned long long c[8];
+        HIP_OK(hipMemcpyAsync(c, e->chk.p, 64, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        double tot = 0;
+        for (int k = 0; k < 8; ++k) tot += (double)c[k];
+        fprintf(stderr, "[bjx] k_lines2 segments (%% of wave clocks): loads %.1f header %.1f host+allow %.1f hits %.1f "
+                "anchored %.1f jobs %.1f stores %.1f flush %.1f\n", 100 * c[0] / tot, 100 * c[1] / tot, 100 * c[2] / tot,
+                100 * c[3] / tot, 100 * c[4] / tot, 100 * c[5] / tot, 100 * c[6] / tot, 100 * c[7] / tot);
+      }
+#endif
     } else {
       const bool img_lds = B.img_bytes <= kLinesImgMax;
       const bool host_lds = B.hl_bytes != 0;
@@ -7148,8 +7233,6 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       throw BjxError(BJX_ERR_DEVICE, msg);
     }
   }
-  if (e->dbg_hash_mask)
-    hipLaunchKernelGGL(k_dbg_mask_hash, dim3(grid_for(n_lines)), dim3(kBlock), 0, st, n_lines, L.ip_hash, e->dbg_hash_mask);
   mark(e, 3);
 
   // ---- RuleResults + events in reference order
@@ -7197,8 +7280,9 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
 static EvSrc local_evsrc(bjx_engine *e) {
   const BatchCtx &c = e->bc;
   EvSrc E;
-  E.bytes = c.buf; E.nl = e->nl.p; E.ip_off = c.L.ip_off; E.ip_pos = nullptr; E.ip_len = c.L.ip_len;
+  E.bytes = c.buf; E.nl = e->nl.p; E.rest_off = c.L.rest_off; E.ip_pos = nullptr; E.ip_len = c.L.ip_len;
   E.ip_hash = c.L.ip_hash; E.ts = c.L.ts; E.counts = c.L.counts; E.ip16 = c.L.ip16; E.n = c.n_lines;
+  E.hmask = e->dbg_hash_mask;
   return E;
 }
 
@@ -7415,7 +7499,7 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, F
     if (n_trips) {
       e->d_trips.ensure(n_trips);
       hipLaunchKernelGGL(k_build_trips, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, e->trip_ev2.p, e->ev_el.p,
-                         e->ev_rule.p, e->nl.p, L, B.rules, e->d_trips.p);
+                         e->ev_rule.p, c.buf, e->nl.p, L, B.rules, e->d_trips.p);
       HIP_OK(hipGetLastError());
       if (flags & BJX_TRIPS_COMPACT) {
         e->d_trips_c.ensure(n_trips);
@@ -7687,8 +7771,9 @@ static int apply_received(bjx_engine *e, const bjx_ruleset *rs, const bjx_event_
   HIP_OK(hipStreamSynchronize(st));
   if (chk[0] != n_ev || chk[1]) throw BjxError(BJX_ERR_ARG, "received event records are inconsistent");
   EvSrc E;
-  E.bytes = d_bytes; E.nl = nullptr; E.ip_off = nullptr; E.ip_pos = e->rx_pos.p; E.ip_len = e->rx_len.p;
+  E.bytes = d_bytes; E.nl = nullptr; E.rest_off = nullptr; E.ip_pos = e->rx_pos.p; E.ip_len = e->rx_len.p;
   E.ip_hash = e->rx_hash.p; E.ts = e->rx_ts.p; E.counts = nullptr; E.ip16 = e->rx_ip16.p; E.n = n_lines;
+  E.hmask = 0;  // k_unpack_lines applied the test mask
   // the clock of this engine's last match phase (the node's batch) as the
   // 12-B records' base; a stale or foreign one only costs the 16-B re-claim
   const bool timed = e->xev_rec;

@@ -234,10 +234,13 @@ struct CandMeta {
 };
 constexpr uint32_t kCertainGap = 256;
 
+// A line's IP is at line start + rest_off - ip_len - 1 (the field before rest);
+// its host field is re-derived from the line for the few lines that trip.
 struct Lines {
   int64_t *ts;
-  uint64_t *ip_hash;
-  uint32_t *ip_off, *ip_len, *host_off, *host_len, *rest_off;
+  uint64_t *ip_hash;   // hash_bytes of the IP, stored only for IPs longer than 15 bytes
+                       // (shorter ones: key16_hash of ip16, computed where it is needed)
+  uint32_t *ip_len, *rest_off;
   int32_t *host_id;
   uint8_t *flags;
   uint64_t *counts;    // (n_results << 32) | n_events per line, then scanned in place
@@ -342,15 +345,17 @@ struct EvRec12 {
 // Rate-limit input: the lines ("event lines") whose matched rules reach
 // RegexRateLimitStates.Apply, and the events themselves in reference order.
 // A local batch uses the line arrays directly (nl != nullptr: the IP is at
-// line start + ip_off); records exchanged between GPUs carry explicit IP
-// offsets into their own byte pool (nl == nullptr).
+// line start + rest_off - ip_len - 1, the hash of an IP of <= 15 bytes comes
+// from its inline key); records exchanged between GPUs carry explicit IP
+// offsets into their own byte pool and every hash (nl == nullptr).
 struct EvSrc {
   const uint8_t *bytes;
   const uint64_t *nl;
-  const uint32_t *ip_off;
+  const uint32_t *rest_off;
   const uint64_t *ip_pos;
   const uint32_t *ip_len;
   const uint64_t *ip_hash;
+  uint64_t hmask;          // test hook (forced 64-bit hash collisions): hashes become (h & hmask) | 1; 0 = off
   const int64_t *ts;
   const uint64_t *counts;  // local batch: low 32 bits = events of line i; nullptr: every record has events
   const uint4 *ip16;       // local batch: per-line key16 of the IP; nullptr: built from the bytes

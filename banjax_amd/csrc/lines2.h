@@ -31,6 +31,22 @@
 // test, a DFA job wherever that test leaves the rule open (k_dfa decides those
 // exactly, so a job for a rule also matched here is dropped, J & ~m).
 
+// BJX_PROF_L2 (timing builds only): wave clocks per segment of k_lines2 into
+// LinesArgs::prof: 0 window loads, 1 header + timestamp, 2 host lookup +
+// CheckIsAllowed, 3 literal hits, 4 anchored entries, 5 jobs + inline automata,
+// 6 per-line stores, 7 job flush
+#ifdef BJX_PROF_L2
+#define L2P(k)                       \
+  do {                               \
+    __builtin_amdgcn_s_waitcnt(0);   \
+    P.mark(k);                       \
+  } while (0)
+#else
+#define L2P(k) \
+  do {         \
+  } while (0)
+#endif
+
 constexpr uint32_t kL2Win = 112;  // bytes of each line's window (odd multiple of 16)
 constexpr int kL2Block = 512;     // 8 waves; two blocks per CU
 constexpr uint32_t kL2WaveLds = 64 * kL2Win + kWaveJobBytes;
@@ -306,6 +322,18 @@ __device__ __forceinline__ uint32_t l2_inline(const uint32_t *hl, uint32_t ent, 
   // literal, no match) stays a job instead of walking the line here
   const uint32_t stop = min(X.n, o + kL2InlineSteps);
   const uint32_t lim = min(stop, X.lim);
+  // in the window: four text bytes per LDS word load, so each step waits on
+  // its table load only
+  while (o + 4 <= lim) {
+    const uint32_t w = ld4(X.wp + o);
+    if (w & 0x80808080u) break;  // a non-ASCII byte ahead: stepped one by one below
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      st = tr[st * 128u + ((w >> (8 * k)) & 0xFFu)];
+      if (st <= 1) return st == kAccept ? 1u : 0u;
+    }
+    o += 4;
+  }
   for (; o < lim; ++o) {
     const uint32_t b = X.wp[o];
     if (b >= 0x80) return 2;
@@ -370,6 +398,10 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
   LT.pool = reinterpret_cast<const uint8_t *>(s_hl + B.lt_pool);
   const Lines &L = A.L;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+#ifdef BJX_PROF_L2
+  LinesProf P;
+  P.start();
+#endif
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + wave * 64u; base < A.n_lines; base += stride) {
     const uint64_t j = base + lane;
     const bool act = j < A.n_lines;
@@ -387,9 +419,24 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
     const uint32_t sk = (uint32_t)(s - a0);
     {
       uint4 v[kL2Win / 16];
+#ifdef BJX_L2_TLOAD
+      // the wave's 64 windows as 448 pieces of 16 B, piece g = 7 line + k at
+      // wbase + 16 g: in step k lane l loads piece 64 k + l, so consecutive
+      // lanes read consecutive 16 B of one line (about 9 lines, 18 cache lines
+      // per instruction instead of 64) and write one contiguous 1 KB of LDS.
+      // A line's window start comes from its lane (offset from lane 0's).
+      const uint64_t w0 = __shfl(a0, 0);
+      const uint32_t rel = (uint32_t)(a0 - w0);
+#pragma unroll
+      for (uint32_t k = 0; k < kL2Win / 16; ++k) {
+        const uint32_t g = 64u * k + lane;
+        const uint32_t ln = (g * 9363u) >> 16;  // g / 7 for g < 448
+        const uint64_t a = w0 + __shfl(rel, (int)ln) + 16ull * (g - 7u * ln);
+#else
 #pragma unroll
       for (uint32_t k = 0; k < kL2Win / 16; ++k) {
         const uint64_t a = a0 + 16ull * k;
+#endif
         if (a + 16 <= A.n) v[k] = *reinterpret_cast<const uint4 *>(A.buf + a);
         else {
           uint32_t w4[4];
@@ -417,9 +464,16 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
           cv[3] = w1.y;
         }
       }
+#ifdef BJX_L2_TLOAD
+#pragma unroll
+      for (uint32_t k = 0; k < kL2Win / 16; ++k) reinterpret_cast<uint4 *>(wbase)[64u * k + lane] = v[k];
+      wave_sync();  // every lane reads the window its neighbours wrote
+#else
 #pragma unroll
       for (uint32_t k = 0; k < kL2Win / 16; ++k) reinterpret_cast<uint4 *>(win)[k] = v[k];
+#endif
     }
+    L2P(0);
     if (act) {
       L2Line X;
       X.wp = win + sk;
@@ -431,6 +485,7 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
       double f = 0.0;
       bool slow = false;
       if (ns >= 4) slow = parse_ts_msec(X.wp, sp0, &f) != 0 && parse_float_fast(X.wp, sp0, &f) != 0;
+      L2P(1);
       if (ns < 4) {
         L.flags[j] = kLineError;
         L.counts[j] = 0;
@@ -451,6 +506,7 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
         const uint32_t first_rule = hid >= 0 ? LT.hinfo[hid].y : 0u;
         const uint32_t pinl = s_hl[dw + 10 * W + 4];  // the class's inline-DFA entries per position (0: none)
         const bool exempt = B.any_allow && check_is_allowed(B, hid, X.gp + ip_off, ip_len);
+        L2P(2);
         const int64_t tsn = ns_from_seconds(f);
         uint8_t fl = 0;
         if (go_sub(A.now_ns, tsn) > 10000000000LL) fl = kLineOld;
@@ -530,6 +586,7 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
           } else if (nlit) {
             l2_or(J, l2_ld_mask<W>(s_hl, dw + 4 * W));
           }
+          L2P(3);
           // anchored and no-literal entries of the class, each lane its own
           // class's list (a wave-uniform walk per class serialised the classes
           // of a wave's lines)
@@ -549,6 +606,7 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
             if (out == 1) l2_set(m, pos);
             else if (out == 2) l2_set(J, pos);
           }
+          L2P(4);
           const L2Mask<W> skp = l2_ld_mask<W>(s_hl, dw + 2 * W);
 #pragma unroll
           for (int k = 0; k < W; ++k) {
@@ -575,6 +633,7 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
               else if (res == 2) emit_job(S, j, r, p, rec | (((skp.w[k] >> (p & 63)) & 1) ? kJobNoCount : 0ull));
             }
           }
+          L2P(5);
           uint32_t n_m = 0, n_ev = 0;
 #pragma unroll
           for (int k = 0; k < W; ++k) {
@@ -587,28 +646,32 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
         }
         L.rest_off[j] = rest_off;
         L.host_id[j] = hid;
-        // the IP and host fields are read only for event lines (claims, node
-        // exchange, trips, bans): the others get ip_len 0 (k_ip_lookup skips
-        // them) and 36 B fewer stores
+        // the IP is read only for event lines (claims, node exchange, trips,
+        // bans): the others get ip_len 0 (the claims skip them).  An event
+        // line stores its IP's inline key; the IP's offset follows from
+        // rest_off and ip_len, its hash (for <= 15 bytes) from the key, and
+        // the host field is found again for the lines that trip
         L.ip_len[j] = evl ? ip_len : 0u;
         if (evl && !(A.dbg2 & 8)) {
-          L.ip_off[j] = ip_off;
-          L.host_off[j] = host_off;
-          L.host_len[j] = host_len;
-          if (l2_in(X, ip_off, ip_len > 16 ? ip_len : 16u)) {
-            L.ip_hash[j] = hash_bytes(X.wp + ip_off, ip_len);
-            L.ip16[j] = ip_key16(X.wp + ip_off, ip_len);
-          } else {
-            L.ip_hash[j] = hash_bytes(X.gp + ip_off, ip_len);
-            L.ip16[j] = ip_key16(X.gp + ip_off, ip_len);
-          }
+          uint4 k16;
+          uint64_t h;
+          if (l2_in(X, ip_off, ip_len > 16 ? ip_len : 16u)) ip_key_hash(X.wp + ip_off, ip_len, k16, h);
+          else ip_key_hash(X.gp + ip_off, ip_len, k16, h);
+          if (ip_len > 15) L.ip_hash[j] = h;
+          L.ip16[j] = k16;
         }
         L.ts[j] = tsn;
         L.flags[j] = fl;
       }
     }
+    L2P(6);
     // ---- append this wave's DFA jobs (from its chunk of the job array)
     flush_jobs(S, JC, lane);
+    L2P(7);
   }
   close_jobs(S, JC, lane, A.null_key, A.job_real);
+#ifdef BJX_PROF_L2
+  if (lane == 0 && A.prof)
+    for (int k = 0; k < 8; ++k) atomicAdd(&A.prof[k], (unsigned long long)P.acc[k]);
+#endif
 }
