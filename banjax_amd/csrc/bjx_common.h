@@ -92,6 +92,32 @@ BJX_HD uint64_t hash_bytes(const uint8_t *p, uint32_t n) {
   return hash_finish(a, b, t);
 }
 
+// The per-line pass's host dictionary hash (Bind::hl in LDS): word k of the
+// host (zero padded, little endian) rotated by 7 k + 3 and folded by xor, then
+// the length and a multiply / xorshift mix.  Two operations per word and no
+// multiply until the end, independent across words: the dictionary compares
+// every candidate in full, so this hash only has to spread the slots.  Never 0
+// (the empty-slot tag).
+BJX_HD uint32_t host_fold_word(uint32_t w, uint32_t k) {
+  const uint32_t r = (7u * k + 3u) & 31u;
+  return (w << r) | (w >> ((32u - r) & 31u));
+}
+BJX_HD uint32_t host_fold_finish(uint32_t a, uint32_t n) {
+  a ^= n * 0x9E3779B9u;
+  a ^= a >> 15; a *= 0x2C1B3C6Du; a ^= a >> 12; a *= 0x297A2D39u; a ^= a >> 15;
+  return a | 1u;
+}
+BJX_HD uint32_t host_fold(const uint8_t *p, uint32_t n) {
+  uint32_t a = 0, k = 0, i = 0;
+  for (; i + 4 <= n; i += 4, ++k) a ^= host_fold_word(ld4(p + i), k);
+  if (i < n) {
+    uint32_t t = 0;
+    for (uint32_t b = 0; i + b < n; ++b) t |= (uint32_t)p[i + b] << (8 * b);
+    a ^= host_fold_word(t, k);
+  }
+  return host_fold_finish(a, n);
+}
+
 // hash_bytes' last step: the tail word t (the 0-3 bytes after the last full
 // word, zero padded) and the finalizer
 BJX_HD uint64_t hash_finish(uint32_t a, uint32_t b, uint32_t t) {

@@ -772,24 +772,22 @@ __device__ __forceinline__ int32_t host_lookup_lds(const uint32_t *hl, const uin
   const uint32_t *offs = hl + 2 + 2 * cap;
   const uint8_t *bytes = reinterpret_cast<const uint8_t *>(hl + 2 + 2 * cap + nh);
   // a host of < 32 bytes (every usual one) as words in registers: its loads
-  // issued at once, hashed and compared from there (hash_bytes' loop waits on
-  // each word in turn)
+  // issued at once, hashed (host_fold: words zero past n, so all eight fold
+  // in) and compared from there
   constexpr uint32_t NW = 8;
   uint32_t w[NW];
-#ifdef BJX_HOST_LOOP
-  const bool short_host = false;  // timing builds: the byte-loop lookup
-#else
   const bool short_host = n < 4 * NW;
-#endif
-  uint64_t hh;
+  uint32_t tag;
   if (short_host) {
     ip_words(h, n, w);
-    hh = hash_words(w, n);
+    uint32_t a = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < NW; ++k) a ^= host_fold_word(w[k], k);
+    tag = host_fold_finish(a, n);
   } else {
-    hh = hash_bytes(h, n);
+    tag = host_fold(h, n);
   }
-  const uint32_t tag = (uint32_t)(hh >> 32) | 1u;
-  uint32_t s = (uint32_t)hh & (cap - 1);
+  uint32_t s = tag & (cap - 1);
   for (;;) {
     const uint2 e = slots[s];
     if (e.x == 0) return -1;
@@ -4512,8 +4510,12 @@ struct HostBuf {
   void resize(size_t want) {
     if (want > cap) {
       // geometric growth with headroom: a pinned (re)allocation stalls the
-      // batch for ~0.1 ms/MB, and per-batch counts (trips) drift upwards
-      const size_t c = std::max<size_t>({want * 2, cap * 2, 1u << 16});
+      // batch for ~0.1 ms/MB, and per-batch counts (trips) drift upwards.
+      // Past 64 MB the headroom is a quarter (cfg5's 40 GB of ban-log text
+      // would otherwise pin 80 GB)
+      const size_t big = (64u << 20) / sizeof(T);
+      const size_t c = want > big ? std::max<size_t>(want + want / 4, cap + cap / 4)
+                                  : std::max<size_t>({want * 2, cap * 2, 1u << 16});
       if (p) (void)hipHostFree(p);
       p = nullptr;
       cap = 0;
@@ -4759,6 +4761,13 @@ struct bjx_engine {
   uint32_t lines2_w = 0;       // ... and the instance (mask width) it was set on
   int dbg_slot_cache = -1;     // bjx_debug_set_slot_cache: -1 = BJX_SLOT_CACHE / default on, 0 off, 1 on
   uint64_t host_counters[3] = {0, 0, 0};
+  // small device -> host reads (counts, flags) through a pinned ring: a copy
+  // into pageable memory makes the host wait for it, so a few in a row cost a
+  // round trip (20-30 us) each; queued here they cost one stream sync
+  static constexpr uint32_t kPinBytes = 16384, kPinReads = 32;
+  uint8_t *pin = nullptr;
+  uint32_t pin_used = 0, pin_n = 0;
+  struct PinRead { void *dst; const uint8_t *slot; uint32_t n; } pin_q[kPinReads];
 
   // batch workspace
   DevBuf<uint8_t> staging;
@@ -5357,11 +5366,15 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
       hl.assign(words, 0);
       hl[0] = ht_cap;
       hl[1] = n_hosts;
-      for (uint32_t sl = 0; sl < ht_cap; ++sl)
-        if (hslot[sl].tag) {
-          hl[2 + 2 * sl] = hslot[sl].tag;
-          hl[2 + 2 * sl + 1] = ((uint32_t)hslot[sl].id << 16) | hslot[sl].len;
-        }
+      // slots by host_fold (the per-line pass's cheap dictionary hash)
+      for (uint32_t h = 0; h < n_hosts; ++h) {
+        const std::string &hs = host_by_id[h];
+        const uint32_t tg = host_fold(reinterpret_cast<const uint8_t *>(hs.data()), (uint32_t)hs.size());
+        uint32_t sl = tg & (ht_cap - 1);
+        while (hl[2 + 2 * sl]) sl = (sl + 1) & (ht_cap - 1);
+        hl[2 + 2 * sl] = tg;
+        hl[2 + 2 * sl + 1] = (h << 16) | (uint32_t)hs.size();
+      }
       uint8_t *by = reinterpret_cast<uint8_t *>(hl.data() + 2 + 2 * ht_cap + n_hosts);
       uint32_t o = 0;
       for (uint32_t h = 0; h < n_hosts; ++h) {
@@ -6294,9 +6307,27 @@ static const uint32_t *ev_words(const bjx_engine *e) {
 }
 static uint32_t rec_stride(const bjx_engine *e) { return e->rec12 ? 3u : 4u; }
 
-void read_counters(bjx_engine *e) {
-  HIP_OK(hipMemcpyAsync(e->host_counters, e->S.counters, 24, hipMemcpyDeviceToHost, e->stream));
+// Small device -> host reads: pin_get queues a copy into the engine's pinned
+// ring (the value lands in dst at the next pin_sync, which waits for the
+// stream once for every read queued)
+void pin_sync(bjx_engine *e) {
   HIP_OK(hipStreamSynchronize(e->stream));
+  for (uint32_t k = 0; k < e->pin_n; ++k) memcpy(e->pin_q[k].dst, e->pin_q[k].slot, e->pin_q[k].n);
+  e->pin_n = 0;
+  e->pin_used = 0;
+}
+void pin_get(bjx_engine *e, void *dst, const void *src, size_t n) {
+  if (n > bjx_engine::kPinBytes) throw BjxError(BJX_ERR_DEVICE, "internal: pinned read too large");
+  if (e->pin_n == bjx_engine::kPinReads || e->pin_used + n > bjx_engine::kPinBytes) pin_sync(e);
+  uint8_t *slot = e->pin + e->pin_used;
+  e->pin_used = (uint32_t)((e->pin_used + n + 15) & ~size_t(15));
+  HIP_OK(hipMemcpyAsync(slot, src, n, hipMemcpyDeviceToHost, e->stream));
+  e->pin_q[e->pin_n++] = {dst, slot, (uint32_t)n};
+}
+
+void read_counters(bjx_engine *e) {
+  pin_get(e, e->host_counters, e->S.counters, 24);
+  pin_sync(e);
 }
 
 // rehash the IP table into one that holds `want` IPs under a 3/4 load factor
@@ -6398,6 +6429,7 @@ extern "C" int bjx_engine_create(int device, const bjx_engine_options *opts, bjx
     e->device = device;
     HIP_OK(hipSetDevice(device));
     HIP_OK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&e->pin), bjx_engine::kPinBytes, hipHostMallocDefault));
     HIP_OK(hipEventCreate(&e->ev0));
     HIP_OK(hipEventCreate(&e->ev1));
     HIP_OK(hipEventCreate(&e->evm0));
@@ -6461,6 +6493,7 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   for (auto &x : e->ph) (void)hipEventDestroy(x);
   for (auto &x : e->xev) (void)hipEventDestroy(x);
   (void)hipStreamDestroy(e->stream);
+  if (e->pin) (void)hipHostFree(e->pin);
   delete e;
 }
 
@@ -6519,8 +6552,8 @@ static uint64_t rl_apply_sorted(bjx_engine *e, const Bind &B, uint64_t n_ev, con
                      out, e->long_heads.p, e->long_count.p, wcnt);
   HIP_OK(hipGetLastError());
   unsigned long long n_long = 0;
-  HIP_OK(hipMemcpyAsync(&n_long, e->long_count.p, 8, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
+  pin_get(e, &n_long, e->long_count.p, 8);
+  pin_sync(e);
   if (n_long) {
     // runs crossing a k_apply chunk (hot keys): ends, a parallel regularity
     // check, the window starts per run, then every record in parallel
@@ -6538,8 +6571,8 @@ static uint64_t rl_apply_sorted(bjx_engine *e, const Bind &B, uint64_t n_ev, con
       cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, o, (int)(n_long + 1), st); });
     }
     uint64_t total = 0;
-    HIP_OK(hipMemcpyAsync(&total, e->lr_off.p + n_long, 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    pin_get(e, &total, e->lr_off.p + n_long, 8);
+    pin_sync(e);
     e->lr_win.ensure(total + 1);
     R.win = e->lr_win.p;
     hipLaunchKernelGGL(k_long_check<Rec>, dim3(grid_for(total)), dim3(kBlock), 0, st, total, rec2, base, B.rules, R);
@@ -6620,8 +6653,8 @@ static void rl_sort_apply(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t
                        B.rules, e->S.st, e->ev_out_s.p, e->bk_big.p, e->bk_nbig.p, wcnt);
     HIP_OK(hipGetLastError());
     unsigned long long n_big = 0;
-    HIP_OK(hipMemcpyAsync(&n_big, e->bk_nbig.p, 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    pin_get(e, &n_big, e->bk_nbig.p, 8);
+    pin_sync(e);
     if (n_big) {
       // oversized buckets (hot keys): their events, in bucket order, through
       // the full sort and k_apply + k_long_*, outcomes back to their positions
@@ -6677,8 +6710,8 @@ static void rl_sort_apply(bjx_engine *e, const Bind &B, const EvSrc &E, uint64_t
                        e->el_slot.p, e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_out_s.p, wcnt, pc, e->chk.p);
     HIP_OK(hipGetLastError());
     unsigned long long c[16];
-    HIP_OK(hipMemcpyAsync(c, e->chk.p, 128, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    pin_get(e, c, e->chk.p, 128);
+    pin_sync(e);
     if (c[0] || c[3] || c[6] || c[8] || c[10] || c[12] || c[14]) {
       char msg[768];
       snprintf(msg, sizeof msg,
@@ -6735,8 +6768,8 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
                          budget / kClaimShards);
       hipLaunchKernelGGL(k_fold_new, dim3(1), dim3(kClaimShards), 0, st, e->S);
       HIP_OK(hipGetLastError());
-      HIP_OK(hipMemcpyAsync(nw_ovf, e->S.counters + 4, 16, hipMemcpyDeviceToHost, st));
-      HIP_OK(hipStreamSynchronize(st));
+      pin_get(e, nw_ovf, e->S.counters + 4, 16);
+      pin_sync(e);
       if (!nw_ovf[1]) break;
       // more new IPs than the table had room for: undo, grow, claim again
       hipLaunchKernelGGL(k_ip_rollback, dim3(grid_for(e->ip_cap)), dim3(kBlock), 0, st, e->ip_cap, e->S, epoch);
@@ -6758,8 +6791,8 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
       HIP_OK(hipGetLastError());
     }
     uint64_t n_coll = 0;
-    HIP_OK(hipMemcpyAsync(&n_coll, e->S.counters + 3, 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    pin_get(e, &n_coll, e->S.counters + 3, 8);
+    pin_sync(e);
     if (n_coll) {  // distinct IPs with one 64-bit hash in this batch: resolve exactly, in line order
       if (n_coll > 1) {
         uint32_t *ki = e->coll.p, *ko = e->ev_st2.p;
@@ -6788,8 +6821,8 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
                            e->el_slot.p, e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_rec.p, rec_base, budget / kClaimShards);
       HIP_OK(hipGetLastError());
       uint64_t ovf[2] = {0, 0};  // state table overflow, a timestamp outside the 12-B records' span
-      HIP_OK(hipMemcpyAsync(ovf, e->S.counters + 7, 16, hipMemcpyDeviceToHost, st));
-      HIP_OK(hipStreamSynchronize(st));
+      pin_get(e, ovf, e->S.counters + 7, 16);
+      pin_sync(e);
       if (!ovf[0]) {
         hipLaunchKernelGGL(k_fold_claims, dim3(1), dim3(kClaimShards), 0, st, e->S);
         HIP_OK(hipGetLastError());
@@ -6938,9 +6971,9 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   {
     uint64_t last_base = 0;
     uint32_t last_cnt = 0;
-    HIP_OK(hipMemcpyAsync(&last_base, e->tile_base.p + (n_tiles - 1), 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(&last_cnt, e->tile_counts.p + (n_tiles - 1), 4, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    pin_get(e, &last_base, e->tile_base.p + (n_tiles - 1), 8);
+    pin_get(e, &last_cnt, e->tile_counts.p + (n_tiles - 1), 4);
+    pin_sync(e);
     n_lines = last_base + last_cnt;
   }
   out->n_lines = n_lines;
@@ -7069,8 +7102,8 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
 #ifdef BJX_PROF_L2
       {
         unsigned long long c[8];
-        HIP_OK(hipMemcpyAsync(c, e->chk.p, 64, hipMemcpyDeviceToHost, st));
-        HIP_OK(hipStreamSynchronize(st));
+        pin_get(e, c, e->chk.p, 64);
+        pin_sync(e);
         double tot = 0;
         for (int k = 0; k < 8; ++k) tot += (double)c[k];
         fprintf(stderr, "[bjx] k_lines2 segments (%% of wave clocks): loads %.1f header %.1f host+allow %.1f hits %.1f "
@@ -7111,8 +7144,8 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
         else if (host_lds) hipLaunchKernelGGL((k_lines<false, true, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
         else hipLaunchKernelGGL((k_lines<false, true>), dim3(grid), dim3(kBlock), lds, st, B, A);
         unsigned long long c[10];
-        HIP_OK(hipMemcpyAsync(c, e->chk.p, 80, hipMemcpyDeviceToHost, st));
-        HIP_OK(hipStreamSynchronize(st));
+        pin_get(e, c, e->chk.p, 80);
+        pin_sync(e);
         double tot = 0;
         for (int k = 0; k < 10; ++k) tot += (double)c[k];
         fprintf(stderr, "[bjx] k_lines segments (%% of wave clocks): loads+staging %.1f header %.1f host %.1f host-rules %.1f "
@@ -7127,10 +7160,10 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       HIP_OK(hipGetLastError());
     }
     HIP_OK(hipEventRecord(e->evk[1], st));
-    HIP_OK(hipMemcpyAsync(&last_nl, e->nl.p + (n_lines - 1), 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(sc4, e->scalars.p + 8, 32, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(sc4 + 4, e->scalars.p, 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    pin_get(e, &last_nl, e->nl.p + (n_lines - 1), 8);
+    pin_get(e, sc4, e->scalars.p + 8, 32);
+    pin_get(e, sc4 + 4, e->scalars.p, 8);
+    pin_sync(e);
     if (sc4[3] <= std::min(std::min(e->jline.n, e->jkey.n), std::min(e->jidx.n, e->jrec.n))) break;
     // more DFA jobs than the buffer holds: grow it and redo the (idempotent) line pass
     if (attempt > 0) throw BjxError(BJX_ERR_DEVICE, "internal: DFA job buffer overflow");
@@ -7145,8 +7178,8 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   out->consumed_bytes = last_nl + 1;
   // job slots taken (sc4[3]; the chunks' unused ones hold null jobs) and real jobs
   unsigned long long n_jobs = 0;
-  HIP_OK(hipMemcpyAsync(&n_jobs, e->scalars.p + 14, 8, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
+  pin_get(e, &n_jobs, e->scalars.p + 14, 8);
+  pin_sync(e);
   const unsigned long long n_slow = sc4[4], n_slots = sc4[3];
   e->last_jobs = n_jobs;
   e->scan_stats[0] = sc4[0]; e->scan_stats[1] = sc4[1]; e->scan_stats[2] = n_slow; e->scan_stats[3] = B.scan_img_bytes;
@@ -7211,8 +7244,8 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     HIP_OK(hipGetLastError());
     if (B.any_wide) {
       unsigned long long n_wl = 0;
-      HIP_OK(hipMemcpyAsync(&n_wl, e->scalars.p + 13, 8, hipMemcpyDeviceToHost, st));
-      HIP_OK(hipStreamSynchronize(st));
+      pin_get(e, &n_wl, e->scalars.p + 13, 8);
+      pin_sync(e);
       if (n_wl > WL.cap) throw BjxError(BJX_ERR_DEVICE, "internal: wide-NFA job list overflow");
       if (n_wl) launch_wide(e, B, buf, n, e->wl_rule.p, nullptr, e->wl_line.p, e->wl_pos.p, 0, n_wl, L, e->wide_max_w, e->wide_max_g);
     }
@@ -7224,8 +7257,8 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     hipLaunchKernelGGL(k_check_masks, dim3(grid_for(n_lines)), dim3(kBlock), 0, st, n_lines, L, B.mask_words, e->chk.p);
     HIP_OK(hipGetLastError());
     unsigned long long c[2];
-    HIP_OK(hipMemcpyAsync(c, e->chk.p, 16, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    pin_get(e, c, e->chk.p, 16);
+    pin_sync(e);
     if (c[0]) {
       char msg[160];
       snprintf(msg, sizeof msg, "BJX_CHECK: %llu lines whose RuleResult count differs from their match mask (first %llu)", c[0],
@@ -7244,8 +7277,8 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     });
   }
   uint64_t tot = 0;
-  HIP_OK(hipMemcpyAsync(&tot, e->l_offs.p + n_lines, 8, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
+  pin_get(e, &tot, e->l_offs.p + n_lines, 8);
+  pin_sync(e);
   const uint64_t n_res = tot >> 32, n_ev = tot & 0xFFFFFFFFull;
   out->n_results = n_res;
   out->n_events = n_ev;
@@ -7265,8 +7298,8 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   mark(e, 4);
   unsigned long long bnd[2] = {0, 0};
   if (n_ev) {
-    HIP_OK(hipMemcpyAsync(bnd, e->scalars.p + 1, 16, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    pin_get(e, bnd, e->scalars.p + 1, 16);
+    pin_sync(e);
   }
   BatchCtx &c = e->bc;
   c.buf = buf; c.n_lines = n_lines; c.n_res = n_res; c.n_ev = n_ev; c.L = L; c.n_el = bnd[0]; c.el_bytes = bnd[1];
@@ -7375,8 +7408,8 @@ static void emit_bans(bjx_engine *e, uint64_t n, bool records_only) {
     cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceScan::InclusiveSum(tmp, bytes, in, o, (int)n, st); });
   }
   uint32_t n_seg = 0;
-  HIP_OK(hipMemcpyAsync(&n_seg, e->bn_seg.p + (n - 1), 4, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
+  pin_get(e, &n_seg, e->bn_seg.p + (n - 1), 4);
+  pin_sync(e);
   const uint64_t log_bytes = e->ban_off.data()[n];
   e->ban_log.resize(log_bytes);
   if (log_bytes) {
@@ -7407,8 +7440,8 @@ static void emit_bans(bjx_engine *e, uint64_t n, bool records_only) {
     cub_call(e, [&](void *tmp, size_t &bytes) { return hipcub::DeviceSelect::Flagged(tmp, bytes, in, fl, o, cnt, (int)n, st); });
   }
   unsigned long long n_ips = 0;
-  HIP_OK(hipMemcpyAsync(&n_ips, e->scalars.p + 5, 8, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
+  pin_get(e, &n_ips, e->scalars.p + 5, 8);
+  pin_sync(e);
   e->ban_ips.resize(n_ips);
   e->ban_ipo.resize(n_ips + 1);
   e->ban_ipo.data()[0] = 0;
@@ -7451,8 +7484,8 @@ static uint64_t trip_events(bjx_engine *e, uint64_t n_ev, FinishFrom from, uint6
                        from == kFinSorted ? e->ev_out_s.p : e->ev_out.p, e->trip_idx.p, e->scalars.p + 4);
     HIP_OK(hipGetLastError());
     unsigned long long nt = 0;
-    HIP_OK(hipMemcpyAsync(&nt, e->scalars.p + 4, 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    pin_get(e, &nt, e->scalars.p + 4, 8);
+    pin_sync(e);
     n_trips = nt;
   }
   if (!n_trips) return 0;
@@ -7472,8 +7505,8 @@ static uint64_t trip_events(bjx_engine *e, uint64_t n_ev, FinishFrom from, uint6
     hipLaunchKernelGGL(k_count_dups, dim3(grid_for(n_trips)), dim3(kBlock), 0, st, n_trips, ko, e->scalars.p + 6);
     HIP_OK(hipGetLastError());
     unsigned long long dups = 0;
-    HIP_OK(hipMemcpyAsync(&dups, e->scalars.p + 6, 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    pin_get(e, &dups, e->scalars.p + 6, 8);
+    pin_sync(e);
     if (dups) throw BjxError(BJX_ERR_ARG, "bjx_finish_batch_trips: an event index appears more than once");
   }
   return n_trips;
@@ -7540,8 +7573,8 @@ static void finish_phase(bjx_engine *e, uint32_t flags, bjx_batch_result *out, F
         hipLaunchKernelGGL(k_check_most, dim3(grid_for(n_res)), dim3(kBlock), 0, st, n_res, e->chk_w.p, 1u, e->chk.p);
         HIP_OK(hipGetLastError());
         unsigned long long c[3];
-        HIP_OK(hipMemcpyAsync(c, e->chk.p, 24, hipMemcpyDeviceToHost, st));
-        HIP_OK(hipStreamSynchronize(st));
+        pin_get(e, c, e->chk.p, 24);
+        pin_sync(e);
         if (c[0] || c[1]) {
           char msg[256];
           snprintf(msg, sizeof msg, "BJX_CHECK: %llu event result indices out of range, %llu RuleResults named by more than "
@@ -7688,10 +7721,10 @@ extern "C" int bjx_events_partition(bjx_engine *e, uint32_t n_parts, uint64_t *c
     }
     hipLaunchKernelGGL(k_part_counts, dim3(1), dim3(64), 0, st, n_parts, n_tiles, e->pk_off.p, e->pk_counts.p, e->pk_bbase.p);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(counts, e->pk_counts.p, 3 * n_parts * 8, hipMemcpyDeviceToHost, st));
     uint64_t wide = 0;
-    HIP_OK(hipMemcpyAsync(&wide, e->pk_counts.p + 3 * n_parts, 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    pin_get(e, counts, e->pk_counts.p, 3 * n_parts * 8);
+    pin_get(e, &wide, e->pk_counts.p + 3 * n_parts, 8);
+    pin_sync(e);
     if (wide) {
       e->partitioned = false;
       throw BjxError(BJX_ERR_CAPACITY, "an event line's IP (or event count) exceeds the exchange record's 16-bit field (65535)");
@@ -7766,9 +7799,9 @@ static int apply_received(bjx_engine *e, const bjx_ruleset *rs, const bjx_event_
                      n_ev, d_events, B.n_rules, e->rx_ev_el.p, e->scalars.p + 6);
   HIP_OK(hipGetLastError());
   uint64_t chk[2] = {0, 0};
-  HIP_OK(hipMemcpyAsync(&chk[0], e->rx_evoff.p + n_lines, 8, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipMemcpyAsync(&chk[1], e->scalars.p + 6, 8, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
+  pin_get(e, &chk[0], e->rx_evoff.p + n_lines, 8);
+  pin_get(e, &chk[1], e->scalars.p + 6, 8);
+  pin_sync(e);
   if (chk[0] != n_ev || chk[1]) throw BjxError(BJX_ERR_ARG, "received event records are inconsistent");
   EvSrc E;
   E.bytes = d_bytes; E.nl = nullptr; E.rest_off = nullptr; E.ip_pos = e->rx_pos.p; E.ip_len = e->rx_len.p;
@@ -7892,8 +7925,8 @@ extern "C" int bjx_finish_batch_trips(bjx_engine *e, const uint32_t *d_trips, ui
                          e->scalars.p + 6);
       HIP_OK(hipGetLastError());
       unsigned long long bad = 0;
-      HIP_OK(hipMemcpyAsync(&bad, e->scalars.p + 6, 8, hipMemcpyDeviceToHost, st));
-      HIP_OK(hipStreamSynchronize(st));
+      pin_get(e, &bad, e->scalars.p + 6, 8);
+      pin_sync(e);
       if (bad) throw BjxError(BJX_ERR_ARG, "bjx_finish_batch_trips: packed event index out of range");
     }
     out->n_lines = c.n_lines;

@@ -589,7 +589,8 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
           L2P(3);
           // anchored and no-literal entries of the class, each lane its own
           // class's list (a wave-uniform walk per class serialised the classes
-          // of a wave's lines)
+          // of a wave's lines; scalar loads of the entries when the whole wave
+          // shares one list measured no faster)
           const uint32_t na = (A.dbg2 & 1) ? 0u : n_anc;
           for (uint32_t i = 0; i < na; ++i) {
             const uint32_t ew = anc + kL2AncWords * i;
