@@ -217,7 +217,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--lines", type=int, default=0, help="lines per GPU (default: workload size)")
     ap.add_argument("--cpu-sample", type=int, default=600_000)
