@@ -148,6 +148,20 @@ def test_workload_parity(engine, name, n_lines, batches):
     pair.compare_state(sorted(ips)[:100])
 
 
+def test_wide_scope_workload(engine):
+    """cfg2k: 1,000 global rules in the TestPerSiteRegexStress shape
+    (regex_rate_limiter_test.go:299-365), so every line's scope has 1,000
+    positions: past k_lines2's 128-position tables, the per-line pass is k_lines
+    (the bench line of this shape is in DESIGN.md §5).  Bit-exact against the
+    oracle over two batches."""
+    w = W.scaled(W.CFG2K, 12_000, n_ips=3_000)
+    pair = Pair(w.rules_yaml, engine)
+    for b in range(2):
+        pair.feed(w.host_lines(b * 6_000, 6_000), w.now_ns(b * 6_000, 6_000))
+        assert pair.engine.line_kernel()[0] == "k_lines"
+    pair.compare_state([ln.split(b" ")[1].decode() for ln in w.host_lines(0, 50).split(b"\n")[:50] if ln])
+
+
 EDGE_CFG = r"""
 global_decision_lists:
   allow:

@@ -431,7 +431,14 @@ CFG5H = Workload("cfg5h", "DDoS hot key: one IP sends 25% of 100M lines, the res
                  DDOS_RULES + "expiring_decision_ttl_seconds: 10\n",
                  seed=6, n_lines=100_000_000, n_ips=10_000_000, n_hosts=32, trigger_permille=50, ip_mode=1, hot_pct=25)
 
-ALL = {w.name: w for w in (CFG1, CFG2, CFG3, CFG4, CFG5, CFG5H)}
+# not a BASELINE config: the reference's TestPerSiteRegexStress shape at 1,000
+# global rules, so every line's scope has 1,000 positions (past the 128 of
+# k_lines2's decision tables: the per-line pass is k_lines)
+CFG2K = Workload("cfg2k", "1k global rules (TestPerSiteRegexStress shape: every line's scope 1,000 rules), 20M lines, 1M IPs",
+                 stress_global_rules(1000) + "expiring_decision_ttl_seconds: 10\n",
+                 seed=7, n_lines=20_000_000, n_ips=1_000_000, n_hosts=100)
+
+ALL = {w.name: w for w in (CFG1, CFG2, CFG3, CFG4, CFG5, CFG5H, CFG2K)}
 
 
 def scaled(w: Workload, n_lines: int, n_ips=None) -> Workload:
