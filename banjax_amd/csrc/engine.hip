@@ -442,8 +442,11 @@ struct WideList {
   uint64_t cap;
 };
 
+__device__ void decide_wide(const Bind &B, const uint8_t *line, uint64_t s, uint32_t n, uint32_t rest_off, int32_t hid, uint64_t j,
+                            const Lines &L, const WideList &WL);
+
 template <bool SLOW>
-__device__ void parse_and_match(const Bind &B, const uint8_t *__restrict__ p, uint32_t n, uint64_t j, int64_t now_ns,
+__device__ void parse_and_match(const Bind &B, const uint8_t *__restrict__ p, uint64_t s, uint32_t n, uint64_t j, int64_t now_ns,
                                 const Lines &L, uint32_t *slow_list, unsigned long long *slow_count, const WideList &WL) {
   uint8_t fl = 0;
   L.counts[j] = 0;
@@ -500,6 +503,13 @@ __device__ void parse_and_match(const Bind &B, const uint8_t *__restrict__ p, ui
   uint32_t s_begin = 0, s_end = 0;
   if (hid >= 0) { s_begin = B.site_off[hid]; s_end = B.site_off[hid + 1]; }
   const uint32_t napp = (s_end - s_begin) + B.n_global;
+  if (SLOW && napp > 128 && B.any_prefilter) {
+    // a scope past the line kernels' 128 positions: the rules the line's
+    // literal hits name, its anchored / no-literal / ALWAYS rules, not every
+    // rule of the scope by its automaton
+    decide_wide(B, p, s, n, rest_off, hid, j, L, WL);
+    return;
+  }
   for (uint32_t k = 0; k < napp; ++k) {
     const uint32_t r = k < s_end - s_begin ? B.site_rules[s_begin + k] : B.global_rules[k - (s_end - s_begin)];
     if (B.any_wide && (B.rules[r].flags & kRuleNfaWide)) {
@@ -527,7 +537,7 @@ __global__ __launch_bounds__(kBlock) void k_parse_match(Bind B, const uint8_t *_
   const uint64_t j = SLOW ? list[t] : t;
   const uint64_t s = j ? nl[j - 1] + 1 : 0;
   const uint32_t n = (uint32_t)(nl[j] - s);
-  parse_and_match<SLOW>(B, buf + s, n, j, now_ns, L, slow_list, slow_count, WL);
+  parse_and_match<SLOW>(B, buf + s, s, n, j, now_ns, L, slow_list, slow_count, WL);
 }
 
 // =====================================================================
@@ -1137,6 +1147,141 @@ __device__ __forceinline__ void decide_rules(const Bind &B, const Tabs &T, const
   if (B.mask_words > 1) mask[1] = m1;
   const uint32_t nres = __popcll(m0) + __popcll(m1);
   const uint32_t nev = __popcll(m0 & ~H.k0) + __popcll(m1 & ~H.k1);
+  L.counts[j] = ((uint64_t)nres << 32) | nev;
+}
+
+// decide_rules for a scope of more than 128 positions (the per-line fallback,
+// k_parse_match<SLOW>): the same literal-driven walk, each rule it names
+// decided here by its automaton (or listed for k_nfa_wide), the matches set
+// straight in the line's mask words, which hold every position of the scope.
+// The reference tries every rule of the scope on every line
+// (regex_rate_limiter.go:175-211); a literal rule none of whose prefilter
+// literals occurs in the line cannot match, so only the rules of the line's
+// hits (all literal rules when the hits overflow the line's slots), its
+// anchored / no-literal rules and its ALWAYS rules are looked at.
+__device__ void decide_wide(const Bind &B, const uint8_t *line, uint64_t s, uint32_t n, uint32_t rest_off, int32_t hid, uint64_t j,
+                            const Lines &L, const WideList &WL) {
+  const Tabs T = make_tabs(B.img, B.il);
+  const uint8_t *rest = line + rest_off;
+  const uint32_t rest_len = n - rest_off;
+  const uint32_t nsite = hid >= 0 ? B.site_off[hid + 1] - B.site_off[hid] : 0u;
+  uint64_t *mask = L.masks + j * B.mask_words;
+  for (uint32_t w = 0; w < B.mask_words; ++w) mask[w] = 0;
+  auto setb = [&](uint32_t pos) { mask[pos >> 6] |= 1ull << (pos & 63); };
+  auto rule_at = [&](uint32_t pos) { return pos < nsite ? B.site_rules[B.site_off[hid] + pos] : pos - nsite; };
+  // rule r (its pattern's first rule) at pos by its automaton; wide NFAs to k_nfa_wide
+  auto eval = [&](uint32_t r, uint32_t pos) {
+    if (B.any_wide && (B.rules[r].flags & kRuleNfaWide)) {
+      const unsigned long long q = atomicAdd(WL.count, 1ull);
+      if (q < WL.cap) { WL.line[q] = (uint32_t)j; WL.rule[q] = r; WL.pos[q] = pos; }
+    } else if (rule_match(B, r, rest, rest_len)) {
+      setb(pos);
+    }
+  };
+  // ALWAYS rules
+  if (hid >= 0)
+    for (uint32_t i = B.alw_site_off[hid]; i < B.alw_site_off[hid + 1]; ++i) setb(B.alw_site[i]);
+  for (uint32_t i = 0; i < B.n_alw_glob; ++i) setb(nsite + B.alw_glob[i]);
+  // anchored / no-literal rules: every line (the anchor literal tested first)
+  auto anchored = [&](uint32_t r, uint32_t pos, const uint4 qa, const uint4 qb) {
+    const uint32_t qk = anchor_quick(qa, qb, rest, rest_len);
+    if (qk == 0) return;
+    if (qk == 1 && ((qa.y >> 9) & 1)) { setb(pos); return; }
+    const DevRule &R = B.rules[r];
+    if (R.anc_len) {
+      bool any = false;
+      for (uint32_t i = 0; i < R.anc_len && !any; ++i) {
+        const uint32_t lit = B.rule_lits[R.anc_off + i];
+        any = lit_len_of(T, lit) <= rest_len && literal_at(T, lit, rest);
+      }
+      if (!any) return;
+      if (R.anc_equiv) { setb(pos); return; }
+    }
+    eval(r, pos);
+  };
+  if (hid >= 0)
+    for (uint32_t i = B.dfa_site_off[hid]; i < B.dfa_site_off[hid + 1]; ++i) {
+      const uint2 e = B.dfa_site[i];
+      anchored(e.x, e.y, B.dfa_site_q[2 * i], B.dfa_site_q[2 * i + 1]);
+    }
+  for (uint32_t i = 0; i < B.n_dfa_glob; ++i) {
+    const uint2 e = B.dfa_glob[i];
+    anchored(e.x, nsite + e.y, B.dfa_glob_q[2 * i], B.dfa_glob_q[2 * i + 1]);
+  }
+  // the line's literal hits inside rest (the scan pass's slots; unverified
+  // ones checked here)
+  const CandMeta cm = L.cand_meta[j];
+  const uint64_t rs = s + rest_off;
+  uint32_t lits[kCandSlots], lpos[kCandSlots], nlit = 0;
+  const bool ovf = cm.cnt > (uint32_t)kCandSlots;
+  for (uint32_t c = 0; c < (uint32_t)kCandSlots && c < cm.cnt && !ovf; ++c) {
+    const uint64_t v = L.cand[j * kCandSlots + c];
+    const uint32_t lit = (uint32_t)(v & 0x7FFFFF);
+    const uint64_t q = v >> 24;
+    if (q < rs) continue;
+    if (!(v & kCandVerified) && (q + lit_len_of(T, lit) > s + n || !literal_at(T, lit, line + (q - s)))) continue;
+    lits[nlit] = lit;
+    lpos[nlit++] = q - rs < 0xFFFF ? (uint32_t)(q - rs) : 0xFFFFu;
+  }
+  if (ovf) {
+    // more hits than slots: every literal rule by its automaton (exact, slower)
+    if (hid >= 0)
+      for (uint32_t i = B.pref_site_off[hid]; i < B.pref_site_off[hid + 1]; ++i) eval(B.pref_site[i].x, B.pref_site[i].y);
+    for (uint32_t i = 0; i < B.n_pref_glob; ++i) eval(B.pref_glob[i].x, nsite + B.pref_glob[i].y);
+  } else {
+    for (uint32_t c = 0; c < nlit; ++c) {
+      const uint32_t lit = lits[c];
+      bool dup = false;
+      for (uint32_t d = 0; d < c; ++d) dup = dup || lits[d] == lit;
+      const uint32_t b = B.lr_off[lit], g = B.lr_gend[lit], e = B.lr_off[lit + 1];
+      if (!dup)
+        for (uint32_t i = b; i < g; ++i) {
+          const uint2 x = B.lr_ent[i];
+          const uint32_t pos = nsite + x.y;
+          if ((mask[pos >> 6] >> (pos & 63)) & 1) continue;  // matched already
+          if (x.x >> 31) setb(pos);
+          else eval(x.x, pos);
+        }
+      if (hid < 0 || g == e) continue;
+      // this host's run of the literal's site entries (decide_rules)
+      uint32_t sl = lit_host_slot(lit, (uint32_t)hid, B.lh_cap);
+      uint4 run = B.lh_tab[sl];
+      while (!(run.x == 0 || (run.x == lit + 1 && run.y == (uint32_t)hid))) {
+        sl = (sl + 1) & (B.lh_cap - 1);
+        run = B.lh_tab[sl];
+      }
+      if (run.x == 0) continue;
+      const uint32_t hp = lpos[c];
+      for (uint32_t i = run.z; i < run.w; ++i) {
+        const uint2 x = B.lr_ent[i];
+        if ((mask[x.y >> 6] >> (x.y & 63)) & 1) continue;
+        const uint32_t full = B.lr_full[i];
+        if (full != kNone && (x.x >> 31)) {
+          // host-split literal of an equivalent rule: matched iff the full
+          // literal surrounds this hit of its piece
+          const uint32_t fl = full >> 8, off = full & 0xFF;
+          if (hp != 0xFFFF && hp >= off && hp - off + lit_len_of(T, fl) <= rest_len && literal_at(T, fl, rest + (hp - off)))
+            setb(x.y);
+          else if (hp == 0xFFFF)
+            eval(x.x & 0x7FFFFFFFu, x.y);
+          continue;
+        }
+        if ((x.x >> 31) && full == kNone) setb(x.y);
+        else eval(x.x & 0x7FFFFFFFu, x.y);
+      }
+    }
+  }
+  // RuleResults and events: every set position; no event for a host's hosts_to_skip rules
+  uint32_t nres = 0, nev = 0;
+  for (uint32_t w = 0; w < B.mask_words; ++w) {
+    uint64_t m = mask[w];
+    nres += __popcll(m);
+    while (m) {
+      const uint32_t pos = 64 * w + (uint32_t)__ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      nev += is_skip(B, rule_at(pos), hid) ? 0u : 1u;
+    }
+  }
   L.counts[j] = ((uint64_t)nres << 32) | nev;
 }
 
@@ -5435,6 +5580,15 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   }
   dfa_site_off[n_hosts] = (uint32_t)dfa_site.size();
   pref_site_off[n_hosts] = (uint32_t)pref_site.size();
+  std::vector<uint32_t> alw_site_off(n_hosts + 1, 0), alw_site, alw_glob;
+  for (uint32_t h = 0; h < n_hosts; ++h) {
+    alw_site_off[h] = (uint32_t)alw_site.size();
+    for (uint32_t k = 0; k < per_host[h].size(); ++k)
+      if (mode_of(per_host[h][k]) == kModeAlways) alw_site.push_back(k);
+  }
+  alw_site_off[n_hosts] = (uint32_t)alw_site.size();
+  for (uint32_t g = 0; g < rs->n_global; ++g)
+    if (mode_of(g) == kModeAlways) alw_glob.push_back(g);
   for (uint32_t g = 0; g < rs->n_global; ++g) {
     const RuleMode m = mode_of(g);
     if (m == kModeAnchored || m == kModeScan) dfa_glob.push_back(make_uint2(canon[g], g));
@@ -6128,6 +6282,7 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
          o_dso = bb.add(dfa_site_off), o_ds = bb.add(dfa_site), o_dg = bb.add(dfa_glob), o_pso = bb.add(pref_site_off),
          o_dsq = bb.add(dfa_site_q), o_dgq = bb.add(dfa_glob_q),
          o_ps = bb.add(pref_site), o_pg = bb.add(pref_glob), o_hslot = bb.add(hslot), o_lh = bb.add(lh_tab),
+         o_aso = bb.add(alw_site_off), o_as = bb.add(alw_site), o_ag = bb.add(alw_glob),
          o_nfa = bb.add(nfa_blob), o_lrf = bb.add(lr_full), o_plan = bb.add(plan), o_plo = bb.add(plan_off),
          o_plg = bb.add(plan_glob), o_hl = bb.add(hl);
   e->bind_blob.ensure(bb.bytes.size());
@@ -6230,6 +6385,10 @@ void bind_ruleset(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *sample, s
   B.pref_site = reinterpret_cast<const uint2 *>(base + o_ps);
   B.pref_glob = reinterpret_cast<const uint2 *>(base + o_pg);
   B.n_pref_glob = (uint32_t)pref_glob.size();
+  B.alw_site_off = reinterpret_cast<const uint32_t *>(base + o_aso);
+  B.alw_site = reinterpret_cast<const uint32_t *>(base + o_as);
+  B.alw_glob = reinterpret_cast<const uint32_t *>(base + o_ag);
+  B.n_alw_glob = (uint32_t)alw_glob.size();
   B.nfa = reinterpret_cast<const uint64_t *>(base + o_nfa);
   B.any_nfa = nfa_blob.empty() ? 0 : 1;
   B.any_wide = 0;

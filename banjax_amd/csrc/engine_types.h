@@ -187,6 +187,13 @@ struct Bind {
   const uint2 *pref_site;
   const uint2 *pref_glob;
   uint32_t n_pref_glob;
+  // ALWAYS rules by position (the scopes past 128 positions, which sc_always
+  // does not cover): site positions of host h [alw_site_off[h],
+  // alw_site_off[h + 1]), global indices alw_glob
+  const uint32_t *alw_site_off;
+  const uint32_t *alw_site;
+  const uint32_t *alw_glob;
+  uint32_t n_alw_glob;
   // bit-parallel NFA tables of the kRuleNfa rules (DevRule::nfa_off)
   const uint64_t *nfa;
   uint32_t any_nfa;
