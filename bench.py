@@ -201,7 +201,7 @@ def tail_inclusive(workload):
     """The committed tail-inclusive measurement for this workload (file ->
     pinned -> HBM -> engine, tools/tail_bench.py on the box), reported beside
     the HBM-resident value, never as it."""
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05_tail", "tail_inclusive.json")
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06_tail", "tail_inclusive.json")
     if workload != "cfg3" or not os.path.exists(path):
         return None
     with open(path) as f:
@@ -209,7 +209,7 @@ def tail_inclusive(workload):
     st = t["steady"]
     return {"lines_per_s": st["lines_per_s_tail_inclusive"], "file_to_HBM_GBps": st["file_to_HBM_GBps"],
             "lines": st["lines"], "batch_MiB": st["batch_MiB"], "engine_only_lines_per_s": st["lines_per_s_engine_only"],
-            "bound": t["parts"]["reading"], "source": "profiles/r05_tail/tail_inclusive.json (%s)" % t["command"],
+            "bound": t["parts"]["reading"], "source": "profiles/r06_tail/tail_inclusive.json (%s)" % t["command"],
             "what": "not measured in this run: the committed tools/tail_bench.py result on the same workload"}
 
 
