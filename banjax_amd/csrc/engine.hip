@@ -570,6 +570,8 @@ constexpr int kScanWaves = 16;        // waves per block (one block per CU)
 constexpr uint32_t kTileLds = kWT + kHalo + 16;
 constexpr uint32_t kWaveJobs = 64;   // DFA jobs staged per wave before one global append
 constexpr uint32_t kCandList = 128;   // candidate positions verified per round (one per lane)
+constexpr uint32_t kBanChunks = 8;                  // ban-log write/copy chunks of a batch (emit_bans)
+constexpr uint64_t kBanChunkMin = 64ull << 20;     // logs up to this size go in one chunk
 constexpr uint32_t kLongList = 64;   // long-line hits listed per round (k_scan flush_long), one per lane
 constexpr uint32_t kWaveLds = kTileLds + kLineCap * (2 + 2) + kCandList * 4 + kLineCap * 4 + kLongList * 8 + 16;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
@@ -4098,9 +4100,10 @@ __global__ void k_ban_len(BanDev A, uint64_t *__restrict__ len, uint8_t *__restr
   len[t] = o.n;
 }
 
-__global__ void k_ban_write(BanDev A, const uint64_t *__restrict__ off, uint8_t *__restrict__ out) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= A.n_trips) return;
+// trips [t0, t1) of the batch (emit_bans writes the log in chunks)
+__global__ void k_ban_write(BanDev A, const uint64_t *__restrict__ off, uint8_t *__restrict__ out, uint64_t t0, uint64_t t1) {
+  const uint64_t t = t0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= t1) return;
   JOut<true> o{out + off[t], 0};
   ban_log_line(A, t, o);
 }
@@ -4872,6 +4875,8 @@ struct bjx_engine {
   // node batches: from bjx_events_partition to the start of the owner's
   // rate-limit stage (partition, pack, the copies' wait, unpack)
   hipEvent_t xev[2] = {};
+  hipStream_t bstream = nullptr;  // the ban log's D2H copies (emit_bans)
+  hipEvent_t bev[kBanChunks + 1] = {};
   bool xev_rec = false;
   double exchange_ms = 0;
   bool phase_rec[kPhases + 1] = {};
@@ -6651,6 +6656,8 @@ extern "C" void bjx_engine_destroy(bjx_engine *e) {
   for (auto &x : e->evk) (void)hipEventDestroy(x);
   for (auto &x : e->ph) (void)hipEventDestroy(x);
   for (auto &x : e->xev) (void)hipEventDestroy(x);
+  for (auto &x : e->bev) if (x) (void)hipEventDestroy(x);
+  if (e->bstream) (void)hipStreamDestroy(e->bstream);
   (void)hipStreamDestroy(e->stream);
   if (e->pin) (void)hipHostFree(e->pin);
   delete e;
@@ -7571,11 +7578,31 @@ static void emit_bans(bjx_engine *e, uint64_t n, bool records_only) {
   pin_sync(e);
   const uint64_t log_bytes = e->ban_off.data()[n];
   e->ban_log.resize(log_bytes);
+  bool log_copy = false;
   if (log_bytes) {
+    // The log leaves on its own stream, in chunks of trips, each chunk as soon
+    // as its lines are written: the PCIe copy overlaps the next chunk's writes
+    // and the per-IP reduce below; the engine stream joins the copies at the
+    // end of emit_bans, so the batch's final sync still covers them.
     e->bn_log.ensure(log_bytes + 16);
-    hipLaunchKernelGGL(k_ban_write, dim3(grid_for(n)), dim3(kBlock), 0, st, A, e->bn_off.p, e->bn_log.p);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(e->ban_log.data(), e->bn_log.p, log_bytes, hipMemcpyDeviceToHost, st));
+    if (!e->bstream) {
+      HIP_OK(hipStreamCreateWithFlags(&e->bstream, hipStreamNonBlocking));
+      for (auto &x : e->bev) HIP_OK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+    }
+    const uint64_t nch = log_bytes > kBanChunkMin ? (uint64_t)kBanChunks : 1u;
+    const uint64_t *ho = e->ban_off.data();
+    for (uint64_t c = 0; c < nch; ++c) {
+      const uint64_t a = n * c / nch, b = n * (c + 1) / nch;
+      if (a == b) continue;
+      hipLaunchKernelGGL(k_ban_write, dim3(grid_for(b - a)), dim3(kBlock), 0, st, A, e->bn_off.p, e->bn_log.p, a, b);
+      HIP_OK(hipGetLastError());
+      if (ho[b] == ho[a]) continue;
+      HIP_OK(hipEventRecord(e->bev[c], st));
+      HIP_OK(hipStreamWaitEvent(e->bstream, e->bev[c], 0));
+      HIP_OK(hipMemcpyAsync(e->ban_log.data() + ho[a], e->bn_log.p + ho[a], ho[b] - ho[a], hipMemcpyDeviceToHost, e->bstream));
+    }
+    HIP_OK(hipEventRecord(e->bev[kBanChunks], e->bstream));
+    log_copy = true;
   }
   e->bn_first.ensure(n_seg); e->bn_cnt.ensure(n_seg); e->bn_ipt.ensure(n_seg); e->bn_coll.ensure(n_seg);
   e->bn_best.ensure(n_seg); e->bn_flag.ensure(n); e->bn_rep.ensure(n); e->bn_sel.ensure(n);
@@ -7623,6 +7650,7 @@ static void emit_bans(bjx_engine *e, uint64_t n, bool records_only) {
     e->ban_ipb.resize(nb);
     if (nb) HIP_OK(hipMemcpyAsync(e->ban_ipb.data(), e->bn_ipb.p, nb, hipMemcpyDeviceToHost, st));
   }
+  if (log_copy) HIP_OK(hipStreamWaitEvent(st, e->bev[kBanChunks], 0));
   e->ban_n_trips = n;
 }
 

@@ -361,7 +361,11 @@ def main():
     dec = None
     if args.bans_steps > 0 and not bans:
         bans = True
-        step()  # untimed: the emission's first-use allocations (pinned host buffers sized to the step's output)
+        # untimed, as many steps as are timed: the emission's first-use
+        # allocations (pinned host buffers grown to the largest output of the
+        # steps' cycle; cfg5's trip count repeats every third step)
+        for _ in range(args.bans_steps):
+            step()
         el2, _ = timed_region(dist, step, sync_all, args.bans_steps, "cuda")
         bans = False
         dec = {"value": round(n_lines * n_parts / (el2 / args.bans_steps), 1), "unit": "lines/s",
@@ -395,7 +399,8 @@ def main():
     # built or copied), single-engine runs
     rec = None
     if args.bans_steps > 0 and not args.bans and ex is None and not node_mode and not dist:
-        eng.process(rs, None, now, device_ptr=data.data_ptr(), nbytes=nbytes, emit_bans=True, ban_log=False)  # untimed
+        for _ in range(args.bans_steps):  # untimed, as above
+            eng.process(rs, None, now, device_ptr=data.data_ptr(), nbytes=nbytes, emit_bans=True, ban_log=False)
         sync_all()
         t2 = time.perf_counter()
         for _ in range(args.bans_steps):
