@@ -3557,9 +3557,11 @@ __global__ __launch_bounds__(kBlock) void k_bucket_bounds(uint64_t n_ev, const u
 }
 
 // One bucket per block.  The low key bits are ranked by a stable block radix
-// sort of the bucket's (low bits, position) pairs; padding ranks take the
-// largest low key and come last (they sit after every real record in the
-// sort's input order, which it keeps for equal keys).  Run heads are compacted
+// sort of the bucket's (low bits << 12 | position) words on bits [12, 12 + L):
+// the position rides in the key's low bits, so the sort moves one word per
+// item and no value array; padding ranks take the largest low key and come
+// last (they sit after every real record in the sort's input order, which it
+// keeps for equal keys).  Run heads are compacted
 // in rank order and taken longest first, as in k_apply; a lane walks its run
 // through the rank -> position table, loading each record from the bucket's
 // few KB of HBM / L2, the next one in flight while the current one is applied.
@@ -3572,7 +3574,8 @@ __global__ __launch_bounds__(kBlock) void k_bucket_apply(const uint32_t *__restr
                                                          const DevRule *__restrict__ rules, StSlot *__restrict__ st,
                                                          uint8_t *__restrict__ out_sorted, uint32_t *__restrict__ big,
                                                          unsigned long long *__restrict__ n_big, uint32_t *__restrict__ wcnt) {
-  using Sort = hipcub::BlockRadixSort<uint32_t, kBlock, kBucketItems, uint16_t>;
+  using Sort = hipcub::BlockRadixSort<uint32_t, kBlock, kBucketItems>;
+  static_assert(kBucketCap <= 4096, "positions ride in 12 key bits");
   constexpr uint32_t kLongRun = 8;
   __shared__ union {
     typename Sort::TempStorage sort;
@@ -3597,21 +3600,19 @@ __global__ __launch_bounds__(kBlock) void k_bucket_apply(const uint32_t *__restr
   if (tid == 0) { s_front = 0; s_back = 0; }
   __syncthreads();
   uint32_t k[kBucketItems];
-  uint16_t v[kBucketItems];
 #pragma unroll
   for (uint32_t j = 0; j < kBucketItems; ++j) {
     const uint32_t i = tid * kBucketItems + j;  // blocked: the sort is stable in this order
-    k[j] = i < n ? s_u.lk[i] : mask;
-    v[j] = (uint16_t)i;
+    k[j] = ((i < n ? s_u.lk[i] : mask) << 12) | i;
   }
   __syncthreads();
-  Sort(s_u.sort).SortBlockedToStriped(k, v, 0, (int)L);
+  Sort(s_u.sort).SortBlockedToStriped(k, 12, 12 + (int)L);
   __syncthreads();
 #pragma unroll
   for (uint32_t j = 0; j < kBucketItems; ++j) {
     const uint32_t r = j * kBlock + tid;
-    s_lk[r] = (uint16_t)k[j];
-    s_perm[r] = v[j];
+    s_lk[r] = (uint16_t)(k[j] >> 12);
+    s_perm[r] = (uint16_t)(k[j] & 0xFFFu);
   }
   __syncthreads();
   // run heads, compacted in rank order (block scan of per-thread counts)
@@ -4911,6 +4912,9 @@ struct bjx_engine {
   uint32_t lines2_w = 0;       // ... and the instance (mask width) it was set on
   int dbg_slot_cache = -1;     // bjx_debug_set_slot_cache: -1 = BJX_SLOT_CACHE / default on, 0 off, 1 on
   uint64_t host_counters[3] = {0, 0, 0};
+  // host_counters were read with the match phase's last counts, nothing has
+  // touched the tables since (run_batch: match, then straight to the rate limit)
+  bool counters_fresh = false, want_counters = false;
   // small device -> host reads (counts, flags) through a pinned ring: a copy
   // into pageable memory makes the host wait for it, so a few in a row cost a
   // round trip (20-30 us) each; queued here they cost one stream sync
@@ -6548,8 +6552,8 @@ void grow_st(bjx_engine *e, uint64_t want) {
 // (claims beyond that roll back and grow, see rate_limit_stage); the arena
 // always fits the batch's IP bytes.  Small tables keep the random probes in
 // cache and the state-slot sort short.
+// (e->host_counters current: the caller has just read them)
 void ensure_capacity(bjx_engine *e, uint64_t new_ips, uint64_t new_bytes, uint64_t new_states) {
-  read_counters(e);
   State &S = e->S;
   const uint64_t n_ips = e->host_counters[0], used = e->host_counters[1], n_st = e->host_counters[2];
   if ((n_ips + new_ips) * 4 > e->ip_cap * 3) grow_ip(e, 2 * (n_ips + new_ips));
@@ -6904,7 +6908,8 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
   if (use12) rec_base = (int64_t)((uint64_t)rec_base - (EvRec12::kSpan >> 1));
   else rec_base = 0;
   if (E.n >= 0x7FFFFFFFull || n_ev >= 0xFFFFFFFFull) throw BjxError(BJX_ERR_ARG, "batch too large (2^31 lines / 2^32 events)");
-  read_counters(e);
+  if (!e->counters_fresh) read_counters(e);
+  e->counters_fresh = false;
   // room for the new entries expected: an eighth of the table's entries, or
   // 1.25 x the previous batch's new entries (a stream of new IPs), whichever
   // is more, at most the batch's worst case
@@ -6917,6 +6922,7 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
   const uint32_t epoch = e->epoch;
   e->el_slot.ensure(E.n); e->el_id.ensure(E.n); e->coll.ensure(E.n);
   uint64_t nw_ovf[2] = {0, 0};  // new-IP event lines (k_ip_claim's list), IP table overflow flag
+  uint64_t cnt6[6] = {};          // S.counters[0..5] after the IP claims
   e->ev_st.ensure(n_ev); e->ev_st2.ensure(n_ev); e->ev_rec.ensure(n_ev); e->ev_rec2.ensure(n_ev);
   e->ev_out.ensure(n_ev); e->ev_out_s.ensure(n_ev);
   mark(e, 5);
@@ -6934,8 +6940,12 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
                          budget / kClaimShards);
       hipLaunchKernelGGL(k_fold_new, dim3(1), dim3(kClaimShards), 0, st, e->S);
       HIP_OK(hipGetLastError());
-      pin_get(e, nw_ovf, e->S.counters + 4, 16);
+      // with the overflow flags, the table counters and the collision count:
+      // a batch without new IPs needs no further read before its state claims
+      pin_get(e, cnt6, e->S.counters, 48);
       pin_sync(e);
+      nw_ovf[0] = cnt6[4];
+      nw_ovf[1] = cnt6[5];
       if (!nw_ovf[1]) break;
       // more new IPs than the table had room for: undo, grow, claim again
       hipLaunchKernelGGL(k_ip_rollback, dim3(grid_for(e->ip_cap)), dim3(kBlock), 0, st, e->ip_cap, e->S, epoch);
@@ -6956,9 +6966,13 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
       hipLaunchKernelGGL(k_ip_commit_total, dim3(1), dim3(64), 0, st, e->S, nb, bn, bno, bb, bbo);
       HIP_OK(hipGetLastError());
     }
-    uint64_t n_coll = 0;
-    pin_get(e, &n_coll, e->S.counters + 3, 8);
-    pin_sync(e);
+    // no new IPs: no commit ran, so the counters read with the flags are final
+    const bool cnt_final = nw_ovf[0] == 0;
+    uint64_t n_coll = cnt6[3];
+    if (!cnt_final) {
+      pin_get(e, &n_coll, e->S.counters + 3, 8);
+      pin_sync(e);
+    }
     if (n_coll) {  // distinct IPs with one 64-bit hash in this batch: resolve exactly, in line order
       if (n_coll > 1) {
         uint32_t *ki = e->coll.p, *ko = e->ev_st2.p;
@@ -6971,7 +6985,8 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
       HIP_OK(hipGetLastError());
     }
     for (int attempt = 0;; ++attempt) {
-      read_counters(e);
+      if (attempt == 0 && cnt_final && n_coll == 0) memcpy(e->host_counters, cnt6, 24);
+      else read_counters(e);
       const uint64_t n_st = e->host_counters[2];
       HIP_OK(hipMemsetAsync(e->S.counters + 6, 0, 3 * 8, st));
       HIP_OK(hipMemsetAsync(e->S.counters + kShardBase, 0, kClaimShards * 128, st));
@@ -6985,13 +7000,15 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
       else
         hipLaunchKernelGGL(k_st_claim<EvRec>, dim3(grid_for(n_ev)), dim3(kBlock), 0, st, E, n_ev, ev_el, ev_rule,
                            e->el_slot.p, e->el_id.p, B.rules, e->S, e->ev_st.p, e->ev_rec.p, rec_base, budget / kClaimShards);
+      // the shard counts folded into the table count right away (an overflow
+      // below rolls the claims back and recounts), read with the flags
+      hipLaunchKernelGGL(k_fold_claims, dim3(1), dim3(kClaimShards), 0, st, e->S);
       HIP_OK(hipGetLastError());
       uint64_t ovf[2] = {0, 0};  // state table overflow, a timestamp outside the 12-B records' span
       pin_get(e, ovf, e->S.counters + 7, 16);
+      pin_get(e, e->host_counters, e->S.counters, 24);
       pin_sync(e);
       if (!ovf[0]) {
-        hipLaunchKernelGGL(k_fold_claims, dim3(1), dim3(kClaimShards), 0, st, e->S);
-        HIP_OK(hipGetLastError());
         if (use12 && ovf[1]) {
           // the same claims again (every key is in the table now, so nothing
           // is claimed twice), writing 16-B records
@@ -7013,8 +7030,7 @@ static void rate_limit_stage(bjx_engine *e, const Bind &B, const EvSrc &E, uint6
       if (!forced) grow_st(e, e->host_counters[2] + n_ev);  // the batch's worst case, as for the IP table
     }
   }
-  mark(e, 6);
-  read_counters(e);
+  mark(e, 6);  // host_counters: read with the last claim pass's flags
   e->last_new_ips = e->host_counters[0] - ips0;
   e->last_new_states = e->host_counters[2] - st0;
   e->rec12 = use12;
@@ -7203,6 +7219,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   // ---- the per-line pass: k_lines2 when the ruleset has its tables, else
   // k_lines (exotic timestamps go to the per-line fallback either way)
   unsigned long long sc4[5] = {0, 0, 0, 0, 0};
+  unsigned long long n_jobs = 0;  // real DFA jobs (read with sc4, same sync)
   int n_cu = 0;
   HIP_OK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, e->device));
   if (!e->lines_attr) {
@@ -7329,6 +7346,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     pin_get(e, &last_nl, e->nl.p + (n_lines - 1), 8);
     pin_get(e, sc4, e->scalars.p + 8, 32);
     pin_get(e, sc4 + 4, e->scalars.p, 8);
+    pin_get(e, &n_jobs, e->scalars.p + 14, 8);
     pin_sync(e);
     if (sc4[3] <= std::min(std::min(e->jline.n, e->jkey.n), std::min(e->jidx.n, e->jrec.n))) break;
     // more DFA jobs than the buffer holds: grow it and redo the (idempotent) line pass
@@ -7342,10 +7360,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     HIP_OK(hipMemsetAsync(e->scalars.p + 14, 0, 8, st));
   }
   out->consumed_bytes = last_nl + 1;
-  // job slots taken (sc4[3]; the chunks' unused ones hold null jobs) and real jobs
-  unsigned long long n_jobs = 0;
-  pin_get(e, &n_jobs, e->scalars.p + 14, 8);
-  pin_sync(e);
+  // job slots taken (sc4[3]; the chunks' unused ones hold null jobs) and real jobs (n_jobs)
   const unsigned long long n_slow = sc4[4], n_slots = sc4[3];
   e->last_jobs = n_jobs;
   e->scan_stats[0] = sc4[0]; e->scan_stats[1] = sc4[1]; e->scan_stats[2] = n_slow; e->scan_stats[3] = B.scan_img_bytes;
@@ -7465,7 +7480,9 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   unsigned long long bnd[2] = {0, 0};
   if (n_ev) {
     pin_get(e, bnd, e->scalars.p + 1, 16);
+    if (e->want_counters) pin_get(e, e->host_counters, e->S.counters, 24);
     pin_sync(e);
+    e->counters_fresh = e->want_counters;
   }
   BatchCtx &c = e->bc;
   c.buf = buf; c.n_lines = n_lines; c.n_res = n_res; c.n_ev = n_ev; c.L = L; c.n_el = bnd[0]; c.el_bytes = bnd[1];
@@ -7820,7 +7837,14 @@ static void run_batch(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *bytes
   // a standalone batch has no exchange: no node batch's figure carries over
   e->exchange_ms = 0;
   e->xev_rec = false;
-  if (!match_phase(e, rs, bytes, n, now_ns, flags, out)) return;
+  e->counters_fresh = false;
+  e->want_counters = true;
+  struct Reset {  // whatever way match_phase leaves
+    bjx_engine *e;
+    ~Reset() { e->want_counters = false; }
+  } reset{e};
+  if (!match_phase(e, rs, bytes, n, now_ns, flags, out)) { e->counters_fresh = false; return; }
+  e->want_counters = false;
   if (e->bc.n_ev) {
     rate_limit_stage(e, e->bind, local_evsrc(e), e->bc.n_el, e->bc.el_bytes, e->bc.n_ev, e->ev_el.p, e->ev_rule.p,
                      e->bc.now_ns);
