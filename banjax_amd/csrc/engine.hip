@@ -483,7 +483,9 @@ __device__ void parse_and_match(const Bind &B, const uint8_t *__restrict__ p, ui
       slow_list[k] = (uint32_t)j;
       return;
     }
-  } else {
+  } else if (parse_float_fast(p, sp1, &f) != 0) {
+    // the general ParseFloat only for the tokens the fast parser declines (a
+    // wide-scope line has an ordinary timestamp and takes the fast one)
     Decimal dec;
     if (go_parse_float(p, sp1, &f, &dec) != 0) { L.flags[j] = kLineError; return; }
   }
@@ -497,7 +499,6 @@ __device__ void parse_and_match(const Bind &B, const uint8_t *__restrict__ p, ui
   // per-site rules first, then global rules, in YAML order (regex_rate_limiter.go:175-211)
   const uint8_t *rest = p + rest_off;
   const uint32_t rest_len = n - rest_off;
-  uint64_t *mask = L.masks + (size_t)j * B.mask_words;
   uint64_t word = 0;
   uint32_t pos = 0, wi = 0, nres = 0, nev = 0;
   uint32_t s_begin = 0, s_end = 0;
@@ -521,10 +522,16 @@ __device__ void parse_and_match(const Bind &B, const uint8_t *__restrict__ p, ui
       nev += is_skip(B, r, hid) ? 0u : 1u;
     }
     ++pos;
-    if ((pos & 63) == 0) { mask[wi++] = word; word = 0; }
+    if ((pos & 63) == 0) { L.mword(j, wi++) = word; word = 0; }
   }
-  if (pos & 63) mask[wi] = word;
+  if (pos & 63) L.mword(j, wi) = word;
   L.counts[j] = ((uint64_t)nres << 32) | nev;
+}
+
+// every line to the per-line fallback (slow count = n; the fallback takes
+// line t as line t, no list)
+__global__ void k_no_line_pass(unsigned long long *slow_count, unsigned long long n) {
+  if (threadIdx.x == 0) *slow_count = n;
 }
 
 template <bool SLOW>
@@ -534,7 +541,7 @@ __global__ __launch_bounds__(kBlock) void k_parse_match(Bind B, const uint8_t *_
                                                         uint32_t *slow_list, unsigned long long *slow_count, WideList WL) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_lines) return;
-  const uint64_t j = SLOW ? list[t] : t;
+  const uint64_t j = SLOW && list ? list[t] : t;
   const uint64_t s = j ? nl[j - 1] + 1 : 0;
   const uint32_t n = (uint32_t)(nl[j] - s);
   parse_and_match<SLOW>(B, buf + s, s, n, j, now_ns, L, slow_list, slow_count, WL);
@@ -1144,9 +1151,8 @@ __device__ __forceinline__ void decide_rules(const Bind &B, const Tabs &T, const
       }
     }
   }
-  uint64_t *mask = L.masks + j * B.mask_words;
-  mask[0] = m0;
-  if (B.mask_words > 1) mask[1] = m1;
+  L.mword(j, 0) = m0;
+  if (B.mask_words > 1) L.mword(j, 1) = m1;
   const uint32_t nres = __popcll(m0) + __popcll(m1);
   const uint32_t nev = __popcll(m0 & ~H.k0) + __popcll(m1 & ~H.k1);
   L.counts[j] = ((uint64_t)nres << 32) | nev;
@@ -1163,13 +1169,16 @@ __device__ __forceinline__ void decide_rules(const Bind &B, const Tabs &T, const
 // anchored / no-literal rules and its ALWAYS rules are looked at.
 __device__ void decide_wide(const Bind &B, const uint8_t *line, uint64_t s, uint32_t n, uint32_t rest_off, int32_t hid, uint64_t j,
                             const Lines &L, const WideList &WL) {
+#ifdef BJX_WIDE_NODECIDE  // timing experiment only (results wrong): the fallback's parse alone
+  L.counts[j] = 0;
+  return;
+#endif
   const Tabs T = make_tabs(B.img, B.il);
   const uint8_t *rest = line + rest_off;
   const uint32_t rest_len = n - rest_off;
   const uint32_t nsite = hid >= 0 ? B.site_off[hid + 1] - B.site_off[hid] : 0u;
-  uint64_t *mask = L.masks + j * B.mask_words;
-  for (uint32_t w = 0; w < B.mask_words; ++w) mask[w] = 0;
-  auto setb = [&](uint32_t pos) { mask[pos >> 6] |= 1ull << (pos & 63); };
+  for (uint32_t w = 0; w < B.mask_words; ++w) L.mword(j, w) = 0;
+  auto setb = [&](uint32_t pos) { L.mword(j, pos >> 6) |= 1ull << (pos & 63); };
   auto rule_at = [&](uint32_t pos) { return pos < nsite ? B.site_rules[B.site_off[hid] + pos] : pos - nsite; };
   // rule r (its pattern's first rule) at pos by its automaton; wide NFAs to k_nfa_wide
   auto eval = [&](uint32_t r, uint32_t pos) {
@@ -1240,7 +1249,7 @@ __device__ void decide_wide(const Bind &B, const uint8_t *line, uint64_t s, uint
         for (uint32_t i = b; i < g; ++i) {
           const uint2 x = B.lr_ent[i];
           const uint32_t pos = nsite + x.y;
-          if ((mask[pos >> 6] >> (pos & 63)) & 1) continue;  // matched already
+          if ((L.mword(j, pos >> 6) >> (pos & 63)) & 1) continue;  // matched already
           if (x.x >> 31) setb(pos);
           else eval(x.x, pos);
         }
@@ -1256,7 +1265,7 @@ __device__ void decide_wide(const Bind &B, const uint8_t *line, uint64_t s, uint
       const uint32_t hp = lpos[c];
       for (uint32_t i = run.z; i < run.w; ++i) {
         const uint2 x = B.lr_ent[i];
-        if ((mask[x.y >> 6] >> (x.y & 63)) & 1) continue;
+        if ((L.mword(j, x.y >> 6) >> (x.y & 63)) & 1) continue;
         const uint32_t full = B.lr_full[i];
         if (full != kNone && (x.x >> 31)) {
           // host-split literal of an equivalent rule: matched iff the full
@@ -1276,7 +1285,7 @@ __device__ void decide_wide(const Bind &B, const uint8_t *line, uint64_t s, uint
   // RuleResults and events: every set position; no event for a host's hosts_to_skip rules
   uint32_t nres = 0, nev = 0;
   for (uint32_t w = 0; w < B.mask_words; ++w) {
-    uint64_t m = mask[w];
+    uint64_t m = L.mword(j, w);
     nres += __popcll(m);
     while (m) {
       const uint32_t pos = 64 * w + (uint32_t)__ffsll((unsigned long long)m) - 1;
@@ -1392,9 +1401,8 @@ __device__ __forceinline__ void decide_plan(const Bind &B, const Tabs &T, const 
   for (uint32_t i = 0; i < B.n_plan_glob; ++i)
     plan_rule<EMIT>(B, T, B.plan_glob[2 * i], B.plan_glob[2 * i + 1], nsite, rest, rest_len, lits, lpos, nlit, ovf, ov, m0, m1,
                     j, S);
-  uint64_t *mask = L.masks + j * B.mask_words;
-  mask[0] = m0;
-  if (B.mask_words > 1) mask[1] = m1;
+  L.mword(j, 0) = m0;
+  if (B.mask_words > 1) L.mword(j, 1) = m1;
   const uint32_t nres = __popcll(m0) + __popcll(m1);
   const uint32_t nev = __popcll(m0 & ~H.k0) + __popcll(m1 & ~H.k1);
   L.counts[j] = ((uint64_t)nres << 32) | nev;
@@ -1557,9 +1565,8 @@ __device__ __forceinline__ void decide_plan_lds(const Bind &B, const Tabs &T, co
     plan_rule<EMIT>(B, T, B.plan_glob[2 * i], B.plan_glob[2 * i + 1], nsite, rest, rest_len, lits, lpos, nlit, ovf, ov, m0, m1,
                     j, S);
   if (P) { __builtin_amdgcn_s_waitcnt(0); P->mark(9); }
-  uint64_t *mask = L.masks + j * B.mask_words;
-  mask[0] = m0;
-  if (B.mask_words > 1) mask[1] = m1;
+  L.mword(j, 0) = m0;
+  if (B.mask_words > 1) L.mword(j, 1) = m1;
   const uint32_t nres = __popcll(m0) + __popcll(m1);
   const uint32_t nev = __popcll(m0 & ~H.k0) + __popcll(m1 & ~H.k1);
   L.counts[j] = ((uint64_t)nres << 32) | nev;
@@ -2662,7 +2669,7 @@ __global__ __launch_bounds__(kBlock) void k_dfa(Bind B, const uint8_t *__restric
   }
   if (!m) return;
   const uint64_t j = jline[slot];
-  atomicOr(reinterpret_cast<unsigned long long *>(L.masks + j * B.mask_words + (pos >> 6)), 1ull << (pos & 63));
+  atomicOr(reinterpret_cast<unsigned long long *>(&L.mword(j, pos >> 6)), 1ull << (pos & 63));
   atomicAdd(reinterpret_cast<unsigned long long *>(L.counts + j), (1ull << 32) | ((rec & kJobNoCount) ? 0ull : 1ull));
 }
 
@@ -2731,7 +2738,7 @@ __global__ __launch_bounds__(kBlock) void k_dfa_legacy(Bind B, const uint8_t *__
   const int32_t hid = L.host_id[j];
   const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
   const bool no_count = (B.sc_skip[2 * sc + (pos >> 6)] >> (pos & 63)) & 1;
-  atomicOr(reinterpret_cast<unsigned long long *>(L.masks + j * B.mask_words + (pos >> 6)), 1ull << (pos & 63));
+  atomicOr(reinterpret_cast<unsigned long long *>(&L.mword(j, pos >> 6)), 1ull << (pos & 63));
   atomicAdd(reinterpret_cast<unsigned long long *>(L.counts + j), (1ull << 32) | (no_count ? 0ull : 1ull));
 }
 
@@ -2810,7 +2817,7 @@ __global__ __launch_bounds__(kBlock) void k_nfa(Bind B, uint32_t rule, const uin
   const int32_t hid = L.host_id[j];
   const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
   const bool skp = (B.sc_skip[2 * sc + (pos >> 6)] >> (pos & 63)) & 1;
-  atomicOr(reinterpret_cast<unsigned long long *>(L.masks + j * B.mask_words + (pos >> 6)), 1ull << (pos & 63));
+  atomicOr(reinterpret_cast<unsigned long long *>(&L.mword(j, pos >> 6)), 1ull << (pos & 63));
   atomicAdd(reinterpret_cast<unsigned long long *>(L.counts + j), (1ull << 32) | (skp ? 0ull : 1ull));
 }
 
@@ -2936,7 +2943,7 @@ __global__ __launch_bounds__(kBlock) void k_nfa_wide(Bind B, const uint8_t *__re
     }
     if (m && tid == 0) {
       const int32_t hid = L.host_id[j];
-      atomicOr(reinterpret_cast<unsigned long long *>(L.masks + j * B.mask_words + (pos >> 6)), 1ull << (pos & 63));
+      atomicOr(reinterpret_cast<unsigned long long *>(&L.mword(j, pos >> 6)), 1ull << (pos & 63));
       atomicAdd(reinterpret_cast<unsigned long long *>(L.counts + j), (1ull << 32) | (is_skip(B, r, hid) ? 0ull : 1ull));
     }
     wide_sync<GLB>();  // the next job reuses A / Yb / gmark / s_flag
@@ -2974,13 +2981,12 @@ __global__ __launch_bounds__(kBlock) void k_emit(Bind B, uint64_t n_lines, Lines
     if (hid >= 0) { s_begin = B.site_off[hid]; s_end = B.site_off[hid + 1]; }
     const uint32_t nsite = s_end - s_begin;
     const uint32_t napp = nsite + B.n_global;
-    const uint64_t *mask = L.masks + j * B.mask_words;
     // HostsToSkip of the line's host by rule position (positions < 128; the
     // per-result binary search only past that)
     const uint32_t sc = hid >= 0 ? (uint32_t)hid : B.n_hosts;
     const uint64_t k0 = B.sc_skip[2 * sc], k1 = B.sc_skip[2 * sc + 1];
     for (uint32_t w = 0; w * 64 < napp; ++w) {
-      uint64_t m = mask[w];
+      uint64_t m = L.mword(j, w);
       while (m) {
         const uint32_t b = (uint32_t)__ffsll((unsigned long long)m) - 1;
         m &= m - 1;
@@ -3961,7 +3967,7 @@ __global__ void k_check_masks(uint64_t n_lines, Lines L, uint32_t mask_words, un
   uint32_t pc = 0;
   const uint8_t f = L.flags[j];
   if (!(f & (kLineError | kLineOld | kLineExempt)))
-    for (uint32_t w = 0; w < mask_words; ++w) pc += __popcll(L.masks[j * mask_words + w]);
+    for (uint32_t w = 0; w < mask_words; ++w) pc += __popcll(L.mword(j, w));
   if ((uint32_t)(L.counts[j] >> 32) != pc && atomicAdd(&chk[0], 1ull) == 0) chk[1] = j;
 }
 
@@ -4869,7 +4875,7 @@ struct bjx_engine {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evm0 = nullptr, evm1 = nullptr;
   hipEvent_t evk[4] = {};      // k_lines launch, DFA-job sort + k_dfa / k_nfa (bench: per-kernel roofline)
   double kernel_ms[3] = {};   // last batch: k_scan, k_lines, DFA jobs
-  uint32_t last_line_kernel = 0;  // last batch's per-line kernel: 2 = k_lines2, 1 = k_lines
+  uint32_t last_line_kernel = 0;  // last batch's per-line kernel: 2 = k_lines2, 1 = k_lines, 3 = k_parse_match (every line)
   static constexpr int kPhases = 8;
   hipEvent_t ph[kPhases + 1] = {};
   double phase_ms[kPhases] = {};
@@ -7173,7 +7179,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   e->scalars.ensure(16);
   L.ts = e->l_ts.p; L.ip_hash = e->l_iph.p; L.ip_len = e->l_iplen.p;
   L.rest_off = e->l_roff.p; L.host_id = e->l_hid.p; L.flags = e->l_flags.p;
-  L.counts = e->l_counts.p; L.masks = e->l_masks.p;
+  L.counts = e->l_counts.p; L.masks = e->l_masks.p; L.mstride = cap;
   L.cand_meta = e->l_ccnt.p; L.cand = e->l_cand.p; L.ip16 = e->l_ip16.p;
   L.cand_first = nullptr;
   if (B.cfirst) {
@@ -7220,6 +7226,8 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
   // k_lines (exotic timestamps go to the per-line fallback either way)
   unsigned long long sc4[5] = {0, 0, 0, 0, 0};
   unsigned long long n_jobs = 0;  // real DFA jobs (read with sc4, same sync)
+  // BJX_LINES=1 (test hook) keeps the line pass for these rulesets too
+  const bool all_wide = B.n_global > 128 && !(getenv("BJX_LINES") && atoi(getenv("BJX_LINES")) == 1);
   int n_cu = 0;
   HIP_OK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, e->device));
   if (!e->lines_attr) {
@@ -7259,8 +7267,14 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
     // k_lines2 (lines2.h) when the ruleset has its tables; BJX_LINES=1 keeps k_lines
     static const int lines_env = getenv("BJX_LINES") ? atoi(getenv("BJX_LINES")) : 2;
     const bool use_l2 = B.l2_bytes && lines_env != 1 && !getenv("BJX_PROF_LINES") && !A.dbg;
-    e->last_line_kernel = use_l2 ? 2u : 1u;
-    if (use_l2) {
+    e->last_line_kernel = all_wide ? 3u : use_l2 ? 2u : 1u;
+    if (all_wide) {
+      // every scope is past 128 positions (more than 128 global rules): no
+      // line-kernel pass, the per-line fallback (decide_wide) takes every line
+      // from its own parse
+      hipLaunchKernelGGL(k_no_line_pass, dim3(1), dim3(64), 0, st, e->scalars.p, (unsigned long long)n_lines);
+      HIP_OK(hipGetLastError());
+    } else if (use_l2) {
       const uint32_t lds = B.l2_bytes + (kL2Block / 64) * kL2WaveLds;
       const void *fn = B.l2_w == 2 ? reinterpret_cast<const void *>(&k_lines2<2>) : reinterpret_cast<const void *>(&k_lines2<1>);
       if (lds != e->lines2_lds || B.l2_w != e->lines2_w) {
@@ -7420,8 +7434,9 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       WL.line = e->wl_line.p; WL.rule = e->wl_rule.p; WL.pos = e->wl_pos.p; WL.cap = cap;
       HIP_OK(hipMemsetAsync(e->scalars.p + 13, 0, 8, st));
     }
+    if (all_wide) HIP_OK(hipEventRecord(e->evk[0], st));  // the per-line kernel of this batch (kernel_ms[1])
     hipLaunchKernelGGL(k_parse_match<true>, dim3(grid_for(n_slow)), dim3(kBlock), 0, st, B, buf, e->nl.p, (uint64_t)n_slow,
-                       e->slow_list.p, now_ns, L, e->slow_list.p, e->scalars.p, WL);
+                       all_wide ? nullptr : e->slow_list.p, now_ns, L, e->slow_list.p, e->scalars.p, WL);
     HIP_OK(hipGetLastError());
     if (B.any_wide) {
       unsigned long long n_wl = 0;
@@ -7430,6 +7445,7 @@ static bool match_phase(bjx_engine *e, const bjx_ruleset *rs, const uint8_t *byt
       if (n_wl > WL.cap) throw BjxError(BJX_ERR_DEVICE, "internal: wide-NFA job list overflow");
       if (n_wl) launch_wide(e, B, buf, n, e->wl_rule.p, nullptr, e->wl_line.p, e->wl_pos.p, 0, n_wl, L, e->wide_max_w, e->wide_max_g);
     }
+    if (all_wide) HIP_OK(hipEventRecord(e->evk[1], st));
   }
   e->last_slow = n_slow;
   if (getenv("BJX_CHECK")) {
@@ -8422,7 +8438,7 @@ extern "C" size_t bjx_debug_kernel_ms(bjx_engine *e, double *out, size_t cap) {
   if (!e) return 0;
   // [3]: which per-line kernel ran (2 = k_lines2, 1 = k_lines), [4]: its line window / staging bytes
   const double v[5] = {e->kernel_ms[0], e->kernel_ms[1], e->kernel_ms[2], (double)e->last_line_kernel,
-                       e->last_line_kernel == 2 ? (double)kL2Win : (double)kSpanBytes};
+                       e->last_line_kernel == 2 ? (double)kL2Win : e->last_line_kernel == 1 ? (double)kSpanBytes : 0.0};
   for (size_t k = 0; k < cap && k < 5; ++k) out[k] = v[k];
   return 5;
 }

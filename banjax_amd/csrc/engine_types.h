@@ -251,13 +251,16 @@ struct Lines {
   int32_t *host_id;
   uint8_t *flags;
   uint64_t *counts;    // (n_results << 32) | n_events per line, then scanned in place
-  uint64_t *masks;     // mask_words per line
+  uint64_t *masks;     // mask_words per line, word-major: word w of line j at masks[w * mstride + j]
+                       // (consecutive lines' words adjacent: coalesced stores / loads for any width)
+  uint64_t mstride;    // lines per mask word plane (the batch's line capacity)
   uint4 *ip16;         // key16 of the line's IP (see IpSlot)
   CandMeta *cand_meta;  // literal hits recorded by the scan pass (zeroed before it)
   uint64_t *cand;       // kCandSlots per line: (literal start << 24) | verified | literal id
   // rulesets of at most kCandFirstLits literals (Bind::cfirst): per line and
   // literal id, the lowest candidate position (~0: none), every hit counted
   uint64_t *cand_first;
+  __host__ __device__ uint64_t &mword(uint64_t j, uint32_t w) const { return masks[(uint64_t)w * mstride + j]; }
 };
 constexpr uint32_t kCandFirstLits = 8;
 

@@ -638,11 +638,11 @@ __global__ __launch_bounds__(kL2Block, 4) void k_lines2(Bind B, LinesArgs A) {
           uint32_t n_m = 0, n_ev = 0;
 #pragma unroll
           for (int k = 0; k < W; ++k) {
-            L.masks[j * B.mask_words + k] = m.w[k];
+            L.mword(j, k) = m.w[k];
             n_m += __popcll(m.w[k]);
             n_ev += __popcll(m.w[k] & ~skp.w[k]);
           }
-          if (W == 1 && B.mask_words > 1) L.masks[j * B.mask_words + 1] = 0;
+          if (W == 1 && B.mask_words > 1) L.mword(j, 1) = 0;
           L.counts[j] = ((uint64_t)n_m << 32) | (uint64_t)n_ev;
         }
         L.rest_off[j] = rest_off;

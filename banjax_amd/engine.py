@@ -280,10 +280,12 @@ class Engine:
         return {"k_scan": out[0], "k_lines": out[1], "dfa_jobs": out[2]}
 
     def line_kernel(self):
-        """The last batch's per-line kernel: ("k_lines2", window bytes per line) or ("k_lines", staging bytes per wave)."""
+        """The last batch's per-line kernel: ("k_lines2", window bytes per line), ("k_lines", staging bytes per
+        wave), or ("k_parse_match", 0) when every scope is past 128 rules and the per-line fallback took every line."""
         out = (C.c_double * 5)()
         _lib.lib().bjx_debug_kernel_ms(self._h, out, 5)
-        return ("k_lines2" if out[3] == 2 else "k_lines" if out[3] == 1 else None), int(out[4])
+        names = {1: "k_lines", 2: "k_lines2", 3: "k_parse_match"}
+        return names.get(int(out[3])), int(out[4])
 
     def state_get(self, ip, name):
         hits, start = C.c_int64(), C.c_int64()

@@ -110,6 +110,8 @@ KERNELS = {
     "k_lines": "k_lines (the per-line fallback for rulesets past k_lines2's tables: each wave's lines staged in "
                "%d B of LDS, the host's rules walked entry by entry; undecided pairs emitted as DFA jobs)",
     "dfa_jobs": "DFA-job sort + k_dfa / k_nfa (the (line, rule) pairs the literals cannot decide)",
+    "k_parse_match": "k_parse_match (scopes past 128 rules: one lane per line parses it and decides the rules its "
+                     "literal hits name plus the anchored / ALWAYS ones by their automata, decide_wide)",
 }
 
 
@@ -117,7 +119,8 @@ def kernel_desc(dom, line_kernel):
     if dom != "k_lines":
         return KERNELS[dom]
     name, nb = line_kernel
-    return KERNELS[name or "k_lines2"] % nb
+    t = KERNELS[name or "k_lines2"]
+    return t % nb if "%d" in t else t
 
 
 def roofline(kms, nbytes, args, line_kernel=("k_lines2", 112)):

@@ -120,6 +120,8 @@ def test_per_site_regex_stress(engine):
     data = "".join(lines).encode()
     out = pair.feed(data, base * S)  # reference: lines at time.Now()+j, never old
     assert out.n_trips == n
+    # 10,000 global rules: no line-kernel pass, the wide per-line kernel (decide_wide) takes every line
+    assert pair.engine.line_kernel()[0] == "k_parse_match"
     for j in range(0, n, 997):
         assert pair.engine.state_get(ips[j], "rule%d" % j) == (0, (base + j) * S)
     pair.compare_state(ips[:50])
@@ -148,17 +150,21 @@ def test_workload_parity(engine, name, n_lines, batches):
     pair.compare_state(sorted(ips)[:100])
 
 
-def test_wide_scope_workload(engine):
+@pytest.mark.parametrize("line_pass", [False, True])
+def test_wide_scope_workload(engine, line_pass, monkeypatch):
     """cfg2k: 1,000 global rules in the TestPerSiteRegexStress shape
     (regex_rate_limiter_test.go:299-365), so every line's scope has 1,000
-    positions: past k_lines2's 128-position tables, the per-line pass is k_lines
-    (the bench line of this shape is in DESIGN.md §5).  Bit-exact against the
-    oracle over two batches."""
+    positions: past k_lines2's 128-position tables, no line-kernel pass runs and
+    the wide per-line kernel (k_parse_match, decide_wide) takes every line (the
+    bench line of this shape is in DESIGN.md §5).  Bit-exact against the oracle
+    over two batches, and again with BJX_LINES=1 (the old k_lines pass first)."""
+    if line_pass:
+        monkeypatch.setenv("BJX_LINES", "1")
     w = W.scaled(W.CFG2K, 12_000, n_ips=3_000)
     pair = Pair(w.rules_yaml, engine)
     for b in range(2):
         pair.feed(w.host_lines(b * 6_000, 6_000), w.now_ns(b * 6_000, 6_000))
-        assert pair.engine.line_kernel()[0] == "k_lines"
+        assert pair.engine.line_kernel()[0] == ("k_lines" if line_pass else "k_parse_match")
     pair.compare_state([ln.split(b" ")[1].decode() for ln in w.host_lines(0, 50).split(b"\n")[:50] if ln])
 
 
