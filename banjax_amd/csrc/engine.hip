@@ -445,19 +445,16 @@ struct WideList {
 __device__ void decide_wide(const Bind &B, const uint8_t *line, uint64_t s, uint32_t n, uint32_t rest_off, int32_t hid, uint64_t j,
                             const Lines &L, const WideList &WL);
 
+__device__ __forceinline__ uint32_t find_spaces(const uint8_t *p, uint32_t n, uint32_t &sp0, uint32_t &sp1,
+                                                uint32_t &sp2, uint32_t &sp3);
+
 template <bool SLOW>
 __device__ void parse_and_match(const Bind &B, const uint8_t *__restrict__ p, uint64_t s, uint32_t n, uint64_t j, int64_t now_ns,
                                 const Lines &L, uint32_t *slow_list, unsigned long long *slow_count, const WideList &WL) {
   uint8_t fl = 0;
   L.counts[j] = 0;
-  const uint32_t sp1 = find_space(p, 0, n);
-  if (sp1 >= n) { L.flags[j] = kLineError; return; }
-  const uint32_t sp2 = find_space(p, sp1 + 1, n);
-  if (sp2 >= n) { L.flags[j] = kLineError; return; }
-  const uint32_t sp3 = find_space(p, sp2 + 1, n);
-  if (sp3 >= n) { L.flags[j] = kLineError; return; }
-  const uint32_t sp4 = find_space(p, sp3 + 1, n);
-  if (sp4 >= n) { L.flags[j] = kLineError; return; }
+  uint32_t sp1 = 0, sp2 = 0, sp3 = 0, sp4 = 0;  // the first four spaces, 16-B loads (find_spaces)
+  if (find_spaces(p, n, sp1, sp2, sp3, sp4) < 4) { L.flags[j] = kLineError; return; }
   const uint32_t ip_off = sp1 + 1, ip_len = sp2 - sp1 - 1;
   const uint32_t rest_off = sp2 + 1, host_off = sp3 + 1, host_len = sp4 - sp3 - 1;
   int32_t hid;
@@ -1167,6 +1164,9 @@ __device__ __forceinline__ void decide_rules(const Bind &B, const Tabs &T, const
 // literals occurs in the line cannot match, so only the rules of the line's
 // hits (all literal rules when the hits overflow the line's slots), its
 // anchored / no-literal rules and its ALWAYS rules are looked at.
+__device__ __forceinline__ uint32_t lead_start(const Bind &B, const Lines &L, uint64_t j, uint32_t pos, uint64_t rs,
+                                               uint32_t rl);
+
 __device__ void decide_wide(const Bind &B, const uint8_t *line, uint64_t s, uint32_t n, uint32_t rest_off, int32_t hid, uint64_t j,
                             const Lines &L, const WideList &WL) {
 #ifdef BJX_WIDE_NODECIDE  // timing experiment only (results wrong): the fallback's parse alone
@@ -1182,12 +1182,26 @@ __device__ void decide_wide(const Bind &B, const uint8_t *line, uint64_t s, uint
   auto rule_at = [&](uint32_t pos) { return pos < nsite ? B.site_rules[B.site_off[hid] + pos] : pos - nsite; };
   // rule r (its pattern's first rule) at pos by its automaton; wide NFAs to k_nfa_wide
   auto eval = [&](uint32_t r, uint32_t pos) {
+#ifdef BJX_WIDE_NOEVAL  // timing experiment only (results wrong): no automaton runs
+    return;
+#endif
     if (B.any_wide && (B.rules[r].flags & kRuleNfaWide)) {
       const unsigned long long q = atomicAdd(WL.count, 1ull);
       if (q < WL.cap) { WL.line[q] = (uint32_t)j; WL.rule[q] = r; WL.pos[q] = pos; }
     } else if (rule_match(B, r, rest, rest_len)) {
       setb(pos);
     }
+  };
+  // a rule named by a literal hit: a lead rule's automaton starts at the first
+  // hit of its literals (lead_start: every match begins there, as k_dfa's jobs
+  // do), not at rest[0]; a lane's run is then a few bytes, not the line
+  auto eval_hit = [&](uint32_t r, uint32_t pos) {
+#ifdef BJX_WIDE_NOEVAL
+    return;
+#endif
+    if ((B.any_wide && (B.rules[r].flags & kRuleNfaWide)) || !(B.rules[r].lead & 1u)) { eval(r, pos); return; }
+    const uint32_t st0 = lead_start(B, L, j, pos, s + rest_off, rest_len);
+    if (st0 < rest_len && rule_match(B, r, rest + st0, rest_len - st0)) setb(pos);
   };
   // ALWAYS rules
   if (hid >= 0)
@@ -1221,7 +1235,12 @@ __device__ void decide_wide(const Bind &B, const uint8_t *line, uint64_t s, uint
   }
   // the line's literal hits inside rest (the scan pass's slots; unverified
   // ones checked here)
-  const CandMeta cm = L.cand_meta[j];
+  const CandMeta cm =
+#ifdef BJX_WIDE_NOHITS  // timing experiment only (results wrong): no literal hits
+      CandMeta{};
+#else
+      L.cand_meta[j];
+#endif
   const uint64_t rs = s + rest_off;
   uint32_t lits[kCandSlots], lpos[kCandSlots], nlit = 0;
   const bool ovf = cm.cnt > (uint32_t)kCandSlots;
@@ -1251,7 +1270,7 @@ __device__ void decide_wide(const Bind &B, const uint8_t *line, uint64_t s, uint
           const uint32_t pos = nsite + x.y;
           if ((L.mword(j, pos >> 6) >> (pos & 63)) & 1) continue;  // matched already
           if (x.x >> 31) setb(pos);
-          else eval(x.x, pos);
+          else eval_hit(x.x, pos);
         }
       if (hid < 0 || g == e) continue;
       // this host's run of the literal's site entries (decide_rules)
@@ -1274,11 +1293,11 @@ __device__ void decide_wide(const Bind &B, const uint8_t *line, uint64_t s, uint
           if (hp != 0xFFFF && hp >= off && hp - off + lit_len_of(T, fl) <= rest_len && literal_at(T, fl, rest + (hp - off)))
             setb(x.y);
           else if (hp == 0xFFFF)
-            eval(x.x & 0x7FFFFFFFu, x.y);
+            eval_hit(x.x & 0x7FFFFFFFu, x.y);
           continue;
         }
         if ((x.x >> 31) && full == kNone) setb(x.y);
-        else eval(x.x & 0x7FFFFFFFu, x.y);
+        else eval_hit(x.x & 0x7FFFFFFFu, x.y);
       }
     }
   }
