@@ -364,10 +364,11 @@ def main():
     dec = None
     if args.bans_steps > 0 and not bans:
         bans = True
-        # untimed, as many steps as are timed: the emission's first-use
-        # allocations (pinned host buffers grown to the largest output of the
-        # steps' cycle; cfg5's trip count repeats every third step)
-        for _ in range(args.bans_steps):
+        # untimed, as many steps as the plain run took: the emission's
+        # first-use allocations (pinned host buffers grown to the largest
+        # output of the steps' cycle: cfg5's trip count repeats every third
+        # step, cfg3 has a trip burst every few dozen)
+        for _ in range(max(args.bans_steps, args.warmup + args.steps)):
             step()
         el2, _ = timed_region(dist, step, sync_all, args.bans_steps, "cuda")
         bans = False

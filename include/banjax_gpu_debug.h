@@ -34,8 +34,10 @@ int bjx_debug_regex_parse(const char *pattern, size_t len, char *err, size_t err
 size_t bjx_debug_phase_ms(bjx_engine *e, double *out, size_t cap);
 /* device ms of the last batch's dominant kernels, from HIP events on the
    engine stream: k_scan, the per-line kernel, DFA-job sort + k_dfa / k_nfa;
-   then which per-line kernel ran (2 = k_lines2, 1 = k_lines) and its window
-   bytes per line (k_lines2) or staging bytes per wave (k_lines) (returns 5) */
+   then which per-line kernel ran (2 = k_lines2, 1 = k_lines, 3 = the wide
+   per-line kernel k_parse_match on every line: rulesets of more than 128
+   global rules) and its window bytes per line (k_lines2) or staging bytes per
+   wave (k_lines), 0 for k_parse_match (returns 5) */
 size_t bjx_debug_kernel_ms(bjx_engine *e, double *out, size_t cap);
 /* last batch: gram bitset hits, recorded literal hits, lines sent to the per-line
    fallback, lines decided by the long-line pass, DFA jobs; then the state
