@@ -4698,6 +4698,15 @@ struct HostBuf {
     }
     n = want;
   }
+  // capacity of at least `want` elements (contents not kept)
+  void reserve(size_t want) {
+    if (want <= cap) return;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&p), want * sizeof(T), hipHostMallocDefault));
+    cap = want;
+  }
   void clear() { n = 0; }
   bool empty() const { return n == 0; }
   T *data() { return p; }
@@ -7629,6 +7638,11 @@ static void emit_bans(bjx_engine *e, uint64_t n, bool records_only) {
   pin_get(e, &n_seg, e->bn_seg.p + (n - 1), 4);
   pin_sync(e);
   const uint64_t log_bytes = e->ban_off.data()[n];
+  // A trip burst's log can be several times the usual one (cfg3: 0.5 -> 3.4 GB
+  // every few dozen batches), and pinning it the first time stalls that batch
+  // for ~0.1 ms/MB: the first log buffer already holds a quarter of the
+  // batch's bytes (at most 16 GB)
+  if (log_bytes) e->ban_log.reserve(std::min<uint64_t>(e->bc.consumed / 4, 16ull << 30));
   e->ban_log.resize(log_bytes);
   bool log_copy = false;
   if (log_bytes) {
