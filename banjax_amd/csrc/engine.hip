@@ -7640,9 +7640,9 @@ static void emit_bans(bjx_engine *e, uint64_t n, bool records_only) {
   const uint64_t log_bytes = e->ban_off.data()[n];
   // A trip burst's log can be several times the usual one (cfg3: 0.5 -> 3.4 GB
   // every few dozen batches), and pinning it the first time stalls that batch
-  // for ~0.1 ms/MB: the first log buffer already holds a quarter of the
-  // batch's bytes (at most 16 GB)
-  if (log_bytes) e->ban_log.reserve(std::min<uint64_t>(e->bc.consumed / 4, 16ull << 30));
+  // for ~0.1 ms/MB: the first log buffer already holds half the batch's
+  // bytes (at most 16 GB; cfg3's largest bursts: 13M trips, about 5 GB)
+  if (log_bytes) e->ban_log.reserve(std::min<uint64_t>(e->bc.consumed / 2, 16ull << 30));
   e->ban_log.resize(log_bytes);
   bool log_copy = false;
   if (log_bytes) {
